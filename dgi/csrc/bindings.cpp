@@ -1,0 +1,309 @@
+// dgi/csrc/bindings.cpp — registers the gfx950 kernels as torch.ops.dgi.*.
+//
+// Every op launches on the current HIP stream and allocates nothing, so the
+// whole decode step can be captured into a hipGraph (torch.cuda.CUDAGraph on
+// ROCm).  Shapes are checked here, on the host, before any launch: a kernel
+// never sees operands that disagree with its grid.
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+extern "C" {
+int dgi_rmsnorm(void* out, const void* x, const void* w, int T, int H, float eps, hipStream_t s);
+int dgi_fused_add_rmsnorm(void* x, void* residual, const void* w, int T, int H, float eps,
+                          hipStream_t s);
+int dgi_rope_cache(void* qkv, int T, int qkv_stride, const int* positions, const float* cos_sin,
+                   int nh, int nkv, int hd, const int* slot_mapping, void* k_cache, void* v_cache,
+                   int block_size, hipStream_t s);
+int dgi_paged_decode(const void* q, int q_stride, const void* k_cache, const void* v_cache,
+                     const int* block_tables, int bt_stride, const int* context_lens, void* out,
+                     int out_stride, float* part_o, float* part_lse, int B, int nh, int nkv, int hd,
+                     int block_size, int max_splits, int part_size, float scale, hipStream_t s);
+int dgi_paged_prefill(const void* q, int q_stride, const void* k_cache, const void* v_cache,
+                      const int* block_tables, int bt_stride, const int* cu_seqlens_q,
+                      const int* context_lens, const int* tiles, int n_tiles, void* out,
+                      int out_stride, int nh, int nkv, int hd, int block_size, float scale,
+                      const unsigned long long* tree_mask, int tree_n, hipStream_t s);
+int dgi_silu_mul(const void* gu, void* out, int T, int I, hipStream_t s);
+int dgi_sample(const void* logits, int is_bf16, int B, int V, int stride, const float* temperature,
+               const long long* seeds, long long step, long long* out, hipStream_t s);
+int dgi_topk(const void* logits, int is_bf16, int B, int V, int stride, int K, float* out_v,
+             long long* out_i, hipStream_t s);
+int dgi_kv_gather(const void* cache, const int* ids, int n, int LK, int num_blocks, int page_elems,
+                  void* buf, hipStream_t s);
+int dgi_kv_scatter(void* cache, const int* ids, int n, int LK, int num_blocks, int page_elems,
+                   const void* buf, hipStream_t s);
+int dgi_kv_copy(void* cache, const int* src, const int* dst, int n, int LK, int num_blocks,
+                int page_elems, hipStream_t s);
+int dgi_tree_mask(const int* parent, int B, int N, unsigned long long* anc, int* depth,
+                  hipStream_t s);
+int dgi_tree_verify(const int* parent, const long long* draft, const long long* target, int B,
+                    int N, const unsigned long long* anc, const int* depth, int* accept_len,
+                    int* path, long long* out_tokens, int max_path, hipStream_t s);
+}
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_rc(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, "dgi kernel ", what, " failed with code ", rc,
+              rc > 0 ? (std::string(" (") + hipGetErrorString((hipError_t)rc) + ")") : std::string());
+}
+
+void check_dev(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+}
+void check_bf16(const at::Tensor& t, const char* name) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16");
+}
+void check_i32(const at::Tensor& t, const char* name) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kInt, name, " must be int32");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+void rmsnorm(at::Tensor out, const at::Tensor& x, const at::Tensor& w, double eps) {
+  check_bf16(out, "out"); check_bf16(x, "x"); check_bf16(w, "w");
+  TORCH_CHECK(x.is_contiguous() && out.is_contiguous() && w.is_contiguous());
+  const int H = (int)x.size(-1);
+  TORCH_CHECK(w.numel() == H && out.numel() == x.numel());
+  check_rc(dgi_rmsnorm(out.data_ptr(), x.data_ptr(), w.data_ptr(), (int)(x.numel() / H), H,
+                       (float)eps, cur_stream()), "rmsnorm");
+}
+
+void fused_add_rmsnorm(at::Tensor x, at::Tensor residual, const at::Tensor& w, double eps) {
+  check_bf16(x, "x"); check_bf16(residual, "residual"); check_bf16(w, "w");
+  TORCH_CHECK(x.is_contiguous() && residual.is_contiguous() && w.is_contiguous());
+  const int H = (int)x.size(-1);
+  TORCH_CHECK(w.numel() == H && residual.numel() == x.numel());
+  check_rc(dgi_fused_add_rmsnorm(x.data_ptr(), residual.data_ptr(), w.data_ptr(),
+                                 (int)(x.numel() / H), H, (float)eps, cur_stream()),
+           "fused_add_rmsnorm");
+}
+
+// k_cache / v_cache: [num_blocks, nkv, bs, hd] (contiguous per-layer views)
+void rope_cache(at::Tensor qkv, const at::Tensor& positions, const at::Tensor& cos_sin, int64_t nh,
+                int64_t nkv, int64_t hd, const at::Tensor& slot_mapping, at::Tensor k_cache,
+                at::Tensor v_cache) {
+  check_bf16(qkv, "qkv"); check_i32(positions, "positions"); check_i32(slot_mapping, "slot_mapping");
+  check_bf16(k_cache, "k_cache"); check_bf16(v_cache, "v_cache");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() && cos_sin.size(1) == hd);
+  TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1 && qkv.size(1) >= (nh + 2 * nkv) * hd);
+  TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous());
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == nkv && k_cache.size(3) == hd);
+  const int T = (int)qkv.size(0);
+  TORCH_CHECK(positions.numel() == T && slot_mapping.numel() == T);
+  check_rc(dgi_rope_cache(qkv.data_ptr(), T, (int)qkv.stride(0), positions.data_ptr<int>(),
+                          cos_sin.data_ptr<float>(), (int)nh, (int)nkv, (int)hd,
+                          slot_mapping.data_ptr<int>(), k_cache.data_ptr(), v_cache.data_ptr(),
+                          (int)k_cache.size(2), cur_stream()),
+           "rope_cache");
+}
+
+// q: [B, >= nh*hd] rows (row stride = q.stride(0)); out: [B, nh*hd]
+void paged_decode(at::Tensor out, const at::Tensor& q, const at::Tensor& k_cache,
+                  const at::Tensor& v_cache, const at::Tensor& block_tables,
+                  const at::Tensor& context_lens, at::Tensor part_o, at::Tensor part_lse,
+                  int64_t nh, int64_t nkv, int64_t max_splits, int64_t part_size, double scale) {
+  check_bf16(out, "out"); check_bf16(q, "q"); check_bf16(k_cache, "k_cache"); check_bf16(v_cache, "v_cache");
+  check_i32(block_tables, "block_tables"); check_i32(context_lens, "context_lens");
+  TORCH_CHECK(q.dim() == 2 && q.stride(1) == 1 && out.dim() == 2 && out.stride(1) == 1);
+  const int hd = (int)k_cache.size(3);
+  const int B = (int)q.size(0);
+  TORCH_CHECK(q.size(1) >= nh * hd && out.size(1) >= nh * hd && out.size(0) == B);
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) >= B && context_lens.numel() >= B);
+  TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous() && k_cache.size(1) == nkv);
+  if (max_splits > 1) {
+    TORCH_CHECK(part_o.scalar_type() == at::kFloat && part_lse.scalar_type() == at::kFloat);
+    TORCH_CHECK(part_o.numel() >= (int64_t)B * nh * max_splits * hd);
+    TORCH_CHECK(part_lse.numel() >= (int64_t)B * nh * max_splits);
+  }
+  check_rc(dgi_paged_decode(q.data_ptr(), (int)q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                            block_tables.data_ptr<int>(), (int)block_tables.stride(0),
+                            context_lens.data_ptr<int>(), out.data_ptr(), (int)out.stride(0),
+                            max_splits > 1 ? part_o.data_ptr<float>() : nullptr,
+                            max_splits > 1 ? part_lse.data_ptr<float>() : nullptr, B, (int)nh,
+                            (int)nkv, hd, (int)k_cache.size(2), (int)max_splits, (int)part_size,
+                            (float)scale, cur_stream()),
+           "paged_decode");
+}
+
+void paged_prefill(at::Tensor out, const at::Tensor& q, const at::Tensor& k_cache,
+                   const at::Tensor& v_cache, const at::Tensor& block_tables,
+                   const at::Tensor& cu_seqlens_q, const at::Tensor& context_lens,
+                   const at::Tensor& tiles, int64_t nh, int64_t nkv, double scale,
+                   const c10::optional<at::Tensor>& tree_mask, int64_t tree_n) {
+  check_bf16(out, "out"); check_bf16(q, "q"); check_bf16(k_cache, "k_cache"); check_bf16(v_cache, "v_cache");
+  check_i32(block_tables, "block_tables"); check_i32(cu_seqlens_q, "cu_seqlens_q");
+  check_i32(context_lens, "context_lens"); check_i32(tiles, "tiles");
+  TORCH_CHECK(q.dim() == 2 && q.stride(1) == 1 && out.dim() == 2 && out.stride(1) == 1);
+  const int hd = (int)k_cache.size(3);
+  TORCH_CHECK(q.size(1) >= nh * hd && out.size(1) >= nh * hd && out.size(0) == q.size(0));
+  TORCH_CHECK(tiles.dim() == 2 && tiles.size(1) == 2);
+  TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous() && k_cache.size(1) == nkv);
+  const unsigned long long* tm = nullptr;
+  if (tree_mask.has_value() && tree_mask->defined()) {
+    TORCH_CHECK(tree_mask->scalar_type() == at::kLong && tree_mask->is_contiguous());
+    TORCH_CHECK(tree_mask->size(-1) == 64 && tree_mask->numel() >= 64 * (cu_seqlens_q.numel() - 1));
+    tm = reinterpret_cast<const unsigned long long*>(tree_mask->data_ptr<int64_t>());
+  }
+  check_rc(dgi_paged_prefill(q.data_ptr(), (int)q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                             block_tables.data_ptr<int>(), (int)block_tables.stride(0),
+                             cu_seqlens_q.data_ptr<int>(), context_lens.data_ptr<int>(),
+                             tiles.data_ptr<int>(), (int)tiles.size(0), out.data_ptr(),
+                             (int)out.stride(0), (int)nh, (int)nkv, hd, (int)k_cache.size(2),
+                             (float)scale, tm, (int)tree_n, cur_stream()),
+           "paged_prefill");
+}
+
+void silu_mul(at::Tensor out, const at::Tensor& gu) {
+  check_bf16(out, "out"); check_bf16(gu, "gu");
+  TORCH_CHECK(gu.is_contiguous() && out.is_contiguous());
+  const int I = (int)out.size(-1);
+  TORCH_CHECK(gu.size(-1) == 2 * I && gu.numel() == 2 * out.numel());
+  check_rc(dgi_silu_mul(gu.data_ptr(), out.data_ptr(), (int)(out.numel() / I), I, cur_stream()),
+           "silu_mul");
+}
+
+void sample(at::Tensor out, const at::Tensor& logits, const c10::optional<at::Tensor>& temperature,
+            const c10::optional<at::Tensor>& seeds, int64_t step) {
+  check_dev(logits, "logits");
+  TORCH_CHECK(out.scalar_type() == at::kLong && out.is_contiguous());
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1);
+  TORCH_CHECK(logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat);
+  const int B = (int)logits.size(0);
+  TORCH_CHECK(out.numel() >= B);
+  const float* tp = nullptr;
+  const long long* sp = nullptr;
+  if (temperature.has_value() && temperature->defined()) {
+    TORCH_CHECK(temperature->scalar_type() == at::kFloat && temperature->numel() >= B);
+    tp = temperature->data_ptr<float>();
+  }
+  if (seeds.has_value() && seeds->defined()) {
+    TORCH_CHECK(seeds->scalar_type() == at::kLong && seeds->numel() >= B);
+    sp = reinterpret_cast<const long long*>(seeds->data_ptr<int64_t>());
+  }
+  check_rc(dgi_sample(logits.data_ptr(), logits.scalar_type() == at::kBFloat16, B,
+                      (int)logits.size(1), (int)logits.stride(0), tp, sp, step,
+                      reinterpret_cast<long long*>(out.data_ptr<int64_t>()), cur_stream()),
+           "sample");
+}
+
+void topk(at::Tensor out_v, at::Tensor out_i, const at::Tensor& logits, int64_t k) {
+  check_dev(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1);
+  const int B = (int)logits.size(0);
+  TORCH_CHECK(out_v.scalar_type() == at::kFloat && out_i.scalar_type() == at::kLong);
+  TORCH_CHECK(out_v.numel() >= B * k && out_i.numel() >= B * k);
+  check_rc(dgi_topk(logits.data_ptr(), logits.scalar_type() == at::kBFloat16, B, (int)logits.size(1),
+                    (int)logits.stride(0), (int)k, out_v.data_ptr<float>(),
+                    reinterpret_cast<long long*>(out_i.data_ptr<int64_t>()), cur_stream()),
+           "topk");
+}
+
+// cache: [L, 2, NB, nkv, bs, hd]; buf: [L, 2, n, nkv, bs, hd]
+void kv_gather(at::Tensor buf, const at::Tensor& cache, const at::Tensor& ids) {
+  check_dev(cache, "cache"); check_i32(ids, "ids");
+  TORCH_CHECK(cache.is_contiguous() && buf.is_contiguous() && cache.dim() == 6);
+  const int n = (int)ids.numel();
+  const int LK = (int)(cache.size(0) * cache.size(1));
+  const int NB = (int)cache.size(2);
+  const int page = (int)(cache.size(3) * cache.size(4) * cache.size(5));
+  TORCH_CHECK(buf.numel() >= (int64_t)LK * n * page && buf.scalar_type() == cache.scalar_type());
+  check_rc(dgi_kv_gather(cache.data_ptr(), ids.data_ptr<int>(), n, LK, NB, page, buf.data_ptr(),
+                         cur_stream()), "kv_gather");
+}
+
+void kv_scatter(at::Tensor cache, const at::Tensor& ids, const at::Tensor& buf) {
+  check_dev(cache, "cache"); check_i32(ids, "ids");
+  TORCH_CHECK(cache.is_contiguous() && buf.is_contiguous() && cache.dim() == 6);
+  const int n = (int)ids.numel();
+  const int LK = (int)(cache.size(0) * cache.size(1));
+  const int NB = (int)cache.size(2);
+  const int page = (int)(cache.size(3) * cache.size(4) * cache.size(5));
+  TORCH_CHECK(buf.numel() >= (int64_t)LK * n * page && buf.scalar_type() == cache.scalar_type());
+  check_rc(dgi_kv_scatter(cache.data_ptr(), ids.data_ptr<int>(), n, LK, NB, page, buf.data_ptr(),
+                          cur_stream()), "kv_scatter");
+}
+
+void kv_copy(at::Tensor cache, const at::Tensor& src, const at::Tensor& dst) {
+  check_dev(cache, "cache"); check_i32(src, "src"); check_i32(dst, "dst");
+  TORCH_CHECK(cache.is_contiguous() && cache.dim() == 6 && src.numel() == dst.numel());
+  const int LK = (int)(cache.size(0) * cache.size(1));
+  const int NB = (int)cache.size(2);
+  const int page = (int)(cache.size(3) * cache.size(4) * cache.size(5));
+  check_rc(dgi_kv_copy(cache.data_ptr(), src.data_ptr<int>(), dst.data_ptr<int>(), (int)src.numel(),
+                       LK, NB, page, cur_stream()), "kv_copy");
+}
+
+void tree_mask(at::Tensor anc, at::Tensor depth, const at::Tensor& parent) {
+  check_i32(parent, "parent"); check_i32(depth, "depth");
+  TORCH_CHECK(anc.scalar_type() == at::kLong && anc.is_contiguous());
+  const int B = (int)parent.size(0), N = (int)parent.size(1);
+  TORCH_CHECK(N <= 64 && anc.numel() >= (int64_t)B * 64 && depth.numel() >= (int64_t)B * N);
+  check_rc(dgi_tree_mask(parent.data_ptr<int>(), B, N,
+                         reinterpret_cast<unsigned long long*>(anc.data_ptr<int64_t>()),
+                         depth.data_ptr<int>(), cur_stream()), "tree_mask");
+}
+
+void tree_verify(at::Tensor accept_len, at::Tensor path, at::Tensor out_tokens,
+                 const at::Tensor& parent, const at::Tensor& draft, const at::Tensor& target,
+                 const at::Tensor& anc, const at::Tensor& depth) {
+  check_i32(parent, "parent"); check_i32(depth, "depth"); check_i32(accept_len, "accept_len");
+  check_i32(path, "path");
+  TORCH_CHECK(draft.scalar_type() == at::kLong && target.scalar_type() == at::kLong);
+  TORCH_CHECK(out_tokens.scalar_type() == at::kLong && anc.scalar_type() == at::kLong);
+  const int B = (int)parent.size(0), N = (int)parent.size(1);
+  const int max_path = (int)path.size(1);
+  TORCH_CHECK(out_tokens.size(1) == max_path + 1 && draft.numel() >= (int64_t)B * N && target.numel() >= (int64_t)B * N);
+  check_rc(dgi_tree_verify(parent.data_ptr<int>(),
+                           reinterpret_cast<const long long*>(draft.data_ptr<int64_t>()),
+                           reinterpret_cast<const long long*>(target.data_ptr<int64_t>()), B, N,
+                           reinterpret_cast<const unsigned long long*>(anc.data_ptr<int64_t>()),
+                           depth.data_ptr<int>(), accept_len.data_ptr<int>(), path.data_ptr<int>(),
+                           reinterpret_cast<long long*>(out_tokens.data_ptr<int64_t>()), max_path,
+                           cur_stream()), "tree_verify");
+}
+
+}  // namespace
+
+TORCH_LIBRARY(dgi, m) {
+  m.def("rmsnorm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
+  m.def("fused_add_rmsnorm(Tensor(a!) x, Tensor(b!) residual, Tensor w, float eps) -> ()");
+  m.def("rope_cache(Tensor(a!) qkv, Tensor positions, Tensor cos_sin, int nh, int nkv, int hd, "
+        "Tensor slot_mapping, Tensor(b!) k_cache, Tensor(c!) v_cache) -> ()");
+  m.def("paged_decode(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
+        "Tensor context_lens, Tensor(b!) part_o, Tensor(c!) part_lse, int nh, int nkv, int max_splits, "
+        "int part_size, float scale) -> ()");
+  m.def("paged_prefill(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
+        "Tensor cu_seqlens_q, Tensor context_lens, Tensor tiles, int nh, int nkv, float scale, "
+        "Tensor? tree_mask, int tree_n) -> ()");
+  m.def("silu_mul(Tensor(a!) out, Tensor gu) -> ()");
+  m.def("sample(Tensor(a!) out, Tensor logits, Tensor? temperature, Tensor? seeds, int step) -> ()");
+  m.def("topk(Tensor(a!) out_v, Tensor(b!) out_i, Tensor logits, int k) -> ()");
+  m.def("kv_gather(Tensor(a!) buf, Tensor cache, Tensor ids) -> ()");
+  m.def("kv_scatter(Tensor(a!) cache, Tensor ids, Tensor buf) -> ()");
+  m.def("kv_copy(Tensor(a!) cache, Tensor src, Tensor dst) -> ()");
+  m.def("tree_mask(Tensor(a!) anc, Tensor(b!) depth, Tensor parent) -> ()");
+  m.def("tree_verify(Tensor(a!) accept_len, Tensor(b!) path, Tensor(c!) out_tokens, Tensor parent, "
+        "Tensor draft, Tensor target, Tensor anc, Tensor depth) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(dgi, CUDA, m) {
+  m.impl("rmsnorm", &rmsnorm);
+  m.impl("fused_add_rmsnorm", &fused_add_rmsnorm);
+  m.impl("rope_cache", &rope_cache);
+  m.impl("paged_decode", &paged_decode);
+  m.impl("paged_prefill", &paged_prefill);
+  m.impl("silu_mul", &silu_mul);
+  m.impl("sample", &sample);
+  m.impl("topk", &topk);
+  m.impl("kv_gather", &kv_gather);
+  m.impl("kv_scatter", &kv_scatter);
+  m.impl("kv_copy", &kv_copy);
+  m.impl("tree_mask", &tree_mask);
+  m.impl("tree_verify", &tree_verify);
+}

@@ -1,0 +1,296 @@
+// dgi/csrc/decode_attention.hip — paged GQA decode attention, split-KV.
+//
+// The reference decodes through HF `model.generate` with a dense per-request
+// cache (worker/engines/llm.py:61-69) and its shard path drops the KV
+// entirely (worker/distributed/grpc_server.py:365-374).  This kernel reads
+// the paged pool written by rope_cache.hip.
+//
+// Work decomposition (CDNA4, wave64):
+//   grid = (max_splits, n_kv_heads, batch), 256 threads = 4 waves.
+//   A workgroup owns one (sequence, kv-head, KV split) and all G = nh/nkv
+//   query heads of that kv head, so each K/V byte is read from HBM once per
+//   decode step regardless of the GQA ratio.
+//   Each wave walks 32-token tiles.  Scores are computed "swapped":
+//     S^T[token][query] = K[token][:] . Q[query][:]   (mfma_f32_16x16x32_bf16,
+//   K fragments straight from HBM into VGPRs, Q fragments resident), so a lane
+//   owns one query column and the online softmax needs only two xor-shuffles.
+//   The probabilities then feed  O^T[dim][query] += V^T[dim][token] . P^T
+//   directly from the accumulator registers; V^T comes from a per-wave LDS
+//   tile through ds_read_b64_tr_b16 (hardware transpose) with an XOR swizzle
+//   that makes the transposed reads bank-conflict free.
+//   The 4 waves merge (m, l, O) through LDS; with more than one split the
+//   partial results (normalised O and log2-sum-exp) go to a workspace and a
+//   small reduce kernel combines them.
+#include "common.h"
+
+using namespace dgi;
+
+namespace {
+
+template <int HD>
+__device__ __forceinline__ int v_lds_off(int row, int col) {
+  constexpr int NCH = HD / 8;  // 16-byte chunks per row
+  const int ch = (col >> 3) ^ (((row & 7) << 1) & (NCH - 1));
+  return row * HD + (ch << 3) + (col & 7);
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) void paged_decode_kernel(
+    const uint16_t* __restrict__ q, int q_stride, const uint16_t* __restrict__ k_cache,
+    const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ context_lens, uint16_t* __restrict__ out, int out_stride,
+    float* __restrict__ part_o, float* __restrict__ part_lse, int max_splits, int nh, int nkv,
+    int bs_log2, int part_size, float scale_log2) {
+  constexpr int KS = HD / 32;   // k-steps of the QK^T product
+  constexpr int NC = HD / 16;   // 16-wide dim blocks of the PV product
+  constexpr int VCH = HD / 8;   // 16-byte chunks per V row
+  constexpr int WREG = 32 * HD * 2 + 128;  // per-wave LDS bytes (V tile, then O/m/l)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int split = blockIdx.x;
+  const int h = blockIdx.y;
+  const int b = blockIdx.z;
+  const int ctx = context_lens[b];
+  const int start = split * part_size;
+  if (start >= ctx) return;
+  const int end = min(start + part_size, ctx);
+  const int nsplit = (ctx + part_size - 1) / part_size;
+  const int G = nh / nkv;
+  const int bs = 1 << bs_log2;
+
+  const int tid = threadIdx.x;
+  const int w = tid >> 6;
+  const int lane = tid & 63;
+  const int qi = lane & 15;
+  const int g = lane >> 4;
+  uint16_t* vt = reinterpret_cast<uint16_t*>(smem + w * WREG);
+
+  // Q fragments (B operand): B[k = 8g + j][col = query qi] = Q[qi][32 s + 8 g + j]
+  u32x4 qf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (qi < G) {
+      qf[s] = *reinterpret_cast<const u32x4*>(q + (size_t)b * q_stride + (h * G + qi) * HD + 32 * s + 8 * g);
+    } else {
+      qf[s] = u32x4{0, 0, 0, 0};
+    }
+  }
+
+  const int* bt = block_tables + (size_t)b * bt_stride;
+  const size_t head_stride = (size_t)bs * HD;
+
+  float m_run = -1e30f, l_run = 0.f;
+  f32x4 o[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) o[c] = f32x4{0, 0, 0, 0};
+
+  const int ntiles = (end - start + 31) >> 5;
+  for (int t = w; t < ntiles; t += 4) {
+    const int tb = start + (t << 5);
+    // ---- K fragments straight to VGPRs (A operand: row = token, k = dims)
+    u32x4 kf[2][KS];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      int tok = tb + 16 * u + qi;
+      tok = min(tok, end - 1);
+      const int blk = bt[tok >> bs_log2];
+      const uint16_t* kp = k_cache + ((size_t)blk * nkv + h) * head_stride + (size_t)(tok & (bs - 1)) * HD;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) kf[u][s] = *reinterpret_cast<const u32x4*>(kp + 32 * s + 8 * g);
+    }
+    // ---- V tile -> registers -> swizzled LDS
+    u32x4 vr[VCH / 2];
+#pragma unroll
+    for (int k = 0; k < VCH / 2; ++k) {
+      // 32 rows x VCH chunks; each pass covers 64/VCH rows
+      const int idx = k * 64 + lane;
+      const int row = idx / VCH;
+      const int ch = idx % VCH;
+      int tok = min(tb + row, end - 1);
+      const int blk = bt[tok >> bs_log2];
+      const uint16_t* vp = v_cache + ((size_t)blk * nkv + h) * head_stride + (size_t)(tok & (bs - 1)) * HD;
+      vr[k] = *reinterpret_cast<const u32x4*>(vp + ch * 8);
+    }
+    // ---- S^T = K Q^T
+    f32x4 sacc[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      sacc[u] = f32x4{0, 0, 0, 0};
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        sacc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(kf[u][s]), as_bf16x8(qf[s]), sacc[u], 0, 0, 0);
+    }
+    // write V (the previous tile's transposed reads are complete: in-order LDS per wave)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < VCH / 2; ++k) {
+      const int idx = k * 64 + lane;
+      const int row = idx / VCH;
+      const int ch = idx % VCH;
+      *reinterpret_cast<u32x4*>(vt + v_lds_off<HD>(row, ch * 8)) = vr[k];
+    }
+    // ---- online softmax (lane owns query qi; tokens 16u + 4g + i)
+    float x[2][4];
+    float mx = -1e30f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int tok = tb + 16 * u + 4 * g + i;
+        const float v = (tok < end) ? sacc[u][i] * scale_log2 : -1e30f;
+        x[u][i] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = exp2f(m_run - m_new);
+    float psum = 0.f;
+    float p[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int tok = tb + 16 * u + 4 * g + i;
+        p[u][i] = (tok < end) ? exp2f(x[u][i] - m_new) : 0.f;
+        psum += p[u][i];
+      }
+    psum += __shfl_xor(psum, 16, 64);
+    psum += __shfl_xor(psum, 32, 64);
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) o[c] *= alpha;
+    u32x4 pf;
+    pf[0] = pack_bf16x2(p[0][0], p[0][1]);
+    pf[1] = pack_bf16x2(p[0][2], p[0][3]);
+    pf[2] = pack_bf16x2(p[1][0], p[1][1]);
+    pf[3] = pack_bf16x2(p[1][2], p[1][3]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    // ---- O^T += V^T P^T ; V^T fragments via transposed LDS reads
+    const int tq = qi >> 2, tp = qi & 3;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_short4*)(vt + v_lds_off<HD>(4 * g + tq, 16 * c + 4 * tp)));
+      short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_short4*)(vt + v_lds_off<HD>(16 + 4 * g + tq, 16 * c + 4 * tp)));
+      u32x4 vf;
+      vf[0] = (uint32_t)(uint16_t)lo[0] | ((uint32_t)(uint16_t)lo[1] << 16);
+      vf[1] = (uint32_t)(uint16_t)lo[2] | ((uint32_t)(uint16_t)lo[3] << 16);
+      vf[2] = (uint32_t)(uint16_t)hi[0] | ((uint32_t)(uint16_t)hi[1] << 16);
+      vf[3] = (uint32_t)(uint16_t)hi[2] | ((uint32_t)(uint16_t)hi[3] << 16);
+      o[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(vf), as_bf16x8(pf), o[c], 0, 0, 0);
+    }
+  }
+
+  // ---- merge the 4 waves through LDS
+  __syncthreads();
+  float* ow = reinterpret_cast<float*>(smem + w * WREG);  // [16 q][HD] fp32 fits in 32*HD*2 bytes
+  float* ml = reinterpret_cast<float*>(smem + w * WREG + 32 * HD * 2);  // m[16], l[16]
+  if (qi < G) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ow[qi * HD + 16 * c + 4 * g + i] = o[c][i];
+    if (g == 0) {
+      ml[qi] = m_run;
+      ml[16 + qi] = l_run;
+    }
+  }
+  __syncthreads();
+  for (int idx = tid; idx < G * HD; idx += 256) {
+    const int qq = idx / HD;
+    const int d = idx - qq * HD;
+    float M = -1e30f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, reinterpret_cast<float*>(smem + ww * WREG + 32 * HD * 2)[qq]);
+    float L = 0.f, acc = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) {
+      const float* mlw = reinterpret_cast<float*>(smem + ww * WREG + 32 * HD * 2);
+      const float sc = exp2f(mlw[qq] - M);
+      L += mlw[16 + qq] * sc;
+      acc += reinterpret_cast<float*>(smem + ww * WREG)[qq * HD + d] * sc;
+    }
+    const int head = h * G + qq;
+    const float r = acc / L;
+    if (nsplit == 1) {
+      out[(size_t)b * out_stride + head * HD + d] = f32_to_bf16(r);
+    } else {
+      const size_t pi = ((size_t)b * nh + head) * max_splits + split;
+      part_o[pi * HD + d] = r;
+      if (d == 0) part_lse[pi] = M + log2f(L);
+    }
+  }
+}
+
+template <int HD>
+__global__ __launch_bounds__(HD) void decode_reduce_kernel(
+    const float* __restrict__ part_o, const float* __restrict__ part_lse,
+    const int* __restrict__ context_lens, uint16_t* __restrict__ out, int out_stride, int max_splits,
+    int nh, int part_size) {
+  const int b = blockIdx.x;
+  const int head = blockIdx.y;
+  const int ctx = context_lens[b];
+  const int nsplit = (ctx + part_size - 1) / part_size;
+  if (nsplit <= 1) return;
+  const size_t base = ((size_t)b * nh + head) * max_splits;
+  float M = -1e30f;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, part_lse[base + s]);
+  float W = 0.f, acc = 0.f;
+  for (int s = 0; s < nsplit; ++s) {
+    const float wgt = exp2f(part_lse[base + s] - M);
+    W += wgt;
+    acc += wgt * part_o[(base + s) * HD + threadIdx.x];
+  }
+  out[(size_t)b * out_stride + head * HD + threadIdx.x] = f32_to_bf16(acc / W);
+}
+
+}  // namespace
+
+extern "C" int dgi_paged_decode(const void* q, int q_stride, const void* k_cache,
+                                const void* v_cache, const int* block_tables, int bt_stride,
+                                const int* context_lens, void* out, int out_stride, float* part_o,
+                                float* part_lse, int B, int nh, int nkv, int hd, int block_size,
+                                int max_splits, int part_size, float scale, hipStream_t s) {
+  if (B == 0) return 0;
+  if (nh % nkv || nh / nkv > 16) return -2;
+  if (part_size % 128) return -3;
+  int bs_log2 = 0;
+  while ((1 << bs_log2) < block_size) ++bs_log2;
+  if ((1 << bs_log2) != block_size) return -4;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  dim3 grid(max_splits, nkv, B);
+  if (hd == 128) {
+    const size_t lds = 4 * (32 * 128 * 2 + 128);
+    paged_decode_kernel<128><<<grid, 256, lds, s>>>(
+        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,
+        block_tables, bt_stride, context_lens, (uint16_t*)out, out_stride, part_o, part_lse,
+        max_splits, nh, nkv, bs_log2, part_size, scale_log2);
+    DGI_CHECK_LAUNCH();
+    if (max_splits > 1) {
+      decode_reduce_kernel<128><<<dim3(B, nh), 128, 0, s>>>(part_o, part_lse, context_lens,
+                                                            (uint16_t*)out, out_stride, max_splits,
+                                                            nh, part_size);
+      DGI_CHECK_LAUNCH();
+    }
+  } else if (hd == 64) {
+    const size_t lds = 4 * (32 * 64 * 2 + 128);
+    paged_decode_kernel<64><<<grid, 256, lds, s>>>(
+        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,
+        block_tables, bt_stride, context_lens, (uint16_t*)out, out_stride, part_o, part_lse,
+        max_splits, nh, nkv, bs_log2, part_size, scale_log2);
+    DGI_CHECK_LAUNCH();
+    if (max_splits > 1) {
+      decode_reduce_kernel<64><<<dim3(B, nh), 64, 0, s>>>(part_o, part_lse, context_lens,
+                                                          (uint16_t*)out, out_stride, max_splits,
+                                                          nh, part_size);
+      DGI_CHECK_LAUNCH();
+    }
+  } else {
+    return -5;
+  }
+  return 0;
+}

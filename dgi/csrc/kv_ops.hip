@@ -1,0 +1,103 @@
+// dgi/csrc/kv_ops.hip — block-level KV movement.
+//
+// The block pool is one tensor per engine: [L, 2, num_blocks, n_kv, bs, hd]
+// bf16, so one block id names the page of every local layer.  These kernels
+// move whole pages:
+//   * gather  : pages of `ids` -> contiguous [L, 2, n, page] buffer (KV
+//               migration send buffer / CPU-tier spill staging),
+//   * scatter : contiguous buffer -> pages of `ids` (migration receive /
+//               CPU-tier restore),
+//   * copy    : page src[i] -> page dst[i] (radix-cache copy-on-write and
+//               speculative-decoding KV compaction).
+// The reference does these moves with per-block torch copies / pickles
+// (worker/distributed/kv_cache.py:447-475, 522-542; grpc_server.py:196-219).
+#include "common.h"
+
+using namespace dgi;
+
+namespace {
+
+// page = n_kv * bs * hd elements; moved as 16-byte chunks.
+__global__ __launch_bounds__(256) void kv_gather_kernel(const u32x4* __restrict__ cache,
+                                                        const int* __restrict__ ids, int n,
+                                                        int num_blocks, int page_chunks, int LK,
+                                                        u32x4* __restrict__ buf) {
+  const long total = (long)LK * n * page_chunks;
+  for (long c = (long)blockIdx.x * 256 + threadIdx.x; c < total; c += (long)gridDim.x * 256) {
+    const int within = (int)(c % page_chunks);
+    const long pg = c / page_chunks;  // (lk, i)
+    const int i = (int)(pg % n);
+    const int lk = (int)(pg / n);
+    buf[c] = cache[((long)lk * num_blocks + ids[i]) * page_chunks + within];
+  }
+}
+
+__global__ __launch_bounds__(256) void kv_scatter_kernel(u32x4* __restrict__ cache,
+                                                         const int* __restrict__ ids, int n,
+                                                         int num_blocks, int page_chunks, int LK,
+                                                         const u32x4* __restrict__ buf) {
+  const long total = (long)LK * n * page_chunks;
+  for (long c = (long)blockIdx.x * 256 + threadIdx.x; c < total; c += (long)gridDim.x * 256) {
+    const int within = (int)(c % page_chunks);
+    const long pg = c / page_chunks;
+    const int i = (int)(pg % n);
+    const int lk = (int)(pg / n);
+    cache[((long)lk * num_blocks + ids[i]) * page_chunks + within] = buf[c];
+  }
+}
+
+__global__ __launch_bounds__(256) void kv_copy_kernel(u32x4* __restrict__ cache,
+                                                      const int* __restrict__ src,
+                                                      const int* __restrict__ dst, int n,
+                                                      int num_blocks, int page_chunks, int LK) {
+  const long total = (long)LK * n * page_chunks;
+  for (long c = (long)blockIdx.x * 256 + threadIdx.x; c < total; c += (long)gridDim.x * 256) {
+    const int within = (int)(c % page_chunks);
+    const long pg = c / page_chunks;
+    const int i = (int)(pg % n);
+    const int lk = (int)(pg / n);
+    cache[((long)lk * num_blocks + dst[i]) * page_chunks + within] =
+        cache[((long)lk * num_blocks + src[i]) * page_chunks + within];
+  }
+}
+
+int grid_for(long total) {
+  long b = (total + 255) / 256;
+  return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
+}
+
+}  // namespace
+
+// LK = L*2 (layer x {k,v}); page_elems = n_kv*bs*hd
+extern "C" int dgi_kv_gather(const void* cache, const int* ids, int n, int LK, int num_blocks,
+                             int page_elems, void* buf, hipStream_t s) {
+  if (n == 0) return 0;
+  if (page_elems % 8) return -2;
+  const int pc = page_elems / 8;
+  kv_gather_kernel<<<grid_for((long)LK * n * pc), 256, 0, s>>>((const u32x4*)cache, ids, n,
+                                                               num_blocks, pc, LK, (u32x4*)buf);
+  DGI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dgi_kv_scatter(void* cache, const int* ids, int n, int LK, int num_blocks,
+                              int page_elems, const void* buf, hipStream_t s) {
+  if (n == 0) return 0;
+  if (page_elems % 8) return -2;
+  const int pc = page_elems / 8;
+  kv_scatter_kernel<<<grid_for((long)LK * n * pc), 256, 0, s>>>((u32x4*)cache, ids, n, num_blocks,
+                                                                pc, LK, (const u32x4*)buf);
+  DGI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dgi_kv_copy(void* cache, const int* src, const int* dst, int n, int LK,
+                           int num_blocks, int page_elems, hipStream_t s) {
+  if (n == 0) return 0;
+  if (page_elems % 8) return -2;
+  const int pc = page_elems / 8;
+  kv_copy_kernel<<<grid_for((long)LK * n * pc), 256, 0, s>>>((u32x4*)cache, src, dst, n,
+                                                             num_blocks, pc, LK);
+  DGI_CHECK_LAUNCH();
+  return 0;
+}

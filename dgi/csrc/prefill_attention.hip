@@ -1,0 +1,231 @@
+// dgi/csrc/prefill_attention.hip — varlen causal flash attention over the paged
+// KV pool (prefill, chunked prefill, prefix-cache hits, EAGLE tree
+// verification).
+//
+// The reference runs prefill inside HF `generate` / `ModelShard.forward`
+// (worker/engines/llm.py:61-69, worker/distributed/model_shard.py:173-228)
+// and has no prefix-aware attention.  Here new queries attend over
+// [cached prefix | freshly written KV] straight from the block pool.
+//
+// CDNA4 structure:
+//   grid = (q_tiles, n_heads), 256 threads = 4 waves x 32 query rows.
+//   K/V tiles of 64 keys are staged through LDS by the whole workgroup:
+//     * K image: 256-byte rows, 16-byte chunk XOR-swizzled by (row & 15) so the
+//       32-row ds_read_b128 fragment reads are conflict free (guide T2);
+//     * V image: chunk XOR (row & 3) << 2 so ds_read_b64_tr_b16 transposed
+//       reads (guide T10) are conflict free.
+//   Scores are computed swapped, S^T = K Q^T with mfma_f32_32x32x16_bf16, so a
+//   lane owns one query: the softmax row reduction is lane-local plus one
+//   xor-32 shuffle, and the probabilities are consumed from the accumulator
+//   registers as the B operand of O^T += V^T P^T (guide §3 "accumulator tile
+//   as the next MFMA's operand").
+//   Optional tree mask: for EAGLE verification the last `tree_n` queries of a
+//   sequence see the cached prefix plus their ancestors, given as one 64-bit
+//   ancestor mask per query (built by tree.hip).
+#include "common.h"
+
+using namespace dgi;
+
+namespace {
+
+__device__ __forceinline__ int k_off(int row, int ch) {  // element offset, HD=128
+  return row * 128 + (((ch) ^ (row & 15)) << 3);
+}
+__device__ __forceinline__ int v_off(int row, int ch) {
+  return row * 128 + (((ch) ^ ((row & 3) << 2)) << 3);
+}
+
+constexpr int HD = 128;
+constexpr int KT = 64;  // keys per tile
+
+__global__ __launch_bounds__(256) void prefill_attn_kernel(
+    const uint16_t* __restrict__ q, int q_stride, const uint16_t* __restrict__ k_cache,
+    const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ cu_seqlens_q, const int* __restrict__ context_lens,
+    const int* __restrict__ tiles, uint16_t* __restrict__ out, int out_stride, int nh, int nkv,
+    int bs_log2, float scale_log2, const unsigned long long* __restrict__ tree_mask, int tree_n) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * KT * HD];
+  uint16_t* ks = lds;
+  uint16_t* vs = lds + KT * HD;
+
+  const int b = tiles[2 * blockIdx.x];
+  const int t0 = tiles[2 * blockIdx.x + 1];  // first query row (within seq) of this tile
+  const int head = blockIdx.y;
+  const int kvh = head / (nh / nkv);
+  const int q0 = cu_seqlens_q[b];
+  const int qlen = cu_seqlens_q[b + 1] - q0;
+  const int ctx = context_lens[b];
+  const int pos_base = ctx - qlen;  // absolute position of query row 0
+  const int bs = 1 << bs_log2;
+  const int* bt = block_tables + (size_t)b * bt_stride;
+
+  const int tid = threadIdx.x;
+  const int w = tid >> 6;
+  const int lane = tid & 63;
+  const int lr = lane & 31;
+  const int hh = lane >> 5;
+
+  const int my_row = t0 + 32 * w + lr;  // query row within the sequence
+  const bool row_valid = my_row < qlen;
+  const int my_pos = pos_base + my_row;
+  const int tree_first = qlen - tree_n;  // rows >= tree_first use the tree mask
+  unsigned long long tmask = 0;
+  const bool is_tree = tree_mask != nullptr && row_valid && my_row >= tree_first;
+  if (is_tree) tmask = tree_mask[(size_t)b * 64 + (my_row - tree_first)];
+  const int tree_key0 = pos_base + tree_first;  // key index of tree node 0
+
+  // Q fragments (B operand): lane holds Q[row lr][16 s + 8 hh + j]
+  u32x4 qf[8];
+  {
+    const uint16_t* qp = q + (size_t)(q0 + (row_valid ? my_row : 0)) * q_stride + head * HD;
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      qf[s] = row_valid ? *reinterpret_cast<const u32x4*>(qp + 16 * s + 8 * hh) : u32x4{0, 0, 0, 0};
+  }
+
+  const int last_row = min(t0 + 128, qlen) - 1;
+  const int kv_end = min(ctx, pos_base + last_row + 1);
+
+  float m_run = -1e30f, l_run = 0.f;
+  f32x16 o[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+
+  const size_t head_stride = (size_t)bs * HD;
+  for (int kb0 = 0; kb0 < kv_end; kb0 += KT) {
+    // ---- stage K and V (64 rows x 16 chunks each = 4 passes of 256 threads)
+    u32x4 kr[4], vr[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int row = p * 16 + (tid >> 4);
+      const int ch = tid & 15;
+      const int key = min(kb0 + row, kv_end - 1);
+      const int blk = bt[key >> bs_log2];
+      const size_t base = ((size_t)blk * nkv + kvh) * head_stride + (size_t)(key & (bs - 1)) * HD + ch * 8;
+      kr[p] = *reinterpret_cast<const u32x4*>(k_cache + base);
+      vr[p] = *reinterpret_cast<const u32x4*>(v_cache + base);
+    }
+    __syncthreads();  // previous tile fully consumed
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int row = p * 16 + (tid >> 4);
+      const int ch = tid & 15;
+      *reinterpret_cast<u32x4*>(ks + k_off(row, ch)) = kr[p];
+      *reinterpret_cast<u32x4*>(vs + v_off(row, ch)) = vr[p];
+    }
+    __syncthreads();
+
+    // ---- S^T = K Q^T for two 32-key blocks
+    f32x16 sc[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sc[kb][r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const u32x4 a = *reinterpret_cast<const u32x4*>(ks + k_off(32 * kb + lr, 2 * s + hh));
+        sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a), as_bf16x8(qf[s]), sc[kb], 0, 0, 0);
+      }
+    }
+    // ---- online softmax; lane owns query lr, keys kb0 + 32kb + (r&3) + 8(r>>2) + 4hh
+    float mx = -1e30f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kb0 + 32 * kb + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        bool ok = row_valid && key <= my_pos && key < kv_end;
+        if (is_tree && key >= tree_key0) ok = ok && ((tmask >> (key - tree_key0)) & 1ull);
+        const float x = ok ? sc[kb][r] * scale_log2 : -1e30f;
+        sc[kb][r] = x;
+        mx = fmaxf(mx, x);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = exp2f(m_run - m_new);
+    float psum = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float x = sc[kb][r];
+        const float pv = (x > -1e29f) ? exp2f(x - m_new) : 0.f;
+        sc[kb][r] = pv;
+        psum += pv;
+      }
+    psum += __shfl_xor(psum, 32, 64);
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) o[d] *= alpha;
+
+    // ---- O^T += V^T P^T
+    const int g16 = lane >> 4;
+    const int idx = lane & 15;
+    const int tq = idx >> 2, tp = idx & 3;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        u32x4 pf;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) pf[jj] = pack_bf16x2(sc[kb][8 * s2 + 2 * jj], sc[kb][8 * s2 + 2 * jj + 1]);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const int col = 32 * d + 16 * (g16 & 1) + 4 * tp;
+          const int r0 = 32 * kb + 16 * s2 + 4 * hh + tq;
+          short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_short4*)(vs + v_off(r0, col >> 3) + (col & 7)));
+          short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_short4*)(vs + v_off(r0 + 8, col >> 3) + (col & 7)));
+          u32x4 vf;
+          vf[0] = (uint32_t)(uint16_t)lo[0] | ((uint32_t)(uint16_t)lo[1] << 16);
+          vf[1] = (uint32_t)(uint16_t)lo[2] | ((uint32_t)(uint16_t)lo[3] << 16);
+          vf[2] = (uint32_t)(uint16_t)hi[0] | ((uint32_t)(uint16_t)hi[1] << 16);
+          vf[3] = (uint32_t)(uint16_t)hi[2] | ((uint32_t)(uint16_t)hi[3] << 16);
+          o[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(vf), as_bf16x8(pf), o[d], 0, 0, 0);
+        }
+      }
+  }
+
+  if (!row_valid) return;
+  const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+  uint16_t* op = out + (size_t)(q0 + my_row) * out_stride + head * HD;
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int dim = 32 * d + 8 * rr + 4 * hh;
+      uint2 v;
+      v.x = pack_bf16x2(o[d][4 * rr] * inv, o[d][4 * rr + 1] * inv);
+      v.y = pack_bf16x2(o[d][4 * rr + 2] * inv, o[d][4 * rr + 3] * inv);
+      *reinterpret_cast<uint2*>(op + dim) = v;
+    }
+}
+
+}  // namespace
+
+// tiles: int32 [n_tiles, 2] = (sequence index, first query row of the 128-row tile)
+extern "C" int dgi_paged_prefill(const void* q, int q_stride, const void* k_cache,
+                                 const void* v_cache, const int* block_tables, int bt_stride,
+                                 const int* cu_seqlens_q, const int* context_lens, const int* tiles,
+                                 int n_tiles, void* out, int out_stride, int nh, int nkv, int hd,
+                                 int block_size, float scale, const unsigned long long* tree_mask,
+                                 int tree_n, hipStream_t s) {
+  if (n_tiles == 0) return 0;
+  if (hd != 128) return -5;
+  if (nh % nkv) return -2;
+  if (tree_n > 64) return -6;
+  int bs_log2 = 0;
+  while ((1 << bs_log2) < block_size) ++bs_log2;
+  if ((1 << bs_log2) != block_size) return -4;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  prefill_attn_kernel<<<dim3(n_tiles, nh), 256, 0, s>>>(
+      (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables,
+      bt_stride, cu_seqlens_q, context_lens, tiles, (uint16_t*)out, out_stride, nh, nkv, bs_log2,
+      scale_log2, tree_mask, tree_n);
+  DGI_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,143 @@
+// dgi/csrc/sampler.hip — on-device token selection.
+//
+// Greedy argmax and temperature sampling by the Gumbel-max trick in one pass
+// over the logits row, so no host sync and no softmax materialisation.  The
+// reference samples inside HF generate / vLLM SamplingParams
+// (worker/engines/llm.py:62-69, worker/engines/llm_vllm.py:144-151) and
+// argmax/multinomial in speculative.py:444-449.
+// top-k / top-p filtering, when requested, is applied to the logits before
+// this kernel (rows with top_k/top_p disabled skip that pass entirely).
+//
+// Also: per-row top-k (k <= 16) candidate extraction used by the EAGLE draft
+// tree builder (K13): each workgroup keeps a wave-level sorted list.
+#include "common.h"
+
+using namespace dgi;
+
+namespace {
+
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+
+template <typename T>
+__device__ __forceinline__ float load_logit(const T* p, int i);
+template <>
+__device__ __forceinline__ float load_logit<float>(const float* p, int i) { return p[i]; }
+template <>
+__device__ __forceinline__ float load_logit<uint16_t>(const uint16_t* p, int i) { return bf16_to_f32(p[i]); }
+
+template <typename T>
+__global__ __launch_bounds__(1024) void sample_kernel(const T* __restrict__ logits, int V, int stride,
+                                                      const float* __restrict__ temperature,
+                                                      const long long* __restrict__ seeds,
+                                                      long long step, long long* __restrict__ out) {
+  const int row = blockIdx.x;
+  const T* lp = logits + (size_t)row * stride;
+  const float temp = temperature ? temperature[row] : 0.f;
+  const bool greedy = temp <= 1e-5f;
+  const float inv_t = greedy ? 1.f : 1.f / temp;
+  const uint32_t seed = seeds ? (uint32_t)(seeds[row] * 2654435761ull) ^ (uint32_t)(step * 40503u) : 0u;
+  float best = -INFINITY;
+  int best_i = 0x7fffffff;
+  for (int i = threadIdx.x; i < V; i += blockDim.x) {
+    float v = load_logit<T>(lp, i);
+    if (!greedy) {
+      const uint32_t h = hash32(seed ^ hash32((uint32_t)i + 0x9e3779b9u));
+      const float u = ((h >> 8) + 0.5f) * (1.0f / 16777216.0f);
+      v = v * inv_t - __logf(-__logf(u));
+    }
+    if (v > best || (v == best && i < best_i)) { best = v; best_i = i; }
+  }
+  // wave reduce
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(best_i, o, 64);
+    if (ob > best || (ob == best && oi < best_i)) { best = ob; best_i = oi; }
+  }
+  __shared__ float sb[16];
+  __shared__ int si[16];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sb[w] = best; si[w] = best_i; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int nw = blockDim.x >> 6;
+    for (int k = 1; k < nw; ++k)
+      if (sb[k] > best || (sb[k] == best && si[k] < best_i)) { best = sb[k]; best_i = si[k]; }
+    out[row] = best_i == 0x7fffffff ? 0 : best_i;
+  }
+}
+
+// top-k (k <= 16) per row: values + indices, descending.  One 256-thread
+// block per row; each thread keeps its own sorted top-k, then a tree merge in LDS.
+template <typename T>
+__global__ __launch_bounds__(256) void topk_kernel(const T* __restrict__ logits, int V, int stride,
+                                                   int K, float* __restrict__ out_v,
+                                                   long long* __restrict__ out_i) {
+  const int row = blockIdx.x;
+  const T* lp = logits + (size_t)row * stride;
+  float tv[16];
+  int ti[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) { tv[k] = -INFINITY; ti[k] = 0x7fffffff; }
+  for (int i = threadIdx.x; i < V; i += 256) {
+    const float v = load_logit<T>(lp, i);
+    if (v > tv[K - 1]) {
+      int k = K - 1;
+      while (k > 0 && tv[k - 1] < v) { tv[k] = tv[k - 1]; ti[k] = ti[k - 1]; --k; }
+      tv[k] = v; ti[k] = i;
+    }
+  }
+  __shared__ float sv[256 * 16];
+  __shared__ int si[256 * 16];
+  for (int k = 0; k < K; ++k) { sv[threadIdx.x * 16 + k] = tv[k]; si[threadIdx.x * 16 + k] = ti[k]; }
+  __syncthreads();
+  for (int half = 128; half > 0; half >>= 1) {
+    if (threadIdx.x < half) {
+      const float* a = sv + threadIdx.x * 16;
+      const int* ai = si + threadIdx.x * 16;
+      const float* bv = sv + (threadIdx.x + half) * 16;
+      const int* bi = si + (threadIdx.x + half) * 16;
+      float mv[16]; int mi[16];
+      int x = 0, y = 0;
+      for (int k = 0; k < K; ++k) {
+        const bool takea = (a[x] > bv[y]) || (a[x] == bv[y] && ai[x] <= bi[y]);
+        if (takea) { mv[k] = a[x]; mi[k] = ai[x]; ++x; } else { mv[k] = bv[y]; mi[k] = bi[y]; ++y; }
+      }
+      for (int k = 0; k < K; ++k) { sv[threadIdx.x * 16 + k] = mv[k]; si[threadIdx.x * 16 + k] = mi[k]; }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < K) {
+    out_v[(size_t)row * K + threadIdx.x] = sv[threadIdx.x];
+    out_i[(size_t)row * K + threadIdx.x] = si[threadIdx.x];
+  }
+}
+
+}  // namespace
+
+extern "C" int dgi_sample(const void* logits, int is_bf16, int B, int V, int stride,
+                          const float* temperature, const long long* seeds, long long step,
+                          long long* out, hipStream_t s) {
+  if (B == 0) return 0;
+  if (is_bf16)
+    sample_kernel<uint16_t><<<B, 1024, 0, s>>>((const uint16_t*)logits, V, stride, temperature, seeds, step, out);
+  else
+    sample_kernel<float><<<B, 1024, 0, s>>>((const float*)logits, V, stride, temperature, seeds, step, out);
+  DGI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dgi_topk(const void* logits, int is_bf16, int B, int V, int stride, int K,
+                        float* out_v, long long* out_i, hipStream_t s) {
+  if (B == 0) return 0;
+  if (K < 1 || K > 16) return -2;
+  if (is_bf16)
+    topk_kernel<uint16_t><<<B, 256, 0, s>>>((const uint16_t*)logits, V, stride, K, out_v, out_i);
+  else
+    topk_kernel<float><<<B, 256, 0, s>>>((const float*)logits, V, stride, K, out_v, out_i);
+  DGI_CHECK_LAUNCH();
+  return 0;
+}

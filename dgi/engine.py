@@ -1,0 +1,159 @@
+"""LLMEngine: the native MI355X serving engine (model + block pool + scheduler).
+
+``LLMEngine.step()`` is one iteration of continuous batching: schedule ->
+one model forward (decode rows + prefill chunks) -> sample -> update request
+state.  ``NativeLLMEngine`` in ``worker/engines/llm_native.py`` wraps it in
+the reference's ``LLMBaseEngine`` contract (worker/engines/llm_base.py:45-188).
+"""
+from __future__ import annotations
+
+import dataclasses
+import time
+from typing import Iterable, Optional
+
+import torch
+
+from dgi.kv.block_pool import BlockPool, num_blocks_for_budget
+from dgi.models.config import ModelConfig, get_config
+from dgi.models.llama import LlamaModel
+from dgi.runtime.model_runner import ModelRunner
+from dgi.sched.request import Request, SamplingParams, Status
+from dgi.sched.scheduler import Scheduler, SchedulerConfig
+
+
+@dataclasses.dataclass
+class EngineConfig:
+    model: str = "llama3-8b"
+    device: str = "cuda"
+    dtype: torch.dtype = torch.bfloat16
+    block_size: int = 16
+    max_num_seqs: int = 256
+    max_num_batched_tokens: int = 8192
+    max_model_len: int = 8192
+    kv_fraction: float = 0.90          # of (device memory - weights - workspace)
+    num_blocks: Optional[int] = None   # override the budget computation
+    enable_prefix_caching: bool = True
+    use_graphs: bool = True
+    seed: int = 0
+    workspace_bytes: int = 8 << 30
+    layer_start: int = 0
+    layer_end: Optional[int] = None
+
+
+@dataclasses.dataclass
+class StepOutput:
+    rid: object
+    token: int
+    finished: bool
+    finish_reason: Optional[str]
+    request: Request
+
+
+def _device_free_bytes(device: torch.device) -> int:
+    if device.type == "cuda":
+        free, _total = torch.cuda.mem_get_info(device)
+        return free
+    return 2 << 30
+
+
+class LLMEngine:
+    def __init__(self, cfg: EngineConfig, model_cfg: Optional[ModelConfig] = None, model=None):
+        self.cfg = cfg
+        self.device = torch.device(cfg.device)
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        self.model_cfg = model_cfg or get_config(cfg.model)
+        self.model_cfg.max_position = max(self.model_cfg.max_position, cfg.max_model_len)
+        t0 = time.perf_counter()
+        self.model = model or LlamaModel(self.model_cfg, self.device, cfg.dtype, cfg.layer_start, cfg.layer_end,
+                                         seed=cfg.seed)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize()
+        self.load_seconds = time.perf_counter() - t0
+        mc = self.model_cfg
+        n_local = self.model.num_local_layers
+        if cfg.num_blocks is not None:
+            nblocks = cfg.num_blocks
+        else:
+            budget = max(0, _device_free_bytes(self.device) - cfg.workspace_bytes) * cfg.kv_fraction
+            nblocks = num_blocks_for_budget(int(budget), max(1, n_local), mc.num_kv_heads, mc.head_dim,
+                                            cfg.block_size)
+            # never more than what max_num_seqs full-length sequences can use (+ prefix cache room)
+            cap = 2 * cfg.max_num_seqs * ((cfg.max_model_len + cfg.block_size - 1) // cfg.block_size) + 1
+            nblocks = max(2, min(nblocks, cap))
+        self.pool = BlockPool(nblocks, cfg.block_size, max(1, n_local), mc.num_kv_heads, mc.head_dim,
+                              cfg.dtype, self.device)
+        self.scheduler = Scheduler(self.pool, SchedulerConfig(cfg.max_num_seqs, cfg.max_num_batched_tokens,
+                                                              cfg.max_model_len, cfg.enable_prefix_caching))
+        self.runner = ModelRunner(self.model, self.pool, cfg.max_num_seqs, cfg.max_model_len,
+                                  cfg.max_num_batched_tokens, cfg.use_graphs)
+        self.requests: dict = {}
+        self.stats = {"steps": 0, "prefill_tokens": 0, "decode_tokens": 0, "generated": 0,
+                      "finished": 0, "step_time": 0.0}
+
+    # ------------------------------------------------------------------ API
+    def add_request(self, prompt_ids: list[int], params: Optional[SamplingParams] = None, rid=None,
+                    user=None) -> Request:
+        req = Request(prompt_ids, params or SamplingParams(), rid=rid, user=user)
+        self.scheduler.add(req)
+        self.requests[req.rid] = req
+        return req
+
+    def abort(self, rid) -> bool:
+        self.requests.pop(rid, None)
+        return self.scheduler.abort(rid)
+
+    def has_unfinished(self) -> bool:
+        return self.scheduler.has_work()
+
+    def warmup(self) -> None:
+        """Capture decode graphs ahead of serving."""
+        if self.runner.graphs is not None:
+            self.runner.graphs.capture()
+
+    def step(self) -> list[StepOutput]:
+        t0 = time.perf_counter()
+        sb = self.scheduler.schedule()
+        if sb.empty:
+            return []
+        res = self.runner.execute(sb)
+        now = time.perf_counter()
+        st = self.stats
+        st["steps"] += 1
+        st["decode_tokens"] += len(sb.decode)
+        for c in sb.prefill:
+            c.req.num_computed += c.length
+            st["prefill_tokens"] += c.length
+        for r in sb.decode:
+            r.num_computed += 1
+        outs = []
+        for req, tok in zip(res.rows, res.tokens):
+            req.output.append(int(tok))
+            req.token_times.append(now)
+            if req.first_token_time is None:
+                req.first_token_time = now
+            st["generated"] += 1
+            reason = self._check_stop(req, int(tok))
+            if reason is not None:
+                self.scheduler.finish(req, reason)
+                st["finished"] += 1
+                self.requests.pop(req.rid, None)
+            outs.append(StepOutput(req.rid, int(tok), reason is not None, reason, req))
+        st["step_time"] += time.perf_counter() - t0
+        return outs
+
+    def _check_stop(self, req: Request, tok: int) -> Optional[str]:
+        p = req.params
+        if len(req.output) >= p.max_tokens:
+            return "length"
+        if not p.ignore_eos and (tok == self.model_cfg.eos_token_id or tok in p.stop_token_ids):
+            return "stop"
+        if req.total_len >= self.cfg.max_model_len - 1:
+            return "length"
+        return None
+
+    def generate(self, prompts: Iterable[list[int]], params: Optional[SamplingParams] = None) -> list[Request]:
+        reqs = [self.add_request(p, params) for p in prompts]
+        while any(r.status is not Status.FINISHED for r in reqs):
+            self.step()
+        return reqs

@@ -1,0 +1,230 @@
+"""Native Llama decoder for the MI355X runtime (Llama-3 8B / 70B).
+
+Replaces the HF modules the reference executes (worker/engines/llm.py:22-69,
+worker/distributed/model_shard.py:28-246).  Per layer the step runs
+
+    fused_add_rmsnorm (HIP) -> QKV GEMM (hipBLASLt) -> RoPE + paged KV write (HIP)
+    -> paged decode / prefill attention (HIP, MFMA) -> O GEMM
+    -> fused_add_rmsnorm (HIP) -> gate|up GEMM -> SiLU*mul (HIP) -> down GEMM
+
+with fused QKV and gate|up weights so each layer issues 4 GEMMs.  A model
+object may hold any contiguous layer range (pipeline stage): stage 0 owns the
+embedding, the last stage the final norm and LM head, exactly like the
+reference's ``ModelShard`` (model_shard.py:28-59).  Between stages a single
+hidden tensor travels: the residual stream (h + residual) — the next stage
+re-normalises it, which is bit-identical to the fused add it replaces.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from dgi import ops
+from dgi.models.config import ModelConfig
+from dgi.runtime.batch import AttnMeta
+
+
+class LlamaLayerWeights:
+    __slots__ = ("in_norm", "qkv", "o", "post_norm", "gate_up", "down")
+
+    def __init__(self, in_norm, qkv, o, post_norm, gate_up, down):
+        self.in_norm, self.qkv, self.o = in_norm, qkv, o
+        self.post_norm, self.gate_up, self.down = post_norm, gate_up, down
+
+
+def _rand(shape, gen, device, dtype, std):
+    t = torch.empty(shape, device=device, dtype=dtype)
+    t.normal_(0.0, std, generator=gen)
+    return t
+
+
+class LlamaModel:
+    """Layer range [layer_start, layer_end) of a Llama causal LM."""
+
+    def __init__(self, cfg: ModelConfig, device: torch.device | str = "cpu", dtype=torch.bfloat16,
+                 layer_start: int = 0, layer_end: Optional[int] = None, has_embed: Optional[bool] = None,
+                 has_head: Optional[bool] = None, seed: int = 0, init: str = "random"):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.layer_start = layer_start
+        self.layer_end = cfg.num_layers if layer_end is None else layer_end
+        self.has_embed = (layer_start == 0) if has_embed is None else has_embed
+        self.has_head = (self.layer_end == cfg.num_layers) if has_head is None else has_head
+        self.num_local_layers = self.layer_end - self.layer_start
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        self.kv_cache: Optional[torch.Tensor] = None  # [L_local, 2, NB, nkv, bs, hd]
+        self.layers: list[LlamaLayerWeights] = []
+        self.embed = self.norm = self.lm_head = None
+        if init == "random":
+            self._init_random(seed)
+        elif init == "empty":
+            self._init_empty()
+        self.cos_sin = ops.rope_cos_sin(cfg.head_dim, cfg.max_position, cfg.rope_theta, cfg.rope_scaling,
+                                        device=self.device)
+
+    # ------------------------------------------------------------------ weights
+    def _init_empty(self):
+        c, dev, dt = self.cfg, self.device, self.dtype
+        H, I = c.hidden_size, c.intermediate_size
+        for _ in range(self.num_local_layers):
+            self.layers.append(LlamaLayerWeights(
+                torch.ones(H, device=dev, dtype=dt), torch.empty(c.qkv_size, H, device=dev, dtype=dt),
+                torch.empty(H, c.q_size, device=dev, dtype=dt), torch.ones(H, device=dev, dtype=dt),
+                torch.empty(2 * I, H, device=dev, dtype=dt), torch.empty(H, I, device=dev, dtype=dt)))
+        if self.has_embed:
+            self.embed = torch.empty(c.vocab_size, H, device=dev, dtype=dt)
+        if self.has_head:
+            self.norm = torch.ones(H, device=dev, dtype=dt)
+            self.lm_head = self.embed if (c.tie_embeddings and self.embed is not None) else \
+                torch.empty(c.vocab_size, H, device=dev, dtype=dt)
+
+    def _init_random(self, seed: int):
+        """Deterministic per-layer seeds, initialised directly on the device.
+
+        Any rank can re-materialise its own layer range without I/O, and a
+        layer's weights do not depend on how the model is sharded (SURVEY
+        §5.5), so PP=k outputs equal PP=1 outputs bit for bit."""
+        c, dev, dt = self.cfg, self.device, self.dtype
+        H, I = c.hidden_size, c.intermediate_size
+        std = 0.02
+        gen = torch.Generator(device=dev)
+        for li in range(self.layer_start, self.layer_end):
+            gen.manual_seed(seed * 1000003 + li * 7919 + 1)
+            ln1 = 1.0 + 0.1 * _rand((H,), gen, dev, torch.float32, 1.0)
+            qkv = _rand((c.qkv_size, H), gen, dev, dt, std)
+            o = _rand((H, c.q_size), gen, dev, dt, std / math.sqrt(2 * c.num_layers))
+            ln2 = 1.0 + 0.1 * _rand((H,), gen, dev, torch.float32, 1.0)
+            gu = _rand((2 * I, H), gen, dev, dt, std)
+            down = _rand((H, I), gen, dev, dt, std / math.sqrt(2 * c.num_layers))
+            self.layers.append(LlamaLayerWeights(ln1.to(dt), qkv, o, ln2.to(dt), gu, down))
+        if self.has_embed or (self.has_head and c.tie_embeddings):
+            gen.manual_seed(seed * 1000003 + 17)
+            emb = _rand((c.vocab_size, H), gen, dev, dt, 1.0)
+            self.embed = emb if self.has_embed else None
+        if self.has_head:
+            gen.manual_seed(seed * 1000003 + 23)
+            self.norm = (1.0 + 0.1 * _rand((H,), gen, dev, torch.float32, 1.0)).to(dt)
+            if c.tie_embeddings:
+                self.lm_head = emb
+            else:
+                self.lm_head = _rand((c.vocab_size, H), gen, dev, dt, std)
+
+    def load_state_dict_hf(self, sd: dict):
+        """Load HF Llama tensor names (``model.layers.N.self_attn.q_proj.weight``...)."""
+        c = self.cfg
+        for i, li in enumerate(range(self.layer_start, self.layer_end)):
+            p = f"model.layers.{li}."
+            L = self.layers[i]
+            qkv = torch.cat([sd[p + "self_attn.q_proj.weight"], sd[p + "self_attn.k_proj.weight"],
+                             sd[p + "self_attn.v_proj.weight"]], 0)
+            L.qkv.copy_(qkv)
+            L.o.copy_(sd[p + "self_attn.o_proj.weight"])
+            L.gate_up.copy_(torch.cat([sd[p + "mlp.gate_proj.weight"], sd[p + "mlp.up_proj.weight"]], 0))
+            L.down.copy_(sd[p + "mlp.down_proj.weight"])
+            L.in_norm.copy_(sd[p + "input_layernorm.weight"])
+            L.post_norm.copy_(sd[p + "post_attention_layernorm.weight"])
+        if self.has_embed:
+            self.embed.copy_(sd["model.embed_tokens.weight"])
+        if self.has_head:
+            self.norm.copy_(sd["model.norm.weight"])
+            if "lm_head.weight" in sd and self.lm_head is not self.embed:
+                self.lm_head.copy_(sd["lm_head.weight"])
+        del c
+
+    def weight_bytes(self) -> int:
+        n = 0
+        for L in self.layers:
+            for t in (L.in_norm, L.qkv, L.o, L.post_norm, L.gate_up, L.down):
+                n += t.numel() * t.element_size()
+        for t in (self.embed, self.norm):
+            if t is not None:
+                n += t.numel() * t.element_size()
+        if self.lm_head is not None and self.lm_head is not self.embed:
+            n += self.lm_head.numel() * self.lm_head.element_size()
+        return n
+
+    # ------------------------------------------------------------------ forward
+    def attention(self, li: int, qkv: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
+        c = self.cfg
+        kc = self.kv_cache[li, 0]
+        vc = self.kv_cache[li, 1]
+        ops.rope_cache(qkv, meta.positions, self.cos_sin, c.num_heads, c.num_kv_heads, c.head_dim,
+                       meta.slot_mapping, kc, vc)
+        T = qkv.shape[0]
+        out = torch.empty(T, c.q_size, device=qkv.device, dtype=qkv.dtype)
+        nd = meta.num_decode
+        if nd > 0:
+            ops.paged_decode(qkv[:nd], kc, vc, meta.dec_block_tables, meta.dec_context_lens, c.num_heads,
+                             c.num_kv_heads, self.scale, meta.dec_max_splits, meta.dec_part_size,
+                             out=out[:nd], workspace=meta.dec_workspace)
+        if meta.num_prefill_tokens > 0:
+            ops.paged_prefill(qkv[nd:], kc, vc, meta.pre_block_tables, meta.pre_cu_seqlens, meta.pre_context_lens,
+                              c.num_heads, c.num_kv_heads, self.scale, tiles=meta.pre_tiles,
+                              tree_mask=meta.tree_mask, tree_n=meta.tree_n, out=out[nd:])
+        return out
+
+    def forward_layers(self, h: torch.Tensor, meta: AttnMeta, residual: Optional[torch.Tensor] = None):
+        c = self.cfg
+        eps = c.rms_eps
+        for i, L in enumerate(self.layers):
+            if residual is None:
+                residual = h
+                h = ops.rmsnorm(h, L.in_norm, eps)
+            else:
+                ops.fused_add_rmsnorm(h, residual, L.in_norm, eps)
+            qkv = F.linear(h, L.qkv)
+            attn = self.attention(i, qkv, meta)
+            h = F.linear(attn, L.o)
+            ops.fused_add_rmsnorm(h, residual, L.post_norm, eps)
+            gu = F.linear(h, L.gate_up)
+            act = ops.silu_mul(gu)
+            h = F.linear(act, L.down)
+        return h, residual
+
+    def embed_tokens(self, input_ids: torch.Tensor) -> torch.Tensor:
+        return F.embedding(input_ids, self.embed)
+
+    def forward(self, meta: AttnMeta, input_ids: Optional[torch.Tensor] = None,
+                hidden: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Stage forward.  Returns logits [n, V] on the last stage, else the
+        residual stream [T, H] for the next stage."""
+        if self.has_embed:
+            h = self.embed_tokens(input_ids)
+        else:
+            h = hidden
+        residual = None
+        if self.num_local_layers:
+            # a fresh residual tensor: fused_add_rmsnorm updates it in place
+            h, residual = self.forward_layers(h.clone() if not self.has_embed else h, meta)
+        if not self.has_head:
+            return h if residual is None else h + residual
+        return self.compute_logits(h, residual, meta.logits_indices)
+
+    def compute_logits(self, h, residual, idx):
+        eps = self.cfg.rms_eps
+        if idx is not None:
+            h = h.index_select(0, idx)
+            residual = residual.index_select(0, idx) if residual is not None else None
+        if residual is None:
+            hn = ops.rmsnorm(h.contiguous(), self.norm, eps)
+        else:
+            h = h.contiguous()
+            residual = residual.contiguous()
+            ops.fused_add_rmsnorm(h, residual, self.norm, eps)
+            hn = h
+        return F.linear(hn, self.lm_head)
+
+    def final_hidden(self, h, residual, idx=None):
+        """Normalised last hidden states (EAGLE draft features)."""
+        eps = self.cfg.rms_eps
+        if idx is not None:
+            h = h.index_select(0, idx)
+            residual = residual.index_select(0, idx)
+        h = h.contiguous()
+        residual = residual.contiguous().clone()
+        ops.fused_add_rmsnorm(h, residual, self.norm, eps)
+        return h

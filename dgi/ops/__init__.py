@@ -1,0 +1,487 @@
+"""Kernel entry points: HIP (gfx950) on GPU tensors, pure-torch references on CPU.
+
+Every op has two implementations:
+
+* ``torch.ops.dgi.<op>`` from ``dgi/_C.so`` (hand-written CDNA4 HIP kernels,
+  see ``dgi/csrc``) — used whenever the tensors live on the GPU.  If the
+  extension is missing on a GPU box the op raises: there is no silent
+  eager fallback on the device path.
+* ``*_ref`` — a plain PyTorch (fp32 accumulate) version of the same math,
+  used for CPU execution (the CPU test-suite, OPT-125m config #1) and as the
+  numerics oracle of the kernel tests.
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import Optional
+
+import torch
+
+_LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_C.so")
+_loaded = False
+_load_error: Optional[str] = None
+
+
+def load_native(required: bool = False) -> bool:
+    """Load ``dgi/_C.so`` once. ``required`` raises if it cannot be loaded."""
+    global _loaded, _load_error
+    if _loaded:
+        return True
+    if os.path.exists(_LIB):
+        try:
+            torch.ops.load_library(_LIB)
+            _loaded = True
+            return True
+        except Exception as e:  # pragma: no cover - depends on the box
+            _load_error = repr(e)
+    else:
+        _load_error = f"{_LIB} not built (run `python -m dgi.build`)"
+    if required:
+        raise RuntimeError(f"dgi native kernels unavailable: {_load_error}")
+    return False
+
+
+def native_available() -> bool:
+    return load_native(False)
+
+
+def _native(t: torch.Tensor) -> bool:
+    if t.is_cuda:
+        load_native(required=True)
+        return True
+    return False
+
+
+# ----------------------------------------------------------------------------
+# RMSNorm
+# ----------------------------------------------------------------------------
+
+def rmsnorm_ref(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    xf = x.float()
+    var = xf.pow(2).mean(-1, keepdim=True)
+    return (xf * torch.rsqrt(var + eps) * w.float()).to(x.dtype)
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if _native(x):
+        out = torch.empty_like(x) if out is None else out
+        torch.ops.dgi.rmsnorm(out, x, w, eps)
+        return out
+    r = rmsnorm_ref(x, w, eps)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
+def fused_add_rmsnorm_ref(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float) -> None:
+    s = (x.float() + residual.float()).to(residual.dtype)
+    residual.copy_(s)
+    x.copy_(rmsnorm_ref(s, w, eps))
+
+
+def fused_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float) -> None:
+    """residual <- x + residual; x <- rmsnorm(residual) * w (in place)."""
+    if _native(x):
+        torch.ops.dgi.fused_add_rmsnorm(x, residual, w, eps)
+    else:
+        fused_add_rmsnorm_ref(x, residual, w, eps)
+
+
+# ----------------------------------------------------------------------------
+# RoPE + paged cache write
+# ----------------------------------------------------------------------------
+
+def rope_cos_sin(head_dim: int, max_pos: int, theta: float, scaling: Optional[dict] = None,
+                 device=None) -> torch.Tensor:
+    """[max_pos, head_dim] fp32 table: first half cos, second half sin.
+
+    Supports Llama-3.1 style ``rope_scaling`` (``rope_type == "llama3"``).
+    """
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    if scaling and scaling.get("rope_type", scaling.get("type")) == "llama3":
+        factor = scaling["factor"]
+        lo = scaling.get("low_freq_factor", 1.0)
+        hi = scaling.get("high_freq_factor", 4.0)
+        old = scaling.get("original_max_position_embeddings", 8192)
+        lo_wl, hi_wl = old / lo, old / hi
+        wl = 2 * math.pi / inv
+        smooth = (old / wl - lo) / (hi - lo)
+        scaled = torch.where(wl > lo_wl, inv / factor, inv)
+        mid = (1 - smooth) * inv / factor + smooth * inv
+        is_mid = (wl <= lo_wl) & (wl >= hi_wl)
+        inv = torch.where(is_mid, mid, scaled)
+    t = torch.arange(max_pos, dtype=torch.float64)
+    f = torch.outer(t, inv)
+    return torch.cat([f.cos(), f.sin()], dim=-1).float().to(device)
+
+
+def _rotate(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    h = x.shape[-1] // 2
+    x1, x2 = x[..., :h], x[..., h:]
+    return torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1)
+
+
+def rope_cache_ref(qkv, positions, cos_sin, nh, nkv, hd, slot_mapping, k_cache, v_cache) -> None:
+    T = qkv.shape[0]
+    if T == 0:
+        return
+    bs = k_cache.shape[2]
+    half = hd // 2
+    cs = cos_sin[positions.long()]
+    cos = cs[:, None, :half]
+    sin = cs[:, None, half:]
+    q = qkv[:, : nh * hd].float().view(T, nh, hd)
+    k = qkv[:, nh * hd:(nh + nkv) * hd].float().view(T, nkv, hd)
+    v = qkv[:, (nh + nkv) * hd:(nh + 2 * nkv) * hd].view(T, nkv, hd)
+    qr = _rotate(q, cos, sin).to(qkv.dtype)
+    kr = _rotate(k, cos, sin).to(qkv.dtype)
+    qkv[:, : nh * hd] = qr.reshape(T, nh * hd)
+    slots = slot_mapping.long()
+    ok = slots >= 0
+    if ok.any():
+        s = slots[ok]
+        blk, off = s // bs, s % bs
+        k_cache[blk, :, off] = kr[ok]
+        v_cache[blk, :, off] = v[ok]
+
+
+def rope_cache(qkv, positions, cos_sin, nh, nkv, hd, slot_mapping, k_cache, v_cache) -> None:
+    """Rotate q in place inside the fused qkv rows, write rotated k and v into the paged cache."""
+    if _native(qkv):
+        torch.ops.dgi.rope_cache(qkv, positions, cos_sin, nh, nkv, hd, slot_mapping, k_cache, v_cache)
+    else:
+        rope_cache_ref(qkv, positions, cos_sin, nh, nkv, hd, slot_mapping, k_cache, v_cache)
+
+
+# ----------------------------------------------------------------------------
+# Attention
+# ----------------------------------------------------------------------------
+
+def _gather_kv(k_cache, v_cache, bt_row, ctx):
+    bs = k_cache.shape[2]
+    nblk = (ctx + bs - 1) // bs
+    ids = bt_row[:nblk].long()
+    k = k_cache[ids].permute(0, 2, 1, 3).reshape(nblk * bs, k_cache.shape[1], -1)[:ctx]
+    v = v_cache[ids].permute(0, 2, 1, 3).reshape(nblk * bs, v_cache.shape[1], -1)[:ctx]
+    return k, v
+
+
+def paged_decode_ref(q, k_cache, v_cache, block_tables, context_lens, nh, nkv, scale) -> torch.Tensor:
+    hd = k_cache.shape[-1]
+    B = q.shape[0]
+    out = torch.empty(B, nh * hd, dtype=q.dtype, device=q.device)
+    G = nh // nkv
+    for b in range(B):
+        ctx = int(context_lens[b])
+        k, v = _gather_kv(k_cache, v_cache, block_tables[b], ctx)
+        qb = q[b, : nh * hd].float().view(nkv, G, hd)
+        s = torch.einsum("hgd,thd->hgt", qb, k.float()) * scale
+        p = torch.softmax(s, dim=-1)
+        o = torch.einsum("hgt,thd->hgd", p, v.float())
+        out[b] = o.reshape(nh * hd).to(q.dtype)
+    return out
+
+
+def decode_split_plan(batch: int, max_ctx: int, nkv: int, num_cus: int = 256) -> tuple[int, int]:
+    """(max_splits, part_size) for the split-KV decode kernel.
+
+    Aim for >= 4 workgroups per CU; part_size is a multiple of 128 tokens
+    (4 waves x 32-token tiles)."""
+    want = max(1, (4 * num_cus + batch * nkv - 1) // max(1, batch * nkv))
+    max_parts = max(1, (max_ctx + 127) // 128)
+    splits = min(want, max_parts)
+    part = ((max_ctx + splits - 1) // splits + 127) // 128 * 128
+    part = max(part, 128)
+    splits = (max_ctx + part - 1) // part
+    return max(1, splits), part
+
+
+def paged_decode(q, k_cache, v_cache, block_tables, context_lens, nh, nkv, scale,
+                 max_splits: int = 1, part_size: int = 1 << 30, out=None, workspace=None) -> torch.Tensor:
+    """Single-token attention for each row of ``q`` over its paged context.
+
+    ``max_splits``/``part_size`` must cover the longest context in the batch
+    (``decode_split_plan``); with ``max_splits > 1`` a workspace
+    ``(part_o[B*nh*splits*hd], part_lse[B*nh*splits])`` fp32 is required.
+    """
+    if _native(q):
+        hd = k_cache.shape[-1]
+        B = q.shape[0]
+        if out is None:
+            out = torch.empty(B, nh * hd, dtype=q.dtype, device=q.device)
+        if max_splits > 1:
+            if workspace is None:
+                workspace = (torch.empty(B * nh * max_splits * hd, dtype=torch.float32, device=q.device),
+                             torch.empty(B * nh * max_splits, dtype=torch.float32, device=q.device))
+            po, pl = workspace
+        else:
+            po = pl = torch.empty(0, dtype=torch.float32, device=q.device)
+            part_size = max(128, ((part_size if part_size < (1 << 30) else 1 << 20) + 127) // 128 * 128)
+        torch.ops.dgi.paged_decode(out, q, k_cache, v_cache, block_tables, context_lens, po, pl,
+                                   nh, nkv, max_splits, part_size, scale)
+        return out
+    r = paged_decode_ref(q, k_cache, v_cache, block_tables, context_lens, nh, nkv, scale)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
+def paged_prefill_ref(q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens, nh, nkv, scale,
+                      tree_mask=None, tree_n: int = 0) -> torch.Tensor:
+    hd = k_cache.shape[-1]
+    T = q.shape[0]
+    out = torch.zeros(T, nh * hd, dtype=q.dtype, device=q.device)
+    G = nh // nkv
+    cu = cu_seqlens_q.tolist()
+    for b in range(len(cu) - 1):
+        q0, q1 = cu[b], cu[b + 1]
+        ql = q1 - q0
+        if ql == 0:
+            continue
+        ctx = int(context_lens[b])
+        k, v = _gather_kv(k_cache, v_cache, block_tables[b], ctx)
+        qb = q[q0:q1, : nh * hd].float().view(ql, nkv, G, hd)
+        s = torch.einsum("qhgd,thd->hgqt", qb, k.float()) * scale
+        qpos = torch.arange(ctx - ql, ctx, device=q.device)
+        kpos = torch.arange(ctx, device=q.device)
+        allow = kpos[None, :] <= qpos[:, None]
+        if tree_mask is not None and tree_n > 0:
+            tf = ql - tree_n
+            key0 = ctx - ql + tf
+            bits = tree_mask[b, :tree_n].cpu().tolist()
+            for i in range(tree_n):
+                m = bits[i] & ((1 << 64) - 1)
+                for a in range(tree_n):
+                    if key0 + a < ctx and not ((m >> a) & 1):
+                        allow[tf + i, key0 + a] = False
+        s = s.masked_fill(~allow[None, None], float("-inf"))
+        p = torch.softmax(s, dim=-1)
+        o = torch.einsum("hgqt,thd->qhgd", p, v.float())
+        out[q0:q1] = o.reshape(ql, nh * hd).to(q.dtype)
+    return out
+
+
+def prefill_tiles(cu_seqlens_q: list[int], tile: int = 128) -> list[tuple[int, int]]:
+    tiles = []
+    for b in range(len(cu_seqlens_q) - 1):
+        ql = cu_seqlens_q[b + 1] - cu_seqlens_q[b]
+        for t0 in range(0, ql, tile):
+            tiles.append((b, t0))
+    return tiles
+
+
+def paged_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens, nh, nkv, scale,
+                  tiles=None, tree_mask=None, tree_n: int = 0, out=None) -> torch.Tensor:
+    """Causal varlen attention of packed queries over the paged KV (prefix + new)."""
+    if _native(q):
+        hd = k_cache.shape[-1]
+        if out is None:
+            out = torch.empty(q.shape[0], nh * hd, dtype=q.dtype, device=q.device)
+        if tiles is None:
+            tl = prefill_tiles(cu_seqlens_q.tolist())
+            tiles = torch.tensor(tl if tl else [[0, 0]], dtype=torch.int32, device=q.device)[: len(tl)]
+        torch.ops.dgi.paged_prefill(out, q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens,
+                                    tiles, nh, nkv, scale, tree_mask, tree_n)
+        return out
+    r = paged_prefill_ref(q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens, nh, nkv, scale,
+                          tree_mask, tree_n)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
+# ----------------------------------------------------------------------------
+# MLP activation
+# ----------------------------------------------------------------------------
+
+def silu_mul_ref(gu: torch.Tensor) -> torch.Tensor:
+    I = gu.shape[-1] // 2
+    g = gu[..., :I].float()
+    return (torch.nn.functional.silu(g) * gu[..., I:].float()).to(gu.dtype)
+
+
+def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if _native(gu):
+        if out is None:
+            out = torch.empty(*gu.shape[:-1], gu.shape[-1] // 2, dtype=gu.dtype, device=gu.device)
+        torch.ops.dgi.silu_mul(out, gu)
+        return out
+    r = silu_mul_ref(gu)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
+# ----------------------------------------------------------------------------
+# Sampling
+# ----------------------------------------------------------------------------
+
+def apply_top_k_top_p(logits: torch.Tensor, top_k: torch.Tensor, top_p: torch.Tensor) -> torch.Tensor:
+    """Mask logits outside top-k / nucleus top-p (rows with k<=0 / p>=1 untouched)."""
+    lf = logits.float()
+    sorted_l, idx = lf.sort(dim=-1, descending=True)
+    V = lf.shape[-1]
+    ranks = torch.arange(V, device=lf.device)[None, :]
+    k = torch.where(top_k > 0, top_k, torch.full_like(top_k, V))
+    mask = ranks >= k[:, None]
+    probs = torch.softmax(sorted_l, dim=-1)
+    cum = probs.cumsum(-1) - probs
+    mask |= cum > top_p[:, None]
+    sorted_l = sorted_l.masked_fill(mask, float("-inf"))
+    return torch.empty_like(lf).scatter_(-1, idx, sorted_l)
+
+
+def sample(logits: torch.Tensor, temperature: Optional[torch.Tensor] = None,
+           seeds: Optional[torch.Tensor] = None, step: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Greedy (temperature 0) or Gumbel-max sampling per row; returns int64 token ids."""
+    B = logits.shape[0]
+    if _native(logits):
+        if out is None:
+            out = torch.empty(B, dtype=torch.long, device=logits.device)
+        torch.ops.dgi.sample(out, logits, temperature, seeds, step)
+        return out
+    lf = logits.float()
+    if temperature is None or bool((temperature <= 1e-5).all()):
+        r = lf.argmax(-1)
+    else:
+        g = torch.Generator(device="cpu")
+        g.manual_seed(int(seeds[0]) * 1000003 + step if seeds is not None else step)
+        u = torch.rand(lf.shape, generator=g).clamp_(1e-10, 1.0)
+        t = temperature.float().clamp(min=1e-5)
+        noisy = lf / t[:, None] - torch.log(-torch.log(u))
+        r = torch.where(temperature <= 1e-5, lf.argmax(-1), noisy.argmax(-1))
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
+def topk(logits: torch.Tensor, k: int):
+    """Top-k (k <= 16) values (fp32) and indices (int64), descending."""
+    if _native(logits):
+        B = logits.shape[0]
+        v = torch.empty(B, k, dtype=torch.float32, device=logits.device)
+        i = torch.empty(B, k, dtype=torch.long, device=logits.device)
+        torch.ops.dgi.topk(v, i, logits, k)
+        return v, i
+    v, i = logits.float().topk(k, dim=-1)
+    return v, i
+
+
+# ----------------------------------------------------------------------------
+# KV block movement
+# ----------------------------------------------------------------------------
+
+def kv_gather(cache: torch.Tensor, ids: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """cache [L,2,NB,...] -> [L,2,n,...] pages of ``ids``."""
+    if _native(cache):
+        if out is None:
+            out = torch.empty(cache.shape[0], cache.shape[1], ids.numel(), *cache.shape[3:],
+                              dtype=cache.dtype, device=cache.device)
+        torch.ops.dgi.kv_gather(out, cache, ids)
+        return out
+    r = cache[:, :, ids.long()]
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
+def kv_scatter(cache: torch.Tensor, ids: torch.Tensor, buf: torch.Tensor) -> None:
+    if _native(cache):
+        torch.ops.dgi.kv_scatter(cache, ids, buf)
+    else:
+        cache[:, :, ids.long()] = buf.view(cache.shape[0], cache.shape[1], ids.numel(), *cache.shape[3:])
+
+
+def kv_copy(cache: torch.Tensor, src: torch.Tensor, dst: torch.Tensor) -> None:
+    """Copy pages src[i] -> dst[i] for every layer (src/dst sets must be disjoint)."""
+    if _native(cache):
+        torch.ops.dgi.kv_copy(cache, src, dst)
+    else:
+        cache[:, :, dst.long()] = cache[:, :, src.long()]
+
+
+# ----------------------------------------------------------------------------
+# EAGLE tree
+# ----------------------------------------------------------------------------
+
+def tree_mask_ref(parent: torch.Tensor):
+    B, N = parent.shape
+    anc = torch.zeros(B, 64, dtype=torch.long)
+    depth = torch.zeros(B, N, dtype=torch.int32)
+    par = parent.cpu().tolist()
+    for b in range(B):
+        for n in range(N):
+            m = 1 << n
+            d = 0
+            p = par[b][n]
+            while p >= 0:
+                m |= 1 << p
+                p = par[b][p]
+                d += 1
+            if m >= 1 << 63:
+                m -= 1 << 64
+            anc[b, n] = m
+            depth[b, n] = d
+    return anc.to(parent.device), depth.to(parent.device)
+
+
+def tree_mask(parent: torch.Tensor):
+    """Ancestor-or-self bitmask [B,64] (int64 bit patterns) and depth [B,N]."""
+    if _native(parent):
+        B, N = parent.shape
+        anc = torch.zeros(B, 64, dtype=torch.long, device=parent.device)
+        depth = torch.empty(B, N, dtype=torch.int32, device=parent.device)
+        torch.ops.dgi.tree_mask(anc, depth, parent)
+        return anc, depth
+    return tree_mask_ref(parent)
+
+
+def tree_verify_ref(parent, draft, target, anc, depth, max_path: int):
+    B, N = parent.shape
+    acc = torch.zeros(B, dtype=torch.int32)
+    path = torch.zeros(B, max_path, dtype=torch.int32)
+    toks = torch.zeros(B, max_path + 1, dtype=torch.long)
+    par, dr, tg = parent.cpu().tolist(), draft.cpu().tolist(), target.cpu().tolist()
+    dp = depth.cpu().tolist()
+    for b in range(B):
+        ok = [False] * N
+        for n in range(N):
+            if n == 0:
+                ok[n] = True
+            else:
+                ok[n] = ok[par[b][n]] and dr[b][n] == tg[b][par[b][n]]
+        best, bd = 0, 0
+        for n in range(N):
+            if ok[n] and dp[b][n] > bd:
+                best, bd = n, dp[b][n]
+        acc[b] = bd
+        node = best
+        for k in range(bd, -1, -1):
+            if k < max_path:
+                path[b, k] = node
+                if k > 0:
+                    toks[b, k - 1] = dr[b][node]
+            node = par[b][node] if node > 0 else 0
+        if bd < max_path + 1:
+            toks[b, bd] = tg[b][best]
+    dev = parent.device
+    return acc.to(dev), path.to(dev), toks.to(dev)
+
+
+def tree_verify(parent, draft, target, anc, depth, max_path: int):
+    """Greedy tree acceptance: (accept_len[B], path[B,max_path], tokens[B,max_path+1])."""
+    if _native(parent):
+        B = parent.shape[0]
+        acc = torch.empty(B, dtype=torch.int32, device=parent.device)
+        path = torch.zeros(B, max_path, dtype=torch.int32, device=parent.device)
+        toks = torch.zeros(B, max_path + 1, dtype=torch.long, device=parent.device)
+        torch.ops.dgi.tree_verify(acc, path, toks, parent, draft, target, anc, depth)
+        return acc, path, toks
+    return tree_verify_ref(parent, draft, target, anc, depth, max_path)

@@ -1,0 +1,272 @@
+"""Model runner: ScheduledBatch -> device metadata -> forward -> sampled tokens.
+
+* All int32 step metadata (token ids, positions, slot mapping, block tables,
+  context lengths, cu_seqlens, attention tiles) is packed into ONE pinned host
+  buffer and moved with a single async H2D copy per step.
+* Pure-decode steps replay a hipGraph captured per batch-size bucket
+  (``GraphRunner``): the 80-layer Llama-3-70B decode step is ~900 kernel
+  launches, which the graph turns into one replay with no host work per
+  kernel (SURVEY §7.1 "fixed-shape decode in hipGraphs").
+* Mixed prefill+decode steps run eagerly (their GEMMs dominate).
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Optional
+
+import numpy as np
+import torch
+
+from dgi import ops
+from dgi.runtime.batch import AttnMeta
+from dgi.sched.scheduler import ScheduledBatch
+
+DEFAULT_BUCKETS = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256, 320, 384, 448, 512)
+
+
+@dataclasses.dataclass
+class StepResult:
+    tokens: list          # sampled token per logits row (decode rows first, then sampled chunks)
+    rows: list            # Request per sampled row
+    hidden: Optional[torch.Tensor] = None
+
+
+class ModelRunner:
+    def __init__(self, model, pool, max_num_seqs: int = 256, max_model_len: int = 8192,
+                 max_num_batched_tokens: int = 8192, use_graphs: bool = True,
+                 graph_buckets=DEFAULT_BUCKETS, decode_part_size: int = 256, num_cus: int = 256):
+        self.model = model
+        self.pool = pool
+        self.device = pool.device
+        self.bs = pool.block_size
+        self.max_num_seqs = max_num_seqs
+        self.max_model_len = max_model_len
+        self.max_blocks = (max_model_len + self.bs - 1) // self.bs
+        self.max_tokens = max_num_batched_tokens
+        self.num_cus = num_cus
+        self.step_id = 0
+        model.kv_cache = pool.kv
+        self.is_cuda = self.device.type == "cuda"
+        # decode split-KV plan used by graphs (fixed) and workspaces
+        self.graph_part = decode_part_size
+        self.graph_splits = (max_model_len + decode_part_size - 1) // decode_part_size
+        self.ws_splits = (max_model_len + 127) // 128
+        nh, hd = model.cfg.num_heads, model.cfg.head_dim
+        maxb = max(max_num_seqs, max(graph_buckets) if graph_buckets else 1)
+        self.dec_ws = None
+        if self.is_cuda:
+            self.dec_ws = (torch.empty(maxb * nh * self.ws_splits * hd, dtype=torch.float32, device=self.device),
+                           torch.empty(maxb * nh * self.ws_splits, dtype=torch.float32, device=self.device))
+        self.graphs = None
+        if use_graphs and self.is_cuda and model.has_head:
+            self.graphs = GraphRunner(self, [b for b in graph_buckets if b <= max_num_seqs])
+
+    # ------------------------------------------------------------------ metadata
+    def build(self, sb: ScheduledBatch, pad_decode_to: int = 0):
+        """Host-side metadata for one step (numpy) -> AttnMeta on device."""
+        bs = self.bs
+        nd = len(sb.decode)
+        ndp = max(nd, pad_decode_to)
+        chunks = sb.prefill
+        npre = sum(c.length for c in chunks)
+        T = ndp + npre
+        ids = np.zeros(T, np.int32)
+        pos = np.zeros(T, np.int32)
+        slots = np.zeros(T, np.int32)
+        maxw = self.max_blocks
+        dec_bt = np.zeros((ndp, maxw), np.int32)
+        dec_ctx = np.ones(ndp, np.int32)
+        for i, r in enumerate(sb.decode):
+            p = r.num_computed
+            ids[i] = r.output[-1] if r.output else r.prompt[-1]
+            pos[i] = p
+            slots[i] = r.blocks[p // bs] * bs + p % bs
+            dec_bt[i, : len(r.blocks)] = r.blocks
+            dec_ctx[i] = p + 1
+        # padded decode rows write into reserved block 0 and read it back
+        nb = len(chunks)
+        pre_bt = np.zeros((nb, maxw), np.int32)
+        cu = np.zeros(nb + 1, np.int32)
+        pctx = np.zeros(nb, np.int32)
+        logit_rows = list(range(nd))
+        row = ndp
+        sampled = list(sb.decode)
+        for j, c in enumerate(chunks):
+            r = c.req
+            toks = r.all_tokens()
+            ids[row: row + c.length] = toks[c.start: c.start + c.length]
+            p = np.arange(c.start, c.start + c.length, dtype=np.int32)
+            pos[row: row + c.length] = p
+            blk = np.asarray(r.blocks, np.int32)
+            slots[row: row + c.length] = blk[p // bs] * bs + p % bs
+            pre_bt[j, : len(r.blocks)] = blk
+            cu[j + 1] = cu[j] + c.length
+            pctx[j] = c.start + c.length
+            if c.sample:
+                logit_rows.append(row + c.length - 1)
+                sampled.append(r)
+            row += c.length
+        tiles = []
+        for j in range(nb):
+            for t0 in range(0, int(cu[j + 1] - cu[j]), 128):
+                tiles.append((j, t0))
+        tiles_np = np.asarray(tiles, np.int32).reshape(-1, 2)
+        lidx = np.asarray(logit_rows, np.int64)
+        # ---- one pinned buffer, one H2D copy
+        parts = [ids, pos, slots, dec_bt.ravel(), dec_ctx, pre_bt.ravel(), cu, pctx, tiles_np.ravel()]
+        sizes = [a.size for a in parts]
+        flat = np.concatenate(parts) if parts else np.zeros(0, np.int32)
+        host = torch.from_numpy(flat)
+        lhost = torch.from_numpy(lidx)
+        if self.is_cuda:
+            host = host.pin_memory()
+            lhost = lhost.pin_memory()
+        dev = host.to(self.device, non_blocking=True)
+        ldev = lhost.to(self.device, non_blocking=True)
+        views = []
+        o = 0
+        for s in sizes:
+            views.append(dev[o: o + s])
+            o += s
+        d_ids, d_pos, d_slots, d_dbt, d_dctx, d_pbt, d_cu, d_pctx, d_tiles = views
+        max_ctx = int(dec_ctx.max()) if ndp else 1
+        if self.is_cuda and ndp:
+            splits, part = ops.decode_split_plan(ndp, max_ctx, self.model.cfg.num_kv_heads, self.num_cus)
+        else:
+            splits, part = 1, 1 << 20
+        meta = AttnMeta(
+            positions=d_pos, slot_mapping=d_slots, num_decode=ndp,
+            dec_block_tables=d_dbt.view(ndp, maxw), dec_context_lens=d_dctx,
+            dec_max_splits=splits, dec_part_size=part, dec_workspace=self.dec_ws,
+            num_prefill_tokens=npre, pre_block_tables=d_pbt.view(nb, maxw), pre_cu_seqlens=d_cu,
+            pre_context_lens=d_pctx, pre_tiles=d_tiles.view(-1, 2), logits_indices=ldev)
+        return d_ids, meta, sampled
+
+    # ------------------------------------------------------------------ run
+    def sampling_tensors(self, reqs):
+        temps = torch.tensor([r.params.temperature for r in reqs], dtype=torch.float32)
+        seeds = torch.tensor([r.seed for r in reqs], dtype=torch.long)
+        if self.is_cuda:
+            temps = temps.pin_memory().to(self.device, non_blocking=True)
+            seeds = seeds.pin_memory().to(self.device, non_blocking=True)
+        return temps, seeds
+
+    def _sample(self, logits, reqs):
+        temps, seeds = self.sampling_tensors(reqs)
+        if any(r.params.needs_filter for r in reqs):
+            tk = torch.tensor([r.params.top_k if not r.params.greedy else 0 for r in reqs], device=logits.device)
+            tp = torch.tensor([r.params.top_p if not r.params.greedy else 1.0 for r in reqs], device=logits.device)
+            logits = ops.apply_top_k_top_p(logits, tk, tp)
+        return ops.sample(logits, temps, seeds, self.step_id)
+
+    @torch.inference_mode()
+    def execute(self, sb: ScheduledBatch) -> StepResult:
+        self.step_id += 1
+        if self.graphs is not None and not sb.prefill and sb.decode and \
+                len(sb.decode) <= self.graphs.max_bucket and not any(r.params.needs_filter for r in sb.decode):
+            toks = self.graphs.run(sb)
+            return StepResult(toks, list(sb.decode))
+        ids, meta, sampled = self.build(sb)
+        logits = self.model.forward(meta, input_ids=ids)
+        if not sampled:
+            return StepResult([], [])
+        toks = self._sample(logits, sampled)
+        return StepResult(toks.tolist(), sampled)
+
+
+class GraphRunner:
+    """hipGraph capture of the decode step (forward + sampling) per batch bucket."""
+
+    def __init__(self, runner: ModelRunner, buckets):
+        self.r = runner
+        self.buckets = sorted(set(buckets))
+        self.max_bucket = self.buckets[-1] if self.buckets else 0
+        self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
+        self.pool_handle = None
+        dev = runner.device
+        maxb = self.max_bucket
+        maxw = runner.max_blocks
+        self.ids = torch.zeros(maxb, dtype=torch.long, device=dev)
+        self.pos = torch.zeros(maxb, dtype=torch.int32, device=dev)
+        self.slots = torch.zeros(maxb, dtype=torch.int32, device=dev)
+        self.bt = torch.zeros(maxb, maxw, dtype=torch.int32, device=dev)
+        self.ctx = torch.ones(maxb, dtype=torch.int32, device=dev)
+        self.temps = torch.zeros(maxb, dtype=torch.float32, device=dev)
+        self.seeds = torch.zeros(maxb, dtype=torch.long, device=dev)
+        self.step = torch.zeros(1, dtype=torch.long, device=dev)
+        self.out = torch.zeros(maxb, dtype=torch.long, device=dev)
+        self.host_in = torch.zeros(maxb * (4 + maxw), dtype=torch.int32).pin_memory()
+        self.host_out = torch.zeros(maxb, dtype=torch.long).pin_memory()
+        self.captured = False
+
+    def _meta(self, b):
+        r = self.r
+        return AttnMeta(positions=self.pos[:b], slot_mapping=self.slots[:b], num_decode=b,
+                        dec_block_tables=self.bt[:b], dec_context_lens=self.ctx[:b],
+                        dec_max_splits=r.graph_splits, dec_part_size=r.graph_part, dec_workspace=r.dec_ws,
+                        num_prefill_tokens=0, logits_indices=None)
+
+    def _body(self, b):
+        logits = self.r.model.forward(self._meta(b), input_ids=self.ids[:b])
+        ops.sample(logits, self.temps[:b], self.seeds[:b], 0, out=self.out[:b])
+
+    @torch.inference_mode()
+    def capture(self):
+        if self.captured:
+            return
+        torch.cuda.synchronize()
+        for b in reversed(self.buckets):
+            # warm up once outside capture (allocator, hipBLASLt heuristics)
+            self._body(b)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.pool_handle):
+                self._body(b)
+            if self.pool_handle is None:
+                self.pool_handle = g.pool()
+            self.graphs[b] = g
+        torch.cuda.synchronize()
+        self.captured = True
+
+    def run(self, sb: ScheduledBatch) -> list:
+        if not self.captured:
+            self.capture()
+        n = len(sb.decode)
+        b = next(x for x in self.buckets if x >= n)
+        r = self.r
+        bs = r.bs
+        maxw = r.max_blocks
+        h = self.host_in.numpy()
+        ids = h[:b]
+        pos = h[b: 2 * b]
+        slots = h[2 * b: 3 * b]
+        ctx = h[3 * b: 4 * b]
+        bt = h[4 * b: 4 * b + b * maxw].reshape(b, maxw)
+        ids[:] = 0
+        pos[:] = 0
+        slots[:] = 0
+        ctx[:] = 1
+        bt[:] = 0
+        temps = np.zeros(b, np.float32)
+        seeds = np.zeros(b, np.int64)
+        for i, rq in enumerate(sb.decode):
+            p = rq.num_computed
+            ids[i] = rq.output[-1]
+            pos[i] = p
+            slots[i] = rq.blocks[p // bs] * bs + p % bs
+            ctx[i] = p + 1
+            bt[i, : len(rq.blocks)] = rq.blocks
+            temps[i] = rq.params.temperature
+            seeds[i] = (rq.seed * 1000003 + r.step_id) & 0x7FFFFFFFFFFF
+        dev = self.host_in[: 4 * b + b * maxw].to(r.device, non_blocking=True)
+        self.ids[:b].copy_(dev[:b])
+        self.pos[:b].copy_(dev[b:2 * b])
+        self.slots[:b].copy_(dev[2 * b:3 * b])
+        self.ctx[:b].copy_(dev[3 * b:4 * b])
+        self.bt[:b].copy_(dev[4 * b:].view(b, maxw))
+        self.temps[:b].copy_(torch.from_numpy(temps).pin_memory(), non_blocking=True)
+        self.seeds[:b].copy_(torch.from_numpy(seeds).pin_memory(), non_blocking=True)
+        self.graphs[b].replay()
+        self.host_out[:b].copy_(self.out[:b], non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        return self.host_out[:n].tolist()

@@ -1,0 +1,215 @@
+"""Iteration-level continuous-batching scheduler.
+
+The reference batches at *request* level: it waits for up to
+``max_batch_size`` jobs and hands them to the engine as one static batch
+(worker/batch_processor.py:60-365), and the live worker runs one job at a
+time (worker/main.py:321).  This scheduler re-forms the batch every model
+step:
+
+1. every running sequence in the decode phase gets one token (a new KV page
+   when it crosses a block boundary); if the pool is exhausted the most
+   recently admitted sequence is preempted (pages released, recomputed
+   later: its prefix is usually still in the radix cache);
+2. the remaining token budget (``max_num_batched_tokens``) is filled with
+   prefill chunks — first unfinished chunks of running sequences, then new
+   requests in FCFS/priority order, each admission starting from its longest
+   radix-cache prefix hit (chunked prefill).
+
+The result is a ``ScheduledBatch`` whose rows are ordered
+[decode rows | prefill rows] for the model runner.
+"""
+from __future__ import annotations
+
+import collections
+import dataclasses
+import time
+from typing import Optional
+
+from dgi.kv.block_pool import BlockPool, OutOfBlocks
+from dgi.kv.radix_cache import RadixCache
+from dgi.sched.request import Request, Status
+
+
+@dataclasses.dataclass
+class SchedulerConfig:
+    max_num_seqs: int = 256
+    max_num_batched_tokens: int = 8192
+    max_model_len: int = 8192
+    enable_prefix_caching: bool = True
+    decode_first: bool = True
+
+
+@dataclasses.dataclass
+class PrefillChunk:
+    req: Request
+    start: int       # first token index of the chunk (== req.num_computed)
+    length: int
+    sample: bool     # chunk completes the prefill target -> sample a token
+
+
+@dataclasses.dataclass
+class ScheduledBatch:
+    decode: list
+    prefill: list
+    preempted: list
+
+    @property
+    def num_tokens(self) -> int:
+        return len(self.decode) + sum(c.length for c in self.prefill)
+
+    @property
+    def empty(self) -> bool:
+        return not self.decode and not self.prefill
+
+
+class Scheduler:
+    def __init__(self, pool: BlockPool, cfg: SchedulerConfig):
+        self.pool = pool
+        self.cfg = cfg
+        self.bs = pool.block_size
+        self.waiting: collections.deque = collections.deque()
+        self.running: list[Request] = []
+        self.radix: Optional[RadixCache] = RadixCache(pool) if cfg.enable_prefix_caching else None
+        self.num_preemptions = 0
+
+    # ------------------------------------------------------------------ queue
+    def add(self, req: Request) -> None:
+        if req.total_len >= self.cfg.max_model_len:
+            raise ValueError(f"prompt of {req.total_len} tokens exceeds max_model_len {self.cfg.max_model_len}")
+        req.status = Status.WAITING
+        self.waiting.append(req)
+
+    def has_work(self) -> bool:
+        return bool(self.waiting or self.running)
+
+    def abort(self, rid) -> bool:
+        for q in (self.waiting, self.running):
+            for r in list(q):
+                if r.rid == rid:
+                    q.remove(r)
+                    self._release(r, cache=False)
+                    r.status = Status.FINISHED
+                    r.finish_reason = "abort"
+                    return True
+        return False
+
+    # ------------------------------------------------------------------ blocks
+    def _blocks_needed(self, req: Request, upto: int) -> int:
+        return max(0, (upto + self.bs - 1) // self.bs - len(req.blocks))
+
+    def _grow(self, req: Request, upto: int) -> None:
+        n = self._blocks_needed(req, upto)
+        if n:
+            req.blocks.extend(self.pool.allocate(n))
+
+    def _release(self, req: Request, cache: bool = True) -> None:
+        if self.radix is not None:
+            if cache and req.num_computed > 0:
+                toks = req.all_tokens()[: req.num_computed]
+                self.radix.insert(toks, req.blocks)
+            self.radix.release(req.radix_path)
+            req.radix_path = []
+        self.pool.free(req.blocks)
+        req.blocks = []
+
+    def _preempt(self, victim: Request) -> None:
+        self.running.remove(victim)
+        self._release(victim, cache=True)
+        victim.num_computed = 0
+        victim.num_cached = 0
+        victim.prefill_target = victim.total_len
+        victim.status = Status.WAITING
+        victim.preempted += 1
+        self.num_preemptions += 1
+        self.waiting.appendleft(victim)
+
+    # ------------------------------------------------------------------ schedule
+    def schedule(self) -> ScheduledBatch:
+        budget = self.cfg.max_num_batched_tokens
+        decode: list[Request] = []
+        preempted: list[Request] = []
+        # 1) decode rows
+        for req in list(self.running):
+            if req.in_prefill or req not in self.running:
+                continue
+            pos = req.num_computed  # position of the token being fed (== total_len - 1)
+            while True:
+                try:
+                    self._grow(req, pos + 1)
+                    break
+                except OutOfBlocks:
+                    victim = self.running[-1]
+                    self._preempt(victim)
+                    preempted.append(victim)
+                    if victim is req:
+                        break
+            if req.status is Status.RUNNING and req in self.running:
+                decode.append(req)
+                budget -= 1
+        # 2) prefill chunks: running (partial) first, then waiting
+        prefill: list[PrefillChunk] = []
+        for req in self.running:
+            if budget <= 0:
+                break
+            if not req.in_prefill:
+                continue
+            n = min(req.prefill_target - req.num_computed, budget)
+            try:
+                self._grow(req, req.num_computed + n)
+            except OutOfBlocks:
+                break
+            prefill.append(PrefillChunk(req, req.num_computed, n, req.num_computed + n == req.prefill_target))
+            budget -= n
+        while self.waiting and budget > 0 and len(self.running) < self.cfg.max_num_seqs:
+            req = self.waiting[0]
+            toks = req.all_tokens()
+            target = req.prefill_target
+            cached_blocks: list[int] = []
+            path: list = []
+            if self.radix is not None and not req.blocks:
+                # keep >= 1 token to compute so the chunk produces logits
+                cached_blocks, path = self.radix.match(toks[: target - 1])
+            start = len(cached_blocks) * self.bs
+            n = min(target - start, budget)
+            need = (start + n + self.bs - 1) // self.bs - len(cached_blocks)
+            if need > self.pool.num_free and not self.pool.can_allocate(need):
+                if self.radix is not None:
+                    self.radix.release(path)
+                    self.pool.free(cached_blocks)
+                break
+            try:
+                own = self.pool.allocate(need)
+            except OutOfBlocks:
+                if self.radix is not None:
+                    self.radix.release(path)
+                    self.pool.free(cached_blocks)
+                break
+            self.waiting.popleft()
+            req.blocks = cached_blocks + own
+            req.radix_path = path
+            req.num_computed = start
+            req.num_cached = start
+            req.status = Status.RUNNING
+            self.running.append(req)
+            prefill.append(PrefillChunk(req, start, n, start + n == target))
+            budget -= n
+        return ScheduledBatch(decode, prefill, preempted)
+
+    # ------------------------------------------------------------------ update
+    def finish(self, req: Request, reason: str) -> None:
+        req.status = Status.FINISHED
+        req.finish_reason = reason
+        req.finish_time = time.perf_counter()
+        if req in self.running:
+            self.running.remove(req)
+        self._release(req, cache=True)
+
+    def stats(self) -> dict:
+        return {
+            "waiting": len(self.waiting),
+            "running": len(self.running),
+            "free_blocks": self.pool.num_free,
+            "used_blocks": self.pool.num_used,
+            "preemptions": self.num_preemptions,
+            "prefix_hit_rate": self.radix.hit_rate() if self.radix else 0.0,
+        }

@@ -1,0 +1,27 @@
+#!/bin/bash
+# One gpurun session: kernel tests, smoke, short benches, rocprof stats.
+# Stops at the first GPU fault / abort / timeout (exit codes other than 0/1).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+run() {  # name timeout cmd...
+  local name=$1; local to=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP: $name rc=$rc"; exit $rc; fi
+  return 0
+}
+STEPS=${STEPS:-"pytest smoke bench8b bench70b"}
+for s in $STEPS; do
+  case $s in
+    pytest) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench8b) run bench8b 900 python bench.py --model llama3-8b --steps 30 --warmup 5 --json-out gpurun_out/bench8b.json ;;
+    bench70b) run bench70b 1200 python bench.py --steps 30 --warmup 5 --json-out gpurun_out/bench70b.json ;;
+    prof8b) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null; run prof8b 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8b -o run --output-format csv -- python3 bench.py --model llama3-8b --steps 10 --warmup 2 --ramp-steps 16 ;;
+  esac
+done
+echo ALLDONE
