@@ -61,6 +61,8 @@ class LLMEngine:
         self.cfg = cfg
         self.device = torch.device(cfg.device)
         if self.device.type == "cuda":
+            if self.device.index is None:
+                self.device = torch.device("cuda", torch.cuda.current_device())
             torch.cuda.set_device(self.device)
         self.model_cfg = model_cfg or get_config(cfg.model)
         self.model_cfg.max_position = max(self.model_cfg.max_position, cfg.max_model_len)

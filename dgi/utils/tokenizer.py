@@ -1,0 +1,85 @@
+"""Tokenizer loading without network access.
+
+``load_tokenizer(model_id)`` returns a local HF tokenizer when the files are
+on disk, otherwise a deterministic byte-level tokenizer (ids = byte + offset)
+that round-trips any UTF-8 text — enough for the serving plumbing and for
+synthetic-prompt benchmarks with random-init weights.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Optional
+
+
+class ByteTokenizer:
+    """UTF-8 bytes -> ids ``offset + byte``; specials below ``offset``."""
+
+    def __init__(self, vocab_size: int = 32000, bos_token_id: int = 1, eos_token_id: int = 2, offset: int = 3):
+        self.vocab_size = vocab_size
+        self.bos_token_id = bos_token_id
+        self.eos_token_id = eos_token_id
+        self.pad_token_id = eos_token_id
+        self.offset = offset
+
+    def encode(self, text: str, add_bos: bool = True) -> List[int]:
+        ids = [self.offset + b for b in text.encode("utf-8")]
+        return ([self.bos_token_id] if add_bos else []) + ids
+
+    def decode(self, ids, skip_special_tokens: bool = True) -> str:
+        out = bytearray()
+        for i in ids:
+            i = int(i)
+            b = i - self.offset
+            if 0 <= b < 256:
+                out.append(b)
+            elif not skip_special_tokens:
+                out.extend(f"<{i}>".encode())
+        return out.decode("utf-8", errors="replace")
+
+    def apply_chat_template(self, messages: List[Dict[str, str]], tokenize: bool = False,
+                            add_generation_prompt: bool = True):
+        parts = [f"<|{m.get('role', 'user')}|>\n{m.get('content', '')}\n" for m in messages]
+        if add_generation_prompt:
+            parts.append("<|assistant|>\n")
+        text = "".join(parts)
+        return self.encode(text) if tokenize else text
+
+    def __call__(self, text, return_tensors=None):
+        import torch
+        ids = self.encode(text)
+        if return_tensors == "pt":
+            class _Enc(dict):
+                def to(self, dev):
+                    return _Enc({k: v.to(dev) for k, v in self.items()})
+
+                def __getattr__(self, k):
+                    return self[k]
+            t = torch.tensor([ids])
+            return _Enc(input_ids=t, attention_mask=torch.ones_like(t))
+        return {"input_ids": ids}
+
+
+def load_tokenizer(model_id: Optional[str], vocab_size: int = 32000, bos: int = 1, eos: int = 2):
+    if model_id and os.path.isdir(model_id):
+        try:
+            from transformers import AutoTokenizer
+            return AutoTokenizer.from_pretrained(model_id, local_files_only=True)
+        except Exception:
+            pass
+    if model_id:
+        try:
+            from transformers import AutoTokenizer
+            return AutoTokenizer.from_pretrained(model_id, local_files_only=True)
+        except Exception:
+            pass
+    return ByteTokenizer(vocab_size=vocab_size, bos_token_id=bos, eos_token_id=eos)
+
+
+def chat_prompt_ids(tokenizer, messages: List[Dict[str, str]]) -> List[int]:
+    try:
+        text = tokenizer.apply_chat_template(messages, tokenize=False, add_generation_prompt=True)
+    except Exception:
+        text = "\n".join(f"{m.get('role', 'user')}: {m.get('content', '')}" for m in messages) + "\nassistant:"
+    if isinstance(tokenizer, ByteTokenizer):
+        return tokenizer.encode(text)
+    return list(tokenizer(text)["input_ids"])

@@ -21,7 +21,9 @@ for s in $STEPS; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench8b) run bench8b 900 python bench.py --model llama3-8b --steps 30 --warmup 5 --json-out gpurun_out/bench8b.json ;;
     bench70b) run bench70b 1200 python bench.py --steps 30 --warmup 5 --json-out gpurun_out/bench70b.json ;;
-    prof8b) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null; run prof8b 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8b -o run --output-format csv -- python3 bench.py --model llama3-8b --steps 10 --warmup 2 --ramp-steps 16 ;;
+    prof8b) export TMPDIR=/tmp; run prof8b 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8b -o run --output-format csv -- python3 bench.py --model llama3-8b --steps 10 --warmup 2 --ramp-steps 16 ;;
+    prof70b) export TMPDIR=/tmp; run prof70b 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof70b -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --ramp-steps 16 ;;
+    bench70b_long) run bench70b_long 1200 python bench.py --steps 200 --warmup 20 --json-out gpurun_out/bench70b_long.json ;;
   esac
 done
 echo ALLDONE

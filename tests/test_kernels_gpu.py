@@ -164,7 +164,9 @@ def test_sample_greedy_and_topk(dtype):
     v, i = ops.topk(logits, 8)
     rv, ri = logits.float().topk(8, dim=-1)
     torch.testing.assert_close(v.cpu(), rv.cpu())
-    assert torch.equal(i.cpu(), ri.cpu())
+    # bf16 logits tie often: indices must point at the reported values, all distinct
+    torch.testing.assert_close(logits.float().gather(1, i).cpu(), v.cpu())
+    assert all(len(set(r)) == 8 for r in i.cpu().tolist())
 
 
 def test_sample_temperature_distribution():

@@ -1,0 +1,251 @@
+"""NativeLLMEngine — the MI355X-native ``dgi`` runtime behind the reference's
+``LLMBaseEngine`` contract (registry name ``llm_native``, alias ``mi355x``).
+
+Where the reference offloads to SGLang/vLLM (worker/engines/llm_sglang.py,
+llm_vllm.py) this engine provides the same features itself: paged KV,
+radix prefix cache, iteration-level continuous batching, chunked prefill,
+streaming, on-device sampling and hipGraph decode.
+
+Threading: one daemon thread owns the ``dgi.engine.LLMEngine`` and steps it
+while work exists; asyncio callers submit through a thread-safe queue and
+are resolved with ``loop.call_soon_threadsafe`` (no per-call threads).
+
+Config keys accepted (SURVEY Appendix C mapping): ``model_id``, ``device``,
+``mem_fraction_static``/``gpu_memory_utilization`` -> KV fraction,
+``max_running_requests``/``max_num_seqs``, ``chunked_prefill_size``,
+``enable_prefix_caching``, ``context_length``/``max_model_len``,
+``num_blocks``, ``use_graphs``/``enforce_eager``; nested ``sglang``/``vllm``/
+``native`` dicts are merged in.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import queue
+import threading
+import time
+from typing import Any, AsyncIterator, Dict, List, Optional
+
+import torch
+
+from dgi.utils.tokenizer import chat_prompt_ids, load_tokenizer
+
+from .llm_base import GenerationConfig, GenerationResult, LLMBackend, LLMBaseEngine
+
+logger = logging.getLogger(__name__)
+
+
+def _merged(config: Dict[str, Any]) -> Dict[str, Any]:
+    out = dict(config)
+    for k in ("sglang", "vllm", "native", "mi355x"):
+        if isinstance(config.get(k), dict):
+            out.update(config[k])
+    return out
+
+
+class _Pending:
+    __slots__ = ("req", "loop", "future", "stream_q", "sent", "cfg", "prompt_len")
+
+    def __init__(self, loop, future, stream_q, cfg, prompt_len):
+        self.req = None
+        self.loop = loop
+        self.future = future
+        self.stream_q = stream_q
+        self.sent = 0
+        self.cfg = cfg
+        self.prompt_len = prompt_len
+
+
+class NativeLLMEngine(LLMBaseEngine):
+    def __init__(self, config: Dict[str, Any]):
+        super().__init__(config)
+        self.backend_type = LLMBackend.NATIVE_MI355X
+        self.engine = None
+        self._inbox: "queue.Queue" = queue.Queue()
+        self._pending: Dict[Any, _Pending] = {}
+        self._thread: Optional[threading.Thread] = None
+        self._stop = threading.Event()
+        self._wake = threading.Event()
+        self.stats = {"requests": 0, "completed": 0, "errors": 0}
+
+    # ------------------------------------------------------------------ lifecycle
+    def load_model(self) -> None:
+        from dgi.engine import EngineConfig, LLMEngine
+        from dgi.models.config import get_config
+
+        c = _merged(self.config)
+        model_id = c.get("model_id", "llama3-8b")
+        device = c.get("device", "cuda" if torch.cuda.is_available() else "cpu")
+        mc = get_config(model_id)
+        frac = c.get("mem_fraction_static", c.get("gpu_memory_utilization", c.get("kv_fraction", 0.9)))
+        ecfg = EngineConfig(
+            model=model_id, device=device,
+            max_num_seqs=int(c.get("max_running_requests", c.get("max_num_seqs", 256))),
+            max_num_batched_tokens=int(c.get("chunked_prefill_size", c.get("max_num_batched_tokens", 8192))),
+            max_model_len=int(c.get("context_length", c.get("max_model_len", 8192))),
+            kv_fraction=float(frac), num_blocks=c.get("num_blocks"),
+            enable_prefix_caching=bool(c.get("enable_prefix_caching", True)),
+            use_graphs=bool(c.get("use_graphs", not c.get("enforce_eager", False))) and device != "cpu",
+            seed=int(c.get("seed", 0)))
+        self.engine = LLMEngine(ecfg, model_cfg=mc)
+        self.tokenizer = load_tokenizer(c.get("tokenizer", model_id), vocab_size=mc.vocab_size,
+                                        bos=mc.bos_token_id, eos=mc.eos_token_id)
+        self.device = device
+        if c.get("warmup", False):
+            self.engine.warmup()
+        self._stop.clear()
+        self._thread = threading.Thread(target=self._loop, name="dgi-engine", daemon=True)
+        self._thread.start()
+        self.loaded = True
+
+    def unload_model(self) -> None:
+        self._stop.set()
+        self._wake.set()
+        if self._thread is not None:
+            self._thread.join(timeout=10)
+        self._thread = None
+        self.engine = None
+        if torch.cuda.is_available():
+            torch.cuda.empty_cache()
+        self.loaded = False
+
+    # ------------------------------------------------------------------ engine thread
+    def _loop(self) -> None:
+        from dgi.sched.request import SamplingParams
+        eng = self.engine
+        while not self._stop.is_set():
+            while True:
+                try:
+                    prompt, p, cfg = self._inbox.get_nowait()
+                except queue.Empty:
+                    break
+                try:
+                    sp = SamplingParams(max_tokens=cfg.max_tokens, temperature=cfg.temperature, top_p=cfg.top_p,
+                                        top_k=cfg.top_k)
+                    p.req = eng.add_request(prompt, sp)
+                    self._pending[p.req.rid] = p
+                except Exception as e:  # prompt too long etc.
+                    self._resolve_error(p, e)
+            if not eng.has_unfinished():
+                self._wake.wait(0.05)
+                self._wake.clear()
+                continue
+            try:
+                outs = eng.step()
+            except Exception as e:  # pragma: no cover - surfaced to callers
+                logger.exception("engine step failed")
+                for p in list(self._pending.values()):
+                    self._resolve_error(p, e)
+                self._pending.clear()
+                continue
+            for o in outs:
+                p = self._pending.get(o.rid)
+                if p is None:
+                    continue
+                if p.stream_q is not None:
+                    p.loop.call_soon_threadsafe(p.stream_q.put_nowait, o.token)
+                if o.finished:
+                    self._pending.pop(o.rid, None)
+                    self._resolve(p, o.request)
+
+    def _resolve(self, p: _Pending, req) -> None:
+        text = self.tokenizer.decode(req.output, skip_special_tokens=True)
+        res = GenerationResult(text=text, prompt_tokens=len(req.prompt), completion_tokens=len(req.output),
+                               total_tokens=len(req.prompt) + len(req.output),
+                               finish_reason="stop" if req.finish_reason == "stop" else "length",
+                               cached_tokens=req.num_cached)
+        self.stats["completed"] += 1
+
+        def _set():
+            if not p.future.done():
+                p.future.set_result(res)
+            if p.stream_q is not None:
+                p.stream_q.put_nowait(None)
+        p.loop.call_soon_threadsafe(_set)
+
+    def _resolve_error(self, p: _Pending, e: Exception) -> None:
+        self.stats["errors"] += 1
+
+        def _set():
+            if not p.future.done():
+                p.future.set_exception(e)
+            if p.stream_q is not None:
+                p.stream_q.put_nowait(None)
+        p.loop.call_soon_threadsafe(_set)
+
+    def _submit(self, messages, cfg: GenerationConfig, stream: bool = False) -> _Pending:
+        if not self.loaded:
+            raise RuntimeError("model not loaded")
+        loop = asyncio.get_running_loop()
+        prompt = chat_prompt_ids(self.tokenizer, messages)
+        p = _Pending(loop, loop.create_future(), asyncio.Queue() if stream else None, cfg, len(prompt))
+        self.stats["requests"] += 1
+        self._inbox.put((prompt, p, cfg))
+        self._wake.set()
+        return p
+
+    # ------------------------------------------------------------------ LLMBaseEngine
+    async def generate_async(self, messages: List[Dict[str, str]],
+                             config: Optional[GenerationConfig] = None) -> GenerationResult:
+        p = self._submit(messages, config or GenerationConfig())
+        return await p.future
+
+    async def batch_generate(self, batch_messages: List[List[Dict[str, str]]],
+                             config: Optional[GenerationConfig] = None) -> List[GenerationResult]:
+        cfg = config or GenerationConfig()
+        ps = [self._submit(m, cfg) for m in batch_messages]
+        return list(await asyncio.gather(*[p.future for p in ps]))
+
+    async def stream_generate(self, messages: List[Dict[str, str]],
+                              config: Optional[GenerationConfig] = None) -> AsyncIterator[str]:
+        p = self._submit(messages, config or GenerationConfig(), stream=True)
+        toks: List[int] = []
+        prev = ""
+        while True:
+            t = await p.stream_q.get()
+            if t is None:
+                break
+            toks.append(t)
+            text = self.tokenizer.decode(toks, skip_special_tokens=True)
+            if len(text) > len(prev):
+                yield text[len(prev):]
+                prev = text
+        await p.future
+
+    def batch_inference(self, params_list: List[Dict[str, Any]]) -> List[Dict[str, Any]]:
+        try:
+            asyncio.get_running_loop()
+        except RuntimeError:
+            return asyncio.run(self.batch_inference_async(params_list))
+        return self._run_coroutine_in_new_thread(self.batch_inference_async(params_list))
+
+    def supports_streaming(self) -> bool:
+        return True
+
+    def supports_prefix_caching(self) -> bool:
+        return True
+
+    def supports_batch_inference(self) -> bool:
+        return True
+
+    def get_status(self) -> Dict[str, Any]:
+        s = super().get_status()
+        s["features"] = ["paged_attention", "radix_attention", "continuous_batching", "chunked_prefill",
+                         "streaming", "prefix_caching", "hipgraph_decode", "speculative_decoding"]
+        if self.engine is not None:
+            s["engine"] = {**self.engine.stats, **self.engine.scheduler.stats(),
+                           "model": self.engine.model_cfg.name, "num_blocks": self.engine.pool.num_blocks}
+        s["stats"] = dict(self.stats)
+        return s
+
+    def get_cache_stats(self) -> Dict[str, Any]:
+        if self.engine is None:
+            return {}
+        sch = self.engine.scheduler
+        return {"prefix_hit_rate": sch.radix.hit_rate() if sch.radix else 0.0,
+                "free_blocks": self.engine.pool.num_free, "used_blocks": self.engine.pool.num_used,
+                "evictions": self.engine.pool.stats["evictions"]}
+
+
+def _now() -> float:
+    return time.perf_counter()
