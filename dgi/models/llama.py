@@ -135,6 +135,27 @@ class LlamaModel:
                 self.lm_head.copy_(sd["lm_head.weight"])
         del c
 
+    def tensors(self):
+        """(name, tensor) pairs of every weight (lm_head omitted when tied)."""
+        for i, L in enumerate(self.layers):
+            for k in LlamaLayerWeights.__slots__:
+                yield f"layers.{self.layer_start + i}.{k}", getattr(L, k)
+        for k in ("embed", "norm"):
+            t = getattr(self, k)
+            if t is not None:
+                yield k, t
+        if self.lm_head is not None and self.lm_head is not self.embed:
+            yield "lm_head", self.lm_head
+
+    def copy_from(self, other: "LlamaModel") -> "LlamaModel":
+        """Copy weights of the overlapping layer range from another instance
+        (any device) — used to compare CPU / GPU / sharded models exactly."""
+        src = dict(other.tensors())
+        for name, t in self.tensors():
+            if name in src:
+                t.copy_(src[name])
+        return self
+
     def weight_bytes(self) -> int:
         n = 0
         for L in self.layers:

@@ -1,0 +1,88 @@
+"""Layer sharding and node layout planning.
+
+* ``get_layer_range_for_worker`` — even split, remainder to the first
+  workers (same outputs as reference worker/distributed/model_shard.py:372-394).
+* ``plan_layer_split`` — memory/FLOP-balanced split that gives the end stages
+  (embedding, LM head) fewer layers.
+* ``plan_node_layout`` — how N MI355X GPUs of one node are assigned to
+  prefill engines and the decode pipeline.  At 288 GB per GPU a full
+  Llama-3-70B (141 GB bf16) fits on one device, so prefill engines are
+  whole-model replicas and the decode side is a layer pipeline whose stages
+  each hold half (or less) of the layers and therefore several times more KV.
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Optional
+
+
+def get_layer_range_for_worker(total_layers: int, num_workers: int, worker_index: int) -> tuple[int, int]:
+    if num_workers <= 0 or not (0 <= worker_index < num_workers):
+        raise ValueError("invalid worker index")
+    base, rem = divmod(total_layers, num_workers)
+    start = worker_index * base + min(worker_index, rem)
+    end = start + base + (1 if worker_index < rem else 0)
+    return start, end
+
+
+def plan_layer_split(total_layers: int, stages: int, layer_cost: float = 1.0, embed_cost: float = 0.0,
+                     head_cost: float = 0.0) -> list[tuple[int, int]]:
+    """Split layers so that per-stage cost (layers * layer_cost + end extras) is balanced."""
+    if stages <= 1:
+        return [(0, total_layers)]
+    extras = [0.0] * stages
+    extras[0] += embed_cost
+    extras[-1] += head_cost
+    total = total_layers * layer_cost + sum(extras)
+    target = total / stages
+    bounds = []
+    start = 0
+    for s in range(stages):
+        left = stages - s - 1
+        if left == 0:
+            end = total_layers
+        else:
+            n = max(1, round((target - extras[s]) / layer_cost))
+            end = min(start + n, total_layers - left)
+        bounds.append((start, end))
+        start = end
+    return bounds
+
+
+@dataclasses.dataclass
+class NodeLayout:
+    kind: str                      # single | dp | pp | pd | pdpp
+    prefill_ranks: list
+    decode_ranks: list             # decode pipeline stages in order (len 1 = no PP)
+    replicas: int = 1
+
+    @property
+    def world(self) -> int:
+        return len(self.prefill_ranks) + len(self.decode_ranks)
+
+    def role(self, rank: int) -> str:
+        if rank in self.prefill_ranks:
+            return "prefill"
+        if self.decode_ranks and rank == self.decode_ranks[0]:
+            return "decode_driver"
+        return "decode_stage"
+
+
+def plan_node_layout(n_gpus: int, kind: str = "pdpp", prefill_ranks: Optional[int] = None,
+                     decode_stages: Optional[int] = None) -> NodeLayout:
+    """Default P:D split for prefill-heavy loads (512-in/128-out on 70B: a
+    prefill costs ~5x the decode-GPU time of its 128 tokens)."""
+    if n_gpus == 1 or kind == "single":
+        return NodeLayout("single", [], [0])
+    if kind == "pp":
+        return NodeLayout("pp", [], list(range(n_gpus)))
+    if kind == "dp":
+        return NodeLayout("dp", [], [0], replicas=n_gpus)
+    if decode_stages is None:
+        decode_stages = 2 if (kind == "pdpp" and n_gpus >= 4) else 1
+    if prefill_ranks is None:
+        prefill_ranks = n_gpus - decode_stages
+    prefill_ranks = max(1, min(prefill_ranks, n_gpus - decode_stages))
+    decode_stages = n_gpus - prefill_ranks
+    k = "pdpp" if decode_stages > 1 else "pd"
+    return NodeLayout(k, list(range(prefill_ranks)), list(range(prefill_ranks, n_gpus)))

@@ -62,8 +62,13 @@ class ModelRunner:
             self.graphs = GraphRunner(self, [b for b in graph_buckets if b <= max_num_seqs])
 
     # ------------------------------------------------------------------ metadata
-    def build(self, sb: ScheduledBatch, pad_decode_to: int = 0):
-        """Host-side metadata for one step (numpy) -> AttnMeta on device."""
+    # header layout (int64): the host-side shape of one step, shipped along
+    # the pipeline so every stage rebuilds the same AttnMeta
+    H_LEN, H_T, H_NDP, H_NPRE, H_NB, H_MAXW, H_SPLITS, H_PART, H_NTILES, H_NLOG, H_STEP = range(1, 12)
+    HEADER_SIZE = 16
+
+    def build_host(self, sb: ScheduledBatch, pad_decode_to: int = 0):
+        """Pack one step's metadata into a flat int32 array + int64 header."""
         bs = self.bs
         nd = len(sb.decode)
         ndp = max(nd, pad_decode_to)
@@ -111,36 +116,54 @@ class ModelRunner:
             for t0 in range(0, int(cu[j + 1] - cu[j]), 128):
                 tiles.append((j, t0))
         tiles_np = np.asarray(tiles, np.int32).reshape(-1, 2)
-        lidx = np.asarray(logit_rows, np.int64)
-        # ---- one pinned buffer, one H2D copy
-        parts = [ids, pos, slots, dec_bt.ravel(), dec_ctx, pre_bt.ravel(), cu, pctx, tiles_np.ravel()]
-        sizes = [a.size for a in parts]
-        flat = np.concatenate(parts) if parts else np.zeros(0, np.int32)
-        host = torch.from_numpy(flat)
-        lhost = torch.from_numpy(lidx)
-        if self.is_cuda:
-            host = host.pin_memory()
-            lhost = lhost.pin_memory()
-        dev = host.to(self.device, non_blocking=True)
-        ldev = lhost.to(self.device, non_blocking=True)
-        views = []
-        o = 0
-        for s in sizes:
-            views.append(dev[o: o + s])
-            o += s
-        d_ids, d_pos, d_slots, d_dbt, d_dctx, d_pbt, d_cu, d_pctx, d_tiles = views
+        nlog = len(logit_rows)
+        lidx = np.asarray(logit_rows, np.int32)
+        temps = np.asarray([r.params.temperature for r in sampled], np.float32).view(np.int32)
+        seeds = np.asarray([(r.seed * 1000003 + self.step_id) & 0x7FFFFFFF for r in sampled], np.int32)
+        parts = [ids, pos, slots, dec_bt.ravel(), dec_ctx, pre_bt.ravel(), cu, pctx, tiles_np.ravel(), lidx,
+                 temps, seeds]
+        flat = np.concatenate(parts)
         max_ctx = int(dec_ctx.max()) if ndp else 1
         if self.is_cuda and ndp:
             splits, part = ops.decode_split_plan(ndp, max_ctx, self.model.cfg.num_kv_heads, self.num_cus)
         else:
             splits, part = 1, 1 << 20
+        hdr = np.zeros(self.HEADER_SIZE, np.int64)
+        hdr[[self.H_LEN, self.H_T, self.H_NDP, self.H_NPRE, self.H_NB, self.H_MAXW, self.H_SPLITS, self.H_PART,
+             self.H_NTILES, self.H_NLOG, self.H_STEP]] = [flat.size, T, ndp, npre, nb, maxw, splits, part,
+                                                          len(tiles), nlog, self.step_id]
+        return flat, hdr, sampled
+
+    def meta_from_device(self, dev: torch.Tensor, hdr):
+        """Views of the device copy of ``flat`` -> (input ids, AttnMeta, temps, seeds)."""
+        h = [int(x) for x in hdr]
+        T, ndp, npre, nb, maxw = h[self.H_T], h[self.H_NDP], h[self.H_NPRE], h[self.H_NB], h[self.H_MAXW]
+        ntiles, nlog = h[self.H_NTILES], h[self.H_NLOG]
+        sizes = [T, T, T, ndp * maxw, ndp, nb * maxw, nb + 1, nb, ntiles * 2, nlog, nlog, nlog]
+        views = []
+        o = 0
+        for sz in sizes:
+            views.append(dev[o: o + sz])
+            o += sz
+        d_ids, d_pos, d_slots, d_dbt, d_dctx, d_pbt, d_cu, d_pctx, d_tiles, d_lidx, d_temps, d_seeds = views
         meta = AttnMeta(
             positions=d_pos, slot_mapping=d_slots, num_decode=ndp,
             dec_block_tables=d_dbt.view(ndp, maxw), dec_context_lens=d_dctx,
-            dec_max_splits=splits, dec_part_size=part, dec_workspace=self.dec_ws,
+            dec_max_splits=h[self.H_SPLITS], dec_part_size=h[self.H_PART], dec_workspace=self.dec_ws,
             num_prefill_tokens=npre, pre_block_tables=d_pbt.view(nb, maxw), pre_cu_seqlens=d_cu,
-            pre_context_lens=d_pctx, pre_tiles=d_tiles.view(-1, 2), logits_indices=ldev)
-        return d_ids, meta, sampled
+            pre_context_lens=d_pctx, pre_tiles=d_tiles.view(-1, 2), logits_indices=d_lidx)
+        return d_ids, meta, d_temps.view(torch.float32), d_seeds.long()
+
+    def to_device(self, flat: np.ndarray) -> torch.Tensor:
+        host = torch.from_numpy(flat)
+        if self.is_cuda:
+            host = host.pin_memory()
+        return host.to(self.device, non_blocking=True)
+
+    def build(self, sb: ScheduledBatch, pad_decode_to: int = 0):
+        flat, hdr, sampled = self.build_host(sb, pad_decode_to)
+        ids, meta, _t, _s = self.meta_from_device(self.to_device(flat), hdr)
+        return ids, meta, sampled
 
     # ------------------------------------------------------------------ run
     def sampling_tensors(self, reqs):
@@ -150,6 +173,11 @@ class ModelRunner:
             temps = temps.pin_memory().to(self.device, non_blocking=True)
             seeds = seeds.pin_memory().to(self.device, non_blocking=True)
         return temps, seeds
+
+    def sample_rows(self, logits, temps, seeds, filt=None):
+        if filt is not None:
+            logits = ops.apply_top_k_top_p(logits, *filt)
+        return ops.sample(logits, temps, seeds, 0)
 
     def _sample(self, logits, reqs):
         temps, seeds = self.sampling_tensors(reqs)
@@ -166,12 +194,21 @@ class ModelRunner:
                 len(sb.decode) <= self.graphs.max_bucket and not any(r.params.needs_filter for r in sb.decode):
             toks = self.graphs.run(sb)
             return StepResult(toks, list(sb.decode))
-        ids, meta, sampled = self.build(sb)
+        flat, hdr, sampled = self.build_host(sb)
+        ids, meta, temps, seeds = self.meta_from_device(self.to_device(flat), hdr)
         logits = self.model.forward(meta, input_ids=ids)
         if not sampled:
             return StepResult([], [])
-        toks = self._sample(logits, sampled)
+        filt = None
+        if any(r.params.needs_filter for r in sampled):
+            filt = self.filter_tensors(sampled)
+        toks = self.sample_rows(logits, temps, seeds, filt)
         return StepResult(toks.tolist(), sampled)
+
+    def filter_tensors(self, reqs):
+        tk = torch.tensor([r.params.top_k if not r.params.greedy else 0 for r in reqs], device=self.device)
+        tp = torch.tensor([r.params.top_p if not r.params.greedy else 1.0 for r in reqs], device=self.device)
+        return tk, tp
 
 
 class GraphRunner:

@@ -124,13 +124,28 @@ class Scheduler:
         self.waiting.appendleft(victim)
 
     # ------------------------------------------------------------------ schedule
-    def schedule(self) -> ScheduledBatch:
-        budget = self.cfg.max_num_batched_tokens
+    def add_prefilled(self, req: Request, blocks: list[int]) -> None:
+        """Adopt a sequence prefilled elsewhere (P/D migration): its KV already
+        sits in ``blocks`` and its first token is in ``req.output``."""
+        req.blocks = list(blocks)
+        req.num_computed = req.total_len - 1
+        req.prefill_target = req.num_computed
+        req.status = Status.RUNNING
+        self.running.append(req)
+
+    def schedule(self, max_seqs: Optional[int] = None, max_tokens: Optional[int] = None,
+                 allow_prefill: bool = True) -> ScheduledBatch:
+        """Form one batch.  ``max_seqs``/``max_tokens`` bound a pipeline
+        microbatch; requests already in flight (``busy``) are skipped."""
+        budget = self.cfg.max_num_batched_tokens if max_tokens is None else max_tokens
+        seq_cap = max_seqs if max_seqs is not None else 1 << 30
         decode: list[Request] = []
         preempted: list[Request] = []
         # 1) decode rows
         for req in list(self.running):
-            if req.in_prefill or req not in self.running:
+            if len(decode) >= seq_cap or budget <= 0:
+                break
+            if req.busy or req.in_prefill or req not in self.running:
                 continue
             pos = req.num_computed  # position of the token being fed (== total_len - 1)
             while True:
@@ -138,20 +153,26 @@ class Scheduler:
                     self._grow(req, pos + 1)
                     break
                 except OutOfBlocks:
-                    victim = self.running[-1]
+                    victim = next((r for r in reversed(self.running) if not r.busy), None)
+                    if victim is None:
+                        break
                     self._preempt(victim)
                     preempted.append(victim)
                     if victim is req:
                         break
-            if req.status is Status.RUNNING and req in self.running:
+            if req.status is Status.RUNNING and req in self.running and \
+                    len(req.blocks) * self.bs > pos:
                 decode.append(req)
                 budget -= 1
         # 2) prefill chunks: running (partial) first, then waiting
         prefill: list[PrefillChunk] = []
+        n_seqs = len(decode)
+        if not allow_prefill:
+            return ScheduledBatch(decode, prefill, preempted)
         for req in self.running:
-            if budget <= 0:
+            if budget <= 0 or n_seqs >= seq_cap:
                 break
-            if not req.in_prefill:
+            if req.busy or not req.in_prefill:
                 continue
             n = min(req.prefill_target - req.num_computed, budget)
             try:
@@ -160,7 +181,8 @@ class Scheduler:
                 break
             prefill.append(PrefillChunk(req, req.num_computed, n, req.num_computed + n == req.prefill_target))
             budget -= n
-        while self.waiting and budget > 0 and len(self.running) < self.cfg.max_num_seqs:
+            n_seqs += 1
+        while self.waiting and budget > 0 and len(self.running) < self.cfg.max_num_seqs and n_seqs < seq_cap:
             req = self.waiting[0]
             toks = req.all_tokens()
             target = req.prefill_target
@@ -193,6 +215,7 @@ class Scheduler:
             self.running.append(req)
             prefill.append(PrefillChunk(req, start, n, start + n == target))
             budget -= n
+            n_seqs += 1
         return ScheduledBatch(decode, prefill, preempted)
 
     # ------------------------------------------------------------------ update
