@@ -77,7 +77,10 @@ class LLMEngine:
         if cfg.num_blocks is not None:
             nblocks = cfg.num_blocks
         else:
-            budget = max(0, _device_free_bytes(self.device) - cfg.workspace_bytes) * cfg.kv_fraction
+            if self.device.type == "cuda":
+                budget = max(0, _device_free_bytes(self.device) - cfg.workspace_bytes) * cfg.kv_fraction
+            else:
+                budget = 1 << 30  # CPU rehearsal runs: a fixed 1 GiB pool
             nblocks = num_blocks_for_budget(int(budget), max(1, n_local), mc.num_kv_heads, mc.head_dim,
                                             cfg.block_size)
             # never more than what max_num_seqs full-length sequences can use (+ prefix cache room)
@@ -119,6 +122,12 @@ class LLMEngine:
         if sb.empty:
             return []
         res = self.runner.execute(sb)
+        outs = self._apply(sb, res.rows, res.tokens)
+        self.stats["step_time"] += time.perf_counter() - t0
+        return outs
+
+    def _apply(self, sb, rows, tokens) -> list[StepOutput]:
+        """Commit one executed batch: advance KV cursors, append tokens, stop checks."""
         now = time.perf_counter()
         st = self.stats
         st["steps"] += 1
@@ -129,7 +138,7 @@ class LLMEngine:
         for r in sb.decode:
             r.num_computed += 1
         outs = []
-        for req, tok in zip(res.rows, res.tokens):
+        for req, tok in zip(rows, tokens):
             req.output.append(int(tok))
             req.token_times.append(now)
             if req.first_token_time is None:
@@ -141,7 +150,6 @@ class LLMEngine:
                 st["finished"] += 1
                 self.requests.pop(req.rid, None)
             outs.append(StepOutput(req.rid, int(tok), reason is not None, reason, req))
-        st["step_time"] += time.perf_counter() - t0
         return outs
 
     def _check_stop(self, req: Request, tok: int) -> Optional[str]:

@@ -1,0 +1,213 @@
+"""Distributed (N > 1) serving benchmark bodies used by the top-level bench.py.
+
+Layouts (dgi.parallel.plan):
+  pp    one S-stage layer pipeline over all N GPUs (rank 0 drives)
+  pd    P prefill ranks + 1 decode rank (KV over RCCL)
+  pdpp  P prefill ranks + a decode layer pipeline (KV over RCCL, then
+        layer-sliced down the pipeline)  — the BASELINE north-star layout
+
+The decode driver is the clock: its steps are the benchmark steps.  Phase
+boundaries (end of warmup, end of timed window) are broadcast to prefill
+ranks over the control store and to pipeline stages as PAUSE messages, then
+every rank meets in a barrier, so the timed window is [barrier, barrier] on
+all ranks; tokens are summed over ranks and the elapsed time is the max.
+"""
+from __future__ import annotations
+
+import random
+import time
+
+import torch
+
+from dgi.engine import EngineConfig
+from dgi.parallel.fabric import Fabric
+from dgi.parallel.plan import plan_node_layout
+from dgi.sched.request import SamplingParams
+
+MSG_PHASE = 9
+
+
+def _prompt(rng, n, vocab):
+    lo = min(1000, vocab // 4)
+    return [rng.randrange(lo, vocab - lo) for _ in range(n)]
+
+
+def run_distributed(args, layout_kind: str, dist):
+    f = Fabric()
+    rank, world = f.rank, f.world
+    layout = plan_node_layout(world, layout_kind, getattr(args, "prefill_ranks", None) or None)
+    conc = args.concurrency or 512
+    cfg = EngineConfig(model=args.model, device=str(f.device), max_num_seqs=conc,
+                       max_num_batched_tokens=args.max_batched_tokens,
+                       max_model_len=max(2048, args.prompt_len + args.output_len + 64),
+                       use_graphs=not args.no_graphs, seed=args.seed, enable_prefix_caching=False)
+    sp = SamplingParams(max_tokens=args.output_len, temperature=0.0, ignore_eos=True)
+    rng = random.Random(777 + rank)
+    role = layout.role(rank)
+    if layout.kind == "pp":
+        res = _run_pp(args, f, cfg, layout, role, sp, rng, conc)
+    else:
+        res = _run_pd(args, f, cfg, layout, role, sp, rng, conc)
+    tokens, elapsed, ttfts, extra = res
+    t = torch.tensor([tokens, elapsed], dtype=torch.float64, device=f.device)
+    tl = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(tl, t)
+    obj = [None] * world
+    dist.all_gather_object(obj, {"ttfts": ttfts, "role": role, **extra})
+    total = int(sum(x[0].item() for x in tl))
+    el = max(x[1].item() for x in tl)
+    all_ttfts = [v for o in obj for v in o["ttfts"]]
+    per_rank = [{k: v for k, v in o.items() if k != "ttfts"} for o in obj]
+    return total, el, all_ttfts, {"layout": {"kind": layout.kind, "prefill": layout.prefill_ranks,
+                                             "decode": layout.decode_ranks}, "ranks": per_rank}
+
+
+# ---------------------------------------------------------------------------- layer pipeline only
+
+def _run_pp(args, f, cfg, layout, role, sp, rng, conc):
+    from dgi.parallel.pipeline import PipelineEngine, StageWorker
+    ranks = layout.decode_ranks
+    if role == "decode_driver":
+        eng = PipelineEngine(cfg, f, ranks)
+        vocab = eng.model_cfg.vocab_size
+        inflight = set()
+
+        def top(limit):
+            while len(inflight) < limit:
+                inflight.add(eng.add_request(_prompt(rng, args.prompt_len, vocab), sp).rid)
+
+        def step():
+            n, firsts = 0, []
+            for o in eng.step():
+                n += 1
+                if len(o.request.output) == 1:
+                    firsts.append(o.request.ttft)
+                if o.finished:
+                    inflight.discard(o.rid)
+            return n, firsts
+
+        ramp = args.ramp_steps if args.ramp_steps >= 0 else args.output_len
+        per = max(1, -(-conc // max(1, ramp)))
+        for i in range(ramp):
+            top(min(conc, (i + 1) * per))
+            step()
+        for _ in range(args.warmup):
+            top(conc)
+            step()
+        eng.pause_stages()
+        torch.cuda.synchronize() if f.on_gpu else None
+        f.barrier()
+        t0 = time.perf_counter()
+        toks, ttfts = 0, []
+        for _ in range(args.steps):
+            top(conc)
+            n, fs = step()
+            toks += n
+            ttfts += fs
+        for o in eng.drain():
+            toks += 1
+        eng.pause_stages()
+        torch.cuda.synchronize() if f.on_gpu else None
+        f.barrier()
+        el = time.perf_counter() - t0
+        eng.stop_stages()
+        return toks, el, ttfts, {"steps": eng.stats["steps"]}
+    w = StageWorker(cfg, f, ranks)
+    w.run()
+    f.barrier()
+    t0 = time.perf_counter()
+    w.run()
+    torch.cuda.synchronize() if f.on_gpu else None
+    f.barrier()
+    el = time.perf_counter() - t0
+    w.run()
+    return 0, el, [], {"stage_steps": w.steps}
+
+
+# ---------------------------------------------------------------------------- P/D (+ decode pipeline)
+
+def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
+    from dgi.parallel.fabric import CtrlChannel
+    from dgi.parallel.pd import DecodeDriver, PrefillServer
+    from dgi.parallel.pipeline import StageWorker
+
+    if role == "prefill":
+        pcfg = EngineConfig(**{**cfg.__dict__, "max_num_seqs": 64})
+        srv = PrefillServer(pcfg, f, layout)
+        phase = CtrlChannel(f, layout.decode_ranks[0], 4, tag="phase")
+        vocab = srv.engine.model_cfg.vocab_size
+        depth = max(2, args.max_batched_tokens // max(1, args.prompt_len))
+
+        def serve_until_phase():
+            n, ttfts = 0, []
+            while phase.poll() is None:
+                while len(srv.pending) + len(srv.engine.scheduler.waiting) < depth:
+                    srv.submit(_prompt(rng, args.prompt_len, vocab), sp)
+                before = len(srv.ttfts)
+                n += len(srv.step())
+                ttfts += srv.ttfts[before:]
+            return n, ttfts
+
+        serve_until_phase()
+        f.barrier()
+        t0 = time.perf_counter()
+        n, ttfts = serve_until_phase()
+        torch.cuda.synchronize() if f.on_gpu else None
+        f.barrier()
+        el = time.perf_counter() - t0
+        srv.finish()
+        return n, el, ttfts, {"migrated": srv.migrated, "migrate_s": round(srv.migrate_time, 3)}
+
+    if role == "decode_driver":
+        drv = DecodeDriver(cfg, f, layout)
+        phases = [CtrlChannel(f, p, 4, tag="phase") for p in layout.prefill_ranks]
+
+        def run_steps(k):
+            """k productive decode steps (idle polling while nothing has arrived does not count)."""
+            n = done = 0
+            while done < k:
+                if not drv.engine.has_unfinished():
+                    drv.poll()
+                    if not drv.engine.has_unfinished():
+                        time.sleep(0.0005)
+                        continue
+                n += len(drv.step())
+                done += 1
+            return n
+
+        ramp = args.ramp_steps if args.ramp_steps >= 0 else 2 * args.output_len
+        run_steps(ramp + args.warmup)
+
+        def boundary():
+            for ph in phases:
+                ph.send([MSG_PHASE])
+            if hasattr(drv.engine, "pause_stages"):
+                drv.engine.pause_stages()
+            torch.cuda.synchronize() if f.on_gpu else None
+            f.barrier()
+
+        boundary()
+        t0 = time.perf_counter()
+        n = run_steps(args.steps)
+        boundary()
+        el = time.perf_counter() - t0
+        running = len(drv.engine.scheduler.running)
+        # receive migrations still in flight so every prefill send completes
+        while not drv.all_prefill_done():
+            drv.poll()
+            time.sleep(0.001)
+        drv.finish()
+        return n, el, [], {"received": drv.received, "running_at_end": running,
+                           "recv_GB": round(drv.recv_bytes / 1e9, 3)}
+
+    # later decode pipeline stages
+    w = StageWorker(cfg, f, layout.decode_ranks)
+    w.run()
+    f.barrier()
+    t0 = time.perf_counter()
+    w.run()
+    torch.cuda.synchronize() if f.on_gpu else None
+    f.barrier()
+    el = time.perf_counter() - t0
+    w.run()
+    return 0, el, [], {"stage_steps": w.steps}

@@ -42,7 +42,9 @@ class Fabric:
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if self.on_gpu else torch.device("cpu")
         self.device = device
-        self.ctrl = dist.new_group(backend="gloo") if self.on_gpu else None
+        # control traffic gets its own gloo group so it never queues behind (or
+        # forms a dependency cycle with) data transfers on the RCCL pair channel
+        self.ctrl = dist.new_group(backend="gloo")
         self.comm_stream = torch.cuda.Stream(device=device) if self.on_gpu else None
         self._pending: list = []
 
@@ -57,7 +59,8 @@ class Fabric:
             self._pending.append((w, t))
             self._reap()
         else:
-            dist.send(t, dst)
+            self._pending.append((dist.isend(t, dst), t))
+            self._reap()
 
     def recv(self, t: torch.Tensor, src: int) -> torch.Tensor:
         """Blocking (stream-ordered on GPU) receive into ``t``."""
@@ -85,6 +88,15 @@ class Fabric:
         self._pending.append((w, t))
         return w
 
+    def ctrl_send_tensor(self, t: torch.Tensor, dst: int) -> None:
+        """Non-blocking host tensor send on the control group."""
+        t = t.detach().cpu().contiguous()
+        self._pending.append((dist.isend(t, dst, group=self.ctrl), t))
+
+    def ctrl_recv_tensor(self, t: torch.Tensor, src: int) -> torch.Tensor:
+        dist.recv(t, src, group=self.ctrl)
+        return t
+
     def ctrl_irecv(self, size: int, src: int):
         t = torch.zeros(size, dtype=torch.int64)
         w = dist.irecv(t, src, group=self.ctrl)
@@ -100,33 +112,49 @@ class Fabric:
 
 
 class CtrlChannel:
-    """Pollable fixed-size int64 control messages from one peer."""
+    """Pollable fixed-size int64 control messages to/from one peer.
 
-    def __init__(self, fabric: Fabric, peer: int, size: int = 32):
+    Carried by the c10d rendezvous store (TCPStore): a gloo ``irecv`` cannot
+    be polled (its completion is only observed by ``wait``), while a store
+    key can be checked without blocking.  Messages are sequence-numbered per
+    direction and deleted once read.  Used for P/D admission headers,
+    credits and end-of-stream markers — a few small messages per step.
+    """
+
+    def __init__(self, fabric: Fabric, peer: int, size: int = 32, tag: str = "ctrl"):
+        from torch.distributed import distributed_c10d as c10d
         self.f = fabric
         self.peer = peer
         self.size = size
-        self._post()
+        self.store = c10d._get_default_store()
+        self.me = fabric.rank
+        self.tag = tag
+        self.sseq = 0
+        self.rseq = 0
 
-    def _post(self):
-        self.work, self.buf = self.f.ctrl_irecv(self.size, self.peer)
-
-    def poll(self) -> Optional[np.ndarray]:
-        if self.work.is_completed():
-            self.work.wait()
-            msg = self.buf.numpy().copy()
-            self._post()
-            return msg
-        return None
-
-    def wait(self) -> np.ndarray:
-        self.work.wait()
-        msg = self.buf.numpy().copy()
-        self._post()
-        return msg
+    def _key(self, src: int, dst: int, seq: int) -> str:
+        return f"dgi/{self.tag}/{src}->{dst}/{seq}"
 
     def send(self, arr) -> None:
         a = np.zeros(self.size, np.int64)
         v = np.asarray(arr, np.int64).ravel()
         a[: v.size] = v
-        self.f.ctrl_isend(a, self.peer)
+        self.store.set(self._key(self.me, self.peer, self.sseq), a.tobytes())
+        self.sseq += 1
+
+    def poll(self) -> Optional[np.ndarray]:
+        k = self._key(self.peer, self.me, self.rseq)
+        if not self.store.check([k]):
+            return None
+        return self._take(k)
+
+    def wait(self) -> np.ndarray:
+        k = self._key(self.peer, self.me, self.rseq)
+        self.store.wait([k])
+        return self._take(k)
+
+    def _take(self, k: str) -> np.ndarray:
+        v = self.store.get(k)
+        self.store.delete_key(k)
+        self.rseq += 1
+        return np.frombuffer(v, dtype=np.int64).copy()

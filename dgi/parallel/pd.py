@@ -1,0 +1,270 @@
+"""Prefill/decode disaggregation inside one MI355X node (DistServe style).
+
+The reference's P/D path is an in-memory scheduler whose KV migration is
+``asyncio.sleep(0.05)`` (server/app/services/pd_scheduler.py:404-479,
+SURVEY §3.5).  Here:
+
+* **Prefill ranks** (``PrefillServer``) run a prefill-only engine: full
+  model per GPU (Llama-3-70B bf16 fits in 288 GB), radix prefix cache,
+  batched/chunked prefill.  When a prompt completes, its first token is
+  sampled locally, its KV pages are packed with the ``kv_gather`` HIP kernel
+  (all layers, one contiguous buffer) and sent to the decode driver with an
+  RCCL send over xGMI; the local pages go back to the prefix cache.
+* **Decode driver** (``DecodeDriver``) owns the decode engine — a single GPU
+  or stage 0 of a decode layer pipeline (``pdpp``).  It receives the
+  buffer, scatters its own layers' pages into freshly allocated blocks
+  (``kv_scatter``) and forwards the remaining layers to the later pipeline
+  stages as KV-install messages on the pipeline channel; the request then
+  joins the next decode iteration.
+* **Flow control**: the decode driver grants block *credits* to each prefill
+  rank (gloo control group); a prefill rank admits a prompt only when it
+  holds credit for the whole sequence (prompt + max_tokens), and credits
+  flow back when sequences finish, so the decode pool can never run out
+  and nothing is ever preempted on the decode side.
+
+Control messages (int64[CTRL]) on the gloo group:
+  MIGRATE n_reqs total_blocks meta_len tok_len | CREDIT blocks | DONE
+"""
+from __future__ import annotations
+
+import collections
+import time
+from typing import Optional
+
+import numpy as np
+import torch
+
+from dgi import ops
+from dgi.engine import EngineConfig, LLMEngine, StepOutput
+from dgi.models.config import get_config
+from dgi.parallel.fabric import CtrlChannel, Fabric
+from dgi.parallel.pipeline import PipelineEngine
+from dgi.parallel.plan import NodeLayout
+from dgi.sched.request import Request, SamplingParams, Status
+
+MSG_MIGRATE, MSG_CREDIT, MSG_DONE = 1, 2, 3
+CTRL = 8
+META_FIELDS = 11
+
+
+def _blocks_for(n_tokens: int, bs: int) -> int:
+    return (n_tokens + bs - 1) // bs
+
+
+def _req_meta(r: Request, nblocks: int) -> list:
+    p = r.params
+    return [int(r.rid) & 0x7FFFFFFF, 0, len(r.prompt), r.output[0], nblocks, p.max_tokens,
+            int(np.float32(p.temperature).view(np.int32)), int(r.seed) & 0x7FFFFFFF, int(p.ignore_eos), p.top_k,
+            int(np.float32(p.top_p).view(np.int32))]
+
+
+class PrefillServer:
+    """One prefill rank."""
+
+    def __init__(self, cfg: EngineConfig, fabric: Fabric, layout: NodeLayout, seed_offset: int = 0):
+        self.f = fabric
+        self.layout = layout
+        self.driver = layout.decode_ranks[0]
+        pcfg = EngineConfig(**{**cfg.__dict__, "device": str(fabric.device), "use_graphs": False})
+        self.engine = LLMEngine(pcfg)
+        self.bs = self.engine.pool.block_size
+        self.ch = CtrlChannel(fabric, self.driver, CTRL)
+        msg = self.ch.wait()  # initial credit grant
+        assert msg[0] == MSG_CREDIT
+        self.credit = int(msg[1])
+        self.seq_credit = int(msg[2])
+        self.pending: collections.deque = collections.deque()
+        self.migrated = 0
+        self.migrate_time = 0.0
+        self.first_tokens = 0
+        self.ttfts: list = []
+
+    # ------------------------------------------------------------------ API
+    def submit(self, prompt: list, params: SamplingParams) -> Request:
+        r = Request(prompt, params)
+        self.pending.append(r)
+        return r
+
+    def busy(self) -> bool:
+        return bool(self.pending) or self.engine.has_unfinished()
+
+    def _poll_credit(self) -> None:
+        while True:
+            m = self.ch.poll()
+            if m is None:
+                break
+            if m[0] == MSG_CREDIT:
+                self.credit += int(m[1])
+                self.seq_credit += int(m[2])
+
+    def _admit(self) -> None:
+        while self.pending:
+            r = self.pending[0]
+            need = _blocks_for(len(r.prompt) + r.params.max_tokens, self.bs)
+            if need > self.credit or self.seq_credit <= 0:
+                break
+            self.credit -= need
+            self.seq_credit -= 1
+            self.pending.popleft()
+            r.spec_state = need  # credit reserved for this sequence
+            self.engine.scheduler.add(r)
+            self.engine.requests[r.rid] = r
+
+    def step(self) -> list[StepOutput]:
+        self._poll_credit()
+        self._admit()
+        if not self.engine.has_unfinished():
+            return []
+        outs = self.engine.step()
+        ready = []
+        for o in outs:
+            self.first_tokens += 1
+            if o.request.ttft is not None:
+                self.ttfts.append(o.request.ttft)
+            if o.finished:  # max_tokens == 1 or EOS at the first token
+                self.credit += int(o.request.spec_state or 0)
+                self.seq_credit += 1
+            else:
+                ready.append(o.request)
+        if ready:
+            self._migrate(ready)
+        return outs
+
+    def _migrate(self, reqs: list) -> None:
+        t0 = time.perf_counter()
+        eng = self.engine
+        dev = self.f.device
+        ids, meta, toks = [], [], []
+        for r in reqs:
+            nb = _blocks_for(r.num_computed, self.bs)
+            ids += r.blocks[:nb]
+            meta += _req_meta(r, nb) + [int(r.spec_state or 0)]
+            toks += r.prompt
+        ids_t = torch.tensor(ids, dtype=torch.int32, device=dev)
+        buf = ops.kv_gather(eng.pool.kv, ids_t)
+        meta_t = torch.tensor(meta, dtype=torch.int32, device=dev)
+        toks_t = torch.tensor(toks, dtype=torch.int32, device=dev)
+        self.ch.send([MSG_MIGRATE, len(reqs), len(ids), meta_t.numel(), toks_t.numel()])
+        self.f.send(meta_t, self.driver)
+        self.f.send(toks_t, self.driver)
+        self.f.send(buf, self.driver)
+        for r in reqs:
+            eng.scheduler.finish(r, "migrated")
+            eng.requests.pop(r.rid, None)
+        self.migrated += len(reqs)
+        self.migrate_time += time.perf_counter() - t0
+
+    def finish(self) -> None:
+        """End of stream: the decode driver keeps receiving until it sees DONE."""
+        self.ch.send([MSG_DONE])
+        self.f.flush()
+
+
+class DecodeDriver:
+    """Decode side: single engine or stage 0 of the decode pipeline."""
+
+    def __init__(self, cfg: EngineConfig, fabric: Fabric, layout: NodeLayout, credit_margin: float = 0.02):
+        self.f = fabric
+        self.layout = layout
+        dcfg = EngineConfig(**{**cfg.__dict__, "device": str(fabric.device), "enable_prefix_caching": False})
+        if len(layout.decode_ranks) > 1:
+            self.engine = PipelineEngine(dcfg, fabric, layout.decode_ranks)
+            self.L_local = self.engine.model.num_local_layers
+        else:
+            self.engine = LLMEngine(dcfg)
+            self.L_local = self.engine.model.num_local_layers
+        mc = self.engine.model_cfg
+        self.mc = mc
+        self.bs = self.engine.pool.block_size
+        self.prefill = list(layout.prefill_ranks)
+        self.chans = {p: CtrlChannel(fabric, p, CTRL) for p in self.prefill}
+        total = int(self.engine.pool.num_free * (1.0 - credit_margin))
+        P = max(1, len(self.prefill))
+        share = total // P
+        seq_share = max(1, cfg.max_num_seqs // P)
+        for p in self.prefill:
+            self.chans[p].send([MSG_CREDIT, share, seq_share])
+        self.origin: dict = {}
+        self.refund = collections.Counter()
+        self.refund_seqs = collections.Counter()
+        self.done = set()
+        self.received = 0
+        self.recv_bytes = 0
+
+    def _recv_migration(self, p: int, msg) -> None:
+        n_reqs, nblk, meta_len, tok_len = (int(x) for x in msg[1:5])
+        dev = self.f.device
+        meta_t = torch.empty(meta_len, dtype=torch.int32, device=dev)
+        toks_t = torch.empty(tok_len, dtype=torch.int32, device=dev)
+        self.f.recv(meta_t, p)
+        self.f.recv(toks_t, p)
+        mc = self.mc
+        L = mc.num_layers
+        buf = torch.empty(L, 2, nblk, mc.num_kv_heads, self.bs, mc.head_dim, dtype=self.engine.pool.dtype, device=dev)
+        self.f.recv(buf, p)
+        self.recv_bytes += buf.numel() * buf.element_size()
+        sch = self.engine.scheduler
+        ids = self.engine.pool.allocate(nblk)
+        ids_t = torch.tensor(ids, dtype=torch.int32, device=dev)
+        ops.kv_scatter(self.engine.pool.kv, ids_t, buf[: self.L_local].contiguous())
+        if isinstance(self.engine, PipelineEngine) and L > self.L_local:
+            self.engine.send_kv_install(ids_t, buf[self.L_local:])
+        meta = meta_t.view(n_reqs, META_FIELDS + 1).tolist()
+        toks = toks_t.tolist()
+        o = k = 0
+        for m in meta:
+            rid, _, plen, first, nb, max_tok, tbits, seed, ign, topk, pbits, credit = m
+            temp = float(np.int32(tbits).view(np.float32))
+            top_p = float(np.int32(pbits).view(np.float32))
+            sp = SamplingParams(max_tokens=max_tok, temperature=temp, top_p=top_p, top_k=topk,
+                                ignore_eos=bool(ign), seed=seed)
+            r = Request(toks[o:o + plen], sp)
+            r.seed = seed
+            r.output = [first]
+            r.first_token_time = time.perf_counter()
+            o += plen
+            sch.add_prefilled(r, ids[k:k + nb])
+            self.engine.requests[r.rid] = r
+            self.origin[r.rid] = (p, credit)
+            k += nb
+        self.received += n_reqs
+
+    def poll(self) -> None:
+        for p, ch in self.chans.items():
+            while True:
+                m = ch.poll()
+                if m is None:
+                    break
+                if m[0] == MSG_MIGRATE:
+                    self._recv_migration(p, m)
+                elif m[0] == MSG_DONE:
+                    self.done.add(p)
+
+    def step(self) -> list[StepOutput]:
+        self.poll()
+        outs = self.engine.step() if self.engine.has_unfinished() else []
+        for o in outs:
+            if o.finished:
+                p, credit = self.origin.pop(o.rid, (None, 0))
+                if p is not None:
+                    self.refund[p] += credit
+                    self.refund_seqs[p] += 1
+        for p in list(self.refund_seqs):
+            self.chans[p].send([MSG_CREDIT, self.refund[p], self.refund_seqs[p]])
+        self.refund.clear()
+        self.refund_seqs.clear()
+        return outs
+
+    def all_prefill_done(self) -> bool:
+        return len(self.done) == len(self.prefill)
+
+    def finish(self) -> None:
+        if isinstance(self.engine, PipelineEngine):
+            self.engine.stop_stages()
+        self.f.flush()
+
+
+def build_engine_config(model: str, **kw) -> EngineConfig:
+    mc = get_config(model)
+    del mc
+    return EngineConfig(model=model, **kw)

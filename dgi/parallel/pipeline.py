@@ -1,0 +1,277 @@
+"""In-node layer pipeline over RCCL p2p (SURVEY §2.10 "Pipeline parallelism").
+
+The reference chains stages with sequential HTTP/JSON hops, keeps no KV on
+the shards and has one stage busy at a time (worker/distributed/session.py:
+271-337, grpc_server.py:351-388).  Here S stages on S GPUs form an ordered
+RCCL channel ring:
+
+    driver (stage 0, scheduler + block tables + layers [0, l1))
+      --[header | step metadata | hidden]--> stage 1 --> ... --> stage S-1
+      <--------------------- sampled token ids ------------------------'
+
+* every stage keeps the paged KV of its own layers; block ids are chosen by
+  the driver's scheduler and are valid in every stage's pool (all pools have
+  the same block count, agreed at start-up);
+* up to S microbatches (disjoint request sets) are in flight, so all GPUs
+  work concurrently (``busy`` requests are skipped by the scheduler);
+* activations travel as ONE bf16 residual-stream tensor [T, H] per hop
+  (8192 * 2 B = 16 KiB per token on 70B);
+* the same channel carries KV-install messages (P/D migration into a decode
+  pipeline) and PAUSE/STOP control, so ordering is never ambiguous.
+"""
+from __future__ import annotations
+
+import collections
+import time
+from typing import Optional
+
+import numpy as np
+import torch
+
+from dgi.engine import EngineConfig, LLMEngine, StepOutput
+from dgi.models.config import ModelConfig, get_config
+from dgi.models.llama import LlamaModel
+from dgi.kv.block_pool import BlockPool, num_blocks_for_budget
+from dgi.parallel.fabric import Fabric
+from dgi.parallel.plan import plan_layer_split
+from dgi.runtime.model_runner import ModelRunner
+
+KIND_STOP, KIND_FWD, KIND_KV, KIND_PAUSE = 0, 1, 2, 3
+HDR = ModelRunner.HEADER_SIZE
+
+
+def stage_split(mc: ModelConfig, stages: int) -> list[tuple[int, int]]:
+    # embedding gather is cheap; the LM head GEMM is ~1.9 layers of 70B decode weight traffic
+    head = (mc.vocab_size * mc.hidden_size) / max(1, (mc.qkv_size + mc.q_size + 3 * mc.intermediate_size) * mc.hidden_size)
+    return plan_layer_split(mc.num_layers, stages, 1.0, 0.0, head)
+
+
+def _hdr_tensor(hdr: np.ndarray, kind: int, device) -> torch.Tensor:
+    h = np.array(hdr, dtype=np.int64, copy=True)
+    h[0] = kind
+    return torch.from_numpy(h).to(device)
+
+
+def agree_num_blocks(fabric: Fabric, ranks: list, mine: int) -> int:
+    """All stages of a pipeline use the minimum of their block budgets."""
+    if len(ranks) == 1:
+        return mine
+    me = ranks.index(fabric.rank)
+    t = torch.tensor([mine], dtype=torch.int64, device=fabric.device)
+    if me == 0:
+        best = mine
+        for r in ranks[1:]:
+            fabric.recv(t, r)
+            best = min(best, int(t.item()))
+        out = torch.tensor([best], dtype=torch.int64, device=fabric.device)
+        for r in ranks[1:]:
+            fabric.send(out.clone(), r)
+        fabric.flush()
+        return best
+    fabric.send(t, ranks[0])
+    fabric.flush()
+    fabric.recv(t, ranks[0])
+    return int(t.item())
+
+
+def stage_block_budget(mc: ModelConfig, device: torch.device, n_layers: int, cfg: EngineConfig) -> int:
+    if device.type != "cuda":
+        return cfg.num_blocks or num_blocks_for_budget(1 << 30, max(1, n_layers), mc.num_kv_heads, mc.head_dim,
+                                                       cfg.block_size)
+    free, _ = torch.cuda.mem_get_info(device)
+    budget = max(0, free - cfg.workspace_bytes) * cfg.kv_fraction
+    n = num_blocks_for_budget(int(budget), max(1, n_layers), mc.num_kv_heads, mc.head_dim, cfg.block_size)
+    cap = 4 * cfg.max_num_seqs * ((cfg.max_model_len + cfg.block_size - 1) // cfg.block_size) + 1
+    if cfg.num_blocks is not None:
+        n = min(n, cfg.num_blocks)
+    return max(2, min(n, cap))
+
+
+class PipelineEngine(LLMEngine):
+    """Stage 0 of an S-stage pipeline; same API as ``LLMEngine``."""
+
+    def __init__(self, cfg: EngineConfig, fabric: Fabric, stage_ranks: list, microbatches: Optional[int] = None,
+                 model_cfg: Optional[ModelConfig] = None, split: Optional[list] = None):
+        self.f = fabric
+        self.ranks = list(stage_ranks)
+        assert self.ranks[0] == fabric.rank
+        mc = model_cfg or get_config(cfg.model)
+        self.split = split or stage_split(mc, len(self.ranks))
+        a, b = self.split[0]
+        device = fabric.device
+        model = LlamaModel(mc, device, cfg.dtype, a, b, has_embed=True, has_head=len(self.ranks) == 1, seed=cfg.seed)
+        nb = stage_block_budget(mc, device, b - a, cfg)
+        nb = agree_num_blocks(fabric, self.ranks, nb)
+        pcfg = EngineConfig(**{**cfg.__dict__, "device": str(device), "layer_start": a, "layer_end": b,
+                               "num_blocks": nb, "use_graphs": False})
+        super().__init__(pcfg, model_cfg=mc, model=model)
+        self.n_mb = microbatches or len(self.ranks)
+        self.mb_cap = max(1, cfg.max_num_seqs // self.n_mb)
+        self.inflight: collections.deque = collections.deque()
+        self.next_rank = self.ranks[1] if len(self.ranks) > 1 else None
+        self.last_rank = self.ranks[-1]
+
+    # ------------------------------------------------------------------ microbatches
+    def _launch(self) -> bool:
+        sb = self.scheduler.schedule(max_seqs=self.mb_cap,
+                                     max_tokens=max(1, self.cfg.max_num_batched_tokens // self.n_mb))
+        if sb.empty:
+            return False
+        for r in sb.decode:
+            r.busy = True
+        for c in sb.prefill:
+            c.req.busy = True
+        self.runner.step_id += 1
+        flat, hdr, sampled = self.runner.build_host(sb)
+        dev = self.runner.to_device(flat)
+        ids, meta, _temps, _seeds = self.runner.meta_from_device(dev, hdr)
+        with torch.inference_mode():
+            hidden = self.model.forward(meta, input_ids=ids)
+        self.f.send(_hdr_tensor(hdr, KIND_FWD, self.f.device), self.next_rank)
+        self.f.send(dev, self.next_rank)
+        self.f.send(hidden.contiguous(), self.next_rank)
+        self.inflight.append((sb, sampled, int(hdr[ModelRunner.H_NLOG])))
+        return True
+
+    def _retire(self) -> list[StepOutput]:
+        sb, sampled, nlog = self.inflight.popleft()
+        # tokens come back on the gloo control group: an RCCL recv here would
+        # queue behind the next microbatch's sends on the (0,1) pair channel
+        toks = torch.empty(self.mb_cap + 1, dtype=torch.long)
+        self.f.ctrl_recv_tensor(toks, self.last_rank)
+        tl = toks[1: 1 + int(toks[0])].tolist()
+        assert len(tl) == nlog, (len(tl), nlog)
+        for r in sb.decode:
+            r.busy = False
+        for c in sb.prefill:
+            c.req.busy = False
+        return self._apply(sb, sampled, tl)
+
+    def step(self) -> list[StepOutput]:
+        if len(self.ranks) == 1:
+            return super().step()
+        t0 = time.perf_counter()
+        launched = False
+        if len(self.inflight) < self.n_mb:
+            launched = self._launch()
+        outs: list[StepOutput] = []
+        if self.inflight and (len(self.inflight) >= self.n_mb or not launched):
+            outs = self._retire()
+        self.stats["step_time"] += time.perf_counter() - t0
+        return outs
+
+    def has_unfinished(self) -> bool:
+        return bool(self.inflight) or self.scheduler.has_work()
+
+    def drain(self) -> list[StepOutput]:
+        outs = []
+        while self.inflight:
+            outs += self._retire()
+        return outs
+
+    # ------------------------------------------------------------------ control
+    def send_kv_install(self, ids: torch.Tensor, kv_rest: torch.Tensor) -> None:
+        """Forward KV pages of layers owned by later stages (P/D into a pipeline)."""
+        if self.next_rank is None:
+            return
+        hdr = np.zeros(HDR, np.int64)
+        hdr[1] = ids.numel()
+        hdr[2] = kv_rest.shape[0]
+        self.f.send(_hdr_tensor(hdr, KIND_KV, self.f.device), self.next_rank)
+        self.f.send(ids.to(self.f.device, torch.int32).contiguous(), self.next_rank)
+        self.f.send(kv_rest.contiguous(), self.next_rank)
+
+    def pause_stages(self) -> None:
+        """Stage workers return from ``run()`` (e.g. to join a barrier)."""
+        self.drain()
+        if self.next_rank is not None:
+            self.f.send(_hdr_tensor(np.zeros(HDR, np.int64), KIND_PAUSE, self.f.device), self.next_rank)
+        self.f.flush()
+
+    def stop_stages(self) -> None:
+        self.drain()
+        if self.next_rank is not None:
+            self.f.send(_hdr_tensor(np.zeros(HDR, np.int64), KIND_STOP, self.f.device), self.next_rank)
+        self.f.flush()
+
+
+class StageWorker:
+    """Stages 1..S-1: receive -> local layers -> forward (or sample on the last stage)."""
+
+    def __init__(self, cfg: EngineConfig, fabric: Fabric, stage_ranks: list, model_cfg: Optional[ModelConfig] = None,
+                 split: Optional[list] = None, microbatches: Optional[int] = None):
+        self.f = fabric
+        self.mb_cap = max(1, cfg.max_num_seqs // (microbatches or len(stage_ranks)))
+        self.ranks = list(stage_ranks)
+        self.idx = self.ranks.index(fabric.rank)
+        assert self.idx > 0
+        mc = model_cfg or get_config(cfg.model)
+        mc.max_position = max(mc.max_position, cfg.max_model_len)
+        self.mc = mc
+        self.split = split or stage_split(mc, len(self.ranks))
+        a, b = self.split[self.idx]
+        self.is_last = self.idx == len(self.ranks) - 1
+        self.prev = self.ranks[self.idx - 1]
+        self.next = None if self.is_last else self.ranks[self.idx + 1]
+        self.driver = self.ranks[0]
+        dev = fabric.device
+        self.model = LlamaModel(mc, dev, cfg.dtype, a, b, has_embed=False, has_head=self.is_last, seed=cfg.seed)
+        nb = stage_block_budget(mc, dev, b - a, cfg)
+        nb = agree_num_blocks(fabric, self.ranks, nb)
+        self.pool = BlockPool(nb, cfg.block_size, b - a, mc.num_kv_heads, mc.head_dim, cfg.dtype, dev)
+        self.runner = ModelRunner(self.model, self.pool, cfg.max_num_seqs, cfg.max_model_len,
+                                  cfg.max_num_batched_tokens, use_graphs=False)
+        self.n_layers = b - a
+        self.steps = 0
+
+    @torch.inference_mode()
+    def run(self) -> str:
+        """Serve until PAUSE (returns "pause") or STOP (returns "stop")."""
+        f, dev = self.f, self.f.device
+        H = self.mc.hidden_size
+        from dgi import ops
+        while True:
+            hb = torch.empty(HDR, dtype=torch.int64, device=dev)
+            f.recv(hb, self.prev)
+            hdr = hb.tolist()
+            kind = hdr[0]
+            if kind in (KIND_STOP, KIND_PAUSE):
+                if self.next is not None:
+                    f.send(hb, self.next)
+                f.flush()
+                return "stop" if kind == KIND_STOP else "pause"
+            if kind == KIND_KV:
+                n, Lrest = hdr[1], hdr[2]
+                ids = torch.empty(n, dtype=torch.int32, device=dev)
+                f.recv(ids, self.prev)
+                buf = torch.empty(Lrest, 2, n, self.mc.num_kv_heads, self.pool.block_size, self.mc.head_dim,
+                                  dtype=self.pool.dtype, device=dev)
+                f.recv(buf, self.prev)
+                ops.kv_scatter(self.pool.kv, ids, buf[: self.n_layers].contiguous())
+                if self.next is not None and Lrest > self.n_layers:
+                    h2 = hb.clone()
+                    h2[2] = Lrest - self.n_layers
+                    f.send(h2, self.next)
+                    f.send(ids, self.next)
+                    f.send(buf[self.n_layers:].contiguous(), self.next)
+                continue
+            # KIND_FWD
+            flat = torch.empty(hdr[ModelRunner.H_LEN], dtype=torch.int32, device=dev)
+            f.recv(flat, self.prev)
+            T = hdr[ModelRunner.H_T]
+            hidden = torch.empty(T, H, dtype=self.pool.dtype, device=dev)
+            f.recv(hidden, self.prev)
+            _ids, meta, temps, seeds = self.runner.meta_from_device(flat, hdr)
+            out = self.model.forward(meta, hidden=hidden)
+            self.steps += 1
+            if self.is_last:
+                nlog = hdr[ModelRunner.H_NLOG]
+                toks = torch.zeros(self.mb_cap + 1, dtype=torch.long)
+                toks[0] = nlog
+                if nlog:
+                    toks[1: 1 + nlog] = ops.sample(out, temps, seeds, 0).cpu()
+                f.ctrl_send_tensor(toks, self.driver)
+            else:
+                f.send(hb, self.next)
+                f.send(flat, self.next)
+                f.send(out.contiguous(), self.next)

@@ -33,19 +33,24 @@ def plan_layer_split(total_layers: int, stages: int, layer_cost: float = 1.0, em
     extras = [0.0] * stages
     extras[0] += embed_cost
     extras[-1] += head_cost
-    total = total_layers * layer_cost + sum(extras)
-    target = total / stages
-    bounds = []
-    start = 0
-    for s in range(stages):
-        left = stages - s - 1
-        if left == 0:
-            end = total_layers
-        else:
-            n = max(1, round((target - extras[s]) / layer_cost))
-            end = min(start + n, total_layers - left)
-        bounds.append((start, end))
-        start = end
+    target = (total_layers * layer_cost + sum(extras)) / stages
+    want = [max(1.0, (target - e) / layer_cost) for e in extras]
+    scale = total_layers / sum(want)
+    want = [w * scale for w in want]
+    counts = [max(1, int(w)) for w in want]
+    # largest remainder to make the counts sum to total_layers
+    order = sorted(range(stages), key=lambda i: -(want[i] - int(want[i])))
+    k = 0
+    while sum(counts) < total_layers:
+        counts[order[k % stages]] += 1
+        k += 1
+    while sum(counts) > total_layers:
+        i = max(range(stages), key=lambda j: counts[j])
+        counts[i] -= 1
+    bounds, start = [], 0
+    for c in counts:
+        bounds.append((start, start + c))
+        start += c
     return bounds
 
 

@@ -1,0 +1,173 @@
+"""Multi-process tests of the distributed runtime on CPU (gloo), world 2-4.
+
+The same code runs over RCCL on MI355X; here every rank is a CPU process and
+tensors move through gloo.  Checks: pipeline outputs == single-process
+outputs, P/D migrated decode == local decode, layer-split planner.
+"""
+import os
+import socket
+import traceback
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from dgi.parallel.plan import get_layer_range_for_worker, plan_layer_split, plan_node_layout
+
+MODEL = "llama-tiny"
+PROMPTS = [[1] + [7 + (i * 13 + j) % 400 for j in range(n)] for i, n in enumerate((9, 33, 5, 20))]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _reference_outputs(max_tokens=6):
+    from dgi.engine import EngineConfig, LLMEngine
+    from dgi.sched.request import SamplingParams
+    e = LLMEngine(EngineConfig(model=MODEL, device="cpu", num_blocks=128, max_num_seqs=8, max_model_len=256,
+                               max_num_batched_tokens=64, enable_prefix_caching=False))
+    return [r.output for r in e.generate(PROMPTS, SamplingParams(max_tokens=max_tokens, temperature=0.0,
+                                                                   ignore_eos=True))]
+
+
+def _worker(rank, world, port, fn_name, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    try:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        res = globals()[fn_name](rank, world)
+        q.put((rank, "ok", res))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        q.put((rank, "err", traceback.format_exc()))
+
+
+def _spawn(fn_name, world, timeout=240):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fn_name, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            rank, status, res = q.get(timeout=timeout)
+            if status != "ok":
+                raise AssertionError(f"rank {rank} failed:\n{res}")
+            out[rank] = res
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    return out
+
+
+# ---------------------------------------------------------------------------- bodies (run in workers)
+
+def _pp_body(rank, world):
+    from dgi.engine import EngineConfig
+    from dgi.parallel.fabric import Fabric
+    from dgi.parallel.pipeline import PipelineEngine, StageWorker
+    from dgi.sched.request import SamplingParams
+    f = Fabric()
+    cfg = EngineConfig(model=MODEL, device="cpu", num_blocks=128, max_num_seqs=8, max_model_len=256,
+                       max_num_batched_tokens=64, enable_prefix_caching=False)
+    ranks = list(range(world))
+    if rank == 0:
+        eng = PipelineEngine(cfg, f, ranks)
+        reqs = [eng.add_request(p, SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)) for p in PROMPTS]
+        while eng.has_unfinished():
+            eng.step()
+        eng.stop_stages()
+        return [r.output for r in reqs]
+    w = StageWorker(cfg, f, ranks)
+    assert w.run() == "stop"
+    f.flush()
+    return None
+
+
+def _pd_body(rank, world):
+    from dgi.engine import EngineConfig
+    from dgi.parallel.fabric import Fabric
+    from dgi.parallel.pd import DecodeDriver, PrefillServer
+    from dgi.parallel.plan import NodeLayout
+    from dgi.sched.request import SamplingParams
+    f = Fabric()
+    cfg = EngineConfig(model=MODEL, device="cpu", num_blocks=128, max_num_seqs=8, max_model_len=256,
+                       max_num_batched_tokens=64, enable_prefix_caching=False)
+    # world 2: 1 prefill + 1 decode ; world 3: 1 prefill + 2-stage decode pipeline
+    layout = NodeLayout("pd" if world == 2 else "pdpp", [0], list(range(1, world)))
+    sp = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
+    if rank == 0:
+        srv = PrefillServer(cfg, f, layout)
+        for p in PROMPTS:
+            srv.submit(p, sp)
+        while srv.busy():
+            srv.step()
+        srv.finish()
+        return "prefill"
+    if rank == layout.decode_ranks[0]:
+        drv = DecodeDriver(cfg, f, layout)
+        done = {}
+        while len(done) < len(PROMPTS):
+            for o in drv.step():
+                if o.finished:
+                    done[tuple(o.request.prompt)] = o.request.output
+        drv.finish()
+        return [done[tuple(p)] for p in PROMPTS]
+    from dgi.parallel.pipeline import StageWorker
+    w = StageWorker(cfg, f, layout.decode_ranks)
+    w.run()
+    f.flush()
+    return None
+
+
+# ---------------------------------------------------------------------------- tests
+
+def test_layer_range_for_worker_covers_all_layers():
+    for L in (1, 7, 32, 80):
+        for n in (1, 2, 3, 8):
+            if n > L:
+                continue
+            rs = [get_layer_range_for_worker(L, n, i) for i in range(n)]
+            assert rs[0][0] == 0 and rs[-1][1] == L
+            assert all(rs[i][1] == rs[i + 1][0] for i in range(n - 1))
+            sizes = [b - a for a, b in rs]
+            assert max(sizes) - min(sizes) <= 1 and sizes == sorted(sizes, reverse=True)
+
+
+def test_plan_layer_split_gives_head_stage_fewer_layers():
+    s = plan_layer_split(80, 4, 1.0, 0.0, 2.0)
+    assert s[0][0] == 0 and s[-1][1] == 80
+    assert (s[-1][1] - s[-1][0]) < (s[0][1] - s[0][0])
+
+
+def test_node_layout_defaults():
+    lay = plan_node_layout(8)
+    assert lay.kind == "pdpp" and len(lay.decode_ranks) == 2 and len(lay.prefill_ranks) == 6
+    assert plan_node_layout(1).kind == "single"
+    assert plan_node_layout(2).kind == "pd"
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pipeline_matches_single_process(world):
+    ref = _reference_outputs()
+    out = _spawn("_pp_body", world)
+    assert out[0] == ref
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pd_migration_matches_local_decode(world):
+    ref = _reference_outputs()
+    out = _spawn("_pd_body", world)
+    assert out[1] == ref
