@@ -49,7 +49,7 @@ def run_distributed(args, layout_kind: str, dist):
     else:
         res = _run_pd(args, f, cfg, layout, role, sp, rng, conc)
     tokens, elapsed, ttfts, extra = res
-    t = torch.tensor([tokens, elapsed], dtype=torch.float64, device=f.device)
+    t = torch.tensor([tokens, elapsed], dtype=torch.float64, device=f.device if f.on_gpu else "cpu")
     tl = [torch.zeros_like(t) for _ in range(world)]
     dist.all_gather(tl, t)
     obj = [None] * world
@@ -95,7 +95,7 @@ def _run_pp(args, f, cfg, layout, role, sp, rng, conc):
             top(conc)
             step()
         eng.pause_stages()
-        torch.cuda.synchronize() if f.on_gpu else None
+        torch.cuda.synchronize() if f.device.type == "cuda" else None
         f.barrier()
         t0 = time.perf_counter()
         toks, ttfts = 0, []
@@ -107,7 +107,7 @@ def _run_pp(args, f, cfg, layout, role, sp, rng, conc):
         for o in eng.drain():
             toks += 1
         eng.pause_stages()
-        torch.cuda.synchronize() if f.on_gpu else None
+        torch.cuda.synchronize() if f.device.type == "cuda" else None
         f.barrier()
         el = time.perf_counter() - t0
         eng.stop_stages()
@@ -117,7 +117,7 @@ def _run_pp(args, f, cfg, layout, role, sp, rng, conc):
     f.barrier()
     t0 = time.perf_counter()
     w.run()
-    torch.cuda.synchronize() if f.on_gpu else None
+    torch.cuda.synchronize() if f.device.type == "cuda" else None
     f.barrier()
     el = time.perf_counter() - t0
     w.run()
@@ -152,7 +152,7 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
         f.barrier()
         t0 = time.perf_counter()
         n, ttfts = serve_until_phase()
-        torch.cuda.synchronize() if f.on_gpu else None
+        torch.cuda.synchronize() if f.device.type == "cuda" else None
         f.barrier()
         el = time.perf_counter() - t0
         srv.finish()
@@ -183,7 +183,7 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
                 ph.send([MSG_PHASE])
             if hasattr(drv.engine, "pause_stages"):
                 drv.engine.pause_stages()
-            torch.cuda.synchronize() if f.on_gpu else None
+            torch.cuda.synchronize() if f.device.type == "cuda" else None
             f.barrier()
 
         boundary()
@@ -206,7 +206,7 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
     f.barrier()
     t0 = time.perf_counter()
     w.run()
-    torch.cuda.synchronize() if f.on_gpu else None
+    torch.cuda.synchronize() if f.device.type == "cuda" else None
     f.barrier()
     el = time.perf_counter() - t0
     w.run()

@@ -39,8 +39,19 @@ class Fabric:
         self.world = dist.get_world_size()
         self.backend = dist.get_backend()
         self.on_gpu = self.backend == "nccl"
+        # "staged" mode: GPU compute with a gloo data plane (tensors bounce
+        # through host memory).  Lets the multi-rank GPU code paths run when
+        # the ranks share one device (rehearsals on a single-GPU box).
+        self.staged = False
         if device is None:
-            device = torch.device("cuda", torch.cuda.current_device()) if self.on_gpu else torch.device("cpu")
+            if self.on_gpu:
+                device = torch.device("cuda", torch.cuda.current_device())
+            elif torch.cuda.is_available() and os.environ.get("DGI_STAGED_GPU", "0") == "1":
+                device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", 0)) % torch.cuda.device_count())
+                torch.cuda.set_device(device)
+                self.staged = True
+            else:
+                device = torch.device("cpu")
         self.device = device
         # control traffic gets its own gloo group so it never queues behind (or
         # forms a dependency cycle with) data transfers on the RCCL pair channel
@@ -51,6 +62,11 @@ class Fabric:
     # ------------------------------------------------------------------ data (device tensors)
     def send(self, t: torch.Tensor, dst: int) -> None:
         """Ordered send on the data group; the compute stream is not blocked."""
+        if self.staged:
+            h = t.detach().cpu()
+            self._pending.append((dist.isend(h, dst), h))
+            self._reap()
+            return
         if self.on_gpu:
             ev = torch.cuda.current_stream().record_event()
             with torch.cuda.stream(self.comm_stream):
@@ -64,6 +80,11 @@ class Fabric:
 
     def recv(self, t: torch.Tensor, src: int) -> torch.Tensor:
         """Blocking (stream-ordered on GPU) receive into ``t``."""
+        if self.staged:
+            h = torch.empty(t.shape, dtype=t.dtype)
+            dist.recv(h, src)
+            t.copy_(h)
+            return t
         w = dist.irecv(t, src)
         w.wait()
         return t

@@ -23,6 +23,8 @@ for s in $STEPS; do
     bench70b) run bench70b 1200 python bench.py --steps 30 --warmup 5 --json-out gpurun_out/bench70b.json ;;
     prof8b) export TMPDIR=/tmp; run prof8b 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8b -o run --output-format csv -- python3 bench.py --model llama3-8b --steps 10 --warmup 2 --ramp-steps 16 ;;
     prof70b) export TMPDIR=/tmp; run prof70b 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof70b -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --ramp-steps 16 ;;
+    staged_pd) run staged_pd 600 env DGI_STAGED_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 4 --model llama3-8b --layout pdpp --steps 40 --warmup 5 --ramp-steps 20 --concurrency 64 --max-batched-tokens 2048 ;;
+    staged_pp) run staged_pp 600 env DGI_STAGED_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29612 bench.py --gpus 2 --model llama3-8b --layout pp --steps 40 --warmup 5 --ramp-steps 20 --concurrency 64 --max-batched-tokens 2048 ;;
     bench70b_long) run bench70b_long 1200 python bench.py --steps 200 --warmup 20 --json-out gpurun_out/bench70b_long.json ;;
   esac
 done
