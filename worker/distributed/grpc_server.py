@@ -1,0 +1,327 @@
+"""Shard server: gRPC (``proto/inference.proto``) and HTTP/JSON front-ends.
+
+API-compatible with reference worker/distributed/grpc_server.py:36-561
+(``InferenceServicer`` RPC names, ``GRPCServer``, ``HTTPInferenceServer``
+routes ``/inference/forward``, ``/inference/close``, ``/health``).  This is
+the cross-node data path; in-node stages talk over RCCL.
+
+Fixes over the reference:
+* the servicer is really registered with grpc.aio (generic handlers over the
+  runtime-built message classes of ``proto/inference_pb.py``, Appendix E-3);
+* shards are stateful: each session owns paged KV blocks in the shard's pool
+  and every forward appends to them (E-6) — decode steps see the whole
+  context;
+* HTTP forward decodes the base64 ``serialize_tensor`` payload the client
+  actually sends (E-4);
+* ``_forward_to_next`` really forwards to the next hop (E-5);
+* ``CloseSession`` frees the session's KV blocks.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import time
+import uuid
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+import torch
+
+from common.serialization import TensorSerializer, deserialize_tensor, serialize_tensor
+
+logger = logging.getLogger(__name__)
+
+
+class _Session:
+    __slots__ = ("session_id", "blocks", "position", "created", "last", "tokens", "max_length")
+
+    def __init__(self, session_id: str, max_length: int = 4096):
+        self.session_id = session_id
+        self.blocks: List[int] = []
+        self.position = 0
+        self.created = time.time()
+        self.last = self.created
+        self.tokens = 0
+        self.max_length = max_length
+
+
+def _get(req: Any, name: str, default=None):
+    if isinstance(req, dict):
+        return req.get(name, default)
+    return getattr(req, name, default)
+
+
+class InferenceServicer:
+    """RPC implementations over a ``ModelShard`` (native dgi backend or HF)."""
+
+    def __init__(self, model_shard=None, kv_cache_manager=None, worker_id: str = "", next_hop=None):
+        self.model_shard = model_shard
+        self.kv_cache_manager = kv_cache_manager
+        self.worker_id = worker_id or uuid.uuid4().hex[:8]
+        self.next_hop = next_hop      # optional async callable(output, position, session_id) -> output
+        self.sessions: Dict[str, _Session] = {}
+        self._stats = {"total_requests": 0, "total_tokens": 0, "total_latency_ms": 0.0, "errors": 0}
+
+    # ------------------------------------------------------------------ shard compute
+    @property
+    def _pool(self):
+        return getattr(self.model_shard, "native_engine", None)
+
+    def _native_forward(self, sess: _Session, x: torch.Tensor, position: int) -> torch.Tensor:
+        from dgi.runtime.batch import AttnMeta
+        shard = self.model_shard
+        m = shard.native
+        pool = self._pool
+        dev = pool.device
+        floating = torch.is_floating_point(x)
+        if (floating and x.dim() == 3) or (not floating and x.dim() == 2):
+            x = x[0]  # [1, S, H] hidden or [1, S] token ids (batch of one session)
+        S = x.shape[0]
+        bs = pool.block_size
+        need = (position + S + bs - 1) // bs - len(sess.blocks)
+        if need > 0:
+            sess.blocks.extend(pool.allocate(need))
+        pos = torch.arange(position, position + S, dtype=torch.int32)
+        blk = torch.tensor(sess.blocks, dtype=torch.int32)
+        slots = blk[(pos // bs).long()] * bs + pos % bs
+        tiles = [[0, t] for t in range(0, S, 128)]
+        meta = AttnMeta(positions=pos.to(dev), slot_mapping=slots.to(dev), num_decode=0,
+                        num_prefill_tokens=S, pre_block_tables=blk.view(1, -1).to(dev),
+                        pre_cu_seqlens=torch.tensor([0, S], dtype=torch.int32, device=dev),
+                        pre_context_lens=torch.tensor([position + S], dtype=torch.int32, device=dev),
+                        pre_tiles=torch.tensor(tiles, dtype=torch.int32, device=dev),
+                        logits_indices=None)
+        with torch.inference_mode():
+            if m.has_embed and not torch.is_floating_point(x):
+                out = m.forward(meta, input_ids=x.to(dev).long())
+            else:
+                out = m.forward(meta, hidden=x.to(dev, m.dtype))
+        return out.unsqueeze(0)
+
+    def _forward(self, sess: _Session, x, position: int):
+        if self.model_shard is None:
+            return x  # identity shard (tests / relay)
+        if getattr(self.model_shard, "native", None) is not None:
+            return self._native_forward(sess, x if torch.is_tensor(x) else torch.as_tensor(x), position)
+        t = x if torch.is_tensor(x) else torch.as_tensor(x)
+        dev = next(self.model_shard.parameters(), torch.empty(0)).device
+        pos_ids = torch.arange(position, position + t.shape[1], device=dev).unsqueeze(0)
+        with torch.inference_mode():
+            out, _kv = self.model_shard.forward(t.to(dev), position_ids=pos_ids, use_cache=False)
+        return out
+
+    async def _forward_to_next(self, output, position: int, session_id: str):
+        if self.next_hop is None:
+            return output
+        return await self.next_hop(output, position, session_id)
+
+    def _session(self, sid: str) -> _Session:
+        s = self.sessions.get(sid)
+        if s is None:
+            s = self.sessions[sid] = _Session(sid)
+        s.last = time.time()
+        return s
+
+    # ------------------------------------------------------------------ RPCs
+    async def Forward(self, request, context=None) -> Dict[str, Any]:
+        t0 = time.perf_counter()
+        self._stats["total_requests"] += 1
+        try:
+            sid = _get(request, "session_id") or uuid.uuid4().hex
+            sess = self._session(sid)
+            x = TensorSerializer.deserialize(_get(request, "input"), tuple(_get(request, "shape")),
+                                             _get(request, "dtype") or "float32")
+            pos = int(_get(request, "position", 0) or 0)
+            out = self._forward(sess, x, pos)
+            out = await self._forward_to_next(out, pos, sid)
+            n = x.shape[1] if x.dim() > 1 else x.shape[0]
+            sess.position = pos + n
+            self._stats["total_tokens"] += n
+            data, shape, dtype = TensorSerializer.serialize(out.detach().cpu() if torch.is_tensor(out) else out)
+            lat = (time.perf_counter() - t0) * 1000
+            self._stats["total_latency_ms"] += lat
+            return {"output": data, "shape": list(shape), "dtype": dtype,
+                    "updated_kv_keys": [f"{sid}:{self.worker_id}:{sess.position}"], "success": True,
+                    "error_message": "", "latency_ms": int(lat)}
+        except Exception as e:
+            self._stats["errors"] += 1
+            logger.exception("Forward failed")
+            return {"output": b"", "shape": [], "dtype": "", "updated_kv_keys": [], "success": False,
+                    "error_message": str(e), "latency_ms": int((time.perf_counter() - t0) * 1000)}
+
+    async def StreamInference(self, request_iterator, context=None):
+        async for req in request_iterator:
+            fwd = {"session_id": _get(req, "session_id"), "input": _get(req, "hidden_states"),
+                   "shape": list(_get(req, "shape")), "dtype": _get(req, "dtype"),
+                   "position": _get(req, "position", 0)}
+            r = await self.Forward(fwd, context)
+            yield {"session_id": fwd["session_id"], "step_id": _get(req, "step_id", ""),
+                   "hidden_states": r["output"], "shape": r["shape"], "dtype": r["dtype"],
+                   "updated_kv_keys": r["updated_kv_keys"], "latency_ms": r["latency_ms"],
+                   "tokens_processed": int(r["shape"][1]) if len(r["shape"]) > 1 else 1,
+                   "success": r["success"], "error_message": r["error_message"]}
+
+    async def TransferKVCache(self, request, context=None) -> Dict[str, Any]:
+        t0 = time.perf_counter()
+        total = 0
+        try:
+            prefix = _get(request, "prefix_key")
+            for layer in _get(request, "layers", []):
+                shape = tuple(_get(layer, "shape"))
+                dt = _get(layer, "dtype") or "float16"
+                k = TensorSerializer.deserialize(_get(layer, "keys"), shape, dt)
+                v = TensorSerializer.deserialize(_get(layer, "values"), shape, dt)
+                total += len(_get(layer, "keys")) + len(_get(layer, "values"))
+                if self.kv_cache_manager is not None:
+                    key = f"{prefix}:{int(_get(layer, 'layer_idx'))}"
+                    self.kv_cache_manager._add_to_cpu_cache(key, k, v)
+            return {"success": True, "error_message": "", "bytes_transferred": total,
+                    "latency_ms": int((time.perf_counter() - t0) * 1000)}
+        except Exception as e:
+            return {"success": False, "error_message": str(e), "bytes_transferred": total, "latency_ms": 0}
+
+    async def CreateSession(self, request, context=None) -> Dict[str, Any]:
+        sid = uuid.uuid4().hex
+        self.sessions[sid] = _Session(sid, int(_get(request, "max_length", 4096) or 4096))
+        avail = self._pool.num_free * self._pool.block_size if self._pool is not None else 0
+        return {"session_id": sid, "success": True, "error_message": "", "cache_tokens_available": int(avail)}
+
+    async def CloseSession(self, request, context=None) -> Dict[str, Any]:
+        sid = _get(request, "session_id")
+        s = self.sessions.pop(sid, None)
+        if s is not None and self._pool is not None and s.blocks:
+            self._pool.free(s.blocks)
+        return {"success": s is not None, "error_message": "" if s is not None else "unknown session"}
+
+    async def HealthCheck(self, request=None, context=None) -> Dict[str, Any]:
+        used = total = 0.0
+        if torch.cuda.is_available():
+            used = torch.cuda.memory_allocated() / 1024 ** 3
+            total = torch.cuda.get_device_properties(0).total_memory / 1024 ** 3
+        pool = self._pool
+        n = self._stats["total_requests"]
+        return {"healthy": True, "worker_id": self.worker_id, "status": "online", "gpu_memory_used_gb": used,
+                "gpu_memory_total_gb": total, "active_sessions": len(self.sessions),
+                "cache_tokens_used": int(pool.num_used * pool.block_size) if pool else 0,
+                "cache_tokens_available": int(pool.num_free * pool.block_size) if pool else 0,
+                "throughput_tokens_per_sec": 0.0,
+                "avg_latency_ms": self._stats["total_latency_ms"] / n if n else 0.0}
+
+    def get_stats(self) -> Dict[str, Any]:
+        return {**self._stats, "active_sessions": len(self.sessions)}
+
+
+class GRPCServer:
+    """grpc.aio server exposing ``distributed_inference.DistributedInference``."""
+
+    def __init__(self, servicer: InferenceServicer, host: str = "0.0.0.0", port: int = 50051, max_workers: int = 16):
+        self.servicer = servicer
+        self.host = host
+        self.port = port
+        self.max_workers = max_workers
+        self.server = None
+
+    def _handlers(self):
+        import grpc
+        from proto import inference_pb as pb
+
+        def to_msg(cls, d):
+            if not isinstance(d, dict):
+                return d
+            m = cls()
+            for k, v in d.items():
+                if v is None or k not in cls.DESCRIPTOR.fields_by_name:
+                    continue
+                f = getattr(m, k)
+                if isinstance(v, (list, tuple)):
+                    f.extend(v)
+                else:
+                    setattr(m, k, v)
+            return m
+
+        handlers = {}
+        for name, (req, resp, cs, ss) in pb.METHODS.items():
+            rq, rs = pb.CLASSES[req], pb.CLASSES[resp]
+            impl = getattr(self.servicer, name)
+            if cs and ss:
+                async def stream(request_iterator, context, impl=impl, rs=rs):
+                    async for out in impl(request_iterator, context):
+                        yield to_msg(rs, out)
+                handlers[name] = grpc.stream_stream_rpc_method_handler(
+                    stream, request_deserializer=rq.FromString, response_serializer=rs.SerializeToString)
+            else:
+                async def unary(request, context, impl=impl, rs=rs):
+                    return to_msg(rs, await impl(request, context))
+                handlers[name] = grpc.unary_unary_rpc_method_handler(
+                    unary, request_deserializer=rq.FromString, response_serializer=rs.SerializeToString)
+        return grpc.method_handlers_generic_handler(pb.FULL_SERVICE, handlers)
+
+    async def start(self) -> None:
+        import grpc
+        self.server = grpc.aio.server(options=[("grpc.max_send_message_length", 1 << 30),
+                                               ("grpc.max_receive_message_length", 1 << 30)])
+        self.server.add_generic_rpc_handlers((self._handlers(),))
+        self.port = self.server.add_insecure_port(f"{self.host}:{self.port}")
+        await self.server.start()
+
+    async def stop(self, grace: float = 1.0) -> None:
+        if self.server is not None:
+            await self.server.stop(grace)
+            self.server = None
+
+    async def wait_for_termination(self) -> None:
+        if self.server is not None:
+            await self.server.wait_for_termination()
+
+
+class HTTPInferenceServer:
+    """aiohttp JSON front-end: ``/inference/forward``, ``/inference/close``, ``/health``."""
+
+    def __init__(self, servicer: InferenceServicer, host: str = "0.0.0.0", port: int = 8001):
+        self.servicer = servicer
+        self.host = host
+        self.port = port
+        self._runner = None
+
+    def make_app(self):
+        from aiohttp import web
+        app = web.Application(client_max_size=1 << 30)
+        app.router.add_post("/inference/forward", self._handle_forward)
+        app.router.add_post("/inference/close", self._handle_close)
+        app.router.add_get("/health", self._handle_health)
+        return app
+
+    async def start(self) -> None:
+        from aiohttp import web
+        self._runner = web.AppRunner(self.make_app())
+        await self._runner.setup()
+        site = web.TCPSite(self._runner, self.host, self.port)
+        await site.start()
+
+    async def stop(self) -> None:
+        if self._runner is not None:
+            await self._runner.cleanup()
+            self._runner = None
+
+    async def _handle_forward(self, request):
+        from aiohttp import web
+        body = await request.json()
+        inp = body["input"]
+        x = deserialize_tensor(inp)
+        data, shape, dtype = TensorSerializer.serialize(x)
+        res = await self.servicer.Forward({"session_id": body.get("session_id"), "input": data, "shape": list(shape),
+                                           "dtype": dtype, "position": body.get("position", 0)})
+        if not res["success"]:
+            return web.json_response({"error": res["error_message"]}, status=500)
+        out = TensorSerializer.deserialize(res["output"], tuple(res["shape"]), res["dtype"])
+        return web.json_response({"output": serialize_tensor(out), "kv_cache_keys": res["updated_kv_keys"],
+                                  "latency_ms": res["latency_ms"]})
+
+    async def _handle_close(self, request):
+        from aiohttp import web
+        body = await request.json()
+        return web.json_response(await self.servicer.CloseSession({"session_id": body.get("session_id")}))
+
+    async def _handle_health(self, request):
+        from aiohttp import web
+        return web.json_response(await self.servicer.HealthCheck({}))

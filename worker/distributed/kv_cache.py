@@ -55,6 +55,7 @@ class CacheBlock:
     created_at: float = field(default_factory=time.time)
     last_access: float = field(default_factory=time.time)
     slot: int = -1                          # physical page index in its PagedKVCache
+    pinned: bool = False                    # owned by a live sequence: never evicted
 
     @property
     def is_full(self) -> bool:
@@ -150,7 +151,7 @@ class PagedKVCache:
     def _evict_lru(self) -> bool:
         for bid in list(self._lru):
             blk = self._blocks[bid]
-            if blk.ref_count <= 1:
+            if blk.ref_count <= 1 and not blk.pinned:
                 blk.ref_count = 1
                 self.free_block(bid)
                 self._stats["evictions"] += 1
@@ -190,14 +191,17 @@ class KVCachePool:
                     b = cache.allocate_block(li, prefix_hash)
                     if b is None:
                         raise RuntimeError(f"Failed to allocate KV block for layer {li}")
+                    b.pinned = True
                     layer_blocks.append(b)
                 out.append(layer_blocks)
         except RuntimeError:
             for li, blocks in enumerate(out):
                 for b in blocks:
+                    b.pinned = False
                     self._layer_caches[li].free_block(b.block_id)
             if "layer_blocks" in locals():
                 for b in layer_blocks:
+                    b.pinned = False
                     self._layer_caches[len(out)].free_block(b.block_id)
             raise
         return out
@@ -205,6 +209,7 @@ class KVCachePool:
     def free_sequence(self, blocks: List[List[CacheBlock]]) -> None:
         for li, layer_blocks in enumerate(blocks):
             for b in layer_blocks:
+                b.pinned = False
                 self._layer_caches[li].free_block(b.block_id)
 
     def get_layer_cache(self, layer_idx: int) -> PagedKVCache:
