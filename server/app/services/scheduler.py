@@ -103,25 +103,25 @@ class SmartScheduler:
         return best
 
     # ------------------------------------------------------------------ pull-style (atomic) assignment
-    def _accepts(self, worker: Optional[Worker]) -> bool:
+    def _accepts(self, worker: Optional[Worker], job_type: str = "llm") -> bool:
+        """Enforce the worker's remote load-control config (acceptance rate, hourly cap, working hours)."""
         if worker is None:
             return True
-        lc = ((worker.config_override or {}).get("load_control") or {})
-        rate = float(lc.get("acceptance_rate", 1.0))
-        if rate < 1.0 and random.random() > rate:
-            return False
-        cap = lc.get("max_jobs_per_hour")
-        if cap:
-            hour = int(datetime.utcnow().timestamp() // 3600)
-            if worker.hour_bucket != hour:
-                worker.hour_bucket, worker.jobs_this_hour = hour, 0
-            if worker.jobs_this_hour >= int(cap):
-                return False
-        return True
+        from app.services.worker_config import LoadControlConfig, WorkerConfigService
+        raw = ((worker.config_override or {}).get("load_control") or {})
+        try:
+            lc = LoadControlConfig(**raw)
+        except Exception:
+            lc = LoadControlConfig()
+        hour = int(datetime.utcnow().timestamp() // 3600)
+        if worker.hour_bucket != hour:
+            worker.hour_bucket, worker.jobs_this_hour = hour, 0
+        ok, _ = WorkerConfigService.should_accept_job(lc, job_type, worker.jobs_this_hour or 0)
+        return ok
 
     def atomic_assign_job(self, worker_id: str, supported_types: List[str], worker: Optional[Worker] = None,
                           candidates: int = 8) -> Optional[Job]:
-        if not supported_types or not self._accepts(worker):
+        if not supported_types:
             return None
         q = (select(Job).where(Job.status == JobStatus.QUEUED.value, Job.type.in_(list(supported_types)))
              .order_by(Job.priority.desc(), Job.created_at.asc()).limit(candidates))
@@ -135,6 +135,9 @@ class SmartScheduler:
                 phase_ok = role == "hybrid" or (j.phase or "prefill") == role or j.phase is None
                 return (j.priority < top, not phase_ok, not region_ok, j.created_at)
             jobs.sort(key=pref)
+        if jobs and not self._accepts(worker, jobs[0].type):
+            self.db.commit()   # persist the hour-bucket roll-over
+            return None
         for job in jobs:
             if worker is not None and job.preferred_region and not job.allow_cross_region \
                     and job.preferred_region != worker.region:

@@ -1,0 +1,304 @@
+"""Control-plane tests: services (geo, privacy, observability, security, worker config,
+P/D scheduler) and an end-to-end FastAPI flow with simulated workers.
+
+Mirrors the reference's server unit tests (tests/test_server_{geo,privacy,
+observability,security,pd_scheduler}.py) and adds the API flow the
+reference never tested (register → submit → pull → complete → usage → admin).
+"""
+import asyncio
+import importlib.util
+import sys
+import threading
+import time
+from datetime import datetime, timedelta
+from pathlib import Path
+from unittest.mock import MagicMock, patch
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+# ----------------------------------------------------------------- geo
+def test_geo_offline_defaults_and_prefixes():
+    from app.services.geo import detect_client_region, get_region_name
+    assert asyncio.run(detect_client_region(None)) == "asia-east"
+    assert asyncio.run(detect_client_region("10.0.0.1")) == "asia-east"
+    assert asyncio.run(detect_client_region("localhost")) == "asia-east"
+    assert asyncio.run(detect_client_region("2.1.1.1")) == "europe-west"
+    assert asyncio.run(detect_client_region("3.9.9.9")) == "america-north"
+    assert "东亚" in get_region_name("asia-east")
+    assert get_region_name("unknown") == "unknown"
+
+
+# ----------------------------------------------------------------- privacy
+def test_privacy_anonymizer():
+    from app.services.privacy import DataAnonymizer
+    a = DataAnonymizer(salt="s")
+    out = a.anonymize_string("user@example.com", preserve_format=True)
+    assert out.endswith("@example.com") and "***@" in out
+    assert a.anonymize_string("1234", preserve_format=True) == "****"
+    m = a.anonymize_string("1234567890", preserve_format=True)
+    assert m.startswith("12") and m.endswith("90") and "*" in m
+    assert a.anonymize_ip("1.2.3.4") == "1.2.xxx.xxx"
+    assert a.anonymize_ip("2001:db8:abcd:0012::1").startswith("2001:db8::")
+    c = a.anonymize_content("contact me at test@example.com and call 13800138000", max_preview=200)
+    assert "[EMAIL]" in c and "[PHONE_CN]" in c
+    d = a.anonymize_dict({"prompt": "secret text", "nested": {"token": "abc", "keep": 1}, "items": [{"password": "p"}]})
+    assert d["prompt"].startswith("[") and d["nested"]["token"] == "[REDACTED]" and d["nested"]["keep"] == 1
+    assert d["items"][0]["password"] == "[REDACTED]"
+    assert a.create_pseudonym("x") == a.create_pseudonym("x") != a.create_pseudonym("y")
+
+
+def test_privacy_encryptor_roundtrip_wrong_key_and_tamper():
+    from app.services.privacy import DataEncryptor
+    e1 = DataEncryptor(encryption_key="k1")
+    ct = e1.encrypt("hello")
+    assert e1.decrypt(ct) == "hello"
+    assert DataEncryptor(encryption_key="k2").decrypt(ct) == "[DECRYPTION_FAILED]"
+    assert e1.decrypt(ct[:-4] + "AAAA") == "[DECRYPTION_FAILED]"
+    d = e1.encrypt_dict({"prompt": {"a": 1}, "keep": 2}, ["prompt"])
+    assert d["prompt"] != {"a": 1} and e1.decrypt_dict(d) == {"prompt": {"a": 1}, "keep": 2}
+
+
+# ----------------------------------------------------------------- observability
+def _load_observability_with_mocks():
+    class _Metric:
+        def __init__(self, name, desc, labels, buckets=None):
+            self.values = {}
+
+        def labels(self, **kw):
+            return self.values.setdefault(tuple(sorted(kw.items())), MagicMock())
+    prom = MagicMock()
+    prom.Counter = prom.Gauge = prom.Histogram = _Metric
+    prom.generate_latest = MagicMock(return_value=b"# metrics")
+    prom.CONTENT_TYPE_LATEST = "text/plain"
+    with patch.dict(sys.modules, {"prometheus_client": prom, "opentelemetry": MagicMock(),
+                                  "opentelemetry.trace": MagicMock()}):
+        spec = importlib.util.spec_from_file_location(
+            "obs_under_test", ROOT / "server" / "app" / "services" / "observability.py")
+        mod = importlib.util.module_from_spec(spec)
+        sys.modules["obs_under_test"] = mod
+        spec.loader.exec_module(mod)
+    return mod
+
+
+def test_observability_collector_and_logger():
+    obs = _load_observability_with_mocks()
+    t = obs.TracingManager("svc")
+    assert t._tracer is None and t._enabled is False
+    with t.span("x") as sp:
+        assert sp is None
+    c = obs.MetricsCollector(worker_id="w1", model_name="m", worker_role="hybrid")
+    for i in range(3):
+        c.record_request("decode", 0.1 * (i + 1), tokens=10, success=i != 1)
+    c.record_batch("prefill", 8)
+    c.record_kv_cache_stats("gpu", 0.9, 100, 2)
+    c.record_gpu_stats(0, 1, 2, 50.0)
+    c.record_speculative_stats(0.7, 1.5)
+    s = c.get_summary()
+    assert s["total_requests"] == 3 and s["error_count"] == 1
+    assert s["avg_latency_ms"] == pytest.approx(200, rel=1e-3)
+    c.update_tokens_per_second()
+    assert c._token_count == 0
+    app = MagicMock()
+    obs.setup_metrics_routes(app)
+    app.include_router.assert_called_once()
+    lg = obs.StructuredLogger("t")
+    lg.set_context(session_id="abc")
+    with patch.object(lg.logger, "info") as mi:
+        lg.info("m", request_id="r1")
+        extra = mi.call_args.kwargs["extra"]
+        assert extra["session_id"] == "abc" and extra["request_id"] == "r1"
+    with patch.object(obs, "HAS_PROMETHEUS", False):
+        assert "error" in asyncio.run(obs.create_metrics_endpoint()())
+
+
+# ----------------------------------------------------------------- security / config
+def test_security_signer_and_tokens():
+    from app.services.security import RequestSigner, TokenManager
+    tok = TokenManager.generate_token()
+    h = TokenManager.hash_token(tok)
+    assert TokenManager.verify_token_hash(tok, h) and not TokenManager.verify_token_hash(tok + "x", h)
+    ts = int(time.time())
+    sig = RequestSigner.sign_request("POST", "/p", {"a": 1}, ts, "sec")
+    ok, _ = RequestSigner.verify_signature("POST", "/p", {"a": 1}, ts, sig, "sec")
+    assert ok
+    ok, _ = RequestSigner.verify_signature("POST", "/p", {"a": 2}, ts, sig, "sec")
+    assert not ok
+    ok, err = RequestSigner.verify_signature("POST", "/p", {"a": 1}, ts - 3600, sig, "sec")
+    assert not ok
+
+
+def test_worker_config_should_accept():
+    import random
+    from app.services.worker_config import LoadControlConfig, WorkerConfigService as S
+    assert S.should_accept_job(LoadControlConfig(), "llm")[0]
+    assert S.should_accept_job(LoadControlConfig(max_jobs_per_hour=2), "llm", 2) == (False, "hourly_limit_reached")
+    lc = LoadControlConfig(working_hours_start=22, working_hours_end=6)
+    assert S.should_accept_job(lc, "llm", now=datetime(2025, 1, 1, 23))[0]
+    assert not S.should_accept_job(lc, "llm", now=datetime(2025, 1, 1, 12))[0]
+    assert S.should_accept_job(LoadControlConfig(type_weights={"llm": 0.0}), "llm")[1] == "job_type_disabled"
+    rng = random.Random(0)
+    n = sum(S.should_accept_job(LoadControlConfig(acceptance_rate=0.3), "llm", rng=rng)[0] for _ in range(2000))
+    assert 450 < n < 750
+
+
+def test_pd_scheduler_tracks_load():
+    from app.services.pd_scheduler import JobPhase, PrefillDecodeScheduler, WorkerCapability, WorkerRole
+    s = PrefillDecodeScheduler()
+    s.register_worker("p", WorkerCapability(worker_id="p", role=WorkerRole.PREFILL, compute_flops=2500))
+    s.register_worker("d", WorkerCapability(worker_id="d", role=WorkerRole.DECODE,
+                                                 memory_bandwidth_gbps=8000))
+
+    async def flow():
+        await s.submit_job("j1", prompt_tokens=100, max_tokens=10)
+        [(job, a)] = await s.get_batch(JobPhase.PREFILL)
+        assert a.worker_id == "p" and s._workers["p"].active_prefill_jobs == 1
+        await s.transition_to_decode("j1", "kv1", "p")
+        assert s._workers["p"].active_prefill_jobs == 0
+        [(job, a)] = await s.get_batch(JobPhase.DECODE)
+        assert a.worker_id == "d" and a.kv_migration_needed and a.migration_source == "p" and s._workers["d"].active_decode_jobs == 1
+        await s.complete_job("j1", JobPhase.DECODE, latency_ms=5.0)
+        assert s._workers["d"].active_decode_jobs == 0
+    asyncio.run(flow())
+    st = s.get_stats()
+    assert st["prefill_jobs"] == 1 and st["decode_jobs"] == 1 and st["kv_cache_entries"] == 1
+
+
+# ----------------------------------------------------------------- end-to-end API
+@pytest.fixture()
+def client():
+    from fastapi.testclient import TestClient
+    from app.db.database import Base, engine
+    from app.main import app
+    Base.metadata.drop_all(bind=engine)
+    with TestClient(app) as c:
+        yield c
+    Base.metadata.drop_all(bind=engine)
+
+
+def _register(c, **kw):
+    body = {"name": "mi355x-node", "region": "asia-east", "gpu_model": "AMD Instinct MI355X", "gpu_memory_gb": 288,
+            "gpu_count": 8, "supported_types": ["llm"], **kw}
+    r = c.post("/api/v1/workers/register", json=body)
+    assert r.status_code == 200, r.text
+    d = r.json()
+    return d["worker_id"], {"X-Worker-Token": d["token"]}, d
+
+
+def test_api_job_lifecycle_with_usage(client):
+    c = client
+    assert c.get("/health").json()["status"] == "healthy"
+    assert len(c.get("/regions").json()["available_regions"]) == 7
+    ent = c.post("/api/v1/admin/enterprises", json={"name": "Acme", "code": "acme"}).json()
+    key = c.post(f"/api/v1/admin/enterprises/{ent['id']}/api-keys", json={"name": "k"}).json()["api_key"]
+    assert key.startswith("ent_")
+    wid, hdr, _ = _register(c)
+    assert c.post(f"/api/v1/workers/{wid}/heartbeat", json={"status": "online"}, headers=hdr).json()["status"] == "ok"
+    assert c.post(f"/api/v1/workers/{wid}/heartbeat", json={"status": "online"},
+                  headers={"X-Worker-Token": "bad"}).status_code == 401
+    r = c.post("/api/v1/jobs", json={"type": "llm", "params": {"messages": [{"role": "user", "content": "hi"}],
+                                                                "max_tokens": 8}}, headers={"X-API-Key": key})
+    assert r.status_code == 200, r.text
+    job_id = r.json()["job_id"]
+    assert r.json()["status"] == "queued"
+    assert c.get("/api/v1/jobs/stats/queue").json()["total_queued"] == 1
+    a = c.get(f"/api/v1/workers/{wid}/next-job", headers=hdr).json()
+    assert a["job_id"] == job_id and a["params"]["max_tokens"] == 8
+    assert c.get(f"/api/v1/workers/{wid}/next-job", headers=hdr).json() is None
+    res = {"response": "hello", "usage": {"prompt_tokens": 3, "completion_tokens": 5, "total_tokens": 8},
+           "finish_reason": "length"}
+    r = c.post(f"/api/v1/workers/{wid}/jobs/{job_id}/complete", json={"success": True, "result": res,
+                                                                       "processing_time_ms": 40}, headers=hdr)
+    assert r.status_code == 200, r.text
+    j = c.get(f"/api/v1/jobs/{job_id}").json()
+    assert j["status"] == "completed" and j["result"]["response"] == "hello" and j["worker_id"] == wid
+    recs = c.get("/api/v1/admin/usage/records").json()
+    assert recs["total"] == 1 and recs["items"][0]["usage_type"] == "llm_tokens"
+    assert recs["items"][0]["total_cost"] == pytest.approx(0.002 * 8 / 1000)
+    assert c.get("/api/v1/admin/dashboard").json()["today"]["jobs"] == 1
+    assert c.get("/api/v1/admin/usage/summary?group_by=type").json()["items"][0]["key"] == "llm_tokens"
+    w = c.get(f"/api/v1/workers/{wid}").json()
+    assert w["completed_jobs"] == 1 and w["success_rate"] == 1.0
+    assert c.get("/api/v1/admin/dashboard/realtime").json()["workers"]["online"] == 1
+    assert c.get("/api/v1/admin/health/detailed").json()["database"] is True
+    # privacy endpoints
+    p = c.get(f"/api/v1/admin/enterprises/{ent['id']}/privacy").json()
+    assert p["data_retention_days"] == 30
+    c.put(f"/api/v1/admin/enterprises/{ent['id']}/privacy", json={"anonymize_data": True})
+    assert c.get(f"/api/v1/admin/enterprises/{ent['id']}/privacy/compliance").json()["compliance_status"][
+        "anonymization_enabled"] is True
+    exp = c.post(f"/api/v1/admin/enterprises/{ent['id']}/privacy/export").json()
+    assert len(exp["usage_records"]) == 1
+    prev = c.delete(f"/api/v1/admin/enterprises/{ent['id']}/privacy/data").json()
+    assert prev["status"] == "preview" and prev["data_to_delete"]["usage_records"] == 1
+    assert c.delete(f"/api/v1/admin/enterprises/{ent['id']}/privacy/data?confirm=true").json()["status"] == "deleted"
+    assert c.get("/api/v1/admin/usage/records").json()["total"] == 0
+    assert c.get("/metrics").status_code == 200 and c.get("/ready").json()["status"] == "ready"
+
+
+def test_api_cancel_offline_requeue_and_concurrency(client):
+    c = client
+    wid, hdr, _ = _register(c)
+    c.put(f"/api/v1/workers/{wid}/config", json={"max_concurrent_jobs": 2}, headers=hdr)
+    cfg = c.get(f"/api/v1/workers/{wid}/config", headers=hdr).json()
+    assert cfg["load_control"]["max_concurrent_jobs"] == 2 and cfg["version"] == 1
+    ids = [c.post("/api/v1/jobs", json={"type": "llm", "params": {"prompt": str(i)}}).json()["job_id"]
+           for i in range(4)]
+    assert c.delete(f"/api/v1/jobs/{ids[3]}").json()["job_id"] == ids[3]
+    got = [c.get(f"/api/v1/workers/{wid}/next-job", headers=hdr).json() for _ in range(3)]
+    assert got[0] and got[1] and got[2] is None          # capped at 2 concurrent
+    assert c.get(f"/api/v1/workers/{wid}").json()["status"] == "busy"
+    assert c.delete(f"/api/v1/jobs/{got[0]['job_id']}").status_code == 400
+    r = c.post(f"/api/v1/workers/{wid}/offline", headers=hdr).json()
+    assert r["requeued"] == 2
+    assert all(c.get(f"/api/v1/jobs/{g['job_id']}").json()["status"] == "queued" for g in got[:2])
+    # a second worker picks the requeued work up
+    wid2, hdr2, _ = _register(c, region="europe-west")
+    assert c.get(f"/api/v1/workers/{wid2}/next-job", headers=hdr2).json()["job_id"] in ids
+    # token refresh
+    _, _, reg = _register(c)
+    r = c.post(f"/api/v1/workers/{reg['worker_id']}/refresh-token", json={"refresh_token": reg["refresh_token"]})
+    assert r.status_code == 200
+    new = {"X-Worker-Token": r.json()["token"]}
+    assert c.post(f"/api/v1/workers/{reg['worker_id']}/verify", headers=new).json()["valid"] is True
+    assert c.post(f"/api/v1/workers/{reg['worker_id']}/verify",
+                  headers={"X-Worker-Token": reg["token"]}).json()["valid"] is False
+
+
+def test_api_sync_job_completed_by_worker_thread(client):
+    c = client
+    wid, hdr, _ = _register(c)
+    stop = threading.Event()
+
+    def worker_loop():
+        from fastapi.testclient import TestClient
+        from app.main import app
+        wc = TestClient(app)
+        while not stop.is_set():
+            a = wc.get(f"/api/v1/workers/{wid}/next-job", headers=hdr).json()
+            if a:
+                wc.post(f"/api/v1/workers/{wid}/jobs/{a['job_id']}/complete",
+                        json={"success": True, "result": {"echo": a["params"]["prompt"]}}, headers=hdr)
+                return
+            time.sleep(0.05)
+    t = threading.Thread(target=worker_loop, daemon=True)
+    t.start()
+    r = c.post("/api/v1/jobs/sync?timeout=20", json={"type": "llm", "params": {"prompt": "ping"}})
+    stop.set()
+    t.join(5)
+    assert r.status_code == 200, r.text
+    assert r.json()["status"] == "completed" and r.json()["result"] == {"echo": "ping"}
+    r = c.post("/api/v1/jobs/sync?timeout=1&wait_for_worker=true", json={"type": "image_gen", "params": {}})
+    assert r.status_code == 408
+
+
+def test_api_no_worker_503_and_direct(client):
+    c = client
+    r = c.post("/api/v1/jobs/sync?wait_for_worker=false", json={"type": "llm", "params": {}})
+    assert r.status_code == 503
+    assert c.get("/api/v1/jobs/direct/nearest?job_type=llm").status_code == 503
+    wid, hdr, _ = _register(c, supports_direct=True, direct_url="http://10.0.0.5:8001")
+    d = c.get("/api/v1/jobs/direct/nearest?job_type=llm").json()
+    assert d["worker_id"] == wid and d["direct_url"].endswith(":8001")
