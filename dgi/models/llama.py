@@ -59,6 +59,9 @@ class LlamaModel:
         self.kv_cache: Optional[torch.Tensor] = None  # [L_local, 2, NB, nkv, bs, hd]
         self.layers: list[LlamaLayerWeights] = []
         self.embed = self.norm = self.lm_head = None
+        # EAGLE-3 feature taps: global layer ids whose output residual stream is kept
+        self.capture_layers: tuple = ()
+        self.captured: dict = {}
         if init == "random":
             self._init_random(seed)
         elif init == "empty":
@@ -204,6 +207,8 @@ class LlamaModel:
             gu = F.linear(h, L.gate_up)
             act = ops.silu_mul(gu)
             h = F.linear(act, L.down)
+            if self.capture_layers and (self.layer_start + i) in self.capture_layers:
+                self.captured[self.layer_start + i] = h + residual
         return h, residual
 
     def embed_tokens(self, input_ids: torch.Tensor) -> torch.Tensor:

@@ -1,0 +1,554 @@
+"""EAGLE-3 speculative decoding on the native runtime.
+
+Replaces the reference's incomplete library (worker/engines/speculative.py:
+``DraftHead :78-125``, ``TreeDraftBuffer :128-245``, ``SpeculativeDecoder
+:248-471``) with a working, batched, lossless
+implementation whose hot paths run on the hand-written HIP kernels:
+
+* **Draft head** (EAGLE-3): target residual-stream features of a low, a mid
+  and a high layer are fused (``fc``: 3H -> H) and combined with the token
+  embedding into ONE Llama decoder layer (qkv input 2H) with its own paged
+  KV cache (sharing the target's block ids); the target's embedding and LM
+  head are shared.
+* **Tree drafting**: depth ``D``; each depth keeps the ``W`` best nodes by
+  cumulative draft log-prob, each expanded to ``K`` children (``dgi_topk``).
+  Draft attention over context + ancestors uses the paged prefill kernel's
+  tree-mask mode (``dgi_tree_mask`` ancestor bits).
+* **Verify**: one target forward over the ``N = 1 + W*D`` tree nodes of
+  every sequence (paged prefill, tree mask, positions = ctx + depth);
+  greedy acceptance of the longest matching root path plus the bonus token
+  by ``dgi_tree_verify``; accepted KV is compacted in place (slot copy).
+
+Greedy (temperature 0) requests speculate; sampled requests decode normally
+in the same engine.  Output is token-for-token identical to non-speculative
+greedy decoding (the target decides every token).
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+import time
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from dgi import ops
+from dgi.engine import EngineConfig, LLMEngine, StepOutput
+from dgi.kv.block_pool import OutOfBlocks
+from dgi.models.config import ModelConfig
+from dgi.models.llama import LlamaModel, _rand
+from dgi.runtime.batch import AttnMeta
+from dgi.sched.request import Request
+
+
+@dataclasses.dataclass
+class SpecConfig:
+    depth: int = 5            # draft tree depth D (max accepted drafts per step)
+    width: int = 4            # frontier nodes kept per depth W
+    topk: int = 4             # children per frontier node K (<= 16, dgi_topk)
+    feature_layers: Optional[tuple] = None  # default: (2, L//2, L-3)
+
+    @property
+    def num_nodes(self) -> int:
+        return 1 + self.width * self.depth
+
+    def validate(self) -> None:
+        if self.num_nodes > 64:
+            raise ValueError("tree of more than 64 nodes (ancestor masks are 64-bit)")
+        if not 1 <= self.width <= self.topk <= 16:
+            raise ValueError("need 1 <= width <= topk <= 16")
+
+
+def default_feature_layers(num_layers: int) -> tuple:
+    lo = min(2, num_layers - 1)
+    return (lo, num_layers // 2, max(num_layers - 3, 0))
+
+
+class Eagle3Draft:
+    """One-layer EAGLE-3 draft decoder sharing the target's embedding / LM head."""
+
+    def __init__(self, target: LlamaModel, num_blocks: int, block_size: int, seed: int = 1234):
+        c = target.cfg
+        self.target = target
+        self.cfg = c
+        dev, dt = target.device, target.dtype
+        H, I = c.hidden_size, c.intermediate_size
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(seed)
+        std = 0.02
+        self.fc = _rand((H, 3 * H), gen, dev, dt, std)
+        self.embed_norm = torch.ones(H, device=dev, dtype=dt)
+        self.hidden_norm = torch.ones(H, device=dev, dtype=dt)
+        self.qkv = _rand((c.qkv_size, 2 * H), gen, dev, dt, std)
+        self.o = _rand((H, c.q_size), gen, dev, dt, std / math.sqrt(2))
+        self.post_norm = torch.ones(H, device=dev, dtype=dt)
+        self.gate_up = _rand((2 * I, H), gen, dev, dt, std)
+        self.down = _rand((H, I), gen, dev, dt, std / math.sqrt(2))
+        self.norm = torch.ones(H, device=dev, dtype=dt)
+        self.kv_cache = torch.zeros(1, 2, num_blocks, c.num_kv_heads, block_size, c.head_dim, device=dev, dtype=dt)
+        self.scale = 1.0 / math.sqrt(c.head_dim)
+
+    # ------------------------------------------------------------------ params (training / checkpoints)
+    PARAM_NAMES = ("fc", "embed_norm", "hidden_norm", "qkv", "o", "post_norm", "gate_up", "down", "norm")
+
+    def parameters(self) -> dict:
+        return {k: getattr(self, k) for k in self.PARAM_NAMES}
+
+    def load(self, params: dict) -> None:
+        for k in self.PARAM_NAMES:
+            getattr(self, k).copy_(params[k])
+
+    # ------------------------------------------------------------------ inference (paged KV, HIP kernels)
+    def fuse(self, feats: torch.Tensor) -> torch.Tensor:
+        return F.linear(feats, self.fc)
+
+    def forward(self, ids: torch.Tensor, hidden: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
+        """Draft hidden states g [T, H] (pre-norm residual stream)."""
+        c = self.cfg
+        eps = c.rms_eps
+        e = ops.rmsnorm(F.embedding(ids, self.target.embed), self.embed_norm, eps)
+        hn = ops.rmsnorm(hidden.contiguous(), self.hidden_norm, eps)
+        qkv = F.linear(torch.cat([e, hn], dim=-1), self.qkv)
+        kc, vc = self.kv_cache[0, 0], self.kv_cache[0, 1]
+        ops.rope_cache(qkv, meta.positions, self.target.cos_sin, c.num_heads, c.num_kv_heads, c.head_dim,
+                       meta.slot_mapping, kc, vc)
+        attn = ops.paged_prefill(qkv, kc, vc, meta.pre_block_tables, meta.pre_cu_seqlens, meta.pre_context_lens,
+                                 c.num_heads, c.num_kv_heads, self.scale, tiles=meta.pre_tiles,
+                                 tree_mask=meta.tree_mask, tree_n=meta.tree_n)
+        h = F.linear(attn, self.o)
+        residual = hidden.contiguous().clone()
+        ops.fused_add_rmsnorm(h, residual, self.post_norm, eps)   # residual <- h + hidden ; h <- norm
+        h = F.linear(ops.silu_mul(F.linear(h, self.gate_up)), self.down)
+        return h + residual
+
+    def logprobs(self, g: torch.Tensor) -> torch.Tensor:
+        hn = ops.rmsnorm(g.contiguous(), self.norm, self.cfg.rms_eps)
+        return torch.log_softmax(F.linear(hn, self.target.lm_head).float(), dim=-1)
+
+    # ------------------------------------------------------------------ training (dense, autograd)
+    def train_forward(self, P: dict, ids: torch.Tensor, hidden: torch.Tensor, pos: torch.Tensor) -> torch.Tensor:
+        """Dense causal forward over [B, S] for self-distillation (plain torch ops)."""
+        c = self.cfg
+        eps = c.rms_eps
+
+        def rms(x, w):
+            xf = x.float()
+            return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)).to(x.dtype) * w
+
+        B, S = ids.shape
+        e = rms(F.embedding(ids, self.target.embed), P["embed_norm"])
+        qkv = F.linear(torch.cat([e, rms(hidden, P["hidden_norm"])], -1), P["qkv"])
+        nh, nkv, hd = c.num_heads, c.num_kv_heads, c.head_dim
+        q, k, v = qkv.split([nh * hd, nkv * hd, nkv * hd], -1)
+        cs = self.target.cos_sin[pos.long()]             # [B, S, hd] (cos | sin halves)
+        cos, sin = cs[..., : hd // 2].float(), cs[..., hd // 2:].float()
+
+        def rot(x, n):
+            x = x.view(B, S, n, hd).float()
+            x1, x2 = x[..., : hd // 2], x[..., hd // 2:]
+            cc, ss = cos[:, :, None], sin[:, :, None]
+            return torch.cat([x1 * cc - x2 * ss, x2 * cc + x1 * ss], -1).to(qkv.dtype)
+        q, k = rot(q, nh), rot(k, nkv)
+        v = v.view(B, S, nkv, hd)
+        rep = nh // nkv
+        k = k.repeat_interleave(rep, 2)
+        v = v.repeat_interleave(rep, 2)
+        a = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), is_causal=True)
+        h = F.linear(a.transpose(1, 2).reshape(B, S, nh * hd), P["o"]) + hidden
+        m = F.linear(rms(h, P["post_norm"]), P["gate_up"])
+        g_, u_ = m.chunk(2, -1)
+        return F.linear(F.silu(g_) * u_, P["down"]) + h
+
+    def train_logits(self, P: dict, g: torch.Tensor) -> torch.Tensor:
+        xf = g.float()
+        hn = (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + self.cfg.rms_eps)).to(g.dtype) * P["norm"]
+        return F.linear(hn, self.target.lm_head)
+
+
+class _SpecState:
+    __slots__ = ("draft_len", "feat_start", "feat")
+
+    def __init__(self, draft_len: int):
+        self.draft_len = draft_len      # positions [0, draft_len) have draft KV
+        self.feat_start = 0             # position of feat[0]
+        self.feat: Optional[torch.Tensor] = None   # fused target features [m, H]
+
+
+def _varlen_meta(runner, positions, slots, block_rows, cu, ctx, device, tree_mask=None, tree_n=0,
+                 logits_idx=None) -> AttnMeta:
+    """Prefill-style metadata from host arrays (one H2D copy)."""
+    nb = len(ctx)
+    maxw = runner.max_blocks
+    bt = np.zeros((nb, maxw), np.int32)
+    for i, blk in enumerate(block_rows):
+        bt[i, : len(blk)] = blk
+    tiles = [(j, t0) for j in range(nb) for t0 in range(0, int(cu[j + 1] - cu[j]), 128)]
+    tiles_np = np.asarray(tiles, np.int32).reshape(-1, 2)
+    parts = [np.asarray(positions, np.int32), np.asarray(slots, np.int32), bt.ravel(), np.asarray(cu, np.int32),
+             np.asarray(ctx, np.int32), tiles_np.ravel()]
+    flat = np.concatenate(parts)
+    dev = runner.to_device(flat)
+    o = 0
+    views = []
+    for p in parts:
+        views.append(dev[o: o + p.size])
+        o += p.size
+    d_pos, d_slots, d_bt, d_cu, d_ctx, d_tiles = views
+    return AttnMeta(positions=d_pos, slot_mapping=d_slots, num_decode=0, num_prefill_tokens=int(cu[-1]),
+                    pre_block_tables=d_bt.view(nb, maxw), pre_cu_seqlens=d_cu, pre_context_lens=d_ctx,
+                    pre_tiles=d_tiles.view(-1, 2), tree_mask=tree_mask, tree_n=tree_n, logits_indices=logits_idx)
+
+
+def kv_slot_copy(kv: torch.Tensor, src: torch.Tensor, dst: torch.Tensor, block_size: int) -> None:
+    """Copy token slots (all layers, K and V) inside a paged cache [L, 2, NB, nkv, bs, hd]."""
+    L, two, NB, nkv, bs, hd = kv.shape
+    c = kv.view(L * two, NB, nkv, bs, hd)
+    src, dst = src.long(), dst.long()
+    vals = c[:, src // bs, :, src % bs]          # [n, L*2, nkv, hd] (advanced dims first)
+    c[:, dst // bs, :, dst % bs] = vals
+
+
+class SpecEngine(LLMEngine):
+    """``LLMEngine`` with EAGLE-3 tree speculation for greedy requests."""
+
+    def __init__(self, cfg: EngineConfig, spec: Optional[SpecConfig] = None, model_cfg: Optional[ModelConfig] = None,
+                 model=None, draft: Optional[Eagle3Draft] = None):
+        cfg = dataclasses.replace(cfg, use_graphs=False)
+        super().__init__(cfg, model_cfg, model)
+        self.spec = spec or SpecConfig()
+        self.spec.validate()
+        L = self.model_cfg.num_layers
+        self.feature_layers = tuple(self.spec.feature_layers or default_feature_layers(L))
+        self.draft = draft or Eagle3Draft(self.model, self.pool.num_blocks, self.pool.block_size)
+        self.spec_stats = {"spec_steps": 0, "spec_rows": 0, "accepted": 0, "spec_tokens": 0, "draft_s": 0.0,
+                           "verify_s": 0.0}
+
+    # ------------------------------------------------------------------ helpers
+    def _eligible(self, r: Request) -> bool:
+        return r.params.greedy and not r.in_prefill and not r.busy
+
+    def _state(self, r: Request) -> _SpecState:
+        if r.spec_state is None:
+            r.spec_state = _SpecState(r.num_cached)
+        return r.spec_state
+
+    def _forward_capture(self, meta: AttnMeta, ids: torch.Tensor, fuse: bool = True):
+        """Target forward that also returns the EAGLE-3 features of every row
+        (fused [T, H], or the raw low|mid|high concatenation [T, 3H])."""
+        m = self.model
+        m.capture_layers, m.captured = self.feature_layers, {}
+        try:
+            logits = m.forward(meta, input_ids=ids)
+            raw = torch.cat([m.captured[li] for li in self.feature_layers], dim=-1)
+        finally:
+            m.capture_layers, m.captured = (), {}
+        return logits, (self.draft.fuse(raw) if fuse else raw)
+
+    def _append_feats(self, r: Request, start: int, feats: torch.Tensor) -> None:
+        st = self._state(r)
+        if st.feat is None or st.feat_start + st.feat.shape[0] != start:
+            st.feat, st.feat_start = feats, start
+        else:
+            st.feat = torch.cat([st.feat, feats])
+
+    # ------------------------------------------------------------------ step
+    def step(self) -> list:
+        t0 = time.perf_counter()
+        outs: list[StepOutput] = []
+        spec_reqs = [r for r in self.scheduler.running if self._eligible(r)]
+        for r in spec_reqs:
+            r.busy = True            # keep them out of the normal batch
+        try:
+            sb = self.scheduler.schedule()
+        finally:
+            for r in spec_reqs:
+                r.busy = False
+        if not sb.empty:
+            outs += self._normal_step(sb)
+        live = [r for r in spec_reqs if r in self.scheduler.running and self._eligible(r)]
+        if live:
+            outs += self._spec_step(live)
+        self.stats["step_time"] += time.perf_counter() - t0
+        return outs
+
+    @torch.inference_mode()
+    def _normal_step(self, sb) -> list:
+        run = self.runner
+        run.step_id += 1
+        flat, hdr, sampled = run.build_host(sb)
+        ids, meta, temps, seeds = run.meta_from_device(run.to_device(flat), hdr)
+        logits, feats = self._forward_capture(meta, ids)
+        nd = len(sb.decode)
+        row = nd
+        for c in sb.prefill:
+            if c.req.params.greedy:
+                self._append_feats(c.req, c.start, feats[row: row + c.length])
+            row += c.length
+        if not sampled:
+            return self._apply(sb, [], [])
+        filt = run.filter_tensors(sampled) if any(r.params.needs_filter for r in sampled) else None
+        toks = run.sample_rows(logits, temps, seeds, filt).tolist()
+        return self._apply(sb, sampled, toks)
+
+    @torch.inference_mode()
+    def _spec_step(self, reqs: list) -> list:
+        sp = self.spec
+        W, K, D, N = sp.width, sp.topk, sp.depth, sp.num_nodes
+        bs = self.pool.block_size
+        dev = self.device
+        run = self.runner
+        sched = self.scheduler
+        # ---- blocks for the tree slots [n-1, n-1+N)
+        ok = []
+        for r in reqs:
+            try:
+                sched._grow(r, r.total_len - 1 + N)
+                ok.append(r)
+            except OutOfBlocks:
+                pass
+        reqs = ok
+        if not reqs:
+            return []
+        R = len(reqs)
+        td = time.perf_counter()
+        # ---- 1) draft catch-up over committed positions [draft_len, n-1]
+        pos, slots, cu, ctx, ids, feat_rows, brows = [], [], [0], [], [], [], []
+        H = self.model_cfg.hidden_size
+        zero = torch.zeros(1, H, device=dev, dtype=self.cfg.dtype)
+        for r in reqs:
+            st = self._state(r)
+            n = r.total_len
+            toks = r.all_tokens()
+            p0 = min(st.draft_len, n - 1)
+            blk = np.asarray(r.blocks, np.int64)
+            ps = np.arange(p0, n)
+            pos.extend(ps.tolist())
+            slots.extend((blk[ps // bs] * bs + ps % bs).tolist())
+            ids.extend(toks[p0:n])
+            cu.append(cu[-1] + len(ps))
+            ctx.append(n)
+            brows.append(r.blocks)
+            # feature of position p-1 for every row p
+            for p in ps.tolist():
+                q = p - 1
+                if st.feat is not None and st.feat_start <= q < st.feat_start + st.feat.shape[0]:
+                    feat_rows.append(st.feat[q - st.feat_start: q - st.feat_start + 1])
+                else:
+                    feat_rows.append(zero)
+        meta = _varlen_meta(run, pos, slots, brows, cu, ctx, dev)
+        d_ids = torch.tensor(ids, dtype=torch.long).pin_memory().to(dev, non_blocking=True) \
+            if dev.type == "cuda" else torch.tensor(ids, dtype=torch.long)
+        g = self.draft.forward(d_ids, torch.cat(feat_rows), meta)
+        last = torch.tensor(cu[1:], device=dev) - 1
+        g_root = g.index_select(0, last)                         # [R, H]
+        for r in reqs:
+            r.spec_state.draft_len = r.total_len
+        # ---- 2) tree drafting
+        lp = self.draft.logprobs(g_root)                         # [R, V]
+        v1, t1 = ops.topk(lp, K)
+        tok = torch.zeros(R, N, dtype=torch.long, device=dev)
+        par = torch.full((R, N), -1, dtype=torch.int32, device=dev)
+        score = torch.zeros(R, N, dtype=torch.float32, device=dev)
+        G = torch.zeros(R, N, H, dtype=g.dtype, device=dev)
+        tok[:, 0] = torch.tensor([r.all_tokens()[-1] for r in reqs], device=dev)
+        G[:, 0] = g_root
+        tok[:, 1:W + 1] = t1[:, :W].long()
+        par[:, 1:W + 1] = 0
+        score[:, 1:W + 1] = v1[:, :W].float()
+        n_vec = np.asarray([r.total_len for r in reqs], np.int64)
+        depth_np = np.concatenate([[0]] + [[d] * W for d in range(1, D + 1)])
+        for d in range(2, D + 1):
+            m = W * (d - 1)                                       # nodes 1..m (depths 1..d-1)
+            cpar = par[:, 1:m + 1] - 1                            # chunk-local parents (root -> -1)
+            cpar = torch.where(cpar < 0, torch.full_like(cpar, -1), cpar)
+            anc, _ = ops.tree_mask(cpar.contiguous())
+            cpos, cslots, cctx, ccu = [], [], [], [0]
+            for i, r in enumerate(reqs):
+                n = int(n_vec[i])
+                blk = np.asarray(r.blocks, np.int64)
+                ps = n - 1 + depth_np[1:m + 1]
+                sl = n + np.arange(m)
+                cpos.extend(ps.tolist())
+                cslots.extend((blk[sl // bs] * bs + sl % bs).tolist())
+                cctx.append(n + m)
+                ccu.append(ccu[-1] + m)
+            cm = _varlen_meta(run, cpos, cslots, brows, ccu, cctx, dev, tree_mask=anc, tree_n=m)
+            pidx = par[:, 1:m + 1].long()                          # parents of chunk nodes
+            hin = torch.gather(G, 1, pidx[:, :, None].expand(R, m, H)).reshape(R * m, H)
+            gc = self.draft.forward(tok[:, 1:m + 1].reshape(-1), hin, cm).view(R, m, H)
+            G[:, 1:m + 1] = gc
+            fr = torch.arange(m - W + 1, m + 1, device=dev)        # frontier = depth d-1 nodes
+            lpf = self.draft.logprobs(gc[:, m - W:].reshape(R * W, H))
+            vf, tf = ops.topk(lpf, K)                              # [R*W, K]
+            cand = (score[:, fr][:, :, None] + vf.view(R, W, K).float()).view(R, W * K)
+            best, bi = torch.topk(cand, W, dim=1)
+            base = 1 + W * (d - 1)
+            tok[:, base: base + W] = torch.gather(tf.view(R, W * K).long(), 1, bi)
+            par[:, base: base + W] = fr[bi // K].int()
+            score[:, base: base + W] = best
+        self.spec_stats["draft_s"] += time.perf_counter() - td
+        tv = time.perf_counter()
+        # ---- 3) target verify over all N tree nodes
+        anc, depth = ops.tree_mask(par)
+        vpos, vslots, vctx, vcu = [], [], [], [0]
+        for i, r in enumerate(reqs):
+            n = int(n_vec[i])
+            blk = np.asarray(r.blocks, np.int64)
+            vpos.extend((n - 1 + depth_np).tolist())
+            sl = n - 1 + np.arange(N)
+            vslots.extend((blk[sl // bs] * bs + sl % bs).tolist())
+            vctx.append(n - 1 + N)
+            vcu.append(vcu[-1] + N)
+        vm = _varlen_meta(run, vpos, vslots, brows, vcu, vctx, dev, tree_mask=anc, tree_n=N)
+        logits, feats = self._forward_capture(vm, tok.view(-1))
+        tgt = logits.argmax(dim=-1).view(R, N)
+        acc, path, toks = ops.tree_verify(par, tok, tgt, anc, depth, D + 1)
+        acc_h = acc.cpu().tolist()
+        path_h = path.cpu().numpy()
+        toks_h = toks.cpu().numpy()
+        # ---- 4) compact accepted KV, keep their features, commit tokens
+        src, dst = [], []
+        fsel = []
+        for i, r in enumerate(reqs):
+            n = int(n_vec[i])
+            a = acc_h[i]
+            blk = np.asarray(r.blocks, np.int64)
+            for k in range(1, a + 1):
+                s_, d_ = n - 1 + int(path_h[i, k]), n - 1 + k
+                if s_ != d_:
+                    src.append(int(blk[s_ // bs] * bs + s_ % bs))
+                    dst.append(int(blk[d_ // bs] * bs + d_ % bs))
+            fsel.extend((i * N + path_h[i, : a + 1]).tolist())
+        if src:
+            kv_slot_copy(self.model.kv_cache, torch.tensor(src, device=dev), torch.tensor(dst, device=dev), bs)
+        fkeep = feats.index_select(0, torch.tensor(fsel, device=dev))
+        self.spec_stats["verify_s"] += time.perf_counter() - tv
+        outs = []
+        now = time.perf_counter()
+        st_all = self.stats
+        st_all["steps"] += 1
+        o = 0
+        for i, r in enumerate(reqs):
+            n = int(n_vec[i])
+            a = acc_h[i]
+            st = r.spec_state
+            st.feat, st.feat_start = fkeep[o: o + a + 1], n - 1
+            o += a + 1
+            r.num_computed = n + a
+            st_all["decode_tokens"] += a + 1
+            self.spec_stats["accepted"] += a
+            for k in range(a + 1):
+                t = int(toks_h[i, k])
+                r.output.append(t)
+                r.token_times.append(now)
+                st_all["generated"] += 1
+                self.spec_stats["spec_tokens"] += 1
+                reason = self._check_stop(r, t)
+                if reason is not None:
+                    self.scheduler.finish(r, reason)
+                    st_all["finished"] += 1
+                    self.requests.pop(r.rid, None)
+                outs.append(StepOutput(r.rid, t, reason is not None, reason, r))
+                if reason is not None:
+                    break
+        self.spec_stats["spec_steps"] += 1
+        self.spec_stats["spec_rows"] += R
+        return outs
+
+    def acceptance(self) -> dict:
+        s = self.spec_stats
+        rows = max(1, s["spec_rows"])
+        return {"mean_accepted": s["accepted"] / rows, "tokens_per_step": s["spec_tokens"] / rows, **s}
+
+
+# ---------------------------------------------------------------------------
+# self-distillation of the draft head (EAGLE-style, with training-time unroll)
+# ---------------------------------------------------------------------------
+
+def collect_features(engine: SpecEngine, seqs: torch.Tensor) -> tuple:
+    """Teacher-forced target pass over token sequences [B, S] -> (raw features [B,S,3H], target argmax [B,S])."""
+    run = engine.runner
+    B, S = seqs.shape
+    dev = engine.device
+    pool = engine.pool
+    bs = pool.block_size
+    need = (S + bs - 1) // bs
+    feats, tgts = [], []
+    for b in range(B):
+        blocks = pool.allocate(need)
+        try:
+            ps = np.arange(S)
+            blk = np.asarray(blocks, np.int64)
+            meta = _varlen_meta(run, ps.tolist(), (blk[ps // bs] * bs + ps % bs).tolist(), [blocks], [0, S], [S],
+                                dev)
+            with torch.inference_mode():
+                logits, f = engine._forward_capture(meta, seqs[b].to(dev), fuse=False)
+            feats.append(f.clone())
+            tgts.append(logits.argmax(-1))
+        finally:
+            pool.free(blocks)
+    return torch.stack(feats), torch.stack(tgts)
+
+
+def generate_corpus(engine: LLMEngine, num_seqs: int, prompt_len: int, gen_len: int, seed: int = 0) -> torch.Tensor:
+    """Random prompts continued greedily by the target -> token sequences [num_seqs, prompt_len + gen_len]."""
+    from dgi.sched.request import SamplingParams
+    g = torch.Generator().manual_seed(seed)
+    V = engine.model_cfg.vocab_size
+    lo = min(1000, V // 4)
+    prompts = [torch.randint(lo, V, (prompt_len,), generator=g).tolist() for _ in range(num_seqs)]
+    reqs = [engine.add_request(p, SamplingParams(max_tokens=gen_len, temperature=0.0, ignore_eos=True))
+            for p in prompts]
+    while engine.has_unfinished():
+        LLMEngine.step(engine)
+    return torch.tensor([r.prompt + r.output[:gen_len] for r in reqs], dtype=torch.long)
+
+
+def train_draft(engine: SpecEngine, steps: int = 200, batch: int = 8, prompt_len: int = 64, gen_len: int = 192,
+                unroll: int = 3, lr: float = 1e-3, num_seqs: int = 64, seed: int = 0, log=None) -> dict:
+    """Self-distil the draft head on the target's own greedy continuations.
+
+    A teacher-forced target pass gives the raw low|mid|high features f_p and
+    the target's next-token choice at every position.  Draft row p sees
+    (x_p, f_{p-1}) and must predict the target token after x_p; unroll step
+    k > 1 feeds the draft its own previous hidden instead of f (EAGLE-3
+    "training-time test"), matching how deeper tree levels are drafted."""
+    dr = engine.draft
+    dev = engine.device
+    g = torch.Generator().manual_seed(seed + 1)
+    V = engine.model_cfg.vocab_size
+    seqs = generate_corpus(engine, num_seqs, prompt_len, gen_len, seed)
+    feats, tgts = collect_features(engine, seqs)
+    P = {k: v.detach().clone().float().requires_grad_(True) for k, v in dr.parameters().items()}
+    opt = torch.optim.AdamW(list(P.values()), lr=lr, weight_decay=0.0)
+    S = seqs.shape[1]
+    pos0 = torch.arange(S, device=dev)[None]
+    hist = []
+    for it in range(steps):
+        idx = torch.randint(0, seqs.shape[0], (batch,), generator=g)
+        ids_k = seqs[idx].to(dev)
+        tg_k = tgts[idx.to(dev)]
+        Pb = {k: v.to(engine.cfg.dtype) for k, v in P.items()}
+        f = F.linear(feats[idx.to(dev)], Pb["fc"])
+        hid_k = torch.cat([torch.zeros_like(f[:, :1]), f[:, :-1]], 1)
+        pos_k = pos0.expand(batch, -1)
+        loss = 0.0
+        for k in range(unroll):
+            gk = dr.train_forward(Pb, ids_k, hid_k, pos_k)
+            lg = dr.train_logits(Pb, gk).float()
+            loss = loss + F.cross_entropy(lg.reshape(-1, V), tg_k.reshape(-1)) / unroll
+            if ids_k.shape[1] <= 1:
+                break
+            ids_k, hid_k, pos_k, tg_k = ids_k[:, 1:], gk[:, :-1], pos_k[:, 1:], tg_k[:, 1:]
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        hist.append(float(loss))
+        if log and (it % 50 == 0 or it == steps - 1):
+            log(f"draft step {it} loss {hist[-1]:.4f}")
+    with torch.no_grad():
+        dr.load({k: v.detach() for k, v in P.items()})
+    return {"loss_first": hist[0] if hist else None, "loss_last": hist[-1] if hist else None, "steps": steps,
+            "tokens": int(seqs.numel())}

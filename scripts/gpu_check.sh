@@ -29,6 +29,7 @@ for s in $STEPS; do
     gemm_tuned) run gemm_tuned 900 env PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=1 PYTORCH_TUNABLEOP_FILENAME=gpurun_out/tunableop_results.csv GEMM_MS=256,1280,2048 python scripts/gemm_bench.py 70b ;;
     sweep70b) for c in 256 384 512; do run sweep70b_c$c 900 python bench.py --steps 40 --warmup 10 --concurrency $c --json-out gpurun_out/sweep70b_c$c.json; done ;;
     sweep70b_mbt) run sweep70b_c384_mbt8k 900 python bench.py --steps 40 --warmup 10 --concurrency 384 --max-batched-tokens 8192 --json-out gpurun_out/sweep70b_c384_mbt8k.json ;;
+    spec8b) run spec8b 900 python scripts/bench_spec.py --out gpurun_out/spec8b.json ;;
     bench70b_long) run bench70b_long 1200 python bench.py --steps 200 --warmup 20 --json-out gpurun_out/bench70b_long.json ;;
   esac
 done

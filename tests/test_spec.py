@@ -1,0 +1,146 @@
+"""EAGLE-3 speculative decoding: lossless vs plain greedy, draft training raises
+acceptance, and the reference-compatible ``worker.engines.speculative`` API
+(mirrors reference tests/test_worker_engines_speculative.py)."""
+import asyncio
+
+import pytest
+import torch
+import torch.nn as nn
+
+from dgi.engine import EngineConfig, LLMEngine
+from dgi.sched.request import SamplingParams
+from dgi.spec.eagle3 import SpecConfig, SpecEngine, kv_slot_copy, train_draft
+
+
+def _engines(model="llama-tiny", device="cpu", spec=SpecConfig(depth=3, width=2, topk=3)):
+    cfg = EngineConfig(model=model, device=device, max_num_seqs=8, max_num_batched_tokens=256, max_model_len=512,
+                       use_graphs=False)
+    base = LLMEngine(cfg)
+    se = SpecEngine(cfg, spec)
+    se.model.copy_from(base.model)
+    return base, se
+
+
+def _prompts(n=3, V=500):
+    g = torch.Generator().manual_seed(0)
+    return [torch.randint(5, V, (L,), generator=g).tolist() for L in (7, 20, 33, 12)[:n]]
+
+
+def test_spec_is_lossless_and_training_raises_acceptance():
+    base, se = _engines()
+    sp = SamplingParams(max_tokens=24, temperature=0.0, ignore_eos=True)
+    ref = [r.output for r in base.generate(_prompts(), sp)]
+    assert [r.output for r in se.generate(_prompts(), sp)] == ref
+    before = se.acceptance()["mean_accepted"]
+    info = train_draft(se, steps=60, batch=8, prompt_len=16, gen_len=48, num_seqs=16)
+    assert info["loss_last"] < info["loss_first"]
+    se.spec_stats.update(spec_steps=0, spec_rows=0, accepted=0, spec_tokens=0)
+    assert [r.output for r in se.generate(_prompts(), sp)] == ref
+    after = se.acceptance()
+    assert after["mean_accepted"] > before + 0.5 and after["tokens_per_step"] > 1.5
+
+
+def test_spec_mixed_greedy_and_sampled_requests():
+    base, se = _engines()
+    g = SamplingParams(max_tokens=10, temperature=0.0, ignore_eos=True)
+    s = SamplingParams(max_tokens=10, temperature=0.8, top_k=0, top_p=1.0, ignore_eos=True, seed=7)
+    p = _prompts(2)
+    r0 = se.add_request(p[0], g)
+    r1 = se.add_request(p[1], s)
+    while se.has_unfinished():
+        se.step()
+    assert r0.output == base.generate([p[0]], g)[0].output
+    assert len(r1.output) == 10
+
+
+def test_kv_slot_copy():
+    kv = torch.randn(3, 2, 5, 2, 4, 8)
+    ref = kv.clone()
+    src, dst = torch.tensor([9, 13]), torch.tensor([5, 6])
+    kv_slot_copy(kv, src, dst, 4)
+    for s_, d_ in zip(src.tolist(), dst.tolist()):
+        ref[:, :, d_ // 4, :, d_ % 4] = ref[:, :, s_ // 4, :, s_ % 4]
+    assert torch.equal(kv, ref)
+
+
+@pytest.mark.gpu
+def test_spec_gpu_matches_plain_greedy():
+    base, se = _engines("llama-tiny-hd128", "cuda", SpecConfig(depth=4, width=3, topk=4))
+    sp = SamplingParams(max_tokens=32, temperature=0.0, ignore_eos=True)
+    prompts = _prompts(4, 1000)
+    ref = [r.output for r in base.generate(prompts, sp)]
+    assert [r.output for r in se.generate(prompts, sp)] == ref
+    train_draft(se, steps=80, batch=8, prompt_len=32, gen_len=96, num_seqs=32)
+    se.spec_stats.update(spec_steps=0, spec_rows=0, accepted=0, spec_tokens=0)
+    assert [r.output for r in se.generate(prompts, sp)] == ref
+    assert se.acceptance()["tokens_per_step"] > 1.3
+
+
+# ------------------------------------------------------------------ reference-compatible API
+def test_compat_config_output_defaults():
+    from worker.engines.speculative import SpeculativeConfig, SpeculativeOutput
+    c = SpeculativeConfig()
+    assert (c.draft_model_id, c.use_self_draft, c.draft_head_hidden_size, c.num_speculative_tokens) == \
+        (None, True, 1024, 5)
+    assert (c.tree_width, c.tree_depth, c.temperature, c.top_p, c.min_accept_rate, c.adaptive_depth) == \
+        (3, 5, 0.0, 1.0, 0.3, True)
+    nc = c.to_native()
+    assert nc.width == 3 and nc.depth == 5 and nc.num_nodes <= 64
+    o = SpeculativeOutput([1, 2], 0.5, 4, 2, 1.0)
+    assert o.accepted_tokens == 2
+
+
+def test_compat_draft_head_tree_buffer_medusa():
+    from worker.engines.speculative import DraftHead, MedusaHead, TreeDraftBuffer
+    d = DraftHead(hidden_size=64, vocab_size=100, num_layers=2, hidden_dim=32)
+    assert d.token_embedding is None
+    with pytest.raises(RuntimeError, match="Token embedding not set"):
+        d(torch.randn(1, 3, 64), torch.randint(0, 100, (1, 3)))
+    d.set_token_embedding(nn.Embedding(100, 64))
+    assert d(torch.randn(2, 5, 64), torch.randint(0, 100, (2, 5))).shape == (2, 5, 64)
+    b = TreeDraftBuffer(3, 5, "cpu")
+    b.add_candidates(torch.tensor([1, 2]), torch.tensor([-0.1, -0.2]), torch.tensor([-1, -1]))
+    b.add_candidates(torch.tensor([3, 4]), torch.tensor([-0.3, -0.4]), torch.tensor([0, 1]))
+    assert b.layer_offsets == [0, 2] and b.get_tree_tokens().tolist() == [1, 2, 3, 4]
+    m = b.get_tree_attention_mask(5)
+    assert m.shape == (4, 9) and m[:, :5].all() and m[2, 5] and not m[2, 6] and m[3, 6]
+    b.nodes = [(1, -0.1, -1), (2, -0.2, 0), (3, -0.3, 1), (4, -0.4, 2)]
+    assert b.trace_accepted_path(torch.tensor([True, True, False, False])) == [1, 2]
+    assert b.trace_accepted_path(torch.tensor([False, False, False, False])) == []
+    mh = MedusaHead(64, 100, num_heads=3, hidden_dim=16)
+    outs = mh(torch.randn(2, 4, 64))
+    assert len(outs) == 3 and outs[0].shape == (2, 4, 100)
+
+
+def test_compat_speculative_decoder_loop_and_stats():
+    from worker.engines.speculative import SpeculativeConfig, SpeculativeDecoder
+
+    class Tiny(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.model = nn.Module()
+            self.model.embed_tokens = nn.Embedding(50, 32)
+            self.lm_head = nn.Linear(32, 50)
+
+        def forward(self, input_ids, output_hidden_states=True, use_cache=False):
+            h = self.model.embed_tokens(input_ids).cumsum(1)
+            return type("O", (), {"logits": self.lm_head(h), "hidden_states": (h,)})()
+    torch.manual_seed(0)
+    tgt = Tiny()
+    dec = SpeculativeDecoder(tgt, SpeculativeConfig(tree_width=1, tree_depth=3), device="cpu")
+    dec.setup_draft_head(32, 50)
+    ids = torch.randint(0, 50, (1, 6))
+    out = asyncio.run(dec.generate(ids, max_new_tokens=8))
+    # lossless: equals plain greedy decoding of the target
+    cur = ids
+    ref = []
+    for _ in range(8):
+        nxt = tgt(cur).logits[0, -1].argmax()
+        ref.append(int(nxt))
+        cur = torch.cat([cur, nxt.view(1, 1)], 1)
+    assert out.tokens == ref
+    st = dec.get_stats()
+    assert st["total_steps"] >= 1 and st["speedup_estimate"] >= 1.0
+    dec._current_depth = 1
+    dec._adapt_depth(0.05)
+    assert dec._current_depth == 1

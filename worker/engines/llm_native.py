@@ -87,7 +87,18 @@ class NativeLLMEngine(LLMBaseEngine):
             enable_prefix_caching=bool(c.get("enable_prefix_caching", True)),
             use_graphs=bool(c.get("use_graphs", not c.get("enforce_eager", False))) and device != "cpu",
             seed=int(c.get("seed", 0)))
-        self.engine = LLMEngine(ecfg, model_cfg=mc)
+        spec = c.get("speculative")
+        if spec:
+            # EAGLE-3 tree speculation for greedy requests (dgi.spec.eagle3)
+            from dgi.spec.eagle3 import SpecConfig, SpecEngine
+            sc = spec if isinstance(spec, dict) else {}
+            self.engine = SpecEngine(ecfg, SpecConfig(**{k: sc[k] for k in ("depth", "width", "topk") if k in sc}),
+                                     model_cfg=mc)
+            if sc.get("draft_path"):
+                from safetensors.torch import load_file
+                self.engine.draft.load(load_file(sc["draft_path"], device=str(self.engine.device)))
+        else:
+            self.engine = LLMEngine(ecfg, model_cfg=mc)
         self.tokenizer = load_tokenizer(c.get("tokenizer", model_id), vocab_size=mc.vocab_size,
                                         bos=mc.bos_token_id, eos=mc.eos_token_id)
         self.device = device
