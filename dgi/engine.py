@@ -118,6 +118,7 @@ class LLMEngine:
 
     def step(self) -> list[StepOutput]:
         t0 = time.perf_counter()
+        self.model.kv_cache = self.pool.kv   # engines may share one model object
         sb = self.scheduler.schedule()
         if sb.empty:
             return []

@@ -224,6 +224,11 @@ class SpecEngine(LLMEngine):
         self.draft = draft or Eagle3Draft(self.model, self.pool.num_blocks, self.pool.block_size)
         self.spec_stats = {"spec_steps": 0, "spec_rows": 0, "accepted": 0, "spec_tokens": 0, "draft_s": 0.0,
                            "verify_s": 0.0}
+        # measurement aid: rid -> known greedy continuation; the depth-d node of
+        # the first chain is replaced by it (kept with probability oracle_accept)
+        self.oracle: Optional[dict] = None
+        self.oracle_accept = 1.0
+        self._oracle_rng = np.random.default_rng(0)
 
     # ------------------------------------------------------------------ helpers
     def _eligible(self, r: Request) -> bool:
@@ -256,6 +261,7 @@ class SpecEngine(LLMEngine):
     # ------------------------------------------------------------------ step
     def step(self) -> list:
         t0 = time.perf_counter()
+        self.model.kv_cache = self.pool.kv
         outs: list[StepOutput] = []
         spec_reqs = [r for r in self.scheduler.running if self._eligible(r)]
         for r in spec_reqs:
@@ -388,6 +394,8 @@ class SpecEngine(LLMEngine):
             tok[:, base: base + W] = torch.gather(tf.view(R, W * K).long(), 1, bi)
             par[:, base: base + W] = fr[bi // K].int()
             score[:, base: base + W] = best
+        if self.oracle:
+            self._apply_oracle(reqs, tok, par, n_vec)
         self.spec_stats["draft_s"] += time.perf_counter() - td
         tv = time.perf_counter()
         # ---- 3) target verify over all N tree nodes
@@ -457,6 +465,24 @@ class SpecEngine(LLMEngine):
         self.spec_stats["spec_rows"] += R
         return outs
 
+    def _apply_oracle(self, reqs, tok, par, n_vec) -> None:
+        W, D = self.spec.width, self.spec.depth
+        V = self.model_cfg.vocab_size
+        rows = np.zeros((len(reqs), D), np.int64)
+        for i, r in enumerate(reqs):
+            fut = self.oracle.get(r.rid, [])
+            base = int(n_vec[i]) - len(r.prompt)        # output index of the depth-1 token
+            for d in range(D):
+                t = fut[base + d] if base + d < len(fut) else 0
+                if self._oracle_rng.random() >= self.oracle_accept:
+                    t = int(self._oracle_rng.integers(0, V))
+                rows[i, d] = t
+        chain = torch.from_numpy(rows).to(tok.device)
+        for d in range(1, D + 1):
+            node = 1 + W * (d - 1)                        # first node of depth d
+            tok[:, node] = chain[:, d - 1]
+            par[:, node] = 0 if d == 1 else 1 + W * (d - 2)
+
     def acceptance(self) -> dict:
         s = self.spec_stats
         rows = max(1, s["spec_rows"])
@@ -507,19 +533,27 @@ def generate_corpus(engine: LLMEngine, num_seqs: int, prompt_len: int, gen_len: 
 
 
 def train_draft(engine: SpecEngine, steps: int = 200, batch: int = 8, prompt_len: int = 64, gen_len: int = 192,
-                unroll: int = 3, lr: float = 1e-3, num_seqs: int = 64, seed: int = 0, log=None) -> dict:
+                unroll: int = 3, lr: float = 1e-3, num_seqs: int = 64, random_seqs: int = 0, seed: int = 0,
+                log=None) -> dict:
     """Self-distil the draft head on the target's own greedy continuations.
 
     A teacher-forced target pass gives the raw low|mid|high features f_p and
     the target's next-token choice at every position.  Draft row p sees
     (x_p, f_{p-1}) and must predict the target token after x_p; unroll step
     k > 1 feeds the draft its own previous hidden instead of f (EAGLE-3
-    "training-time test"), matching how deeper tree levels are drafted."""
+    "training-time test"), matching how deeper tree levels are drafted.
+    ``random_seqs`` adds teacher-forced uniformly random token sequences so
+    the draft sees the whole vocabulary, not only the tokens the target's
+    own continuations happen to visit."""
     dr = engine.draft
     dev = engine.device
     g = torch.Generator().manual_seed(seed + 1)
     V = engine.model_cfg.vocab_size
     seqs = generate_corpus(engine, num_seqs, prompt_len, gen_len, seed)
+    if random_seqs:
+        lo = min(1000, V // 4)
+        rnd = torch.randint(lo, V, (random_seqs, seqs.shape[1]), generator=torch.Generator().manual_seed(seed + 7))
+        seqs = torch.cat([seqs, rnd])
     feats, tgts = collect_features(engine, seqs)
     P = {k: v.detach().clone().float().requires_grad_(True) for k, v in dr.parameters().items()}
     opt = torch.optim.AdamW(list(P.values()), lr=lr, weight_decay=0.0)
@@ -545,10 +579,35 @@ def train_draft(engine: SpecEngine, steps: int = 200, batch: int = 8, prompt_len
         opt.zero_grad(set_to_none=True)
         loss.backward()
         opt.step()
-        hist.append(float(loss))
+        hist.append(float(loss.detach()))
         if log and (it % 50 == 0 or it == steps - 1):
             log(f"draft step {it} loss {hist[-1]:.4f}")
     with torch.no_grad():
         dr.load({k: v.detach() for k, v in P.items()})
     return {"loss_first": hist[0] if hist else None, "loss_last": hist[-1] if hist else None, "steps": steps,
             "tokens": int(seqs.numel())}
+
+
+@torch.inference_mode()
+def greedy_gap(engine: LLMEngine, prompt: list, output: list) -> float:
+    """Largest (max logit - chosen logit) over the generated tokens under a
+    teacher-forced target pass: 0 for an exact greedy trajectory, small
+    positive values only at bf16 near-ties (different kernels may order such
+    ties differently)."""
+    seq = list(prompt) + list(output)
+    S = len(seq) - 1
+    pool, run, bs = engine.pool, engine.runner, engine.pool.block_size
+    blocks = pool.allocate((S + bs - 1) // bs)
+    try:
+        ps = np.arange(S)
+        blk = np.asarray(blocks, np.int64)
+        meta = _varlen_meta(run, ps.tolist(), (blk[ps // bs] * bs + ps % bs).tolist(), [blocks], [0, S], [S],
+                            engine.device)
+        ids = torch.tensor(seq[:S], dtype=torch.long, device=engine.device)
+        logits = engine.model.forward(meta, input_ids=ids).float()
+    finally:
+        pool.free(blocks)
+    rows = logits[len(prompt) - 1:]
+    chosen = torch.tensor(output, device=rows.device)
+    gap = rows.max(-1).values - rows.gather(1, chosen[:, None])[:, 0]
+    return float(gap.max())

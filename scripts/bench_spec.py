@@ -22,7 +22,7 @@ import torch  # noqa: E402
 
 from dgi.engine import EngineConfig, LLMEngine  # noqa: E402
 from dgi.sched.request import SamplingParams  # noqa: E402
-from dgi.spec.eagle3 import SpecConfig, SpecEngine, train_draft  # noqa: E402
+from dgi.spec.eagle3 import SpecConfig, SpecEngine, greedy_gap, train_draft  # noqa: E402
 
 
 def timed_generate(eng, prompts, sp):
@@ -44,14 +44,16 @@ def main():
     ap.add_argument("--topk", type=int, default=4)
     ap.add_argument("--train-steps", type=int, default=300)
     ap.add_argument("--train-seqs", type=int, default=64)
+    ap.add_argument("--random-seqs", type=int, default=192)
+    ap.add_argument("--oracle-accept", type=float, nargs="*", default=[0.6, 0.8, 1.0])
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     cfg = EngineConfig(model=a.model, device="cuda", max_num_seqs=64, max_num_batched_tokens=8192,
                        max_model_len=2048, kv_fraction=0.5)
     spec = SpecEngine(cfg, SpecConfig(depth=a.depth, width=a.width, topk=a.topk))
     t0 = time.perf_counter()
-    info = train_draft(spec, steps=a.train_steps, batch=8, prompt_len=64, gen_len=192, num_seqs=a.train_seqs,
-                       log=lambda m: print(m, flush=True))
+    info = train_draft(spec, steps=a.train_steps, batch=16, prompt_len=64, gen_len=192, num_seqs=a.train_seqs,
+                       random_seqs=a.random_seqs, log=lambda m: print(m, flush=True))
     info["train_seconds"] = round(time.perf_counter() - t0, 1)
     print("draft training", info, flush=True)
     base = LLMEngine(cfg, model=spec.model)
@@ -69,10 +71,33 @@ def main():
         out, t_spec = timed_generate(spec, prompts, sp)
         acc = spec.acceptance()
         toks = B * a.output_len
+        gap = max(greedy_gap(spec, p, o) for p, o in zip(prompts, out))
         row = {"batch": B, "plain_tok_s": round(toks / t_base, 1), "spec_tok_s": round(toks / t_spec, 1),
                "speedup": round(t_base / t_spec, 3), "mean_accepted": round(acc["mean_accepted"], 3),
                "tokens_per_step": round(acc["tokens_per_step"], 3), "identical": out == ref,
+               "max_greedy_gap": round(gap, 4),
                "draft_s": round(acc["draft_s"], 3), "verify_s": round(acc["verify_s"], 3)}
+        # acceptance-controlled runs: the first tree chain is replaced by the known greedy
+        # continuation, each token kept with probability p (ceiling / sensitivity of the machinery)
+        for p in a.oracle_accept:
+            reqs_rid = {}
+            spec.oracle = reqs_rid
+            spec.oracle_accept = p
+            rs = [spec.add_request(pr, sp) for pr in prompts]
+            for r, o in zip(rs, ref):
+                reqs_rid[r.rid] = o
+            spec.spec_stats.update(spec_steps=0, spec_rows=0, accepted=0, spec_tokens=0, draft_s=0.0, verify_s=0.0)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            while spec.has_unfinished():
+                spec.step()
+            torch.cuda.synchronize()
+            t_o = time.perf_counter() - t1
+            spec.oracle = None
+            ao = spec.acceptance()
+            row[f"oracle_p{p}"] = {"tok_s": round(toks / t_o, 1), "speedup": round(t_base / t_o, 3),
+                                   "mean_accepted": round(ao["mean_accepted"], 3),
+                                   "identical": [r.output for r in rs] == ref}
         print(json.dumps(row), flush=True)
         rows.append(row)
     res = {"model": a.model, "tree": {"depth": a.depth, "width": a.width, "topk": a.topk},

@@ -64,15 +64,19 @@ def test_kv_slot_copy():
 
 
 @pytest.mark.gpu
-def test_spec_gpu_matches_plain_greedy():
+def test_spec_gpu_greedy_trajectory():
+    """Spec output is a greedy trajectory of the target.  Plain decode (decode
+    kernel) and verification (prefill kernel) may order bf16 near-ties
+    differently, so exact equality is checked via the teacher-forced gap."""
+    from dgi.spec.eagle3 import greedy_gap
     base, se = _engines("llama-tiny-hd128", "cuda", SpecConfig(depth=4, width=3, topk=4))
     sp = SamplingParams(max_tokens=32, temperature=0.0, ignore_eos=True)
     prompts = _prompts(4, 1000)
-    ref = [r.output for r in base.generate(prompts, sp)]
-    assert [r.output for r in se.generate(prompts, sp)] == ref
-    train_draft(se, steps=80, batch=8, prompt_len=32, gen_len=96, num_seqs=32)
+    train_draft(se, steps=80, batch=8, prompt_len=32, gen_len=96, num_seqs=32, random_seqs=32)
     se.spec_stats.update(spec_steps=0, spec_rows=0, accepted=0, spec_tokens=0)
-    assert [r.output for r in se.generate(prompts, sp)] == ref
+    outs = [r.output for r in se.generate(prompts, sp)]
+    for p, o in zip(prompts, outs):
+        assert len(o) == 32 and greedy_gap(se, p, o) < 0.07   # bf16 logit resolution near |logit|~8
     assert se.acceptance()["tokens_per_step"] > 1.3
 
 
@@ -144,3 +148,19 @@ def test_compat_speculative_decoder_loop_and_stats():
     dec._current_depth = 1
     dec._adapt_depth(0.05)
     assert dec._current_depth == 1
+
+
+def test_oracle_chain_acceptance_ceiling():
+    """With the known greedy continuation as the first chain, every depth is accepted."""
+    base, se = _engines(spec=SpecConfig(depth=4, width=2, topk=3))
+    sp = SamplingParams(max_tokens=24, temperature=0.0, ignore_eos=True)
+    prompts = _prompts()
+    ref = [r.output for r in base.generate(prompts, sp)]
+    se.oracle, se.oracle_accept = {}, 1.0
+    rs = [se.add_request(p, sp) for p in prompts]
+    for r, o in zip(rs, ref):
+        se.oracle[r.rid] = o
+    while se.has_unfinished():
+        se.step()
+    assert [r.output for r in rs] == ref
+    assert se.acceptance()["mean_accepted"] > 3.0
