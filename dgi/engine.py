@@ -38,6 +38,7 @@ class EngineConfig:
     workspace_bytes: int = 8 << 30
     layer_start: int = 0
     layer_end: Optional[int] = None
+    host_kv_gb: float = 0.0            # pinned host KV tier for evicted prefix pages (0 = off)
 
 
 @dataclasses.dataclass
@@ -90,6 +91,13 @@ class LLMEngine:
                               cfg.dtype, self.device)
         self.scheduler = Scheduler(self.pool, SchedulerConfig(cfg.max_num_seqs, cfg.max_num_batched_tokens,
                                                               cfg.max_model_len, cfg.enable_prefix_caching))
+        self.host_tier = None
+        if cfg.host_kv_gb > 0 and cfg.enable_prefix_caching:
+            from dgi.kv.host_tier import HostKVTier
+            from dgi.kv.radix_cache import RadixCache
+            cap = max(1, int(cfg.host_kv_gb * (1 << 30) // self.pool.page_bytes()))
+            self.host_tier = HostKVTier(self.pool, cap)
+            self.scheduler.radix = RadixCache(self.pool, self.host_tier)
         self.runner = ModelRunner(self.model, self.pool, cfg.max_num_seqs, cfg.max_model_len,
                                   cfg.max_num_batched_tokens, cfg.use_graphs)
         self.requests: dict = {}

@@ -15,6 +15,11 @@ reference (Appendix E-12).  Here a radix tree whose edges are full KV blocks
 Block granularity (not token granularity) matches the paged attention
 kernels: a hit skips whole pages of prefill and the partially filled tail
 page is always private to its sequence (no copy-on-write needed for it).
+
+With a ``HostKVTier`` attached, eviction *spills* LRU pages to pinned host
+memory instead of dropping them (the node stays in the tree with
+``block == -1``); a later match restores them into fresh GPU pages.  Only
+when the host tier is full are host-resident leaves dropped.
 """
 from __future__ import annotations
 
@@ -26,11 +31,12 @@ from dgi.kv.block_pool import BlockPool
 
 
 class _Node:
-    __slots__ = ("key", "block", "children", "parent", "last", "lock")
+    __slots__ = ("key", "block", "host", "children", "parent", "last", "lock")
 
     def __init__(self, key, block, parent):
         self.key = key
-        self.block = block
+        self.block = block      # GPU page id, -1 while the page lives in the host tier
+        self.host = -1          # host-tier slot
         self.children: dict = {}
         self.parent = parent
         self.last = time.monotonic()
@@ -38,8 +44,10 @@ class _Node:
 
 
 class RadixCache:
-    def __init__(self, pool: BlockPool):
+    def __init__(self, pool: BlockPool, host_tier=None):
         self.pool = pool
+        self.host = host_tier
+        self.host_hits_blocks = 0
         self.bs = pool.block_size
         self.root = _Node(None, -1, None)
         self.num_nodes = 0
@@ -65,6 +73,9 @@ class RadixCache:
             blocks.append(child.block)
             path.append(child)
             node = child
+        if any(n.block < 0 for n in path):
+            path = self._restore(path)
+            blocks = [n.block for n in path]
         if lock:
             for n in path:
                 n.lock += 1
@@ -72,6 +83,28 @@ class RadixCache:
         self.query_tokens += len(tokens)
         self.hits_tokens += len(blocks) * bs
         return blocks, path
+
+    def _restore(self, path: list) -> list:
+        """Bring host-resident pages of ``path`` back to the GPU (truncating the
+        match at the first page that cannot be restored)."""
+        for n in path:
+            n.lock += 1                      # keep the path out of eviction while allocating
+        try:
+            need = [n for n in path if n.block < 0]
+            try:
+                fresh = self.pool.allocate(len(need))
+            except Exception:
+                cut = path.index(need[0])
+                return path[:cut]
+            self.host.restore([n.host for n in need], fresh)
+            self.host.release([n.host for n in need])
+            for n, b in zip(need, fresh):
+                n.block, n.host = b, -1
+            self.host_hits_blocks += len(need)
+            return path
+        finally:
+            for n in path:
+                n.lock -= 1
 
     def release(self, path: list) -> None:
         for n in path:
@@ -94,12 +127,18 @@ class RadixCache:
                 self.pool.incref([blocks[j]])
                 self.num_nodes += 1
                 new += 1
+            elif child.block < 0:             # page was spilled: adopt the recomputed copy
+                child.block = blocks[j]
+                self.pool.incref([blocks[j]])
+                self.host.release([child.host])
+                child.host = -1
             child.last = now
             node = child
         return new
 
     # ------------------------------------------------------------------ evict
     def _evictable_leaves(self):
+        """Unpinned GPU-resident nodes none of whose children hold a GPU page."""
         out = []
         stack = [self.root]
         while stack:
@@ -107,33 +146,74 @@ class RadixCache:
             for c in n.children.values():
                 if c.children:
                     stack.append(c)
-                elif c.lock == 0:
+                if c.block >= 0 and c.lock == 0 and all(g.block < 0 for g in c.children.values()):
                     out.append(c)
         return out
 
+    def _drop_host_leaves(self, n: int) -> int:
+        """Free host slots by deleting LRU host-resident leaves."""
+        cands = []
+        stack = [self.root]
+        while stack:
+            x = stack.pop()
+            for c in x.children.values():
+                stack.append(c)
+                if c.block < 0 and not c.children and c.lock == 0:
+                    cands.append(c)
+        cands.sort(key=lambda c: c.last)
+        dropped = 0
+        for c in cands[:n]:
+            del c.parent.children[c.key]
+            self.host.release([c.host])
+            self.num_nodes -= 1
+            dropped += 1
+        self.host.stats["dropped"] += dropped
+        return dropped
+
     def evict(self, n: int) -> int:
-        """Free >= n blocks from unpinned LRU leaves.  n == 0: report capacity."""
+        """Free >= n GPU blocks from unpinned LRU leaves.  n == 0: report capacity."""
         if n == 0:
             return sum(1 for c in self._evictable_leaves() if self.pool.ref[c.block] == 1)
         freed = 0
         while freed < n:
-            leaves = [c for c in self._evictable_leaves()]
+            leaves = [c for c in self._evictable_leaves() if self.pool.ref[c.block] == 1] if self.host is not None \
+                else [c for c in self._evictable_leaves()]
             if not leaves:
                 break
             leaves.sort(key=lambda c: c.last)
-            progressed = False
-            for c in leaves:
-                if freed >= n:
+            victims = leaves[: max(1, n - freed)]
+            if self.host is not None:
+                if self.host.num_free < len(victims):
+                    self._drop_host_leaves(len(victims) - self.host.num_free)
+                victims = victims[: self.host.num_free]
+            if not victims:
+                # host tier cannot take more: fall back to dropping GPU leaves
+                victims = [c for c in leaves if not c.children][: max(1, n - freed)]
+                if not victims:
                     break
-                del c.parent.children[c.key]
-                self.num_nodes -= 1
-                if self.pool.ref[c.block] == 1:
+                for c in victims:
+                    del c.parent.children[c.key]
+                    self.num_nodes -= 1
+                    if self.pool.ref[c.block] == 1:
+                        freed += 1
+                    self.pool.free([c.block])
+                    self.evicted += 1
+                continue
+            if self.host is not None:
+                slots = self.host.spill([c.block for c in victims])
+                for c, s_ in zip(victims, slots):
+                    self.pool.free([c.block])
+                    c.block, c.host = -1, s_
                     freed += 1
-                self.pool.free([c.block])
-                self.evicted += 1
-                progressed = True
-            if not progressed:
-                break
+                    self.evicted += 1
+            else:
+                for c in victims:
+                    del c.parent.children[c.key]
+                    self.num_nodes -= 1
+                    if self.pool.ref[c.block] == 1:
+                        freed += 1
+                    self.pool.free([c.block])
+                    self.evicted += 1
         self.pool.stats["evictions"] += freed
         return freed
 
@@ -146,6 +226,9 @@ class RadixCache:
             n = stack.pop()
             for c in n.children.values():
                 stack.append(c)
-                self.pool.free([c.block])
+                if c.block >= 0:
+                    self.pool.free([c.block])
+                elif self.host is not None:
+                    self.host.release([c.host])
         self.root = _Node(None, -1, None)
         self.num_nodes = 0

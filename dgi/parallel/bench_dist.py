@@ -14,6 +14,7 @@ all ranks; tokens are summed over ranks and the elapsed time is the max.
 """
 from __future__ import annotations
 
+import os
 import random
 import time
 
@@ -37,10 +38,13 @@ def run_distributed(args, layout_kind: str, dist):
     rank, world = f.rank, f.world
     layout = plan_node_layout(world, layout_kind, getattr(args, "prefill_ranks", None) or None)
     conc = args.concurrency or 512
+    # staged rehearsal: every rank shares one GPU, so each takes a slice of its memory
+    kv_frac = float(os.environ.get("DGI_KV_FRACTION", 0.5 / world if f.staged else 0.9))
     cfg = EngineConfig(model=args.model, device=str(f.device), max_num_seqs=conc,
                        max_num_batched_tokens=args.max_batched_tokens,
                        max_model_len=max(2048, args.prompt_len + args.output_len + 64),
-                       use_graphs=not args.no_graphs, seed=args.seed, enable_prefix_caching=False)
+                       use_graphs=not args.no_graphs, seed=args.seed, enable_prefix_caching=False,
+                       kv_fraction=kv_frac)
     sp = SamplingParams(max_tokens=args.output_len, temperature=0.0, ignore_eos=True)
     rng = random.Random(777 + rank)
     role = layout.role(rank)

@@ -1,0 +1,84 @@
+"""Pinned host KV tier under the radix cache: spill on eviction, restore on hit."""
+import pytest
+import torch
+
+from dgi.engine import EngineConfig, LLMEngine
+from dgi.kv.block_pool import BlockPool
+from dgi.kv.host_tier import HostKVTier
+from dgi.kv.radix_cache import RadixCache
+from dgi.sched.request import SamplingParams
+
+
+def _pool(nb=9, device="cpu"):
+    p = BlockPool(nb, 4, num_layers=2, num_kv_heads=1, head_dim=8, dtype=torch.float32, device=device)
+    p.kv.copy_(torch.randn_like(p.kv))
+    return p
+
+
+def test_spill_and_restore_roundtrip():
+    pool = _pool()
+    tier = HostKVTier(pool, 8)
+    rc = RadixCache(pool, tier)
+    toks = list(range(16))                       # 4 full blocks
+    blocks = pool.allocate(4)
+    want = pool.kv[:, :, blocks].clone()
+    rc.insert(toks, blocks)
+    pool.free(blocks)                            # only the cache holds them now
+    assert rc.evict(4) == 4                      # all spilled, GPU pages free
+    assert tier.stats["spilled"] == 4 and pool.num_free == 8
+    pool.kv.zero_()
+    got, path = rc.match(toks + [99])
+    assert len(got) == 4 and rc.host_hits_blocks == 4
+    assert torch.equal(pool.kv[:, :, got], want)
+    rc.release(path)
+    pool.free(got)
+
+
+def test_host_full_drops_lru_leaves():
+    pool = _pool()
+    tier = HostKVTier(pool, 2)
+    rc = RadixCache(pool, tier)
+    for base in (0, 100):
+        b = pool.allocate(2)
+        rc.insert(list(range(base, base + 8)), b)
+        pool.free(b)
+    assert rc.evict(4) >= 2
+    assert tier.num_free >= 0 and pool.num_free >= 6
+
+
+def test_engine_prefix_reuse_through_host_tier():
+    cfg = EngineConfig(model="llama-tiny", device="cpu", max_num_seqs=4, max_num_batched_tokens=128,
+                       max_model_len=256, use_graphs=False, num_blocks=24, host_kv_gb=0.01)
+    eng = LLMEngine(cfg)
+    ref = LLMEngine(EngineConfig(**{**cfg.__dict__, "host_kv_gb": 0.0, "enable_prefix_caching": False}),
+                    model=eng.model)
+    g = torch.Generator().manual_seed(1)
+    shared = torch.randint(5, 500, (64,), generator=g).tolist()
+    sp = SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True)
+    a = eng.generate([shared + [7, 8]], sp)[0].output
+    # unrelated traffic pushes the shared prefix out of the 24-page GPU pool
+    for i in range(6):
+        eng.generate([torch.randint(5, 500, (80,), generator=g).tolist()], sp)
+    assert eng.host_tier.stats["spilled"] > 0
+    b = eng.generate([shared + [9, 10]], sp)[0].output
+    assert eng.scheduler.radix.host_hits_blocks > 0
+    assert b == ref.generate([shared + [9, 10]], sp)[0].output
+    assert a == ref.generate([shared + [7, 8]], sp)[0].output
+
+
+@pytest.mark.gpu
+def test_host_tier_gpu_roundtrip():
+    pool = BlockPool(17, 16, num_layers=4, num_kv_heads=8, head_dim=128, dtype=torch.bfloat16, device="cuda")
+    pool.kv.copy_(torch.randn_like(pool.kv))
+    tier = HostKVTier(pool, 16)
+    rc = RadixCache(pool, tier)
+    toks = list(range(16 * 6))
+    blocks = pool.allocate(6)
+    want = pool.kv[:, :, blocks].clone()
+    rc.insert(toks, blocks)
+    pool.free(blocks)
+    assert rc.evict(6) == 6
+    pool.kv.zero_()
+    got, path = rc.match(toks + [1])
+    torch.cuda.synchronize()
+    assert torch.equal(pool.kv[:, :, got], want)
