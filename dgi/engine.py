@@ -57,6 +57,21 @@ def _device_free_bytes(device: torch.device) -> int:
     return 2 << 30
 
 
+def engine_block_budget(cfg: EngineConfig, mc: ModelConfig, n_local: int, device: torch.device) -> int:
+    """KV pages for this engine: ``kv_fraction`` of free HBM after weights and the
+    activation workspace, capped by what ``max_num_seqs`` full sequences can use."""
+    if cfg.num_blocks is not None:
+        return cfg.num_blocks
+    if device.type == "cuda":
+        budget = max(0, _device_free_bytes(device) - cfg.workspace_bytes) * cfg.kv_fraction
+    else:
+        budget = 1 << 30  # CPU rehearsal runs: a fixed 1 GiB pool
+    nblocks = num_blocks_for_budget(int(budget), max(1, n_local), mc.num_kv_heads, mc.head_dim, cfg.block_size)
+    # never more than what max_num_seqs full-length sequences can use (+ prefix cache room)
+    cap = 2 * cfg.max_num_seqs * ((cfg.max_model_len + cfg.block_size - 1) // cfg.block_size) + 1
+    return max(2, min(nblocks, cap))
+
+
 class LLMEngine:
     def __init__(self, cfg: EngineConfig, model_cfg: Optional[ModelConfig] = None, model=None):
         self.cfg = cfg
@@ -75,18 +90,7 @@ class LLMEngine:
         self.load_seconds = time.perf_counter() - t0
         mc = self.model_cfg
         n_local = self.model.num_local_layers
-        if cfg.num_blocks is not None:
-            nblocks = cfg.num_blocks
-        else:
-            if self.device.type == "cuda":
-                budget = max(0, _device_free_bytes(self.device) - cfg.workspace_bytes) * cfg.kv_fraction
-            else:
-                budget = 1 << 30  # CPU rehearsal runs: a fixed 1 GiB pool
-            nblocks = num_blocks_for_budget(int(budget), max(1, n_local), mc.num_kv_heads, mc.head_dim,
-                                            cfg.block_size)
-            # never more than what max_num_seqs full-length sequences can use (+ prefix cache room)
-            cap = 2 * cfg.max_num_seqs * ((cfg.max_model_len + cfg.block_size - 1) // cfg.block_size) + 1
-            nblocks = max(2, min(nblocks, cap))
+        nblocks = engine_block_budget(cfg, mc, n_local, self.device)
         self.pool = BlockPool(nblocks, cfg.block_size, max(1, n_local), mc.num_kv_heads, mc.head_dim,
                               cfg.dtype, self.device)
         self.scheduler = Scheduler(self.pool, SchedulerConfig(cfg.max_num_seqs, cfg.max_num_batched_tokens,

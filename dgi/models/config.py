@@ -104,6 +104,10 @@ PRESETS: dict[str, ModelConfig] = {
     "llama-tiny-hd128": ModelConfig(name="llama-tiny-hd128", vocab_size=1024, hidden_size=1024,
                                     intermediate_size=2048, num_layers=4, num_heads=8, num_kv_heads=1,
                                     head_dim=128, max_position=4096, bos_token_id=1, eos_token_id=2),
+    # GQA with 2 KV heads so tensor parallelism of degree 2 has a head per rank
+    "llama-tiny-tp": ModelConfig(name="llama-tiny-tp", vocab_size=1024, hidden_size=1024, intermediate_size=2048,
+                                 num_layers=2, num_heads=8, num_kv_heads=2, head_dim=128, max_position=4096,
+                                 bos_token_id=1, eos_token_id=2),
     "opt-125m": ModelConfig(name="opt-125m", arch="opt", vocab_size=50272, hidden_size=768,
                             intermediate_size=3072, num_layers=12, num_heads=12, num_kv_heads=12, head_dim=64,
                             max_position=2048, tie_embeddings=True, bos_token_id=2, eos_token_id=2),

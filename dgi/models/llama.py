@@ -62,6 +62,9 @@ class LlamaModel:
         # EAGLE-3 feature taps: global layer ids whose output residual stream is kept
         self.capture_layers: tuple = ()
         self.captured: dict = {}
+        # tensor parallelism: in-place sum of partial outputs across the TP group
+        # after the row-parallel O and down projections (dgi.parallel.tensor)
+        self.reduce = None
         if init == "random":
             self._init_random(seed)
         elif init == "empty":
@@ -203,10 +206,14 @@ class LlamaModel:
             qkv = F.linear(h, L.qkv)
             attn = self.attention(i, qkv, meta)
             h = F.linear(attn, L.o)
+            if self.reduce is not None:
+                self.reduce(h)
             ops.fused_add_rmsnorm(h, residual, L.post_norm, eps)
             gu = F.linear(h, L.gate_up)
             act = ops.silu_mul(gu)
             h = F.linear(act, L.down)
+            if self.reduce is not None:
+                self.reduce(h)
             if self.capture_layers and (self.layer_start + i) in self.capture_layers:
                 self.captured[self.layer_start + i] = h + residual
         return h, residual

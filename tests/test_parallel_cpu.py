@@ -171,3 +171,23 @@ def test_pd_migration_matches_local_decode(world):
     ref = _reference_outputs()
     out = _spawn("_pd_body", world)
     assert out[1] == ref
+
+
+def _tp_body(rank, world):
+    from dgi.engine import EngineConfig, LLMEngine
+    from dgi.parallel.tensor import TPEngine
+    from dgi.sched.request import SamplingParams
+    cfg = EngineConfig(model="llama-tiny-tp", device="cpu", max_num_seqs=4, max_num_batched_tokens=128,
+                       max_model_len=256, use_graphs=False)
+    g = torch.Generator().manual_seed(0)
+    prompts = [torch.randint(5, 1000, (n,), generator=g).tolist() for n in (9, 17, 30)]
+    sp = SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True)
+    out = [r.output for r in TPEngine(cfg, rank, world).generate(prompts, sp)]
+    if rank == 0:
+        ref = [r.output for r in LLMEngine(cfg).generate(prompts, sp)]
+        assert out == ref, (out, ref)
+    return out
+
+
+def test_tensor_parallel_matches_single_process():
+    _spawn("_tp_body", 2)
