@@ -37,7 +37,9 @@ def run_distributed(args, layout_kind: str, dist):
     f = Fabric()
     rank, world = f.rank, f.world
     layout = plan_node_layout(world, layout_kind, getattr(args, "prefill_ranks", None) or None)
-    conc = args.concurrency or 512
+    # decode-side concurrency: 2 x 512-row microbatches keep the decode GEMMs
+    # out of the small-M regime (70B down-proj costs the same at M=256 and 512)
+    conc = args.concurrency or 1024
     # staged rehearsal: every rank shares one GPU, so each takes a slice of its memory
     kv_frac = float(os.environ.get("DGI_KV_FRACTION", 0.5 / world if f.staged else 0.9))
     cfg = EngineConfig(model=args.model, device=str(f.device), max_num_seqs=conc,
@@ -163,19 +165,33 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
         return n, el, ttfts, {"migrated": srv.migrated, "migrate_s": round(srv.migrate_time, 3)}
 
     if role == "decode_driver":
-        drv = DecodeDriver(cfg, f, layout)
+        # single decode GPU: let it also serve local prompts with a slice of its pool
+        local_frac = float(getattr(args, "decode_local_frac", -1.0))
+        if local_frac < 0:
+            local_frac = 0.35 if layout.kind == "pd" else 0.0
+        drv = DecodeDriver(cfg, f, layout, local_fraction=local_frac)
         phases = [CtrlChannel(f, p, 4, tag="phase") for p in layout.prefill_ranks]
+        vocab = drv.engine.model_cfg.vocab_size
+        local_ttfts = []
+
+        def top_local():
+            while local_frac > 0 and drv.admit_local(_prompt(rng, args.prompt_len, vocab), sp) is not None:
+                pass
 
         def run_steps(k):
             """k productive decode steps (idle polling while nothing has arrived does not count)."""
             n = done = 0
             while done < k:
+                top_local()
                 if not drv.engine.has_unfinished():
                     drv.poll()
                     if not drv.engine.has_unfinished():
                         time.sleep(0.0005)
                         continue
-                n += len(drv.step())
+                for o in drv.step():
+                    n += 1
+                    if o.rid in drv.local_used and len(o.request.output) == 1:
+                        local_ttfts.append(o.request.ttft)
                 done += 1
             return n
 
@@ -192,6 +208,7 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
 
         boundary()
         t0 = time.perf_counter()
+        local_ttfts.clear()
         n = run_steps(args.steps)
         boundary()
         el = time.perf_counter() - t0
@@ -201,8 +218,8 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
             drv.poll()
             time.sleep(0.001)
         drv.finish()
-        return n, el, [], {"received": drv.received, "running_at_end": running,
-                           "recv_GB": round(drv.recv_bytes / 1e9, 3)}
+        return n, el, list(local_ttfts), {"received": drv.received, "running_at_end": running,
+                                          "recv_GB": round(drv.recv_bytes / 1e9, 3), "local_fraction": local_frac}
 
     # later decode pipeline stages
     w = StageWorker(cfg, f, layout.decode_ranks)

@@ -163,7 +163,8 @@ class PrefillServer:
 class DecodeDriver:
     """Decode side: single engine or stage 0 of the decode pipeline."""
 
-    def __init__(self, cfg: EngineConfig, fabric: Fabric, layout: NodeLayout, credit_margin: float = 0.02):
+    def __init__(self, cfg: EngineConfig, fabric: Fabric, layout: NodeLayout, credit_margin: float = 0.02,
+                 local_fraction: float = 0.0):
         self.f = fabric
         self.layout = layout
         dcfg = EngineConfig(**{**cfg.__dict__, "device": str(fabric.device), "enable_prefix_caching": False})
@@ -178,7 +179,13 @@ class DecodeDriver:
         self.bs = self.engine.pool.block_size
         self.prefill = list(layout.prefill_ranks)
         self.chans = {p: CtrlChannel(fabric, p, CTRL) for p in self.prefill}
-        total = int(self.engine.pool.num_free * (1.0 - credit_margin))
+        free = self.engine.pool.num_free
+        total = int(free * (1.0 - credit_margin - local_fraction))
+        # hybrid decode: a slice of the pool serves prompts admitted locally (mixed
+        # prefill+decode steps on the decode GPU) so it is never idle when the
+        # prefill side cannot saturate it; migrated sequences keep their credits
+        self.local_cap_blocks = int(free * local_fraction)
+        self.local_used: dict = {}
         P = max(1, len(self.prefill))
         share = total // P
         seq_share = max(1, cfg.max_num_seqs // P)
@@ -229,6 +236,17 @@ class DecodeDriver:
             k += nb
         self.received += n_reqs
 
+    def local_blocks_free(self) -> int:
+        return self.local_cap_blocks - sum(self.local_used.values())
+
+    def admit_local(self, prompt: list, params: SamplingParams) -> Optional[Request]:
+        need = _blocks_for(len(prompt) + params.max_tokens, self.bs)
+        if need > self.local_blocks_free():
+            return None
+        r = self.engine.add_request(prompt, params)
+        self.local_used[r.rid] = need
+        return r
+
     def poll(self) -> None:
         for p, ch in self.chans.items():
             while True:
@@ -245,6 +263,7 @@ class DecodeDriver:
         outs = self.engine.step() if self.engine.has_unfinished() else []
         for o in outs:
             if o.finished:
+                self.local_used.pop(o.rid, None)
                 p, credit = self.origin.pop(o.rid, (None, 0))
                 if p is not None:
                     self.refund[p] += credit

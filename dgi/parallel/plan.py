@@ -76,7 +76,14 @@ class NodeLayout:
 def plan_node_layout(n_gpus: int, kind: str = "pdpp", prefill_ranks: Optional[int] = None,
                      decode_stages: Optional[int] = None) -> NodeLayout:
     """Default P:D split for prefill-heavy loads (512-in/128-out on 70B: a
-    prefill costs ~5x the decode-GPU time of its 128 tokens)."""
+    prefill costs ~5x the decode-GPU time of its 128 tokens).
+
+    70B numbers behind the defaults (1 MI355X, hipBLASLt ~1.4 PF/s): a prefill
+    GPU turns ~18 prompts/s (4096-token steps) = ~2.3k output tok/s of demand;
+    one full-model decode GPU sustains ~8k tok/s (M ~ 600 rows/step, KV-bound),
+    a 2-stage decode pipeline ~13-15k tok/s (two 512-row microbatches).  So
+    below 8 GPUs a single decode GPU behind N-1 prefill GPUs is the balanced
+    layout; at 8 GPUs 6 prefill GPUs feed a 2-stage decode layer pipeline."""
     if n_gpus == 1 or kind == "single":
         return NodeLayout("single", [], [0])
     if kind == "pp":
@@ -84,7 +91,7 @@ def plan_node_layout(n_gpus: int, kind: str = "pdpp", prefill_ranks: Optional[in
     if kind == "dp":
         return NodeLayout("dp", [], [0], replicas=n_gpus)
     if decode_stages is None:
-        decode_stages = 2 if (kind == "pdpp" and n_gpus >= 4) else 1
+        decode_stages = 2 if (kind == "pdpp" and n_gpus >= 8) else 1
     if prefill_ranks is None:
         prefill_ranks = n_gpus - decode_stages
     prefill_ranks = max(1, min(prefill_ranks, n_gpus - decode_stages))

@@ -157,6 +157,8 @@ def test_node_layout_defaults():
     assert lay.kind == "pdpp" and len(lay.decode_ranks) == 2 and len(lay.prefill_ranks) == 6
     assert plan_node_layout(1).kind == "single"
     assert plan_node_layout(2).kind == "pd"
+    four = plan_node_layout(4)
+    assert four.kind == "pd" and len(four.prefill_ranks) == 3
 
 
 @pytest.mark.parametrize("world", [2, 3])
