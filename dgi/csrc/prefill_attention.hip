@@ -38,7 +38,7 @@ __device__ __forceinline__ int v_off(int row, int ch) {
 constexpr int HD = 128;
 constexpr int KT = 64;  // keys per tile
 
-__global__ __launch_bounds__(256) void prefill_attn_kernel(
+__global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
     const uint16_t* __restrict__ q, int q_stride, const uint16_t* __restrict__ k_cache,
     const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_seqlens_q, const int* __restrict__ context_lens,
@@ -94,9 +94,12 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
     for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
 
   const size_t head_stride = (size_t)bs * HD;
-  for (int kb0 = 0; kb0 < kv_end; kb0 += KT) {
-    // ---- stage K and V (64 rows x 16 chunks each = 4 passes of 256 threads)
-    u32x4 kr[4], vr[4];
+  // K/V tile loads are software-pipelined one tile ahead through registers:
+  // the global loads of tile i+1 are in flight while tile i is consumed from
+  // LDS (1 workgroup per CU at this register budget, so latency must be hidden
+  // inside the wave, not by occupancy).
+  u32x4 kr[4], vr[4];
+  auto load_tile = [&](int kb0) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int row = p * 16 + (tid >> 4);
@@ -107,6 +110,14 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
       kr[p] = *reinterpret_cast<const u32x4*>(k_cache + base);
       vr[p] = *reinterpret_cast<const u32x4*>(v_cache + base);
     }
+  };
+  if (kv_end > 0) load_tile(0);
+  // last key this wave can see (causal); tiles beyond it are skipped
+  const int wave_last_pos = pos_base + min(t0 + 32 * w + 31, qlen - 1);
+  // keys <= wave_first_pos are visible to every row of the wave
+  const int wave_first_pos = pos_base + t0 + 32 * w;
+  const bool wave_tree = tree_mask != nullptr && (t0 + 32 * w + 31 >= tree_first);
+  for (int kb0 = 0; kb0 < kv_end; kb0 += KT) {
     __syncthreads();  // previous tile fully consumed
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
@@ -116,6 +127,8 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
       *reinterpret_cast<u32x4*>(vs + v_off(row, ch)) = vr[p];
     }
     __syncthreads();
+    if (kb0 + KT < kv_end) load_tile(kb0 + KT);
+    if (kb0 > wave_last_pos) continue;  // whole tile above this wave's diagonal
 
     // ---- S^T = K Q^T for two 32-key blocks
     f32x16 sc[2];
@@ -129,37 +142,64 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
         sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a), as_bf16x8(qf[s]), sc[kb], 0, 0, 0);
       }
     }
-    // ---- online softmax; lane owns query lr, keys kb0 + 32kb + (r&3) + 8(r>>2) + 4hh
+    // ---- online softmax; lane owns query lr, keys kb0 + 32kb + (r&3) + 8(r>>2) + 4hh.
+    // Interior tiles (every key visible to every row of this wave, no tree
+    // rows) skip the per-element mask entirely.
+    const bool interior = (kb0 + KT <= kv_end) && (kb0 + KT - 1 <= wave_first_pos) && !wave_tree;
     float mx = -1e30f;
+    if (interior) {
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kb0 + 32 * kb + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        bool ok = row_valid && key <= my_pos && key < kv_end;
-        if (is_tree && key >= tree_key0) ok = ok && ((tmask >> (key - tree_key0)) & 1ull);
-        const float x = ok ? sc[kb][r] * scale_log2 : -1e30f;
-        sc[kb][r] = x;
-        mx = fmaxf(mx, x);
-      }
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[kb][r]);
+      mx = row_valid ? mx * scale_log2 : -1e30f;
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kb0 + 32 * kb + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          bool ok = row_valid && key <= my_pos && key < kv_end;
+          if (is_tree && key >= tree_key0) ok = ok && ((tmask >> (key - tree_key0)) & 1ull);
+          const float x = ok ? sc[kb][r] * scale_log2 : -1e30f;
+          sc[kb][r] = x;
+          mx = fmaxf(mx, x);
+        }
+    }
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
-    const float alpha = exp2f(m_run - m_new);
+    // deferred max: rescale O / l only when the running max grows by > 2^8, so
+    // most tiles skip the 64 O multiplies (P stays <= 256, safe in f32 / bf16)
+    if (__any(mx > m_run + 8.f)) {
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = exp2f(m_run - m_new);
+      l_run *= alpha;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) o[d] *= alpha;
+      m_run = m_new;
+    }
     float psum = 0.f;
+    if (interior) {
+      const float nm = -m_run;
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float x = sc[kb][r];
-        const float pv = (x > -1e29f) ? exp2f(x - m_new) : 0.f;
-        sc[kb][r] = pv;
-        psum += pv;
-      }
+        for (int r = 0; r < 16; ++r) {
+          const float pv = exp2f(fmaf(sc[kb][r], scale_log2, nm));
+          sc[kb][r] = pv;
+          psum += pv;
+        }
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float pv = exp2f(sc[kb][r] - m_run);
+          sc[kb][r] = pv;
+          psum += pv;
+        }
+    }
     psum += __shfl_xor(psum, 32, 64);
-    l_run = l_run * alpha + psum;
-    m_run = m_new;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) o[d] *= alpha;
+    l_run += psum;
 
     // ---- O^T += V^T P^T
     const int g16 = lane >> 4;
