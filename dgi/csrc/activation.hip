@@ -3,37 +3,56 @@
 // out[t, :] = silu(gu[t, :I]) * gu[t, I:]  where gu is the fused gate|up GEMM
 // output.  One pass, 16-byte vectors, fp32 math.  Halves the HBM traffic of
 // the unfused silu -> mul sequence HF runs inside the reference's Llama MLP.
+//
+// Grid = (chunk groups, rows): no integer division in the index math, and
+// each thread keeps CPT 16-byte gate + up loads in flight before any math
+// (memory-bound op: bytes in flight per CU set the achieved bandwidth).
+// silu(g) = g * rcp(1 + exp(-g)) with the hardware reciprocal.
 #include "common.h"
 
 using namespace dgi;
 
+namespace {
+constexpr int CPT = 4;  // 16-byte chunks per thread
+
 __global__ __launch_bounds__(256) void silu_mul_kernel(const uint16_t* __restrict__ gu,
                                                        uint16_t* __restrict__ out, int I,
-                                                       int in_stride, int out_stride, int nchunk_row,
-                                                       long total) {
-  for (long c = (long)blockIdx.x * 256 + threadIdx.x; c < total; c += (long)gridDim.x * 256) {
-    const int t = (int)(c / nchunk_row);
-    const int i = (int)(c - (long)t * nchunk_row) * 8;
-    const u32x4 a = *reinterpret_cast<const u32x4*>(gu + (size_t)t * in_stride + i);
-    const u32x4 bb = *reinterpret_cast<const u32x4*>(gu + (size_t)t * in_stride + I + i);
-    float g[8], u[8], o[8];
-    unpack8(a, g);
-    unpack8(bb, u);
+                                                       int nchunk_row) {
+  const int t = blockIdx.y;
+  const int c0 = blockIdx.x * (256 * CPT) + threadIdx.x;
+  const uint16_t* grow = gu + (size_t)t * (2 * I);
+  uint16_t* orow = out + (size_t)t * I;
+  u32x4 a[CPT], b[CPT];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = g[j] / (1.f + __expf(-g[j])) * u[j];
-    *reinterpret_cast<u32x4*>(out + (size_t)t * out_stride + i) = pack8(o);
+  for (int k = 0; k < CPT; ++k) {
+    const int c = c0 + k * 256;
+    if (c < nchunk_row) {
+      a[k] = *reinterpret_cast<const u32x4*>(grow + c * 8);
+      b[k] = *reinterpret_cast<const u32x4*>(grow + I + c * 8);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const int c = c0 + k * 256;
+    if (c < nchunk_row) {
+      float g[8], u[8], o[8];
+      unpack8(a[k], g);
+      unpack8(b[k], u);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = g[j] * __builtin_amdgcn_rcpf(1.f + __expf(-g[j])) * u[j];
+      *reinterpret_cast<u32x4*>(orow + c * 8) = pack8(o);
+    }
   }
 }
+}  // namespace
 
 extern "C" int dgi_silu_mul(const void* gu, void* out, int T, int I, hipStream_t s) {
   if (I % 8) return -2;
   if (T == 0) return 0;
+  if (T > 65535) return -3;
   const int nchunk_row = I / 8;
-  const long total = (long)T * nchunk_row;
-  long blocks = (total + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  silu_mul_kernel<<<(int)blocks, 256, 0, s>>>((const uint16_t*)gu, (uint16_t*)out, I, 2 * I, I,
-                                              nchunk_row, total);
+  dim3 grid((nchunk_row + 256 * CPT - 1) / (256 * CPT), T);
+  silu_mul_kernel<<<grid, 256, 0, s>>>((const uint16_t*)gu, (uint16_t*)out, I, nchunk_row);
   DGI_CHECK_LAUNCH();
   return 0;
 }

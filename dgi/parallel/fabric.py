@@ -163,6 +163,11 @@ class CtrlChannel:
         self.store.set(self._key(self.me, self.peer, self.sseq), a.tobytes())
         self.sseq += 1
 
+    def send_var(self, arr) -> None:
+        """Variable-length message (e.g. a prompt's token ids)."""
+        self.store.set(self._key(self.me, self.peer, self.sseq), np.asarray(arr, np.int64).ravel().tobytes())
+        self.sseq += 1
+
     def poll(self) -> Optional[np.ndarray]:
         k = self._key(self.peer, self.me, self.rseq)
         if not self.store.check([k]):

@@ -42,7 +42,8 @@ from dgi.parallel.pipeline import PipelineEngine
 from dgi.parallel.plan import NodeLayout
 from dgi.sched.request import Request, SamplingParams, Status
 
-MSG_MIGRATE, MSG_CREDIT, MSG_DONE = 1, 2, 3
+MSG_MIGRATE, MSG_CREDIT, MSG_DONE, MSG_FINISHED = 1, 2, 3, 4
+REASONS = {0: None, 1: "length", 2: "stop"}
 CTRL = 8
 META_FIELDS = 11
 
@@ -80,8 +81,8 @@ class PrefillServer:
         self.ttfts: list = []
 
     # ------------------------------------------------------------------ API
-    def submit(self, prompt: list, params: SamplingParams) -> Request:
-        r = Request(prompt, params)
+    def submit(self, prompt: list, params: SamplingParams, rid=None) -> Request:
+        r = Request(prompt, params, rid=rid)
         self.pending.append(r)
         return r
 
@@ -124,6 +125,8 @@ class PrefillServer:
             if o.finished:  # max_tokens == 1 or EOS at the first token
                 self.credit += int(o.request.spec_state or 0)
                 self.seq_credit += 1
+                code = {"length": 1, "stop": 2}.get(o.finish_reason, 0)
+                self.ch.send([MSG_FINISHED, int(o.rid), int(o.token), code])
             else:
                 ready.append(o.request)
         if ready:
@@ -192,6 +195,9 @@ class DecodeDriver:
         for p in self.prefill:
             self.chans[p].send([MSG_CREDIT, share, seq_share])
         self.origin: dict = {}
+        self.arrivals: list = []   # migrated requests not yet reported (first token known)
+        self.track_arrivals = False
+        self.prefill_finished: list = []   # (rid, token, reason) of sequences done at their first token
         self.refund = collections.Counter()
         self.refund_seqs = collections.Counter()
         self.done = set()
@@ -226,6 +232,7 @@ class DecodeDriver:
             sp = SamplingParams(max_tokens=max_tok, temperature=temp, top_p=top_p, top_k=topk,
                                 ignore_eos=bool(ign), seed=seed)
             r = Request(toks[o:o + plen], sp)
+            r.user = rid            # the prefill side's request id (node router key)
             r.seed = seed
             r.output = [first]
             r.first_token_time = time.perf_counter()
@@ -233,6 +240,8 @@ class DecodeDriver:
             sch.add_prefilled(r, ids[k:k + nb])
             self.engine.requests[r.rid] = r
             self.origin[r.rid] = (p, credit)
+            if self.track_arrivals:
+                self.arrivals.append(r)
             k += nb
         self.received += n_reqs
 
@@ -257,6 +266,9 @@ class DecodeDriver:
                     self._recv_migration(p, m)
                 elif m[0] == MSG_DONE:
                     self.done.add(p)
+                elif m[0] == MSG_FINISHED:
+                    if self.track_arrivals:
+                        self.prefill_finished.append((int(m[1]), int(m[2]), REASONS.get(int(m[3]))))
 
     def step(self) -> list[StepOutput]:
         self.poll()

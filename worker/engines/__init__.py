@@ -3,6 +3,7 @@
 Registered engines:
   llm          HF Transformers (CPU / portable path)
   llm_native   dgi MI355X-native runtime (alias: ``mi355x``, ``dgi``)
+  llm_node     dgi node server (whole-node P/D + pipeline; alias ``mi355x-node``)
   image_gen    diffusers pipeline (lazy dependency)
   vision       HF vision-language model (lazy dependency)
 Lazy optional adapters (external servers, never required):
@@ -17,6 +18,7 @@ from .image_gen import ImageGenEngine
 from .llm import LLMEngine
 from .llm_base import GenerationConfig, GenerationResult, LLMBackend, LLMBaseEngine
 from .llm_native import NativeLLMEngine
+from .llm_node import NodeLLMEngine
 from .vision import VisionEngine
 
 
@@ -38,6 +40,7 @@ def _get_vllm_async_engine():
 ENGINE_REGISTRY: Dict[str, type] = {
     "llm": LLMEngine,
     "llm_native": NativeLLMEngine,
+    "llm_node": NodeLLMEngine,
     "image_gen": ImageGenEngine,
     "vision": VisionEngine,
 }
@@ -53,6 +56,8 @@ _BACKEND_ALIASES = {
     "transformers": "llm",
     "mi355x": "llm_native",
     "dgi": "llm_native",
+    "mi355x-node": "llm_node",
+    "node": "llm_node",
     "sglang": "llm_sglang",
     "vllm": "llm_vllm",
     "vllm_async": "llm_vllm_async",
@@ -113,5 +118,5 @@ def get_recommended_backend() -> str:
 
 
 __all__ = ["BaseEngine", "LLMBaseEngine", "LLMBackend", "GenerationConfig", "GenerationResult", "LLMEngine",
-           "NativeLLMEngine", "ImageGenEngine", "VisionEngine", "ENGINE_REGISTRY", "get_engine",
+           "NativeLLMEngine", "NodeLLMEngine", "ImageGenEngine", "VisionEngine", "ENGINE_REGISTRY", "get_engine",
            "create_llm_engine", "list_engines", "get_recommended_backend"]

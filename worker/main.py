@@ -31,7 +31,8 @@ from engines import ENGINE_REGISTRY, create_llm_engine, get_engine  # noqa: E402
 
 logger = logging.getLogger("worker")
 
-LLM_BACKENDS = {"native", "transformers", "mi355x", "dgi", "llm_native", "sglang", "vllm", "vllm_async"}
+LLM_BACKENDS = {"native", "transformers", "mi355x", "dgi", "llm_native", "sglang", "vllm", "vllm_async",
+                "mi355x-node", "node", "llm_node"}
 
 
 class Worker:
@@ -174,6 +175,8 @@ class Worker:
         model_cfgs = self.remote_config.get("model_configs", {}) if self.remote_config else {}
         for t in list(self.config.supported_types):
             cfg = self.config.engine_config(t)
+            if t == "llm" and len(cfg.get("device_ids") or []) > 1 and cfg.get("backend") in ("mi355x", "dgi"):
+                cfg["backend"] = "mi355x-node"      # a multi-GPU worker serves through the node server
             if t in model_cfgs:
                 cfg.update({k: v for k, v in model_cfgs[t].items() if v is not None and k != "model_id"})
             try:
