@@ -17,7 +17,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (ROOT, os.path.join(ROOT, "worker"), os.path.join(ROOT, "server"), os.path.join(ROOT, "sdk", "python")):
     if p not in sys.path:
         sys.path.insert(0, p)
-os.environ.setdefault("DATABASE_URL", "sqlite+aiosqlite:///:memory:")
+# a file database: the API tests drive the app from several threads at once, and
+# an in-memory SQLite database is one shared connection (not thread-safe)
+import tempfile  # noqa: E402
+os.environ.setdefault("DATABASE_URL", "sqlite+aiosqlite:///" + os.path.join(tempfile.gettempdir(),
+                                                                       f"dgi_test_{os.getpid()}.db"))
 
 
 def pytest_configure(config):
