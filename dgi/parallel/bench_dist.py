@@ -50,10 +50,16 @@ def run_distributed(args, layout_kind: str, dist):
     sp = SamplingParams(max_tokens=args.output_len, temperature=0.0, ignore_eos=True)
     rng = random.Random(777 + rank)
     role = layout.role(rank)
-    if layout.kind == "pp":
-        res = _run_pp(args, f, cfg, layout, role, sp, rng, conc)
-    else:
-        res = _run_pd(args, f, cfg, layout, role, sp, rng, conc)
+    try:
+        if layout.kind == "pp":
+            res = _run_pp(args, f, cfg, layout, role, sp, rng, conc)
+        else:
+            res = _run_pd(args, f, cfg, layout, role, sp, rng, conc)
+    except BaseException as e:
+        # tell the other ranks (their watchdogs exit instead of waiting in RCCL forever)
+        if f.watchdog is not None:
+            f.watchdog.report_failure(f"{role}: {type(e).__name__}: {e}")
+        raise
     tokens, elapsed, ttfts, extra = res
     t = torch.tensor([tokens, elapsed], dtype=torch.float64, device=f.device if f.on_gpu else "cpu")
     tl = [torch.zeros_like(t) for _ in range(world)]

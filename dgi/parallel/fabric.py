@@ -58,6 +58,11 @@ class Fabric:
         self.ctrl = dist.new_group(backend="gloo")
         self.comm_stream = torch.cuda.Stream(device=device) if self.on_gpu else None
         self._pending: list = []
+        # liveness watchdog over the rendezvous store (dgi.parallel.fault)
+        self.watchdog = None
+        if self.world > 1 and os.environ.get("DGI_WATCHDOG", "1") != "0":
+            from dgi.parallel.fault import Watchdog
+            self.watchdog = Watchdog(self.rank, self.world).start()
 
     # ------------------------------------------------------------------ data (device tensors)
     def send(self, t: torch.Tensor, dst: int) -> None:
@@ -127,6 +132,8 @@ class Fabric:
         dist.barrier()
 
     def close(self) -> None:
+        if self.watchdog is not None:
+            self.watchdog.stop()
         self.flush()
         if self.owns_pg and dist.is_initialized():
             dist.destroy_process_group()

@@ -112,6 +112,9 @@ class PrefillServer:
             self.engine.requests[r.rid] = r
 
     def step(self) -> list[StepOutput]:
+        from dgi.parallel.fault import plan
+        if plan():
+            plan().check(self.f.rank, self.engine.stats["steps"])
         self._poll_credit()
         self._admit()
         if not self.engine.has_unfinished():
@@ -145,6 +148,11 @@ class PrefillServer:
             toks += r.prompt
         ids_t = torch.tensor(ids, dtype=torch.int32, device=dev)
         buf = ops.kv_gather(eng.pool.kv, ids_t)
+        from dgi.parallel.fault import plan
+        if plan():
+            def corrupt():
+                buf.view(-1)[: max(1, buf.numel() // 64)] = float("nan")
+            plan().check(self.f.rank, self.migrated + 100000, corrupt=corrupt)
         meta_t = torch.tensor(meta, dtype=torch.int32, device=dev)
         toks_t = torch.tensor(toks, dtype=torch.int32, device=dev)
         self.ch.send([MSG_MIGRATE, len(reqs), len(ids), meta_t.numel(), toks_t.numel()])

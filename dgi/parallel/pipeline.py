@@ -113,6 +113,9 @@ class PipelineEngine(LLMEngine):
 
     # ------------------------------------------------------------------ microbatches
     def _launch(self) -> bool:
+        from dgi.parallel.fault import plan
+        if plan():
+            plan().check(self.f.rank, self.stats["steps"])
         sb = self.scheduler.schedule(max_seqs=self.mb_cap,
                                      max_tokens=max(1, self.cfg.max_num_batched_tokens // self.n_mb))
         if sb.empty:
@@ -256,6 +259,9 @@ class StageWorker:
                     f.send(buf[self.n_layers:].contiguous(), self.next)
                 continue
             # KIND_FWD
+            from dgi.parallel.fault import plan
+            if plan():
+                plan().check(f.rank, self.steps)
             flat = torch.empty(hdr[ModelRunner.H_LEN], dtype=torch.int32, device=dev)
             f.recv(flat, self.prev)
             T = hdr[ModelRunner.H_T]

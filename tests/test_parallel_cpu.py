@@ -193,3 +193,67 @@ def _tp_body(rank, world):
 
 def test_tensor_parallel_matches_single_process():
     _spawn("_tp_body", 2)
+
+
+# ---------------------------------------------------------------------------- failure detection / fault injection
+def test_fault_plan_parsing_and_delay():
+    import time as _t
+    from dgi.parallel.fault import FaultPlan, InjectedFault
+    p = FaultPlan("0:3:delay:50,1:2:raise")
+    t0 = _t.time()
+    p.check(0, 3)
+    assert _t.time() - t0 >= 0.04
+    p.check(0, 3)                      # fires once
+    with pytest.raises(InjectedFault):
+        p.check(1, 2)
+    p.check(1, 2)
+    hit = []
+    FaultPlan("2:0:corrupt").check(2, 0, corrupt=lambda: hit.append(1))
+    assert hit == [1]
+
+
+def test_pipeline_survives_injected_delay():
+    os.environ["DGI_FAULT"] = "1:3:delay:100"
+    try:
+        import dgi.parallel.fault as fault
+        fault._plan = None
+        _spawn("_pp_body", 2)
+    finally:
+        os.environ.pop("DGI_FAULT", None)
+
+
+def _killed_body(rank, world):
+    import time as _t
+    from dgi.parallel.fabric import Fabric
+    f = Fabric()
+    if rank == 1:
+        os._exit(17)                   # dies without a word
+    t0 = _t.time()
+    while _t.time() - t0 < 60:        # rank 0 would wait forever; its watchdog must end it
+        _t.sleep(0.2)
+    return "not reached"
+
+
+def test_watchdog_ends_survivor_of_dead_rank():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    env_before = os.environ.get("DGI_WATCHDOG_S")
+    os.environ["DGI_WATCHDOG_S"] = "3"
+    try:
+        procs = [ctx.Process(target=_worker, args=(r, 2, port, "_killed_body", q)) for r in range(2)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=45)
+        codes = [p.exitcode for p in procs]
+    finally:
+        if env_before is None:
+            os.environ.pop("DGI_WATCHDOG_S", None)
+        else:
+            os.environ["DGI_WATCHDOG_S"] = env_before
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+    assert codes[1] == 17
+    assert codes[0] not in (0, None)   # the survivor was stopped by its watchdog, not left hanging

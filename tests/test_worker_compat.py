@@ -452,3 +452,41 @@ def test_proto_messages_roundtrip():
     assert pb.KVCacheRequest.FromString(kv.SerializeToString()).layers[0].layer_idx == 3
     assert set(pb.METHODS) == {"StreamInference", "Forward", "TransferKVCache", "CreateSession", "CloseSession",
                                "HealthCheck"}
+
+
+# ---------------------------------------------------------------- optional external-server adapters
+def test_vllm_and_sglang_adapters_with_mocked_libraries():
+    import asyncio
+    from unittest.mock import MagicMock, patch
+    mv = MagicMock()
+    with patch.dict(sys.modules, {"vllm": mv, "sglang": MagicMock()}):
+        from engines.llm_base import GenerationConfig, LLMBackend
+        from engines.llm_sglang import SGLangEngine
+        from engines.llm_vllm import VLLMAsyncEngine, VLLMEngine
+        e = VLLMEngine({"model_id": "m", "vllm": {"tensor_parallel_size": 2, "enable_prefix_caching": True}})
+        assert e.backend_type == LLMBackend.VLLM and e.llm is None and e._vllm_config["tensor_parallel_size"] == 2
+        assert "assistant:" in e._format_messages([{"role": "user", "content": "hi"}])
+        out = MagicMock()
+        out.outputs = [MagicMock(text="ok", token_ids=[1, 2], finish_reason="stop")]
+        out.prompt_token_ids = [5]
+        e.llm = MagicMock()
+        e.llm.generate.return_value = [out]
+        r = e._generate_sync([{"role": "user", "content": "hi"}], GenerationConfig(max_tokens=4))
+        assert (r.text, r.prompt_tokens, r.completion_tokens) == ("ok", 1, 2)
+        assert len(asyncio.run(e.batch_generate([[{"role": "user", "content": "a"}]]))) == 1
+        assert e.supports_prefix_caching() and not e.supports_streaming()
+        assert "tensor_parallelism" in e.get_status()["features"]
+        assert VLLMAsyncEngine({"model_id": "m"}).supports_streaming()
+        s = SGLangEngine({"model_id": "m", "sglang": {"tp_size": 2}})
+        assert s.runtime is None and s._server_process is None and s.get_cache_stats()["hit_rate"] == 0.0
+        s._cache_hits, s._cache_misses = 10, 5
+        assert s.get_cache_stats()["hit_rate"] == 10 / 15
+        assert "radix_attention" in s.get_status()["features"]
+        proc = MagicMock()
+        s._server_process, s.loaded = proc, True
+        s.unload_model()
+        proc.terminate.assert_called_once()
+        assert s._server_process is None and not s.loaded
+    from engines import get_engine
+    with patch.dict(sys.modules, {"vllm": mv}):
+        assert get_engine("vllm").__name__ == "VLLMEngine"
