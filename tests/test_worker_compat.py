@@ -5,6 +5,7 @@ Behaviour pinned here follows the reference's own suite plus
 the fixed defects listed in Appendix E."""
 import asyncio
 import time
+import sys
 import types
 from unittest.mock import MagicMock, patch
 
