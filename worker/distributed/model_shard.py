@@ -52,7 +52,9 @@ class ModelShard(nn.Module):
         self.end_layer = end_layer
         self.device = device
         self.dtype = dtype
-        self.layers = nn.ModuleList()
+        # a plain list: layers may be HF blocks, native stages or any callable
+        # returning (hidden, kv) (the reference's tests append stubs)
+        self.layers: List[Any] = []
         self.config = None
         self.is_first_shard = False
         self.is_last_shard = False
@@ -163,8 +165,14 @@ class ModelShard(nn.Module):
 
     def get_memory_usage(self) -> float:
         n = 0
-        for p in self.parameters():
-            n += p.numel() * p.element_size()
+        seen = set()
+        mods = [m for m in self.layers if isinstance(m, nn.Module)]
+        mods += [m for m in (self.embed_tokens, self.embed_positions, self.norm, self.lm_head) if m is not None]
+        for m in mods:
+            for p in m.parameters():
+                if id(p) not in seen:
+                    seen.add(id(p))
+                    n += p.numel() * p.element_size()
         if self.native is not None:
             n += self.native.weight_bytes()
         return n / 1024 ** 3
