@@ -174,6 +174,8 @@ class SpeculativeDecoder:
     def setup_draft_head(self, hidden_size: int, vocab_size: int, num_layers: int = 2) -> DraftHead:
         self.draft_head = DraftHead(hidden_size, vocab_size, num_layers, self.config.draft_head_hidden_size)
         emb = getattr(getattr(self.target, "model", None), "embed_tokens", None)
+        if emb is None:  # GPT-style
+            emb = getattr(getattr(self.target, "transformer", None), "wte", None)
         if emb is not None:
             self.draft_head.set_token_embedding(emb)
         self.draft_head.to(self.device)
@@ -234,8 +236,9 @@ class SpeculativeDecoder:
         drafted = accepted = 0
         ids = input_ids
         while len(out) < max_new_tokens:
+            before = self._stats["total_draft_tokens"]
             new, k = await self.decode_step(ids)
-            drafted += self._current_depth
+            drafted += self._stats["total_draft_tokens"] - before
             accepted += k
             out.extend(new.tolist())
             ids = torch.cat([ids, new[None].to(ids.dtype)], 1)
