@@ -17,7 +17,7 @@ run() {  # name timeout cmd...
 STEPS=${STEPS:-"pytest smoke bench8b bench70b"}
 for s in $STEPS; do
   case $s in
-    pytest) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench8b) run bench8b 900 python bench.py --model llama3-8b --steps 30 --warmup 5 --json-out gpurun_out/bench8b.json ;;
     bench70b) run bench70b 1200 python bench.py --steps 30 --warmup 5 --json-out gpurun_out/bench70b.json ;;

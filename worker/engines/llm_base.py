@@ -104,8 +104,17 @@ class LLMBaseEngine(BaseEngine):
     def _run_coroutine_in_new_thread(coro):
         return _LoopThread.run(coro)
 
+    @staticmethod
+    def _messages_of(params: Dict[str, Any]) -> List[Dict[str, str]]:
+        """Chat messages of a job; a bare ``prompt`` becomes one user turn."""
+        if params.get("messages"):
+            return params["messages"]
+        if params.get("prompt") is not None:
+            return [{"role": "user", "content": str(params["prompt"])}]
+        return []
+
     def inference(self, params: Dict[str, Any]) -> Dict[str, Any]:
-        messages = params.get("messages", [])
+        messages = self._messages_of(params)
         cfg = generation_config_from_params(params)
         try:
             asyncio.get_running_loop()
@@ -120,7 +129,7 @@ class LLMBaseEngine(BaseEngine):
         if not params_list:
             return []
         cfg = generation_config_from_params(params_list[0])
-        res = await self.batch_generate([p.get("messages", []) for p in params_list], cfg)
+        res = await self.batch_generate([self._messages_of(p) for p in params_list], cfg)
         return [result_to_response(r) for r in res]
 
     def supports_streaming(self) -> bool:

@@ -47,30 +47,62 @@ class SGLangEngine(LLMBaseEngine):
     def _format_messages(self, messages) -> str:
         return format_messages(self.tokenizer, messages)
 
-    async def _post(self, prompt: str, cfg: GenerationConfig) -> Dict[str, Any]:
-        import httpx
-        body = {"text": prompt, "sampling_params": {"max_new_tokens": cfg.max_tokens, "temperature": cfg.temperature,
-                                                    "top_p": cfg.top_p, "top_k": cfg.top_k if cfg.top_k else -1,
-                                                    "stop": cfg.stop_sequences}}
-        async with httpx.AsyncClient(timeout=None) as c:
-            r = await c.post(f"{self.server_url.rstrip('/')}/generate", json=body)
-            r.raise_for_status()
-            return r.json()
+    def _url(self) -> str:
+        return (self.server_url or "http://localhost:30000").rstrip("/")
 
-    async def generate_async(self, messages, config: Optional[GenerationConfig] = None) -> GenerationResult:
-        cfg = config or GenerationConfig()
-        d = await self._post(self._format_messages(messages), cfg)
+    async def _generate_with_native_api(self, messages, cfg: GenerationConfig) -> GenerationResult:
+        """SGLang's own ``/generate`` route (carries ``cached_tokens`` in meta_info)."""
+        import aiohttp
+        body = {"text": self._format_messages(messages),
+                "sampling_params": {"max_new_tokens": cfg.max_tokens, "temperature": cfg.temperature,
+                                    "top_p": cfg.top_p, "top_k": cfg.top_k if cfg.top_k else -1,
+                                    "stop": cfg.stop_sequences}}
+        async with aiohttp.ClientSession() as session:
+            async with session.post(f"{self._url()}/generate", json=body) as resp:
+                if resp.status != 200:
+                    raise RuntimeError(f"SGLang /generate error {resp.status}: {await resp.text()}")
+                d = await resp.json()
         meta = d.get("meta_info", {}) or {}
         p, c = int(meta.get("prompt_tokens", 0)), int(meta.get("completion_tokens", 0))
-        cached = int(meta.get("cached_tokens", 0))
-        if cached:
-            self._cache_hits += 1
-        else:
-            self._cache_misses += 1
         fr = meta.get("finish_reason")
         fr = fr.get("type") if isinstance(fr, dict) else (fr or "stop")
         return GenerationResult(text=d.get("text", ""), prompt_tokens=p, completion_tokens=c, total_tokens=p + c,
-                                finish_reason=fr, cached_tokens=cached)
+                                finish_reason=fr, cached_tokens=int(meta.get("cached_tokens", 0)))
+
+    async def _generate_with_http_api(self, messages, cfg: GenerationConfig) -> GenerationResult:
+        """OpenAI-compatible ``/v1/chat/completions`` (fallback route)."""
+        import aiohttp
+        payload = {"model": self.config.get("model_id"), "messages": messages, "max_tokens": cfg.max_tokens,
+                   "temperature": cfg.temperature, "top_p": cfg.top_p}
+        if cfg.stop_sequences:
+            payload["stop"] = cfg.stop_sequences
+        async with aiohttp.ClientSession() as session:
+            async with session.post(f"{self._url()}/v1/chat/completions", json=payload) as resp:
+                if resp.status != 200:
+                    raise RuntimeError(f"SGLang API error {resp.status}: {await resp.text()}")
+                d = await resp.json()
+        if "error" in d:
+            raise RuntimeError(f"SGLang API error: {d['error']}")
+        choice = (d.get("choices") or [{}])[0]
+        usage = d.get("usage", {}) or {}
+        return GenerationResult(text=(choice.get("message") or {}).get("content", ""),
+                                prompt_tokens=int(usage.get("prompt_tokens", 0)),
+                                completion_tokens=int(usage.get("completion_tokens", 0)),
+                                total_tokens=int(usage.get("total_tokens", 0)),
+                                finish_reason=choice.get("finish_reason") or "stop",
+                                cached_tokens=int(usage.get("cached_tokens", 0)))
+
+    async def generate_async(self, messages, config: Optional[GenerationConfig] = None) -> GenerationResult:
+        cfg = config or GenerationConfig()
+        try:
+            res = await self._generate_with_native_api(messages, cfg)
+        except Exception:
+            res = await self._generate_with_http_api(messages, cfg)
+        if res.cached_tokens:
+            self._cache_hits += 1
+        else:
+            self._cache_misses += 1
+        return res
 
     async def batch_generate(self, batch_messages, config: Optional[GenerationConfig] = None) -> List[GenerationResult]:
         res = await asyncio.gather(*[self.generate_async(m, config) for m in batch_messages], return_exceptions=True)
@@ -79,8 +111,30 @@ class SGLangEngine(LLMBaseEngine):
                 for r in res]
 
     async def stream_generate(self, messages, config: Optional[GenerationConfig] = None) -> AsyncIterator[str]:
-        res = await self.generate_async(messages, config)
-        yield res.text
+        """SSE stream of ``/generate`` (``stream: true``): yields text deltas."""
+        import json
+
+        import aiohttp
+        cfg = config or GenerationConfig()
+        body = {"text": self._format_messages(messages), "stream": True,
+                "sampling_params": {"max_new_tokens": cfg.max_tokens, "temperature": cfg.temperature,
+                                    "top_p": cfg.top_p, "stop": cfg.stop_sequences}}
+        sent = ""
+        async with aiohttp.ClientSession() as session:
+            async with session.post(f"{self._url()}/generate", json=body) as resp:
+                if resp.status != 200:
+                    raise RuntimeError(f"SGLang stream error {resp.status}: {await resp.text()}")
+                async for raw in resp.content:
+                    line = raw.decode("utf-8", "ignore").strip()
+                    if not line.startswith("data:"):
+                        continue
+                    data = line[5:].strip()
+                    if data == "[DONE]":
+                        break
+                    text = json.loads(data).get("text", "")
+                    if len(text) > len(sent):   # SGLang streams the cumulative text
+                        yield text[len(sent):]
+                        sent = text
 
     def supports_streaming(self) -> bool:
         return True

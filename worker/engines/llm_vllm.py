@@ -26,6 +26,12 @@ def _sampling(cfg: GenerationConfig):
                           top_k=cfg.top_k if cfg.top_k and cfg.top_k > 0 else -1, stop=cfg.stop_sequences)
 
 
+def _free_device_memory() -> None:
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.empty_cache()
+
+
 def _result(out) -> GenerationResult:
     o = out.outputs[0]
     p = len(out.prompt_token_ids or [])
@@ -85,7 +91,9 @@ class VLLMEngine(LLMBaseEngine):
     def unload_model(self) -> None:
         self.llm = None
         self.tokenizer = None
+        self._default_sampling_params = None
         self.loaded = False
+        _free_device_memory()
 
 
 class VLLMAsyncEngine(LLMBaseEngine):
@@ -137,10 +145,13 @@ class VLLMAsyncEngine(LLMBaseEngine):
 
     def get_status(self) -> Dict[str, Any]:
         s = super().get_status()
-        s.update(backend="vllm_async", features=["paged_attention", "continuous_batching", "tensor_parallelism",
-                                                 "streaming"])
+        s.update(backend="vllm_async", async_mode=True,
+                 features=["paged_attention", "continuous_batching", "tensor_parallelism", "async_inference",
+                           "streaming"] + (["prefix_caching"] if self.supports_prefix_caching() else []))
         return s
 
     def unload_model(self) -> None:
         self.engine = None
+        self.tokenizer = None
         self.loaded = False
+        _free_device_memory()
