@@ -7,8 +7,10 @@ Signatures are HMAC-SHA256 over ``METHOD:PATH:sha256(body):timestamp`` with a
 """
 from __future__ import annotations
 
+import asyncio
 import hashlib
 import hmac
+import inspect
 import json
 import logging
 import secrets
@@ -106,33 +108,57 @@ class AuditLogger:
 
 
 class SecurityService:
-    def __init__(self, db: Session):
-        self.db = db
+    """Worker authentication over either a sync ``Session`` (this server) or an
+    ``AsyncSession`` (reference API: the same methods become awaitable)."""
 
-    def verify_worker_auth(self, worker_id: str, token: str, ip: Optional[str] = None) -> Tuple[Optional[Worker], str]:
-        w = self.db.get(Worker, str(worker_id)) if worker_id else None
+    def __init__(self, db):
+        self.db = db
+        ex = getattr(db, "execute", None)
+        self._async = asyncio.iscoroutinefunction(ex) or inspect.iscoroutinefunction(ex)
+
+    def _check(self, w, token: str, ip: Optional[str], worker_id) -> Tuple[Optional[Worker], str, bool]:
+        """Pure decision: (worker or None, error, needs_commit)."""
         if w is None:
             AuditLogger.log_auth_event("verify", str(worker_id), False, ip, reason="worker_not_found")
-            return None, "worker_not_found"
+            return None, "worker_not_found", False
         now = datetime.utcnow()
         if w.locked_until and w.locked_until > now:
-            return None, "account_locked"
+            return None, "account_locked", False
         if not TokenManager.verify_token_hash(token, w.auth_token_hash):
             w.failed_auth_attempts = (w.failed_auth_attempts or 0) + 1
             w.last_failed_auth = now
             if w.failed_auth_attempts >= SecuritySettings.MAX_FAILED_ATTEMPTS:
                 w.locked_until = now + timedelta(minutes=SecuritySettings.LOCKOUT_MINUTES)
                 AuditLogger.log_security_event("worker_locked", "high", worker_id=str(w.id))
-            self.db.commit()
             AuditLogger.log_auth_event("verify", str(w.id), False, ip, reason="invalid_token")
-            return None, "invalid_token"
+            return None, "invalid_token", True
         if w.token_expires_at and w.token_expires_at < now:
-            return None, "token_expired"
+            return None, "token_expired", False
         if w.failed_auth_attempts:
             w.failed_auth_attempts = 0
             w.locked_until = None
+            return w, "", True
+        return w, "", False
+
+    def verify_worker_auth(self, worker_id: str, token: str, ip: Optional[str] = None):
+        if self._async:
+            return self._verify_worker_auth_async(worker_id, token, ip)
+        w = self.db.get(Worker, str(worker_id)) if worker_id else None
+        w, err, dirty = self._check(w, token, ip, worker_id)
+        if dirty:
             self.db.commit()
-        return w, ""
+        return w, err
+
+    async def _verify_worker_auth_async(self, worker_id: str, token: str, ip: Optional[str] = None):
+        from sqlalchemy import select
+        w = None
+        if worker_id:
+            res = await self.db.execute(select(Worker).where(Worker.id == str(worker_id)))
+            w = res.scalar_one_or_none()
+        w, err, dirty = self._check(w, token, ip, worker_id)
+        if dirty:
+            await self.db.commit()
+        return w, err
 
     def should_refresh_token(self, worker) -> bool:
         exp = getattr(worker, "token_expires_at", None)
@@ -155,11 +181,19 @@ class SecurityService:
             return None
         return self.issue_tokens(worker)
 
-    def verify_request_signature(self, worker, method: str, path: str, body: Any, timestamp: Optional[int],
-                                 signature: Optional[str]) -> Tuple[bool, str]:
+    def _signature(self, worker, method, path, body, timestamp, signature) -> Tuple[bool, str]:
         secret = getattr(worker, "signing_secret", None)
         if not secret:
             return False, "no_signing_secret"
         if timestamp is None or not signature:
             return False, "missing_signature"
         return RequestSigner.verify_signature(method, path, body, int(timestamp), signature, secret)
+
+    def verify_request_signature(self, worker, method: str, path: str, body: Any, timestamp: Optional[int],
+                                 signature: Optional[str]):
+        out = self._signature(worker, method, path, body, timestamp, signature)
+        if self._async:
+            async def _done():
+                return out
+            return _done()
+        return out
