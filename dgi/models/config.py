@@ -1,4 +1,4 @@
-"""Model configurations (Llama-3 8B/70B, OPT-125m, tiny test models).
+"""Model configurations (Llama-3 8B/70B, Qwen2.5 7B/0.5B, OPT-125m, tiny test models).
 
 Mirrors the fields the reference reads from HF ``AutoConfig``
 (worker/distributed/model_shard.py:273-311 uses hidden_size,
@@ -18,7 +18,7 @@ from typing import Optional
 @dataclasses.dataclass
 class ModelConfig:
     name: str
-    arch: str = "llama"  # "llama" | "opt"
+    arch: str = "llama"  # "llama" | "qwen2" | "opt"
     vocab_size: int = 128256
     hidden_size: int = 4096
     intermediate_size: int = 14336
@@ -31,6 +31,7 @@ class ModelConfig:
     rms_eps: float = 1e-5
     max_position: int = 8192
     tie_embeddings: bool = False
+    qkv_bias: bool = False          # Qwen2: biased q/k/v projections
     bos_token_id: int = 128000
     eos_token_id: int = 128001
 
@@ -49,6 +50,8 @@ class ModelConfig:
     def param_count(self) -> int:
         H, I, V, L = self.hidden_size, self.intermediate_size, self.vocab_size, self.num_layers
         per_layer = H * self.qkv_size + self.q_size * H + 2 * H * I + I * H + 2 * H
+        if self.qkv_bias:
+            per_layer += self.qkv_size
         emb = V * H * (1 if self.tie_embeddings else 2)
         return L * per_layer + emb + H
 
@@ -73,16 +76,24 @@ class ModelConfig:
                                eos_token_id=d.get("eos_token_id", 2), rms_eps=1e-5)
         H = d["hidden_size"]
         nh = d["num_attention_heads"]
+        # transformers >= 5 nests RoPE settings under ``rope_parameters``
+        rp = d.get("rope_parameters") or {}
+        theta = d.get("rope_theta", rp.get("rope_theta", 10000.0))
+        scaling = d.get("rope_scaling")
+        if scaling is None and rp.get("rope_type", "default") != "default":
+            scaling = dict(rp)
         eos = d.get("eos_token_id", 2)
         if isinstance(eos, list):
             eos = eos[0]
-        return ModelConfig(name=name, arch="llama", vocab_size=d["vocab_size"], hidden_size=H,
+        arch = "qwen2" if mt == "qwen2" else "llama"
+        return ModelConfig(name=name, arch=arch, vocab_size=d["vocab_size"], hidden_size=H,
                            intermediate_size=d["intermediate_size"], num_layers=d["num_hidden_layers"],
                            num_heads=nh, num_kv_heads=d.get("num_key_value_heads", nh),
-                           head_dim=d.get("head_dim", H // nh), rope_theta=d.get("rope_theta", 10000.0),
-                           rope_scaling=d.get("rope_scaling"), rms_eps=d.get("rms_norm_eps", 1e-5),
+                           head_dim=d.get("head_dim") or H // nh, rope_theta=float(theta),
+                           rope_scaling=scaling, rms_eps=d.get("rms_norm_eps", 1e-5),
                            max_position=d.get("max_position_embeddings", 8192),
                            tie_embeddings=d.get("tie_word_embeddings", False),
+                           qkv_bias=bool(d.get("attention_bias", mt == "qwen2")),
                            bos_token_id=d.get("bos_token_id", 1), eos_token_id=eos)
 
     @staticmethod
@@ -108,6 +119,21 @@ PRESETS: dict[str, ModelConfig] = {
     "llama-tiny-tp": ModelConfig(name="llama-tiny-tp", vocab_size=1024, hidden_size=1024, intermediate_size=2048,
                                  num_layers=2, num_heads=8, num_kv_heads=2, head_dim=128, max_position=4096,
                                  bos_token_id=1, eos_token_id=2),
+    # Qwen2 / Qwen2.5 family (the reference's default LLM is Qwen2.5-7B-Instruct):
+    # Llama block + biased QKV, GQA 7:1 (7B) / 7:1 (0.5B), theta 1e6
+    "qwen2.5-7b": ModelConfig(name="qwen2.5-7b", arch="qwen2", vocab_size=152064, hidden_size=3584,
+                              intermediate_size=18944, num_layers=28, num_heads=28, num_kv_heads=4, head_dim=128,
+                              rope_theta=1000000.0, rms_eps=1e-6, max_position=32768, qkv_bias=True,
+                              bos_token_id=151643, eos_token_id=151645),
+    "qwen2.5-0.5b": ModelConfig(name="qwen2.5-0.5b", arch="qwen2", vocab_size=151936, hidden_size=896,
+                                intermediate_size=4864, num_layers=24, num_heads=14, num_kv_heads=2, head_dim=64,
+                                rope_theta=1000000.0, rms_eps=1e-6, max_position=32768, tie_embeddings=True,
+                                qkv_bias=True, bos_token_id=151643, eos_token_id=151645),
+    # shape-faithful tiny Qwen2 (biased QKV, GQA 7:1, tied embeddings) for tests
+    "qwen-tiny": ModelConfig(name="qwen-tiny", arch="qwen2", vocab_size=1024, hidden_size=1024,
+                             intermediate_size=1536, num_layers=2, num_heads=14, num_kv_heads=2, head_dim=128,
+                             rope_theta=1000000.0, rms_eps=1e-6, max_position=4096, tie_embeddings=True,
+                             qkv_bias=True, bos_token_id=1, eos_token_id=2),
     "opt-125m": ModelConfig(name="opt-125m", arch="opt", vocab_size=50272, hidden_size=768,
                             intermediate_size=3072, num_layers=12, num_heads=12, num_kv_heads=12, head_dim=64,
                             max_position=2048, tie_embeddings=True, bos_token_id=2, eos_token_id=2),
@@ -120,6 +146,10 @@ ALIASES = {
     "meta-llama/Meta-Llama-3-70B": "llama3-70b",
     "meta-llama/Meta-Llama-3-70B-Instruct": "llama3-70b",
     "facebook/opt-125m": "opt-125m",
+    "Qwen/Qwen2.5-7B-Instruct": "qwen2.5-7b",
+    "Qwen/Qwen2.5-7B": "qwen2.5-7b",
+    "Qwen/Qwen2-7B-Instruct": "qwen2.5-7b",
+    "Qwen/Qwen2.5-0.5B-Instruct": "qwen2.5-0.5b",
 }
 
 
@@ -130,6 +160,8 @@ def get_config(name_or_path: str) -> ModelConfig:
     if os.path.exists(name_or_path):
         return ModelConfig.from_file(name_or_path)
     lk = key.lower()
+    if "qwen" in lk:
+        return dataclasses.replace(PRESETS["qwen2.5-0.5b" if "0.5b" in lk else "qwen2.5-7b"], name=name_or_path)
     if "70b" in lk:
         return dataclasses.replace(PRESETS["llama3-70b"], name=name_or_path)
     if "8b" in lk or "7b" in lk:

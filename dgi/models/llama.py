@@ -1,4 +1,4 @@
-"""Native Llama decoder for the MI355X runtime (Llama-3 8B / 70B).
+"""Native Llama-family decoder for the MI355X runtime (Llama-3 8B / 70B, Qwen2 / Qwen2.5).
 
 Replaces the HF modules the reference executes (worker/engines/llm.py:22-69,
 worker/distributed/model_shard.py:28-246).  Per layer the step runs
@@ -7,7 +7,9 @@ worker/distributed/model_shard.py:28-246).  Per layer the step runs
     -> paged decode / prefill attention (HIP, MFMA) -> O GEMM
     -> fused_add_rmsnorm (HIP) -> gate|up GEMM -> SiLU*mul (HIP) -> down GEMM
 
-with fused QKV and gate|up weights so each layer issues 4 GEMMs.  A model
+with fused QKV and gate|up weights so each layer issues 4 GEMMs.  Qwen2's biased
+q/k/v projections ride in the QKV GEMM's bias epilogue (hipBLASLt), so the
+family adds no kernel.  A model
 object may hold any contiguous layer range (pipeline stage): stage 0 owns the
 embedding, the last stage the final norm and LM head, exactly like the
 reference's ``ModelShard`` (model_shard.py:28-59).  Between stages a single
@@ -28,11 +30,12 @@ from dgi.runtime.batch import AttnMeta
 
 
 class LlamaLayerWeights:
-    __slots__ = ("in_norm", "qkv", "o", "post_norm", "gate_up", "down")
+    __slots__ = ("in_norm", "qkv", "o", "post_norm", "gate_up", "down", "qkv_bias")
 
-    def __init__(self, in_norm, qkv, o, post_norm, gate_up, down):
+    def __init__(self, in_norm, qkv, o, post_norm, gate_up, down, qkv_bias=None):
         self.in_norm, self.qkv, self.o = in_norm, qkv, o
         self.post_norm, self.gate_up, self.down = post_norm, gate_up, down
+        self.qkv_bias = qkv_bias   # [qkv_size] for Qwen2, else None (fused into the QKV GEMM epilogue)
 
 
 def _rand(shape, gen, device, dtype, std):
@@ -80,7 +83,8 @@ class LlamaModel:
             self.layers.append(LlamaLayerWeights(
                 torch.ones(H, device=dev, dtype=dt), torch.empty(c.qkv_size, H, device=dev, dtype=dt),
                 torch.empty(H, c.q_size, device=dev, dtype=dt), torch.ones(H, device=dev, dtype=dt),
-                torch.empty(2 * I, H, device=dev, dtype=dt), torch.empty(H, I, device=dev, dtype=dt)))
+                torch.empty(2 * I, H, device=dev, dtype=dt), torch.empty(H, I, device=dev, dtype=dt),
+                torch.zeros(c.qkv_size, device=dev, dtype=dt) if c.qkv_bias else None))
         if self.has_embed:
             self.embed = torch.empty(c.vocab_size, H, device=dev, dtype=dt)
         if self.has_head:
@@ -106,7 +110,8 @@ class LlamaModel:
             ln2 = 1.0 + 0.1 * _rand((H,), gen, dev, torch.float32, 1.0)
             gu = _rand((2 * I, H), gen, dev, dt, std)
             down = _rand((H, I), gen, dev, dt, std / math.sqrt(2 * c.num_layers))
-            self.layers.append(LlamaLayerWeights(ln1.to(dt), qkv, o, ln2.to(dt), gu, down))
+            bias = _rand((c.qkv_size,), gen, dev, dt, std) if c.qkv_bias else None
+            self.layers.append(LlamaLayerWeights(ln1.to(dt), qkv, o, ln2.to(dt), gu, down, bias))
         if self.has_embed or (self.has_head and c.tie_embeddings):
             gen.manual_seed(seed * 1000003 + 17)
             emb = _rand((c.vocab_size, H), gen, dev, dt, 1.0)
@@ -128,6 +133,9 @@ class LlamaModel:
             qkv = torch.cat([sd[p + "self_attn.q_proj.weight"], sd[p + "self_attn.k_proj.weight"],
                              sd[p + "self_attn.v_proj.weight"]], 0)
             L.qkv.copy_(qkv)
+            if L.qkv_bias is not None:
+                L.qkv_bias.copy_(torch.cat([sd[p + "self_attn.q_proj.bias"], sd[p + "self_attn.k_proj.bias"],
+                                            sd[p + "self_attn.v_proj.bias"]], 0))
             L.o.copy_(sd[p + "self_attn.o_proj.weight"])
             L.gate_up.copy_(torch.cat([sd[p + "mlp.gate_proj.weight"], sd[p + "mlp.up_proj.weight"]], 0))
             L.down.copy_(sd[p + "mlp.down_proj.weight"])
@@ -145,7 +153,8 @@ class LlamaModel:
         """(name, tensor) pairs of every weight (lm_head omitted when tied)."""
         for i, L in enumerate(self.layers):
             for k in LlamaLayerWeights.__slots__:
-                yield f"layers.{self.layer_start + i}.{k}", getattr(L, k)
+                if getattr(L, k) is not None:
+                    yield f"layers.{self.layer_start + i}.{k}", getattr(L, k)
         for k in ("embed", "norm"):
             t = getattr(self, k)
             if t is not None:
@@ -165,8 +174,9 @@ class LlamaModel:
     def weight_bytes(self) -> int:
         n = 0
         for L in self.layers:
-            for t in (L.in_norm, L.qkv, L.o, L.post_norm, L.gate_up, L.down):
-                n += t.numel() * t.element_size()
+            for t in (L.in_norm, L.qkv, L.o, L.post_norm, L.gate_up, L.down, L.qkv_bias):
+                if t is not None:
+                    n += t.numel() * t.element_size()
         for t in (self.embed, self.norm):
             if t is not None:
                 n += t.numel() * t.element_size()
@@ -203,7 +213,7 @@ class LlamaModel:
                 h = ops.rmsnorm(h, L.in_norm, eps)
             else:
                 ops.fused_add_rmsnorm(h, residual, L.in_norm, eps)
-            qkv = F.linear(h, L.qkv)
+            qkv = F.linear(h, L.qkv, L.qkv_bias)
             attn = self.attention(i, qkv, meta)
             h = F.linear(attn, L.o)
             if self.reduce is not None:

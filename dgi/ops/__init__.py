@@ -42,6 +42,16 @@ def load_native(required: bool = False) -> bool:
     return False
 
 
+_WARNED: set = set()
+
+
+def _warn_once(key: str, msg: str) -> None:
+    if key not in _WARNED:
+        _WARNED.add(key)
+        import warnings
+        warnings.warn(msg, RuntimeWarning, stacklevel=3)
+
+
 def native_available() -> bool:
     return load_native(False)
 
@@ -276,7 +286,10 @@ def prefill_tiles(cu_seqlens_q: list[int], tile: int = 128) -> list[tuple[int, i
 def paged_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens, nh, nkv, scale,
                   tiles=None, tree_mask=None, tree_n: int = 0, out=None) -> torch.Tensor:
     """Causal varlen attention of packed queries over the paged KV (prefix + new)."""
-    if _native(q):
+    if _native(q) and k_cache.shape[-1] != 128:
+        _warn_once("paged_prefill", f"head_dim {k_cache.shape[-1]}: the MFMA prefill kernel is built for 128; "
+                                    "using the PyTorch reference")
+    elif _native(q):
         hd = k_cache.shape[-1]
         if out is None:
             out = torch.empty(q.shape[0], nh * hd, dtype=q.dtype, device=q.device)

@@ -78,12 +78,14 @@ class TPLlamaModel(LlamaModel):
             ln2 = 1.0 + 0.1 * _rand((H,), gen, dev, torch.float32, 1.0)
             gu = _rand((2 * I, H), gen, dev, dt, std)
             down = _rand((H, I), gen, dev, dt, std / math.sqrt(2 * full.num_layers))
+            bias = _rand((full.qkv_size,), gen, dev, dt, std) if full.qkv_bias else None
+            bias_l = None if bias is None else torch.cat([bias[q0:q1], bias[k0:k0 + kl], bias[v0:v0 + kl]])
             qkv_l = torch.cat([qkv[q0:q1], qkv[k0:k0 + kl], qkv[v0:v0 + kl]]).contiguous()
             o_l = o[:, q0:q1].contiguous()
             gu_l = torch.cat([gu[r * Il:(r + 1) * Il], gu[I + r * Il:I + (r + 1) * Il]]).contiguous()
             down_l = down[:, r * Il:(r + 1) * Il].contiguous()
             del qkv, o, gu, down
-            self.layers.append(LlamaLayerWeights(ln1.to(dt), qkv_l, o_l, ln2.to(dt), gu_l, down_l))
+            self.layers.append(LlamaLayerWeights(ln1.to(dt), qkv_l, o_l, ln2.to(dt), gu_l, down_l, bias_l))
         gen.manual_seed(seed * 1000003 + 17)
         emb = _rand((full.vocab_size, H), gen, dev, dt, 1.0)
         self.embed = emb

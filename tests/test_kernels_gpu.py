@@ -82,7 +82,8 @@ def _block_tables(ctx_lens, bs, nblocks, maxw):
     return bt.to(DEV)
 
 
-@pytest.mark.parametrize("nh,nkv,hd", [(32, 8, 128), (64, 8, 128), (8, 1, 64), (8, 8, 128)])
+@pytest.mark.parametrize("nh,nkv,hd", [(32, 8, 128), (64, 8, 128), (8, 1, 64), (8, 8, 128), (28, 4, 128),
+                                       (14, 2, 64)])
 @pytest.mark.parametrize("ctx_lens", [[1], [17, 300, 64, 1000], [4097, 33]])
 def test_paged_decode(nh, nkv, hd, ctx_lens):
     bs = 16
@@ -107,7 +108,7 @@ def test_paged_decode(nh, nkv, hd, ctx_lens):
     torch.testing.assert_close(out3.float(), ref.float(), atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("nh,nkv", [(32, 8), (64, 8), (8, 1)])
+@pytest.mark.parametrize("nh,nkv", [(32, 8), (64, 8), (8, 1), (28, 4)])
 @pytest.mark.parametrize("qlens,ctxs", [([5], [5]), ([130, 1, 64], [130, 40, 600]), ([512], [512]),
                                         ([300, 77], [1000, 77])])
 def test_paged_prefill(nh, nkv, qlens, ctxs):
@@ -235,3 +236,23 @@ def test_model_decode_matches_eager_and_graph():
     # bf16 rounding differs between CPU and GPU GEMMs: demand the first tokens agree
     agree = sum(a[:2] == b[:2] for a, b in zip(outs[0], cpu))
     assert agree >= 3, (outs[0], cpu)
+
+
+def test_qwen2_engine_gpu_matches_cpu():
+    """Qwen2 family (biased QKV, GQA 7:1) through the native kernels vs the CPU engine."""
+    from dgi.engine import EngineConfig, LLMEngine
+    from dgi.models.config import get_config
+    from dgi.models.llama import LlamaModel
+    from dgi.sched.request import SamplingParams
+    mc = get_config("qwen-tiny")
+    cpu_model = LlamaModel(mc, "cpu", seed=5)
+    prompts = [[1] + list(range(7, 7 + n)) for n in (3, 60, 150)]
+    sp = SamplingParams(max_tokens=10, temperature=0.0, ignore_eos=True)
+    gm = LlamaModel(mc, "cuda", init="empty").copy_from(cpu_model)
+    ge = LLMEngine(EngineConfig(model="qwen-tiny", device="cuda", num_blocks=128, max_num_seqs=4, max_model_len=512,
+                                max_num_batched_tokens=256, use_graphs=True), model_cfg=mc, model=gm)
+    gpu = [r.output for r in ge.generate(prompts, sp)]
+    ce = LLMEngine(EngineConfig(model="qwen-tiny", device="cpu", num_blocks=128, max_num_seqs=4, max_model_len=512,
+                                max_num_batched_tokens=256, use_graphs=False), model_cfg=mc, model=cpu_model)
+    cpu = [r.output for r in ce.generate(prompts, sp)]
+    assert sum(a[:2] == b[:2] for a, b in zip(gpu, cpu)) >= 2, (gpu, cpu)
