@@ -39,6 +39,7 @@ class EngineConfig:
     layer_start: int = 0
     layer_end: Optional[int] = None
     host_kv_gb: float = 0.0            # pinned host KV tier for evicted prefix pages (0 = off)
+    graph_buckets: Optional[tuple] = None   # decode batch sizes captured as hipGraphs (None = defaults)
 
 
 @dataclasses.dataclass
@@ -102,8 +103,9 @@ class LLMEngine:
             cap = max(1, int(cfg.host_kv_gb * (1 << 30) // self.pool.page_bytes()))
             self.host_tier = HostKVTier(self.pool, cap)
             self.scheduler.radix = RadixCache(self.pool, self.host_tier)
+        rkw = {"graph_buckets": tuple(cfg.graph_buckets)} if cfg.graph_buckets else {}
         self.runner = ModelRunner(self.model, self.pool, cfg.max_num_seqs, cfg.max_model_len,
-                                  cfg.max_num_batched_tokens, cfg.use_graphs)
+                                  cfg.max_num_batched_tokens, cfg.use_graphs, **rkw)
         self.requests: dict = {}
         self.stats = {"steps": 0, "prefill_tokens": 0, "decode_tokens": 0, "generated": 0,
                       "finished": 0, "step_time": 0.0}

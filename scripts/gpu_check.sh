@@ -27,6 +27,8 @@ for s in $STEPS; do
     staged_pp) run staged_pp 600 env DGI_STAGED_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29612 bench.py --gpus 2 --model llama3-8b --layout pp --steps 40 --warmup 5 --ramp-steps 20 --concurrency 64 --max-batched-tokens 2048 ;;
     staged_pdpp8) run staged_pdpp8 900 env DGI_STAGED_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29613 bench.py --gpus 8 --model llama3-8b --steps 200 --warmup 5 --ramp-steps 60 --concurrency 96 --max-batched-tokens 2048 --output-len 64 --json-out gpurun_out/staged_pdpp8.json ;;
     gemm) run gemm 600 python scripts/gemm_bench.py 70b ;;
+    listpmc) export TMPDIR=/tmp; run listpmc 120 rocprofv3 -L ;;
+    pdcap) run pdcap 1000 python scripts/pd_capacity.py --mbt 4096 --out gpurun_out/pdcap.jsonl ;;
     gemm_tuned) run gemm_tuned 900 env PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=1 PYTORCH_TUNABLEOP_FILENAME=gpurun_out/tunableop_results.csv GEMM_MS=256,1280,2048 python scripts/gemm_bench.py 70b ;;
     sweep70b) for c in 256 384 512; do run sweep70b_c$c 900 python bench.py --steps 40 --warmup 10 --concurrency $c --json-out gpurun_out/sweep70b_c$c.json; done ;;
     sweep70b_mbt) run sweep70b_c384_mbt8k 900 python bench.py --steps 40 --warmup 10 --concurrency 384 --max-batched-tokens 8192 --json-out gpurun_out/sweep70b_c384_mbt8k.json ;;

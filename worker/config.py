@@ -66,6 +66,95 @@ class LoadControlConfig(BaseModel):
     working_hours_end: Optional[int] = Field(default_factory=_env("GPU_WORKING_HOURS_END", None, int))
 
 
+# ---------------------------------------------------------------------------
+# v2.0 sections documented by the reference README (README.md:815-910) but
+# never parsed there; here they are typed and feed the engines.
+# ---------------------------------------------------------------------------
+
+class BatchConfig(BaseModel):
+    max_batch_size: int = 32
+    max_wait_ms: float = 50.0
+
+
+class NativeRuntimeConfig(BaseModel):
+    """``dgi`` runtime knobs (``DGI_*`` env > yaml ``inference.native`` > defaults)."""
+    block_size: int = Field(default_factory=_env("DGI_BLOCK_SIZE", 16, int))
+    max_num_seqs: int = Field(default_factory=_env("DGI_MAX_NUM_SEQS", 256, int))
+    max_num_batched_tokens: int = Field(default_factory=_env("DGI_MAX_BATCHED_TOKENS", 8192, int))
+    graph_batch_buckets: List[int] = Field(
+        default_factory=lambda: [int(x) for x in get_env("DGI_GRAPH_BATCH_BUCKETS", [], list)])
+    kv_fraction: float = Field(default_factory=_env("DGI_KV_FRACTION", 0.9, float))
+    cpu_tier_gb: float = Field(default_factory=_env("DGI_CPU_TIER_GB", 0.0, float))
+    pp: int = Field(default_factory=_env("DGI_PP", 1, int))
+    pd: Optional[str] = Field(default_factory=_env("DGI_PD", None))          # "P:D", e.g. "6:2"
+    spec: Optional[str] = Field(default_factory=_env("DGI_SPEC", None))      # "eagle3"
+
+
+class InferenceConfig(BaseModel):
+    engine: Optional[str] = None        # llm | llm_native | llm_sglang | llm_vllm | llm_vllm_async
+    sglang: Dict[str, Any] = Field(default_factory=dict)
+    vllm: Dict[str, Any] = Field(default_factory=dict)
+    batch: BatchConfig = Field(default_factory=BatchConfig)
+    native: NativeRuntimeConfig = Field(default_factory=NativeRuntimeConfig)
+
+
+class ModelShardSection(BaseModel):
+    model_id: Optional[str] = None
+    start_layer: int = 0
+    end_layer: Optional[int] = None
+
+
+class GrpcSection(BaseModel):
+    host: str = "0.0.0.0"
+    port: int = 50051
+
+
+class KVCacheSection(BaseModel):
+    gpu_cache_size_gb: float = 4.0
+    cpu_cache_size_gb: float = 16.0
+    enable_redis: bool = False
+    redis_url: str = "redis://localhost:6379"
+
+
+class DistributedConfig(BaseModel):
+    enabled: bool = False
+    role: str = "hybrid"                # prefill | decode | hybrid
+    model_shard: ModelShardSection = Field(default_factory=ModelShardSection)
+    grpc: GrpcSection = Field(default_factory=GrpcSection)
+    kv_cache: KVCacheSection = Field(default_factory=KVCacheSection)
+
+
+class SpeculativeSection(BaseModel):
+    enabled: bool = False
+    num_speculative_tokens: int = 5
+    tree_width: int = 3
+    tree_depth: int = 5
+    adaptive_depth: bool = True
+    min_accept_rate: float = 0.3
+    draft_path: Optional[str] = None    # trained EAGLE-3 draft (safetensors)
+
+
+class MetricsSection(BaseModel):
+    enabled: bool = True
+    port: int = 9090
+
+
+class TracingSection(BaseModel):
+    enabled: bool = False
+    exporter: str = "otlp"              # otlp | console
+    endpoint: Optional[str] = None
+    sample_rate: float = 1.0
+
+
+class ObservabilityConfig(BaseModel):
+    metrics: MetricsSection = Field(default_factory=MetricsSection)
+    tracing: TracingSection = Field(default_factory=TracingSection)
+
+
+_ENGINE_ALIASES = {"llm": "native", "llm_native": "mi355x", "llm_sglang": "sglang", "llm_vllm": "vllm",
+                   "llm_vllm_async": "vllm_async"}
+
+
 class WorkerConfig(BaseModel):
     worker_id: Optional[str] = Field(default_factory=_env("GPU_WORKER_ID", None))
     token: Optional[str] = Field(default_factory=_env("GPU_WORKER_TOKEN", None))
@@ -85,6 +174,10 @@ class WorkerConfig(BaseModel):
     engines: Dict[str, Dict[str, Any]] = Field(default_factory=dict)
     heartbeat_interval: int = Field(default_factory=_env("GPU_HEARTBEAT_INTERVAL", 30, int))
     poll_interval: float = Field(default_factory=_env("GPU_POLL_INTERVAL", 2.0, float))
+    inference: InferenceConfig = Field(default_factory=InferenceConfig)
+    distributed: DistributedConfig = Field(default_factory=DistributedConfig)
+    speculative: SpeculativeSection = Field(default_factory=SpeculativeSection)
+    observability: ObservabilityConfig = Field(default_factory=ObservabilityConfig)
 
     def save(self, path: str = "config.yaml") -> None:
         with open(path, "w", encoding="utf-8") as f:
@@ -101,7 +194,39 @@ class WorkerConfig(BaseModel):
         if self.gpu.device_ids:
             cfg.setdefault("device_ids", list(self.gpu.device_ids))
         cfg.setdefault("layout", self.gpu.layout)
+        if engine_type == "llm":
+            self._apply_llm_sections(cfg)
         return cfg
+
+    def _apply_llm_sections(self, cfg: Dict[str, Any]) -> None:
+        inf = self.inference
+        if inf.engine and "backend" not in self.engines.get("llm", {}):
+            cfg["backend"] = _ENGINE_ALIASES.get(inf.engine, inf.engine)
+        for k in ("sglang", "vllm"):
+            d = getattr(inf, k)
+            if d:
+                cfg[k] = {**d, **cfg.get(k, {})}
+        n = inf.native
+        native = {"block_size": n.block_size, "max_num_seqs": n.max_num_seqs,
+                  "max_num_batched_tokens": n.max_num_batched_tokens, "kv_fraction": n.kv_fraction,
+                  "host_kv_gb": n.cpu_tier_gb}
+        if n.graph_batch_buckets:
+            native["graph_batch_buckets"] = list(n.graph_batch_buckets)
+        cfg["native"] = {**native, **cfg.get("native", {})}
+        if n.pd:
+            cfg.setdefault("layout", "pdpp" if n.pp > 1 else "pd")
+            cfg["prefill_ranks"] = int(n.pd.split(":")[0])
+        elif n.pp > 1:
+            cfg["layout"] = "pp"
+        sp = self.speculative
+        if (sp.enabled or (n.spec or "").lower() == "eagle3") and "speculative" not in cfg:
+            cfg["speculative"] = {"depth": sp.tree_depth, "width": sp.tree_width,
+                                  "topk": max(sp.tree_width, 1), "adaptive_depth": sp.adaptive_depth,
+                                  "min_accept_rate": sp.min_accept_rate,
+                                  **({"draft_path": sp.draft_path} if sp.draft_path else {})}
+        d = self.distributed
+        if d.enabled:
+            cfg["distributed"] = d.model_dump()
 
 
 def load_dotenv(path: str = ".env") -> None:
@@ -123,7 +248,9 @@ def load_dotenv(path: str = ".env") -> None:
         os.environ.setdefault(k, v)
 
 
-_SECTIONS = {"server": ServerConfig, "gpu": GPUConfig, "direct": DirectConfig, "load_control": LoadControlConfig}
+_SECTIONS = {"server": ServerConfig, "gpu": GPUConfig, "direct": DirectConfig, "load_control": LoadControlConfig,
+             "inference": InferenceConfig, "distributed": DistributedConfig, "speculative": SpeculativeSection,
+             "observability": ObservabilityConfig}
 
 
 def load_config(path: str = "config.yaml") -> WorkerConfig:

@@ -58,6 +58,13 @@ class DirectServer:
 
     def _setup_routes(self) -> None:
         app = self.app
+        try:   # /metrics (Prometheus), /live, /ready — same routes as the control plane
+            from observability_bridge import load_observability
+            obs = load_observability()
+            if obs is not None:
+                obs.setup_metrics_routes(app, ready_check=lambda: bool(self.worker.engines))
+        except Exception as e:  # pragma: no cover - optional deps
+            logger.info("metrics routes not mounted: %s", e)
 
         @app.get("/health")
         async def health():

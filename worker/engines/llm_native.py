@@ -86,13 +86,16 @@ class NativeLLMEngine(LLMBaseEngine):
             kv_fraction=float(frac), num_blocks=c.get("num_blocks"),
             enable_prefix_caching=bool(c.get("enable_prefix_caching", True)),
             use_graphs=bool(c.get("use_graphs", not c.get("enforce_eager", False))) and device != "cpu",
-            seed=int(c.get("seed", 0)))
+            seed=int(c.get("seed", 0)), block_size=int(c.get("block_size", 16)),
+            host_kv_gb=float(c.get("host_kv_gb", 0.0)),
+            graph_buckets=tuple(c["graph_batch_buckets"]) if c.get("graph_batch_buckets") else None)
         spec = c.get("speculative")
         if spec:
             # EAGLE-3 tree speculation for greedy requests (dgi.spec.eagle3)
             from dgi.spec.eagle3 import SpecConfig, SpecEngine
             sc = spec if isinstance(spec, dict) else {}
-            self.engine = SpecEngine(ecfg, SpecConfig(**{k: sc[k] for k in ("depth", "width", "topk") if k in sc}),
+            self.engine = SpecEngine(ecfg, SpecConfig(**{k: sc[k] for k in ("depth", "width", "topk")
+                                                          if k in sc}),
                                      model_cfg=mc)
             if sc.get("draft_path"):
                 from safetensors.torch import load_file

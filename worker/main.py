@@ -28,8 +28,36 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from api_client import APIClient  # noqa: E402
 from config import WorkerConfig, load_config  # noqa: E402
 from engines import ENGINE_REGISTRY, create_llm_engine, get_engine  # noqa: E402
+from observability_bridge import load_observability  # noqa: E402
 
 logger = logging.getLogger("worker")
+
+
+class _JobBatcher:
+    """Job-level ``ContinuousBatcher`` on its own event-loop thread, for engines
+    that batch whole requests (HF / vLLM / SGLang adapters).  The native dgi
+    engines batch per iteration themselves and bypass it."""
+
+    def __init__(self, engine, max_batch_size: int, max_wait_ms: float):
+        import asyncio
+        from batch_processor import ContinuousBatcher
+        self.loop = asyncio.new_event_loop()
+        self.thread = threading.Thread(target=self.loop.run_forever, name="job-batcher", daemon=True)
+        self.thread.start()
+        self.batcher = ContinuousBatcher(engine, max_batch_size=max_batch_size, max_wait_ms=max_wait_ms)
+        asyncio.run_coroutine_threadsafe(self.batcher.start(), self.loop).result()
+
+    def run(self, job_id: str, params: Dict[str, Any], timeout: float) -> Dict[str, Any]:
+        import asyncio
+        return asyncio.run_coroutine_threadsafe(self.batcher.submit(job_id, params, timeout=timeout),
+                                                self.loop).result()
+
+    def close(self) -> None:
+        import asyncio
+        try:
+            asyncio.run_coroutine_threadsafe(self.batcher.stop(), self.loop).result(timeout=10)
+        finally:
+            self.loop.call_soon_threadsafe(self.loop.stop)
 
 LLM_BACKENDS = {"native", "transformers", "mi355x", "dgi", "llm_native", "sglang", "vllm", "vllm_async",
                 "mi355x-node", "node", "llm_node"}
@@ -56,6 +84,10 @@ class Worker:
         self._last_job_end = 0.0
         self.direct_server = None
         self._hb_thread: Optional[threading.Thread] = None
+        self._batchers: Dict[str, _JobBatcher] = {}
+        self.metrics = None
+        self.tracer = None
+        self._setup_observability()
 
     # ------------------------------------------------------------------ state
     @property
@@ -186,6 +218,7 @@ class Worker:
                     engine = get_engine(t)(cfg)
                 engine.load_model()
                 self.engines[t] = engine
+                self._maybe_batcher(t, engine)
                 logger.info("engine %s loaded (%s)", t, type(engine).__name__)
             except Exception as e:
                 logger.error("failed to load engine %s: %s", t, e)
@@ -200,11 +233,55 @@ class Worker:
         return out
 
     # ------------------------------------------------------------------ jobs
+    def _setup_observability(self) -> None:
+        obs_cfg = self.config.observability
+        try:
+            obs = load_observability()
+        except Exception as e:  # pragma: no cover - optional deps
+            logger.info("observability unavailable: %s", e)
+            return
+        if obs is None:
+            return
+        if obs_cfg.metrics.enabled:
+            self.metrics = obs.MetricsCollector(worker_id=self.config.worker_id or "unregistered",
+                                                model_name=str(self.config.engine_config("llm").get("model_id", "")),
+                                                worker_role=self.config.role)
+        self.tracer = obs.TracingManager(service_name="gpu-worker")
+        if obs_cfg.tracing.enabled:
+            self.tracer.setup(obs_cfg.tracing.exporter, obs_cfg.tracing.endpoint, obs_cfg.tracing.sample_rate)
+
+    def _maybe_batcher(self, job_type: str, engine) -> None:
+        b = self.config.inference.batch
+        native = type(engine).__name__ in ("NativeLLMEngine", "NodeLLMEngine")
+        batchable = hasattr(engine, "batch_inference_async") or hasattr(engine, "batch_inference")
+        if job_type == "llm" and not native and batchable and b.max_batch_size > 1:
+            self._batchers[job_type] = _JobBatcher(engine, b.max_batch_size, b.max_wait_ms)
+
     def execute(self, job_type: str, params: Dict[str, Any], job_id: str = "direct") -> Dict[str, Any]:
         engine = self.engines.get(job_type)
         if engine is None:
             raise ValueError(f"No engine for type: {job_type}")
-        return engine.inference(params)
+        t0 = time.perf_counter()
+        ok = False
+        span = self.tracer.span("job.execute", {"job.id": job_id, "job.type": job_type}) if self.tracer else None
+        try:
+            if span is not None:
+                span.__enter__()
+            batcher = self._batchers.get(job_type)
+            if batcher is not None:
+                out = batcher.run(job_id, params, timeout=float(params.get("timeout", 300)))
+            else:
+                out = engine.inference(params)
+            ok = True
+            return out
+        finally:
+            if span is not None:
+                span.__exit__(None, None, None)
+            if self.metrics is not None:
+                toks = 0
+                if ok and isinstance(out, dict):
+                    toks = int((out.get("usage") or {}).get("completion_tokens", 0) or 0)
+                self.metrics.record_request("e2e", time.perf_counter() - t0, toks, ok)
 
     def _process_job(self, job: Dict[str, Any]) -> None:
         job_id, t0 = job["job_id"], time.time()
@@ -326,6 +403,9 @@ class Worker:
         self.shutdown_event.set()
         if self._executor is not None:
             self._executor.shutdown(wait=True)
+        for b in self._batchers.values():
+            b.close()
+        self._batchers.clear()
         if self.worker_id:
             self.api_client.notify_offline(self.worker_id)
         if self.direct_server is not None:
