@@ -37,9 +37,10 @@ def run_distributed(args, layout_kind: str, dist):
     f = Fabric()
     rank, world = f.rank, f.world
     layout = plan_node_layout(world, layout_kind, getattr(args, "prefill_ranks", None) or None)
-    # decode-side concurrency: 2 x 512-row microbatches keep the decode GEMMs
-    # out of the small-M regime (70B down-proj costs the same at M=256 and 512)
-    conc = args.concurrency or 1024
+    # decode-side concurrency: one microbatch of 768 rows per decode stage keeps the
+    # decode GEMMs out of the small-M regime (70B down-proj: 0.76 PF/s at M=512,
+    # 1.28 at 1024); a single decode GPU is capped by its KV pool (credits) instead
+    conc = args.concurrency or (768 * len(layout.decode_ranks) if len(layout.decode_ranks) > 1 else 1024)
     # staged rehearsal: every rank shares one GPU, so each takes a slice of its memory
     kv_frac = float(os.environ.get("DGI_KV_FRACTION", 0.5 / world if f.staged else 0.9))
     cfg = EngineConfig(model=args.model, device=str(f.device), max_num_seqs=conc,
@@ -71,7 +72,8 @@ def run_distributed(args, layout_kind: str, dist):
     all_ttfts = [v for o in obj for v in o["ttfts"]]
     per_rank = [{k: v for k, v in o.items() if k != "ttfts"} for o in obj]
     return total, el, all_ttfts, {"layout": {"kind": layout.kind, "prefill": layout.prefill_ranks,
-                                             "decode": layout.decode_ranks}, "ranks": per_rank}
+                                             "decode": layout.decode_ranks}, "concurrency": conc,
+                                  "ranks": per_rank}
 
 
 # ---------------------------------------------------------------------------- layer pipeline only

@@ -57,6 +57,9 @@ class Fabric:
         # forms a dependency cycle with) data transfers on the RCCL pair channel
         self.ctrl = dist.new_group(backend="gloo")
         self.comm_stream = torch.cuda.Stream(device=device) if self.on_gpu else None
+        # KV-migration receives land on their own stream so decode compute never
+        # queues behind a multi-hundred-MB transfer (see ``irecv_async``)
+        self.recv_stream = torch.cuda.Stream(device=device) if self.on_gpu else None
         self._pending: list = []
         # liveness watchdog over the rendezvous store (dgi.parallel.fault)
         self.watchdog = None
@@ -93,6 +96,22 @@ class Fabric:
         w = dist.irecv(t, src)
         w.wait()
         return t
+
+    def irecv_async(self, t: torch.Tensor, src: int) -> "AsyncRecv":
+        """Post a receive into ``t`` without ordering it before later compute.
+
+        On RCCL the receive is enqueued with ``recv_stream`` as the issuing
+        stream, so nothing on the compute stream waits for it; poll
+        ``ready()`` from the host and call ``complete()`` to order follow-up
+        work (e.g. a page scatter) on ``recv_stream``."""
+        if self.staged:
+            h = torch.empty(t.shape, dtype=t.dtype)
+            return AsyncRecv(self, dist.irecv(h, src), t, host=h)
+        if self.on_gpu:
+            with torch.cuda.stream(self.recv_stream):
+                w = dist.irecv(t, src)
+            return AsyncRecv(self, w, t)
+        return AsyncRecv(self, dist.irecv(t, src), t)
 
     def _reap(self) -> None:
         self._pending = [(w, t) for (w, t) in self._pending if not w.is_completed()]
@@ -137,6 +156,36 @@ class Fabric:
         self.flush()
         if self.owns_pg and dist.is_initialized():
             dist.destroy_process_group()
+
+
+class AsyncRecv:
+    """Handle of one ``Fabric.irecv_async``."""
+
+    __slots__ = ("f", "work", "t", "host", "done")
+
+    def __init__(self, fabric: Fabric, work, t: torch.Tensor, host: Optional[torch.Tensor] = None):
+        self.f, self.work, self.t, self.host, self.done = fabric, work, t, host, False
+
+    def ready(self) -> bool:
+        # gloo completes a p2p receive only inside wait(): on CPU / staged runs
+        # report ready and let complete() block (rehearsals, not a hot path)
+        if self.done or not self.f.on_gpu:
+            return True
+        return self.work.is_completed()
+
+    def complete(self) -> None:
+        """Make the data visible: afterwards work issued on ``fabric.recv_stream``
+        (GPU) or the host (CPU / staged) sees the received bytes."""
+        if self.done:
+            return
+        if self.f.on_gpu:
+            with torch.cuda.stream(self.f.recv_stream):
+                self.work.wait()
+        else:
+            self.work.wait()
+            if self.host is not None:
+                self.t.copy_(self.host)
+        self.done = True
 
 
 class CtrlChannel:

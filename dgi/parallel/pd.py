@@ -7,15 +7,16 @@ SURVEY §3.5).  Here:
 * **Prefill ranks** (``PrefillServer``) run a prefill-only engine: full
   model per GPU (Llama-3-70B bf16 fits in 288 GB), radix prefix cache,
   batched/chunked prefill.  When a prompt completes, its first token is
-  sampled locally, its KV pages are packed with the ``kv_gather`` HIP kernel
-  (all layers, one contiguous buffer) and sent to the decode driver with an
-  RCCL send over xGMI; the local pages go back to the prefix cache.
+  sampled locally and its KV pages are packed per decode stage with the
+  ``kv_gather`` HIP kernel (that stage's layer slice, one contiguous
+  buffer); each slice goes straight to its stage with an RCCL send over
+  that pair's own xGMI link.  Request metadata rides the control store.
 * **Decode driver** (``DecodeDriver``) owns the decode engine — a single GPU
-  or stage 0 of a decode layer pipeline (``pdpp``).  It receives the
-  buffer, scatters its own layers' pages into freshly allocated blocks
-  (``kv_scatter``) and forwards the remaining layers to the later pipeline
-  stages as KV-install messages on the pipeline channel; the request then
-  joins the next decode iteration.
+  or stage 0 of a decode layer pipeline (``pdpp``).  It allocates pages,
+  posts its slice receive on a side stream (decode compute never waits on
+  a migration in flight), tells the later stages the page ids (they post
+  their own receives from the prefill rank), and admits the requests to
+  the next decode iteration once its slice has landed (``kv_scatter``).
 * **Flow control**: the decode driver grants block *credits* to each prefill
   rank (gloo control group); a prefill rank admits a prompt only when it
   holds credit for the whole sequence (prompt + max_tokens), and credits
@@ -77,6 +78,10 @@ class PrefillServer:
         self.pending: collections.deque = collections.deque()
         self.migrated = 0
         self.migrate_time = 0.0
+        self.sent_bytes = 0
+        # decode stages' layer ranges: each stage is sent its own slice of every page
+        from dgi.parallel.pipeline import stage_split
+        self.split = stage_split(self.engine.model_cfg, len(layout.decode_ranks))
         self.first_tokens = 0
         self.ttfts: list = []
 
@@ -137,6 +142,12 @@ class PrefillServer:
         return outs
 
     def _migrate(self, reqs: list) -> None:
+        """Hand finished prefills to the decode side.
+
+        Request metadata (ids, sampling params, prompt tokens) travels on the
+        control store; each decode stage receives ONLY its own layer slice of
+        the pages, straight from this rank over its own xGMI link (no relay
+        through the decode driver)."""
         t0 = time.perf_counter()
         eng = self.engine
         dev = self.f.device
@@ -147,22 +158,21 @@ class PrefillServer:
             meta += _req_meta(r, nb) + [int(r.spec_state or 0)]
             toks += r.prompt
         ids_t = torch.tensor(ids, dtype=torch.int32, device=dev)
-        buf = ops.kv_gather(eng.pool.kv, ids_t)
+        bufs = [ops.kv_gather(eng.pool.kv[a:b], ids_t) for a, b in self.split]
         from dgi.parallel.fault import plan
         if plan():
             def corrupt():
-                buf.view(-1)[: max(1, buf.numel() // 64)] = float("nan")
+                bufs[0].view(-1)[: max(1, bufs[0].numel() // 64)] = float("nan")
             plan().check(self.f.rank, self.migrated + 100000, corrupt=corrupt)
-        meta_t = torch.tensor(meta, dtype=torch.int32, device=dev)
-        toks_t = torch.tensor(toks, dtype=torch.int32, device=dev)
-        self.ch.send([MSG_MIGRATE, len(reqs), len(ids), meta_t.numel(), toks_t.numel()])
-        self.f.send(meta_t, self.driver)
-        self.f.send(toks_t, self.driver)
-        self.f.send(buf, self.driver)
+        self.ch.send([MSG_MIGRATE, len(reqs), len(ids), len(meta), len(toks)])
+        self.ch.send_var(np.asarray(meta + toks, dtype=np.int64))
+        for rank, buf in zip(self.layout.decode_ranks, bufs):
+            self.f.send(buf, rank)
         for r in reqs:
             eng.scheduler.finish(r, "migrated")
             eng.requests.pop(r.rid, None)
         self.migrated += len(reqs)
+        self.sent_bytes += sum(b.numel() * b.element_size() for b in bufs)
         self.migrate_time += time.perf_counter() - t0
 
     def finish(self) -> None:
@@ -209,29 +219,53 @@ class DecodeDriver:
         self.refund = collections.Counter()
         self.refund_seqs = collections.Counter()
         self.done = set()
+        self.inflight: list = []    # migrations whose pages are still on the wire
         self.received = 0
         self.recv_bytes = 0
 
-    def _recv_migration(self, p: int, msg) -> None:
+    def _post_migration(self, p: int, msg) -> None:
+        """Start receiving a migration from prefill rank ``p``: allocate pages,
+        post this stage's slice receive off the compute stream, tell the later
+        pipeline stages (which post their own receives from ``p``)."""
         n_reqs, nblk, meta_len, tok_len = (int(x) for x in msg[1:5])
+        payload = self.chans[p].wait()
+        meta = payload[:meta_len].reshape(n_reqs, META_FIELDS + 1).tolist()
+        toks = payload[meta_len:meta_len + tok_len].tolist()
         dev = self.f.device
-        meta_t = torch.empty(meta_len, dtype=torch.int32, device=dev)
-        toks_t = torch.empty(tok_len, dtype=torch.int32, device=dev)
-        self.f.recv(meta_t, p)
-        self.f.recv(toks_t, p)
-        mc = self.mc
-        L = mc.num_layers
-        buf = torch.empty(L, 2, nblk, mc.num_kv_heads, self.bs, mc.head_dim, dtype=self.engine.pool.dtype, device=dev)
-        self.f.recv(buf, p)
-        self.recv_bytes += buf.numel() * buf.element_size()
-        sch = self.engine.scheduler
         ids = self.engine.pool.allocate(nblk)
         ids_t = torch.tensor(ids, dtype=torch.int32, device=dev)
-        ops.kv_scatter(self.engine.pool.kv, ids_t, buf[: self.L_local].contiguous())
-        if isinstance(self.engine, PipelineEngine) and L > self.L_local:
-            self.engine.send_kv_install(ids_t, buf[self.L_local:])
-        meta = meta_t.view(n_reqs, META_FIELDS + 1).tolist()
-        toks = toks_t.tolist()
+        mc = self.mc
+        buf = torch.empty(self.L_local, 2, nblk, mc.num_kv_heads, self.bs, mc.head_dim, dtype=self.engine.pool.dtype,
+                          device=dev)
+        rec = self.f.irecv_async(buf, p)
+        if isinstance(self.engine, PipelineEngine):
+            self.engine.send_kv_notice(ids_t, p)
+        self.inflight.append((p, rec, buf, ids, ids_t, meta, toks))
+        self.recv_bytes += buf.numel() * buf.element_size()     # this stage's slice
+
+    def _admit_arrived(self, block: bool = False) -> None:
+        """Scatter every completed migration into the pool and admit its requests."""
+        keep = []
+        for item in self.inflight:
+            p, rec, buf, ids, ids_t, meta, toks = item
+            if not (block or rec.ready()):
+                keep.append(item)
+                continue
+            rec.complete()
+            if self.f.on_gpu:
+                rs = self.f.recv_stream
+                rs.wait_stream(torch.cuda.current_stream())     # ids_t was made on the compute stream
+                with torch.cuda.stream(rs):
+                    ops.kv_scatter(self.engine.pool.kv, ids_t, buf)
+                torch.cuda.current_stream().wait_stream(rs)
+                buf.record_stream(rs)
+            else:
+                ops.kv_scatter(self.engine.pool.kv, ids_t, buf)
+            self._admit(p, ids, meta, toks)
+        self.inflight = keep
+
+    def _admit(self, p: int, ids: list, meta: list, toks: list) -> None:
+        sch = self.engine.scheduler
         o = k = 0
         for m in meta:
             rid, _, plen, first, nb, max_tok, tbits, seed, ign, topk, pbits, credit = m
@@ -251,7 +285,7 @@ class DecodeDriver:
             if self.track_arrivals:
                 self.arrivals.append(r)
             k += nb
-        self.received += n_reqs
+        self.received += len(meta)
 
     def local_blocks_free(self) -> int:
         return self.local_cap_blocks - sum(self.local_used.values())
@@ -271,15 +305,20 @@ class DecodeDriver:
                 if m is None:
                     break
                 if m[0] == MSG_MIGRATE:
-                    self._recv_migration(p, m)
+                    self._post_migration(p, m)
                 elif m[0] == MSG_DONE:
                     self.done.add(p)
                 elif m[0] == MSG_FINISHED:
                     if self.track_arrivals:
                         self.prefill_finished.append((int(m[1]), int(m[2]), REASONS.get(int(m[3]))))
+        self._admit_arrived()
 
-    def step(self) -> list[StepOutput]:
-        self.poll()
+    def step(self, poll: bool = True) -> list[StepOutput]:
+        """One decode iteration.  ``poll`` first takes in control messages and
+        admits landed migrations (callers that emit first tokens of arrivals
+        before the step poll themselves and pass ``poll=False``)."""
+        if poll:
+            self.poll()
         outs = self.engine.step() if self.engine.has_unfinished() else []
         for o in outs:
             if o.finished:
@@ -295,9 +334,12 @@ class DecodeDriver:
         return outs
 
     def all_prefill_done(self) -> bool:
-        return len(self.done) == len(self.prefill)
+        if len(self.done) == len(self.prefill) and self.inflight:
+            self._admit_arrived(block=True)
+        return len(self.done) == len(self.prefill) and not self.inflight
 
     def finish(self) -> None:
+        self._admit_arrived(block=True)
         if isinstance(self.engine, PipelineEngine):
             self.engine.stop_stages()
         self.f.flush()

@@ -173,16 +173,16 @@ class PipelineEngine(LLMEngine):
         return outs
 
     # ------------------------------------------------------------------ control
-    def send_kv_install(self, ids: torch.Tensor, kv_rest: torch.Tensor) -> None:
-        """Forward KV pages of layers owned by later stages (P/D into a pipeline)."""
+    def send_kv_notice(self, ids: torch.Tensor, src: int) -> None:
+        """Tell later stages that pages ``ids`` of a P/D migration are on their
+        way from prefill rank ``src`` (each stage receives its own layer slice)."""
         if self.next_rank is None:
             return
         hdr = np.zeros(HDR, np.int64)
         hdr[1] = ids.numel()
-        hdr[2] = kv_rest.shape[0]
+        hdr[2] = src
         self.f.send(_hdr_tensor(hdr, KIND_KV, self.f.device), self.next_rank)
         self.f.send(ids.to(self.f.device, torch.int32).contiguous(), self.next_rank)
-        self.f.send(kv_rest.contiguous(), self.next_rank)
 
     def pause_stages(self) -> None:
         """Stage workers return from ``run()`` (e.g. to join a barrier)."""
@@ -200,6 +200,31 @@ class PipelineEngine(LLMEngine):
 
 class StageWorker:
     """Stages 1..S-1: receive -> local layers -> forward (or sample on the last stage)."""
+
+    def _install_kv(self) -> None:
+        """Scatter migrated page slices posted so far into the pool.  The driver
+        announced them before any step that reads them, so ordering the
+        compute stream after the scatter here is all the sync needed; the
+        transfers themselves ran off the compute stream."""
+        if not self.kv_pending:
+            return
+        from dgi import ops
+        f = self.f
+        if f.on_gpu:
+            rs = f.recv_stream
+            rs.wait_stream(torch.cuda.current_stream())
+            for rec, buf, ids in self.kv_pending:
+                rec.complete()
+                with torch.cuda.stream(rs):
+                    ops.kv_scatter(self.pool.kv, ids, buf)
+                buf.record_stream(rs)
+                ids.record_stream(rs)
+            torch.cuda.current_stream().wait_stream(rs)
+        else:
+            for rec, buf, ids in self.kv_pending:
+                rec.complete()
+                ops.kv_scatter(self.pool.kv, ids, buf)
+        self.kv_pending = []
 
     def __init__(self, cfg: EngineConfig, fabric: Fabric, stage_ranks: list, model_cfg: Optional[ModelConfig] = None,
                  split: Optional[list] = None, microbatches: Optional[int] = None):
@@ -226,6 +251,7 @@ class StageWorker:
                                   cfg.max_num_batched_tokens, use_graphs=False)
         self.n_layers = b - a
         self.steps = 0
+        self.kv_pending: list = []   # (AsyncRecv, buf, ids) of P/D page slices in flight
 
     @torch.inference_mode()
     def run(self) -> str:
@@ -239,29 +265,27 @@ class StageWorker:
             hdr = hb.tolist()
             kind = hdr[0]
             if kind in (KIND_STOP, KIND_PAUSE):
+                self._install_kv()
                 if self.next is not None:
                     f.send(hb, self.next)
                 f.flush()
                 return "stop" if kind == KIND_STOP else "pause"
             if kind == KIND_KV:
-                n, Lrest = hdr[1], hdr[2]
+                n, src = hdr[1], hdr[2]
                 ids = torch.empty(n, dtype=torch.int32, device=dev)
                 f.recv(ids, self.prev)
-                buf = torch.empty(Lrest, 2, n, self.mc.num_kv_heads, self.pool.block_size, self.mc.head_dim,
-                                  dtype=self.pool.dtype, device=dev)
-                f.recv(buf, self.prev)
-                ops.kv_scatter(self.pool.kv, ids, buf[: self.n_layers].contiguous())
-                if self.next is not None and Lrest > self.n_layers:
-                    h2 = hb.clone()
-                    h2[2] = Lrest - self.n_layers
-                    f.send(h2, self.next)
+                if self.next is not None:
+                    f.send(hb, self.next)
                     f.send(ids, self.next)
-                    f.send(buf[self.n_layers:].contiguous(), self.next)
+                buf = torch.empty(self.n_layers, 2, n, self.mc.num_kv_heads, self.pool.block_size, self.mc.head_dim,
+                                  dtype=self.pool.dtype, device=dev)
+                self.kv_pending.append((f.irecv_async(buf, src), buf, ids))
                 continue
             # KIND_FWD
             from dgi.parallel.fault import plan
             if plan():
                 plan().check(f.rank, self.steps)
+            self._install_kv()
             flat = torch.empty(hdr[ModelRunner.H_LEN], dtype=torch.int32, device=dev)
             f.recv(flat, self.prev)
             T = hdr[ModelRunner.H_T]

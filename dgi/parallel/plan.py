@@ -75,15 +75,17 @@ class NodeLayout:
 
 def plan_node_layout(n_gpus: int, kind: str = "pdpp", prefill_ranks: Optional[int] = None,
                      decode_stages: Optional[int] = None) -> NodeLayout:
-    """Default P:D split for prefill-heavy loads (512-in/128-out on 70B: a
-    prefill costs ~5x the decode-GPU time of its 128 tokens).
+    """Default P:D split for prefill-heavy loads (512-in/128-out on 70B).
 
-    70B numbers behind the defaults (1 MI355X, hipBLASLt ~1.4 PF/s): a prefill
-    GPU turns ~18 prompts/s (4096-token steps) = ~2.3k output tok/s of demand;
-    one full-model decode GPU sustains ~8k tok/s (M ~ 600 rows/step, KV-bound),
-    a 2-stage decode pipeline ~13-15k tok/s (two 512-row microbatches).  So
-    below 8 GPUs a single decode GPU behind N-1 prefill GPUs is the balanced
-    layout; at 8 GPUs 6 prefill GPUs feed a 2-stage decode layer pipeline."""
+    Measured on one MI355X (scripts/pd_capacity.py, profiles/r1_pd_capacity_70b.md):
+    a prefill GPU turns 19.3 prompts/s (4096-token steps) = 2.47k output tok/s of
+    decode demand; a full-model decode GPU steps 512 rows in 111 ms (4.6k tok/s,
+    KV-capped near 640 sequences); a 40-layer stage steps 512 / 1024 / 1536 rows
+    in 56 / 89 / 129 ms.  An S-stage decode pipeline with S microbatches of R
+    rows emits R / t_stage(R) tok/s: 2 stages top out near 11.9k, 3 stages
+    (~27 layers each) reach ~15k at R = 768.  So at 8 GPUs 5 prefill GPUs
+    (12.4k demand) feed a 3-stage decode pipeline; below 8, N-1 prefill GPUs
+    feed one decode GPU."""
     if n_gpus == 1 or kind == "single":
         return NodeLayout("single", [], [0])
     if kind == "pp":
@@ -91,7 +93,7 @@ def plan_node_layout(n_gpus: int, kind: str = "pdpp", prefill_ranks: Optional[in
     if kind == "dp":
         return NodeLayout("dp", [], [0], replicas=n_gpus)
     if decode_stages is None:
-        decode_stages = 2 if (kind == "pdpp" and n_gpus >= 8) else 1
+        decode_stages = 3 if (kind == "pdpp" and n_gpus >= 8) else 1
     if prefill_ranks is None:
         prefill_ranks = n_gpus - decode_stages
     prefill_ranks = max(1, min(prefill_ranks, n_gpus - decode_stages))

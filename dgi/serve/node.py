@@ -170,7 +170,7 @@ class Router:
                     self.load[p.dst] -= 1
                     self._emit(p, r.output[0], False, None)
             self.drv.arrivals.clear()
-            outs = self.drv.step() if self.engine.has_unfinished() else []
+            outs = self.drv.step(poll=False)
         else:
             outs = self.engine.step() if self.engine.has_unfinished() else []
         for o in outs:

@@ -103,15 +103,18 @@ def _pd_body(rank, world):
     from dgi.parallel.plan import NodeLayout
     from dgi.sched.request import SamplingParams
     f = Fabric()
-    cfg = EngineConfig(model=MODEL, device="cpu", num_blocks=128, max_num_seqs=8, max_model_len=256,
+    model = os.environ.get("DGI_TEST_MODEL", MODEL)
+    cfg = EngineConfig(model=model, device="cpu", num_blocks=128, max_num_seqs=8, max_model_len=256,
                        max_num_batched_tokens=64, enable_prefix_caching=False)
-    # world 2: 1 prefill + 1 decode ; world 3: 1 prefill + 2-stage decode pipeline
-    layout = NodeLayout("pd" if world == 2 else "pdpp", [0], list(range(1, world)))
+    # DGI_TEST_PREFILL prefill ranks, the rest a decode pipeline (1 stage = plain P/D)
+    npre = int(os.environ.get("DGI_TEST_PREFILL", "1"))
+    layout = NodeLayout("pd" if world - npre == 1 else "pdpp", list(range(npre)), list(range(npre, world)))
     sp = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
-    if rank == 0:
+    if rank in layout.prefill_ranks:
         srv = PrefillServer(cfg, f, layout)
-        for p in PROMPTS:
-            srv.submit(p, sp)
+        for i, p in enumerate(PROMPTS):
+            if i % npre == rank:
+                srv.submit(p, sp)
         while srv.busy():
             srv.step()
         srv.finish()
@@ -154,7 +157,7 @@ def test_plan_layer_split_gives_head_stage_fewer_layers():
 
 def test_node_layout_defaults():
     lay = plan_node_layout(8)
-    assert lay.kind == "pdpp" and len(lay.decode_ranks) == 2 and len(lay.prefill_ranks) == 6
+    assert lay.kind == "pdpp" and len(lay.decode_ranks) == 3 and len(lay.prefill_ranks) == 5
     assert plan_node_layout(1).kind == "single"
     assert plan_node_layout(2).kind == "pd"
     four = plan_node_layout(4)
@@ -173,6 +176,23 @@ def test_pd_migration_matches_local_decode(world):
     ref = _reference_outputs()
     out = _spawn("_pd_body", world)
     assert out[1] == ref
+
+
+@pytest.mark.parametrize("npre,world", [(2, 4), (1, 4)])
+def test_pd_multi_prefill_and_three_stage_decode(npre, world, monkeypatch):
+    """Several prefill ranks feeding one decode pipeline, and a 3-stage decode
+    pipeline: every stage receives its own layer slice straight from the
+    prefill rank (async receive) and the outputs equal local decoding."""
+    model = "llama-tiny-hd128"          # 4 layers: room for 3 stages
+    monkeypatch.setenv("DGI_TEST_MODEL", model)
+    monkeypatch.setenv("DGI_TEST_PREFILL", str(npre))
+    from dgi.engine import EngineConfig, LLMEngine
+    from dgi.sched.request import SamplingParams
+    e = LLMEngine(EngineConfig(model=model, device="cpu", num_blocks=128, max_num_seqs=8, max_model_len=256,
+                               max_num_batched_tokens=64, enable_prefix_caching=False))
+    ref = [r.output for r in e.generate(PROMPTS, SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True))]
+    out = _spawn("_pd_body", world)
+    assert out[npre] == ref
 
 
 def _tp_body(rank, world):
