@@ -19,6 +19,7 @@ from dgi.models.llama import LlamaModel
 from dgi.runtime.model_runner import ModelRunner
 from dgi.sched.request import Request, SamplingParams, Status
 from dgi.sched.scheduler import Scheduler, SchedulerConfig
+from dgi.utils.trace import phase
 
 
 @dataclasses.dataclass
@@ -133,11 +134,14 @@ class LLMEngine:
     def step(self) -> list[StepOutput]:
         t0 = time.perf_counter()
         self.model.kv_cache = self.pool.kv   # engines may share one model object
-        sb = self.scheduler.schedule()
+        with phase("schedule"):
+            sb = self.scheduler.schedule()
         if sb.empty:
             return []
-        res = self.runner.execute(sb)
-        outs = self._apply(sb, res.rows, res.tokens)
+        with phase("execute", decode=len(sb.decode), prefill=len(sb.prefill)):
+            res = self.runner.execute(sb)
+        with phase("apply"):
+            outs = self._apply(sb, res.rows, res.tokens)
         self.stats["step_time"] += time.perf_counter() - t0
         return outs
 

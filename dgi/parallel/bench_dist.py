@@ -66,7 +66,8 @@ def run_distributed(args, layout_kind: str, dist):
     tl = [torch.zeros_like(t) for _ in range(world)]
     dist.all_gather(tl, t)
     obj = [None] * world
-    dist.all_gather_object(obj, {"ttfts": ttfts, "role": role, **extra})
+    from dgi.utils.trace import phase_summary
+    dist.all_gather_object(obj, {"ttfts": ttfts, "role": role, "phases": phase_summary(), **extra})
     total = int(sum(x[0].item() for x in tl))
     el = max(x[1].item() for x in tl)
     all_ttfts = [v for o in obj for v in o["ttfts"]]

@@ -42,6 +42,7 @@ from dgi.parallel.fabric import CtrlChannel, Fabric
 from dgi.parallel.pipeline import PipelineEngine
 from dgi.parallel.plan import NodeLayout
 from dgi.sched.request import Request, SamplingParams, Status
+from dgi.utils.trace import mark, phase
 
 MSG_MIGRATE, MSG_CREDIT, MSG_DONE, MSG_FINISHED = 1, 2, 3, 4
 REASONS = {0: None, 1: "length", 2: "stop"}
@@ -138,7 +139,8 @@ class PrefillServer:
             else:
                 ready.append(o.request)
         if ready:
-            self._migrate(ready)
+            with phase("migrate_send", reqs=len(ready)):
+                self._migrate(ready)
         return outs
 
     def _migrate(self, reqs: list) -> None:
@@ -252,6 +254,7 @@ class DecodeDriver:
                 keep.append(item)
                 continue
             rec.complete()
+            mark("kv_migration_landed", len(meta))
             if self.f.on_gpu:
                 rs = self.f.recv_stream
                 rs.wait_stream(torch.cuda.current_stream())     # ids_t was made on the compute stream

@@ -35,6 +35,7 @@ from dgi.kv.block_pool import BlockPool, num_blocks_for_budget
 from dgi.parallel.fabric import Fabric
 from dgi.parallel.plan import plan_layer_split
 from dgi.runtime.model_runner import ModelRunner
+from dgi.utils.trace import phase
 
 KIND_STOP, KIND_FWD, KIND_KV, KIND_PAUSE = 0, 1, 2, 3
 HDR = ModelRunner.HEADER_SIZE
@@ -292,7 +293,8 @@ class StageWorker:
             hidden = torch.empty(T, H, dtype=self.pool.dtype, device=dev)
             f.recv(hidden, self.prev)
             _ids, meta, temps, seeds = self.runner.meta_from_device(flat, hdr)
-            out = self.model.forward(meta, hidden=hidden)
+            with phase("stage_forward", rows=T):
+                out = self.model.forward(meta, hidden=hidden)
             self.steps += 1
             if self.is_last:
                 nlog = hdr[ModelRunner.H_NLOG]

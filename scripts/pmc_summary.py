@@ -19,6 +19,16 @@ import sys
 SIMDS = 256 * 4
 
 
+def _key(name: str) -> str:
+    n = name.replace("void ", "").replace("(anonymous namespace)::", "").strip()
+    for sep in ("(", "<"):
+        i = n.find(sep)
+        if i > 0:
+            n = n[:i] + ("<..>" if sep == "<" else "")
+            break
+    return n[:60]
+
+
 def load(path):
     files = [path] if os.path.isfile(path) else glob.glob(os.path.join(path, "**", "*counter_collection.csv"),
                                                            recursive=True)
@@ -27,8 +37,7 @@ def load(path):
     seen = set()
     for f in files:
         for r in csv.DictReader(open(f)):
-            name = r.get("Kernel_Name", "?")
-            key = name.split("(")[0].replace("void ", "").strip()[:60]
+            key = _key(r.get("Kernel_Name", "?"))
             disp = (f, r.get("Dispatch_Id"))
             per[key][r["Counter_Name"]] += float(r["Counter_Value"])
             if disp not in seen and r.get("Start_Timestamp") and r.get("End_Timestamp"):
@@ -42,7 +51,7 @@ def load(path):
             if not f.endswith("kernel_trace.csv"):
                 continue
             for r in csv.DictReader(open(f)):
-                key = r.get("Kernel_Name", "?").split("(")[0].replace("void ", "").strip()[:60]
+                key = _key(r.get("Kernel_Name", "?"))
                 dur[key] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
                 per[key]["_dispatches"] += 1
     return per, dur

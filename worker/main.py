@@ -247,8 +247,10 @@ class Worker:
                                                 model_name=str(self.config.engine_config("llm").get("model_id", "")),
                                                 worker_role=self.config.role)
         self.tracer = obs.TracingManager(service_name="gpu-worker")
-        if obs_cfg.tracing.enabled:
-            self.tracer.setup(obs_cfg.tracing.exporter, obs_cfg.tracing.endpoint, obs_cfg.tracing.sample_rate)
+        if obs_cfg.tracing.enabled and self.tracer.setup(obs_cfg.tracing.exporter, obs_cfg.tracing.endpoint,
+                                                         obs_cfg.tracing.sample_rate):
+            from dgi.utils.trace import set_tracer
+            set_tracer(self.tracer)      # engine step phases become child spans
 
     def _maybe_batcher(self, job_type: str, engine) -> None:
         b = self.config.inference.batch
