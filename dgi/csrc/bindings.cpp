@@ -14,8 +14,8 @@ int dgi_rmsnorm(void* out, const void* x, const void* w, int T, int H, float eps
 int dgi_fused_add_rmsnorm(void* x, void* residual, const void* w, int T, int H, float eps,
                           hipStream_t s);
 int dgi_rope_cache(void* qkv, int T, int qkv_stride, const int* positions, const float* cos_sin,
-                   int nh, int nkv, int hd, const int* slot_mapping, void* k_cache, void* v_cache,
-                   int block_size, hipStream_t s);
+                   int nh, int nkv, int hd, int rd, int mode, const int* slot_mapping, void* k_cache,
+                   void* v_cache, int block_size, hipStream_t s);
 int dgi_paged_decode(const void* q, int q_stride, const void* k_cache, const void* v_cache,
                      const int* block_tables, int bt_stride, const int* context_lens, void* out,
                      int out_stride, float* part_o, float* part_lse, int B, int nh, int nkv, int hd,
@@ -85,20 +85,23 @@ void fused_add_rmsnorm(at::Tensor x, at::Tensor residual, const at::Tensor& w, d
 }
 
 // k_cache / v_cache: [num_blocks, nkv, bs, hd] (contiguous per-layer views)
+// cos_sin: [max_pos, rd] fp32 (rd/2 cos | rd/2 sin); rd = rotary dims (<= hd);
+// mode 0 = NeoX pairing, 1 = interleaved (GPT-J / GLM)
 void rope_cache(at::Tensor qkv, const at::Tensor& positions, const at::Tensor& cos_sin, int64_t nh,
                 int64_t nkv, int64_t hd, const at::Tensor& slot_mapping, at::Tensor k_cache,
-                at::Tensor v_cache) {
+                at::Tensor v_cache, int64_t mode) {
   check_bf16(qkv, "qkv"); check_i32(positions, "positions"); check_i32(slot_mapping, "slot_mapping");
   check_bf16(k_cache, "k_cache"); check_bf16(v_cache, "v_cache");
-  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() && cos_sin.size(1) == hd);
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() && cos_sin.size(1) <= hd);
+  TORCH_CHECK(positions.numel() == 0 || cos_sin.dim() == 2);
   TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1 && qkv.size(1) >= (nh + 2 * nkv) * hd);
   TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous());
   TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == nkv && k_cache.size(3) == hd);
   const int T = (int)qkv.size(0);
   TORCH_CHECK(positions.numel() == T && slot_mapping.numel() == T);
   check_rc(dgi_rope_cache(qkv.data_ptr(), T, (int)qkv.stride(0), positions.data_ptr<int>(),
-                          cos_sin.data_ptr<float>(), (int)nh, (int)nkv, (int)hd,
-                          slot_mapping.data_ptr<int>(), k_cache.data_ptr(), v_cache.data_ptr(),
+                          cos_sin.data_ptr<float>(), (int)nh, (int)nkv, (int)hd, (int)cos_sin.size(1),
+                          (int)mode, slot_mapping.data_ptr<int>(), k_cache.data_ptr(), v_cache.data_ptr(),
                           (int)k_cache.size(2), cur_stream()),
            "rope_cache");
 }
@@ -274,7 +277,7 @@ TORCH_LIBRARY(dgi, m) {
   m.def("rmsnorm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
   m.def("fused_add_rmsnorm(Tensor(a!) x, Tensor(b!) residual, Tensor w, float eps) -> ()");
   m.def("rope_cache(Tensor(a!) qkv, Tensor positions, Tensor cos_sin, int nh, int nkv, int hd, "
-        "Tensor slot_mapping, Tensor(b!) k_cache, Tensor(c!) v_cache) -> ()");
+        "Tensor slot_mapping, Tensor(b!) k_cache, Tensor(c!) v_cache, int mode=0) -> ()");
   m.def("paged_decode(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor context_lens, Tensor(b!) part_o, Tensor(c!) part_lse, int nh, int nkv, int max_splits, "
         "int part_size, float scale) -> ()");

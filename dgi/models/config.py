@@ -1,4 +1,4 @@
-"""Model configurations (Llama-3 8B/70B, Qwen2.5 7B/0.5B, OPT-125m, tiny test models).
+"""Model configurations (Llama-3 8B/70B, Qwen2.5 7B/0.5B, GLM-4-9B, OPT-125m, tiny test models).
 
 Mirrors the fields the reference reads from HF ``AutoConfig``
 (worker/distributed/model_shard.py:273-311 uses hidden_size,
@@ -31,9 +31,15 @@ class ModelConfig:
     rms_eps: float = 1e-5
     max_position: int = 8192
     tie_embeddings: bool = False
-    qkv_bias: bool = False          # Qwen2: biased q/k/v projections
+    qkv_bias: bool = False          # Qwen2 / GLM-4: biased q/k/v projections
+    rotary_dim: Optional[int] = None  # rotated dims per head (GLM-4: head_dim / 2); None = head_dim
+    rope_interleaved: bool = False  # GLM-4 / GPT-J pairing (2i, 2i+1) instead of NeoX (i, i+rd/2)
     bos_token_id: int = 128000
     eos_token_id: int = 128001
+
+    @property
+    def rope_dim(self) -> int:
+        return self.rotary_dim or self.head_dim
 
     @property
     def q_size(self) -> int:
@@ -85,7 +91,10 @@ class ModelConfig:
         eos = d.get("eos_token_id", 2)
         if isinstance(eos, list):
             eos = eos[0]
-        arch = "qwen2" if mt == "qwen2" else "llama"
+        arch = {"qwen2": "qwen2", "glm": "glm"}.get(mt, "llama")
+        hd = d.get("head_dim") or H // nh
+        prf = d.get("partial_rotary_factor", rp.get("partial_rotary_factor", 1.0))
+        rot = int(hd * prf) if prf and prf < 1.0 else None
         return ModelConfig(name=name, arch=arch, vocab_size=d["vocab_size"], hidden_size=H,
                            intermediate_size=d["intermediate_size"], num_layers=d["num_hidden_layers"],
                            num_heads=nh, num_kv_heads=d.get("num_key_value_heads", nh),
@@ -94,6 +103,7 @@ class ModelConfig:
                            max_position=d.get("max_position_embeddings", 8192),
                            tie_embeddings=d.get("tie_word_embeddings", False),
                            qkv_bias=bool(d.get("attention_bias", mt == "qwen2")),
+                           rotary_dim=rot, rope_interleaved=(mt == "glm"),
                            bos_token_id=d.get("bos_token_id", 1), eos_token_id=eos)
 
     @staticmethod
@@ -134,6 +144,15 @@ PRESETS: dict[str, ModelConfig] = {
                              intermediate_size=1536, num_layers=2, num_heads=14, num_kv_heads=2, head_dim=128,
                              rope_theta=1000000.0, rms_eps=1e-6, max_position=4096, tie_embeddings=True,
                              qkv_bias=True, bos_token_id=1, eos_token_id=2),
+    # GLM-4-9B (HF "glm"): Llama block + biased QKV, GQA 16:1, half-dim interleaved RoPE
+    "glm-4-9b": ModelConfig(name="glm-4-9b", arch="glm", vocab_size=151552, hidden_size=4096,
+                            intermediate_size=13696, num_layers=40, num_heads=32, num_kv_heads=2, head_dim=128,
+                            rope_theta=10000.0, rms_eps=1.5625e-07, max_position=131072, qkv_bias=True,
+                            rotary_dim=64, rope_interleaved=True, bos_token_id=151331, eos_token_id=151329),
+    "glm-tiny": ModelConfig(name="glm-tiny", arch="glm", vocab_size=1024, hidden_size=1024, intermediate_size=1536,
+                            num_layers=2, num_heads=8, num_kv_heads=2, head_dim=128, rope_theta=10000.0,
+                            rms_eps=1.5625e-07, max_position=4096, qkv_bias=True, rotary_dim=64,
+                            rope_interleaved=True, bos_token_id=1, eos_token_id=2),
     "opt-125m": ModelConfig(name="opt-125m", arch="opt", vocab_size=50272, hidden_size=768,
                             intermediate_size=3072, num_layers=12, num_heads=12, num_kv_heads=12, head_dim=64,
                             max_position=2048, tie_embeddings=True, bos_token_id=2, eos_token_id=2),
@@ -150,6 +169,9 @@ ALIASES = {
     "Qwen/Qwen2.5-7B": "qwen2.5-7b",
     "Qwen/Qwen2-7B-Instruct": "qwen2.5-7b",
     "Qwen/Qwen2.5-0.5B-Instruct": "qwen2.5-0.5b",
+    "THUDM/glm-4-9b-chat-hf": "glm-4-9b",
+    "THUDM/glm-4-9b-chat": "glm-4-9b",
+    "THUDM/glm-4-9b-hf": "glm-4-9b",
 }
 
 
@@ -160,6 +182,8 @@ def get_config(name_or_path: str) -> ModelConfig:
     if os.path.exists(name_or_path):
         return ModelConfig.from_file(name_or_path)
     lk = key.lower()
+    if "glm-4" in lk or "glm4" in lk:
+        return dataclasses.replace(PRESETS["glm-4-9b"], name=name_or_path)
     if "qwen" in lk:
         return dataclasses.replace(PRESETS["qwen2.5-0.5b" if "0.5b" in lk else "qwen2.5-7b"], name=name_or_path)
     if "70b" in lk:

@@ -1,4 +1,4 @@
-"""Native Llama-family decoder for the MI355X runtime (Llama-3 8B / 70B, Qwen2 / Qwen2.5).
+"""Native Llama-family decoder for the MI355X runtime (Llama-3 8B / 70B, Qwen2 / Qwen2.5, GLM-4).
 
 Replaces the HF modules the reference executes (worker/engines/llm.py:22-69,
 worker/distributed/model_shard.py:28-246).  Per layer the step runs
@@ -9,7 +9,8 @@ worker/distributed/model_shard.py:28-246).  Per layer the step runs
 
 with fused QKV and gate|up weights so each layer issues 4 GEMMs.  Qwen2's biased
 q/k/v projections ride in the QKV GEMM's bias epilogue (hipBLASLt), so the
-family adds no kernel.  A model
+family adds no kernel; GLM-4 adds biased QKV and half-dim interleaved RoPE
+(``rope_cache`` mode 1 over the first ``rotary_dim`` dims).  A model
 object may hold any contiguous layer range (pipeline stage): stage 0 owns the
 embedding, the last stage the final norm and LM head, exactly like the
 reference's ``ModelShard`` (model_shard.py:28-59).  Between stages a single
@@ -72,8 +73,9 @@ class LlamaModel:
             self._init_random(seed)
         elif init == "empty":
             self._init_empty()
-        self.cos_sin = ops.rope_cos_sin(cfg.head_dim, cfg.max_position, cfg.rope_theta, cfg.rope_scaling,
+        self.cos_sin = ops.rope_cos_sin(cfg.rope_dim, cfg.max_position, cfg.rope_theta, cfg.rope_scaling,
                                         device=self.device)
+        self.rope_mode = 1 if cfg.rope_interleaved else 0
 
     # ------------------------------------------------------------------ weights
     def _init_empty(self):
@@ -137,7 +139,10 @@ class LlamaModel:
                 L.qkv_bias.copy_(torch.cat([sd[p + "self_attn.q_proj.bias"], sd[p + "self_attn.k_proj.bias"],
                                             sd[p + "self_attn.v_proj.bias"]], 0))
             L.o.copy_(sd[p + "self_attn.o_proj.weight"])
-            L.gate_up.copy_(torch.cat([sd[p + "mlp.gate_proj.weight"], sd[p + "mlp.up_proj.weight"]], 0))
+            if p + "mlp.gate_up_proj.weight" in sd:     # GLM: fused [gate; up]
+                L.gate_up.copy_(sd[p + "mlp.gate_up_proj.weight"])
+            else:
+                L.gate_up.copy_(torch.cat([sd[p + "mlp.gate_proj.weight"], sd[p + "mlp.up_proj.weight"]], 0))
             L.down.copy_(sd[p + "mlp.down_proj.weight"])
             L.in_norm.copy_(sd[p + "input_layernorm.weight"])
             L.post_norm.copy_(sd[p + "post_attention_layernorm.weight"])
@@ -190,7 +195,7 @@ class LlamaModel:
         kc = self.kv_cache[li, 0]
         vc = self.kv_cache[li, 1]
         ops.rope_cache(qkv, meta.positions, self.cos_sin, c.num_heads, c.num_kv_heads, c.head_dim,
-                       meta.slot_mapping, kc, vc)
+                       meta.slot_mapping, kc, vc, self.rope_mode)
         T = qkv.shape[0]
         out = torch.empty(T, c.q_size, device=qkv.device, dtype=qkv.dtype)
         nd = meta.num_decode

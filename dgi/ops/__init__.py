@@ -133,20 +133,30 @@ def _rotate(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tens
     return torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1)
 
 
-def rope_cache_ref(qkv, positions, cos_sin, nh, nkv, hd, slot_mapping, k_cache, v_cache) -> None:
+def _rotate_interleaved(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    x1, x2 = x[..., 0::2], x[..., 1::2]
+    return torch.stack([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1).flatten(-2)
+
+
+def _rope(x: torch.Tensor, cs: torch.Tensor, mode: int) -> torch.Tensor:
+    """Rotate the first rd = cs.shape[-1] dims of x (fp32); the rest pass through."""
+    rd = cs.shape[-1]
+    cos, sin = cs[:, None, : rd // 2], cs[:, None, rd // 2:]
+    rot = _rotate(x[..., :rd], cos, sin) if mode == 0 else _rotate_interleaved(x[..., :rd], cos, sin)
+    return rot if rd == x.shape[-1] else torch.cat([rot, x[..., rd:]], dim=-1)
+
+
+def rope_cache_ref(qkv, positions, cos_sin, nh, nkv, hd, slot_mapping, k_cache, v_cache, mode: int = 0) -> None:
     T = qkv.shape[0]
     if T == 0:
         return
     bs = k_cache.shape[2]
-    half = hd // 2
     cs = cos_sin[positions.long()]
-    cos = cs[:, None, :half]
-    sin = cs[:, None, half:]
     q = qkv[:, : nh * hd].float().view(T, nh, hd)
     k = qkv[:, nh * hd:(nh + nkv) * hd].float().view(T, nkv, hd)
     v = qkv[:, (nh + nkv) * hd:(nh + 2 * nkv) * hd].view(T, nkv, hd)
-    qr = _rotate(q, cos, sin).to(qkv.dtype)
-    kr = _rotate(k, cos, sin).to(qkv.dtype)
+    qr = _rope(q, cs, mode).to(qkv.dtype)
+    kr = _rope(k, cs, mode).to(qkv.dtype)
     qkv[:, : nh * hd] = qr.reshape(T, nh * hd)
     slots = slot_mapping.long()
     ok = slots >= 0
@@ -157,12 +167,15 @@ def rope_cache_ref(qkv, positions, cos_sin, nh, nkv, hd, slot_mapping, k_cache, 
         v_cache[blk, :, off] = v[ok]
 
 
-def rope_cache(qkv, positions, cos_sin, nh, nkv, hd, slot_mapping, k_cache, v_cache) -> None:
-    """Rotate q in place inside the fused qkv rows, write rotated k and v into the paged cache."""
+def rope_cache(qkv, positions, cos_sin, nh, nkv, hd, slot_mapping, k_cache, v_cache, mode: int = 0) -> None:
+    """Rotate q in place inside the fused qkv rows, write rotated k and v into the paged cache.
+
+    ``cos_sin`` is [max_pos, rd] (rd <= hd rotary dims); ``mode`` 0 = NeoX
+    pairing (Llama, Qwen2), 1 = interleaved pairs (GLM-4, GPT-J)."""
     if _native(qkv):
-        torch.ops.dgi.rope_cache(qkv, positions, cos_sin, nh, nkv, hd, slot_mapping, k_cache, v_cache)
+        torch.ops.dgi.rope_cache(qkv, positions, cos_sin, nh, nkv, hd, slot_mapping, k_cache, v_cache, mode)
     else:
-        rope_cache_ref(qkv, positions, cos_sin, nh, nkv, hd, slot_mapping, k_cache, v_cache)
+        rope_cache_ref(qkv, positions, cos_sin, nh, nkv, hd, slot_mapping, k_cache, v_cache, mode)
 
 
 # ----------------------------------------------------------------------------

@@ -113,7 +113,7 @@ class Eagle3Draft:
         qkv = F.linear(torch.cat([e, hn], dim=-1), self.qkv)
         kc, vc = self.kv_cache[0, 0], self.kv_cache[0, 1]
         ops.rope_cache(qkv, meta.positions, self.target.cos_sin, c.num_heads, c.num_kv_heads, c.head_dim,
-                       meta.slot_mapping, kc, vc)
+                       meta.slot_mapping, kc, vc, self.target.rope_mode)
         attn = ops.paged_prefill(qkv, kc, vc, meta.pre_block_tables, meta.pre_cu_seqlens, meta.pre_context_lens,
                                  c.num_heads, c.num_kv_heads, self.scale, tiles=meta.pre_tiles,
                                  tree_mask=meta.tree_mask, tree_n=meta.tree_n)
@@ -142,14 +142,11 @@ class Eagle3Draft:
         qkv = F.linear(torch.cat([e, rms(hidden, P["hidden_norm"])], -1), P["qkv"])
         nh, nkv, hd = c.num_heads, c.num_kv_heads, c.head_dim
         q, k, v = qkv.split([nh * hd, nkv * hd, nkv * hd], -1)
-        cs = self.target.cos_sin[pos.long()]             # [B, S, hd] (cos | sin halves)
-        cos, sin = cs[..., : hd // 2].float(), cs[..., hd // 2:].float()
+        cs = self.target.cos_sin[pos.long()].reshape(B * S, -1).float()   # [B*S, rd] (cos | sin halves)
 
-        def rot(x, n):
-            x = x.view(B, S, n, hd).float()
-            x1, x2 = x[..., : hd // 2], x[..., hd // 2:]
-            cc, ss = cos[:, :, None], sin[:, :, None]
-            return torch.cat([x1 * cc - x2 * ss, x2 * cc + x1 * ss], -1).to(qkv.dtype)
+        def rot(x, n):   # differentiable RoPE, same pairing / partial dims as the target's kernel
+            y = ops._rope(x.reshape(B * S, n, hd).float(), cs, self.target.rope_mode)
+            return y.view(B, S, n, hd).to(qkv.dtype)
         q, k = rot(q, nh), rot(k, nkv)
         v = v.view(B, S, nkv, hd)
         rep = nh // nkv

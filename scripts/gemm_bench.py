@@ -30,13 +30,17 @@ def bench(M, N, K, iters=20):
 
 
 def main():
+    lib = os.environ.get("GEMM_LIB", "")
+    if lib:   # "cublas" selects rocBLAS on ROCm, "cublaslt" hipBLASLt
+        torch.backends.cuda.preferred_blas_library(lib)
     out = []
     for name, (N, K) in SHAPES.items():
         if len(sys.argv) > 1 and not name.startswith(sys.argv[1]):
             continue
         for M in MS:
             us, tf = bench(M, N, K)
-            out.append({"gemm": name, "M": M, "N": N, "K": K, "us": round(us, 1), "TFLOPs": round(tf, 1),
+            out.append({"gemm": name, "lib": lib or "default", "M": M, "N": N, "K": K, "us": round(us, 1),
+                        "TFLOPs": round(tf, 1),
                         "weight_GBs": round(N * K * 2 / (us * 1e-6) / 1e9, 1)})
             print(json.dumps(out[-1]), flush=True)
 

@@ -27,6 +27,9 @@ for s in $STEPS; do
     staged_pp) run staged_pp 600 env DGI_STAGED_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29612 bench.py --gpus 2 --model llama3-8b --layout pp --steps 40 --warmup 5 --ramp-steps 20 --concurrency 64 --max-batched-tokens 2048 ;;
     staged_pdpp8) run staged_pdpp8 900 env DGI_STAGED_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29613 bench.py --gpus 8 --model llama3-8b --steps 200 --warmup 5 --ramp-steps 60 --concurrency 96 --max-batched-tokens 2048 --output-len 64 --json-out gpurun_out/staged_pdpp8.json ;;
     gemm) run gemm 600 python scripts/gemm_bench.py 70b ;;
+    gemm_libs) run gemm_hipblaslt 600 env GEMM_MS=256,512,768,1024,1536,2048,3072,4096 GEMM_LIB=cublaslt python scripts/gemm_bench.py 70b && run gemm_rocblas 600 env GEMM_MS=256,512,768,1024,1536,2048,3072,4096 GEMM_LIB=cublas python scripts/gemm_bench.py 70b ;;
+    staged_pd2) run staged_pd2 600 env DGI_STAGED_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29614 bench.py --gpus 2 --model llama3-8b --steps 60 --warmup 5 --ramp-steps 30 --concurrency 64 --max-batched-tokens 2048 --output-len 64 --json-out gpurun_out/staged_pd2.json ;;
+    staged_pd4) run staged_pd4 600 env DGI_STAGED_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29615 bench.py --gpus 4 --model llama3-8b --steps 60 --warmup 5 --ramp-steps 30 --concurrency 64 --max-batched-tokens 2048 --output-len 64 --json-out gpurun_out/staged_pd4.json ;;
     pmc_attn) export TMPDIR=/tmp; run pmc_attn 240 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_attn -o run -- python3 scripts/attn_bench.py ;;
     listpmc) export TMPDIR=/tmp; run listpmc 120 rocprofv3 -L ;;
     pdcap) run pdcap 1000 python scripts/pd_capacity.py --mbt 4096 --out gpurun_out/pdcap.jsonl ;;

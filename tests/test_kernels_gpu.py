@@ -52,19 +52,21 @@ def _make_cache(nblocks, nkv, bs, hd):
     return k, v
 
 
-@pytest.mark.parametrize("nh,nkv,hd", [(32, 8, 128), (8, 1, 64), (64, 8, 128)])
-def test_rope_cache(nh, nkv, hd):
+@pytest.mark.parametrize("nh,nkv,hd,rd,mode", [(32, 8, 128, 128, 0), (8, 1, 64, 64, 0), (64, 8, 128, 128, 0),
+                                               (32, 2, 128, 64, 1), (8, 2, 128, 128, 1), (16, 4, 128, 64, 0)])
+def test_rope_cache(nh, nkv, hd, rd, mode):
+    """NeoX (mode 0) and interleaved GLM-style (mode 1) pairing, full and partial rotary dims."""
     T, bs, nb = 19, 16, 40
     qkv = _bf(T, (nh + 2 * nkv) * hd)
     pos = torch.randint(0, 4000, (T,), device=DEV, dtype=torch.int32)
     slots = torch.randperm(nb * bs, device=DEV)[:T].to(torch.int32)
     slots[3] = -1
-    cs = ops.rope_cos_sin(hd, 4096, 500000.0, device=DEV)
+    cs = ops.rope_cos_sin(rd, 4096, 500000.0 if mode == 0 else 10000.0, device=DEV)
     k1, v1 = _make_cache(nb, nkv, bs, hd)
     k2, v2 = k1.clone(), v1.clone()
     q1, q2 = qkv.clone(), qkv.clone()
-    ops.rope_cache(q1, pos, cs, nh, nkv, hd, slots, k1, v1)
-    ops.rope_cache_ref(q2, pos, cs, nh, nkv, hd, slots, k2, v2)
+    ops.rope_cache(q1, pos, cs, nh, nkv, hd, slots, k1, v1, mode)
+    ops.rope_cache_ref(q2, pos, cs, nh, nkv, hd, slots, k2, v2, mode)
     torch.testing.assert_close(q1[:, : nh * hd].float(), q2[:, : nh * hd].float(), atol=2e-2, rtol=2e-2)
     torch.testing.assert_close(k1.float(), k2.float(), atol=2e-2, rtol=2e-2)
     torch.testing.assert_close(v1.float(), v2.float(), atol=0, rtol=0)
@@ -253,6 +255,26 @@ def test_qwen2_engine_gpu_matches_cpu():
                                 max_num_batched_tokens=256, use_graphs=True), model_cfg=mc, model=gm)
     gpu = [r.output for r in ge.generate(prompts, sp)]
     ce = LLMEngine(EngineConfig(model="qwen-tiny", device="cpu", num_blocks=128, max_num_seqs=4, max_model_len=512,
+                                max_num_batched_tokens=256, use_graphs=False), model_cfg=mc, model=cpu_model)
+    cpu = [r.output for r in ce.generate(prompts, sp)]
+    assert sum(a[:2] == b[:2] for a, b in zip(gpu, cpu)) >= 2, (gpu, cpu)
+
+
+def test_glm_engine_gpu_matches_cpu():
+    """GLM-4 family (biased QKV, half-dim interleaved RoPE) through the native kernels vs the CPU engine."""
+    from dgi.engine import EngineConfig, LLMEngine
+    from dgi.models.config import get_config
+    from dgi.models.llama import LlamaModel
+    from dgi.sched.request import SamplingParams
+    mc = get_config("glm-tiny")
+    cpu_model = LlamaModel(mc, "cpu", seed=7)
+    prompts = [[1] + list(range(9, 9 + n)) for n in (4, 70, 140)]
+    sp = SamplingParams(max_tokens=10, temperature=0.0, ignore_eos=True)
+    gm = LlamaModel(mc, "cuda", init="empty").copy_from(cpu_model)
+    ge = LLMEngine(EngineConfig(model="glm-tiny", device="cuda", num_blocks=128, max_num_seqs=4, max_model_len=512,
+                                max_num_batched_tokens=256, use_graphs=True), model_cfg=mc, model=gm)
+    gpu = [r.output for r in ge.generate(prompts, sp)]
+    ce = LLMEngine(EngineConfig(model="glm-tiny", device="cpu", num_blocks=128, max_num_seqs=4, max_model_len=512,
                                 max_num_batched_tokens=256, use_graphs=False), model_cfg=mc, model=cpu_model)
     cpu = [r.output for r in ce.generate(prompts, sp)]
     assert sum(a[:2] == b[:2] for a, b in zip(gpu, cpu)) >= 2, (gpu, cpu)

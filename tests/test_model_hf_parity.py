@@ -2,7 +2,8 @@
 
 The reference serves these families through HF ``transformers`` (its live
 path is ``AutoModelForCausalLM.generate``, worker/engines/llm.py:43-86; the
-default model is Qwen2.5-7B-Instruct).  Here a tiny random HF model of each
+default model is Qwen2.5-7B-Instruct and its README lists Llama-3.1-8B and
+GLM-4-9B, worker/README.md:86-97).  Here a tiny random HF model of each
 family is built in fp32, its state dict is loaded into the native
 ``LlamaModel`` with ``load_state_dict_hf``, and the native engine (paged KV,
 chunked prefill, decode steps) must reproduce HF's prefill logits and its
@@ -29,6 +30,10 @@ def _hf(family):
     if family == "llama":
         cfg = transformers.LlamaConfig(rope_theta=500000.0, attention_bias=False, **common)
         model = transformers.LlamaForCausalLM(cfg)
+    elif family == "glm":
+        cfg = transformers.GlmConfig(rope_theta=10000.0, partial_rotary_factor=0.5, attention_bias=True,
+                                     head_dim=HD, pad_token_id=0, **common)
+        model = transformers.GlmForCausalLM(cfg)
     else:
         cfg = transformers.Qwen2Config(rope_theta=1000000.0, **common)
         model = transformers.Qwen2ForCausalLM(cfg)
@@ -52,18 +57,22 @@ def _native(cfg, model):
     return mc, eng
 
 
-@pytest.mark.parametrize("family", ["llama", "qwen2"])
+FAMILIES = ["llama", "qwen2", "glm"]
+
+
+@pytest.mark.parametrize("family", FAMILIES)
 def test_config_translation(family):
     _, cfg = _hf(family)
     mc = ModelConfig.from_hf_dict(cfg.to_dict())
     assert (mc.hidden_size, mc.num_heads, mc.num_kv_heads, mc.head_dim) == (H, NH, NKV, HD)
-    assert mc.qkv_bias == (family == "qwen2")
-    assert mc.arch == ("qwen2" if family == "qwen2" else "llama")
+    assert mc.qkv_bias == (family in ("qwen2", "glm"))
+    assert mc.arch == family
     # transformers >= 5 nests theta under rope_parameters; it must not fall back to 1e4
-    assert mc.rope_theta == (1e6 if family == "qwen2" else 5e5)
+    assert mc.rope_theta == {"qwen2": 1e6, "llama": 5e5, "glm": 1e4}[family]
+    assert (mc.rope_dim, mc.rope_interleaved) == ((HD // 2, True) if family == "glm" else (HD, False))
 
 
-@pytest.mark.parametrize("family", ["llama", "qwen2"])
+@pytest.mark.parametrize("family", FAMILIES)
 def test_greedy_continuation_matches_hf(family):
     model, cfg = _hf(family)
     _, eng = _native(cfg, model)
@@ -77,7 +86,7 @@ def test_greedy_continuation_matches_hf(family):
         assert r.output == ref, (family, r.output, ref)
 
 
-@pytest.mark.parametrize("family", ["llama", "qwen2"])
+@pytest.mark.parametrize("family", FAMILIES)
 def test_prefill_logits_match_hf(family):
     from dgi.runtime.batch import AttnMeta  # noqa: F401  (engine path below builds it)
     model, cfg = _hf(family)
