@@ -26,6 +26,8 @@ int dgi_paged_prefill(const void* q, int q_stride, const void* k_cache, const vo
                       int out_stride, int nh, int nkv, int hd, int block_size, float scale,
                       const unsigned long long* tree_mask, int tree_n, hipStream_t s);
 int dgi_silu_mul(const void* gu, void* out, int T, int I, hipStream_t s);
+int dgi_skinny_gemm(const void* x, int ldx, const void* w, const void* bias, void* y, int ldy, int M,
+                    int N, int K, int nw, hipStream_t s);
 int dgi_sample(const void* logits, int is_bf16, int B, int V, int stride, const float* temperature,
                const long long* seeds, long long step, long long* out, hipStream_t s);
 int dgi_topk(const void* logits, int is_bf16, int B, int V, int stride, int K, float* out_v,
@@ -171,6 +173,25 @@ void silu_mul(at::Tensor out, const at::Tensor& gu) {
            "silu_mul");
 }
 
+void skinny_gemm(at::Tensor out, const at::Tensor& x, const at::Tensor& w,
+                 const c10::optional<at::Tensor>& bias, int64_t nw) {
+  check_bf16(out, "out"); check_bf16(x, "x"); check_bf16(w, "w");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "skinny_gemm: 2-D operands");
+  TORCH_CHECK(x.stride(1) == 1 && out.stride(1) == 1 && w.is_contiguous(), "skinny_gemm: row-major operands");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && out.size(0) == M && out.size(1) == N, "skinny_gemm: shape mismatch");
+  TORCH_CHECK(M <= 32 && K % 64 == 0 && N % 16 == 0 && x.stride(0) % 8 == 0, "skinny_gemm: M<=32, K%64, N%16");
+  const void* b = nullptr;
+  if (bias.has_value()) {
+    check_bf16(*bias, "bias");
+    TORCH_CHECK(bias->is_contiguous() && bias->numel() == N);
+    b = bias->data_ptr();
+  }
+  check_rc(dgi_skinny_gemm(x.data_ptr(), (int)x.stride(0), w.data_ptr(), b, out.data_ptr(), (int)out.stride(0),
+                           (int)M, (int)N, (int)K, (int)nw, cur_stream()),
+           "skinny_gemm");
+}
+
 void sample(at::Tensor out, const at::Tensor& logits, const c10::optional<at::Tensor>& temperature,
             const c10::optional<at::Tensor>& seeds, int64_t step) {
   check_dev(logits, "logits");
@@ -285,6 +306,7 @@ TORCH_LIBRARY(dgi, m) {
         "Tensor cu_seqlens_q, Tensor context_lens, Tensor tiles, int nh, int nkv, float scale, "
         "Tensor? tree_mask, int tree_n) -> ()");
   m.def("silu_mul(Tensor(a!) out, Tensor gu) -> ()");
+  m.def("skinny_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor? bias, int nw=0) -> ()");
   m.def("sample(Tensor(a!) out, Tensor logits, Tensor? temperature, Tensor? seeds, int step) -> ()");
   m.def("topk(Tensor(a!) out_v, Tensor(b!) out_i, Tensor logits, int k) -> ()");
   m.def("kv_gather(Tensor(a!) buf, Tensor cache, Tensor ids) -> ()");
@@ -302,6 +324,7 @@ TORCH_LIBRARY_IMPL(dgi, CUDA, m) {
   m.impl("paged_decode", &paged_decode);
   m.impl("paged_prefill", &paged_prefill);
   m.impl("silu_mul", &silu_mul);
+  m.impl("skinny_gemm", &skinny_gemm);
   m.impl("sample", &sample);
   m.impl("topk", &topk);
   m.impl("kv_gather", &kv_gather);

@@ -218,15 +218,15 @@ class LlamaModel:
                 h = ops.rmsnorm(h, L.in_norm, eps)
             else:
                 ops.fused_add_rmsnorm(h, residual, L.in_norm, eps)
-            qkv = F.linear(h, L.qkv, L.qkv_bias)
+            qkv = ops.linear(h, L.qkv, L.qkv_bias)
             attn = self.attention(i, qkv, meta)
-            h = F.linear(attn, L.o)
+            h = ops.linear(attn, L.o)
             if self.reduce is not None:
                 self.reduce(h)
             ops.fused_add_rmsnorm(h, residual, L.post_norm, eps)
-            gu = F.linear(h, L.gate_up)
+            gu = ops.linear(h, L.gate_up)
             act = ops.silu_mul(gu)
-            h = F.linear(act, L.down)
+            h = ops.linear(act, L.down)
             if self.reduce is not None:
                 self.reduce(h)
             if self.capture_layers and (self.layer_start + i) in self.capture_layers:
@@ -264,7 +264,7 @@ class LlamaModel:
             residual = residual.contiguous()
             ops.fused_add_rmsnorm(h, residual, self.norm, eps)
             hn = h
-        return F.linear(hn, self.lm_head)
+        return ops.linear(hn, self.lm_head)
 
     def final_hidden(self, h, residual, idx=None):
         """Normalised last hidden states (EAGLE draft features)."""

@@ -324,6 +324,36 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens,
 # MLP activation
 # ----------------------------------------------------------------------------
 
+# ----------------------------------------------------------------------------
+# Linear: weight-streaming MFMA kernel for decode-sized M, hipBLASLt otherwise
+# ----------------------------------------------------------------------------
+
+# Largest M the skinny kernel takes; above it hipBLASLt's tiles win (measured:
+# profiles/r1_skinny_gemm.md).  DGI_SKINNY_MAX_M=0 disables the kernel.
+SKINNY_MAX_M = int(os.environ.get("DGI_SKINNY_MAX_M", "32"))
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
+           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = x @ w.T (+ bias) for a 2-D activation; [N, K] weights as stored."""
+    if x.dim() != 2:
+        return torch.nn.functional.linear(x, w, bias)
+    M, K = x.shape
+    N = w.shape[0]
+    if (x.is_cuda and M <= SKINNY_MAX_M and K % 64 == 0 and N % 16 == 0 and x.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and x.stride(1) == 1 and x.stride(0) % 8 == 0 and w.is_contiguous()):
+        load_native(required=True)
+        if out is None:
+            out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+        torch.ops.dgi.skinny_gemm(out, x, w, bias, 0)
+        return out
+    r = torch.nn.functional.linear(x, w, bias)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
 def silu_mul_ref(gu: torch.Tensor) -> torch.Tensor:
     I = gu.shape[-1] // 2
     g = gu[..., :I].float()

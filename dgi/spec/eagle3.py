@@ -49,6 +49,7 @@ class SpecConfig:
     width: int = 4            # frontier nodes kept per depth W
     topk: int = 4             # children per frontier node K (<= 16, dgi_topk)
     feature_layers: Optional[tuple] = None  # default: (2, L//2, L-3)
+    graphs: bool = True       # hipGraph-capture the tree verify pass per batch bucket (GPU)
 
     @property
     def num_nodes(self) -> int:
@@ -102,7 +103,7 @@ class Eagle3Draft:
 
     # ------------------------------------------------------------------ inference (paged KV, HIP kernels)
     def fuse(self, feats: torch.Tensor) -> torch.Tensor:
-        return F.linear(feats, self.fc)
+        return ops.linear(feats, self.fc)
 
     def forward(self, ids: torch.Tensor, hidden: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
         """Draft hidden states g [T, H] (pre-norm residual stream)."""
@@ -110,22 +111,22 @@ class Eagle3Draft:
         eps = c.rms_eps
         e = ops.rmsnorm(F.embedding(ids, self.target.embed), self.embed_norm, eps)
         hn = ops.rmsnorm(hidden.contiguous(), self.hidden_norm, eps)
-        qkv = F.linear(torch.cat([e, hn], dim=-1), self.qkv)
+        qkv = ops.linear(torch.cat([e, hn], dim=-1), self.qkv)
         kc, vc = self.kv_cache[0, 0], self.kv_cache[0, 1]
         ops.rope_cache(qkv, meta.positions, self.target.cos_sin, c.num_heads, c.num_kv_heads, c.head_dim,
                        meta.slot_mapping, kc, vc, self.target.rope_mode)
         attn = ops.paged_prefill(qkv, kc, vc, meta.pre_block_tables, meta.pre_cu_seqlens, meta.pre_context_lens,
                                  c.num_heads, c.num_kv_heads, self.scale, tiles=meta.pre_tiles,
                                  tree_mask=meta.tree_mask, tree_n=meta.tree_n)
-        h = F.linear(attn, self.o)
+        h = ops.linear(attn, self.o)
         residual = hidden.contiguous().clone()
         ops.fused_add_rmsnorm(h, residual, self.post_norm, eps)   # residual <- h + hidden ; h <- norm
-        h = F.linear(ops.silu_mul(F.linear(h, self.gate_up)), self.down)
+        h = ops.linear(ops.silu_mul(ops.linear(h, self.gate_up)), self.down)
         return h + residual
 
     def logprobs(self, g: torch.Tensor) -> torch.Tensor:
         hn = ops.rmsnorm(g.contiguous(), self.norm, self.cfg.rms_eps)
-        return torch.log_softmax(F.linear(hn, self.target.lm_head).float(), dim=-1)
+        return torch.log_softmax(ops.linear(hn, self.target.lm_head).float(), dim=-1)
 
     # ------------------------------------------------------------------ training (dense, autograd)
     def train_forward(self, P: dict, ids: torch.Tensor, hidden: torch.Tensor, pos: torch.Tensor) -> torch.Tensor:
@@ -207,6 +208,107 @@ def kv_slot_copy(kv: torch.Tensor, src: torch.Tensor, dst: torch.Tensor, block_s
     c[:, dst // bs, :, dst % bs] = vals
 
 
+VERIFY_BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128)
+
+
+class _VerifyGraph:
+    """hipGraph of the tree-verify pass for ``Rb`` sequences of ``N`` tree nodes.
+
+    Static inputs: one int32 metadata buffer (positions, slots, block tables,
+    context lengths; cu_seqlens and tiles are fixed by Rb and N), draft
+    tokens and tree parents.  The graph runs the ancestor masks, the target
+    forward with EAGLE-3 feature capture (tree-masked paged prefill
+    attention), argmax and ``tree_verify``.  Rows past the live batch are
+    padding that reads/writes only the reserved scratch page 0."""
+
+    def __init__(self, eng: "SpecEngine", Rb: int):
+        sp, run = eng.spec, eng.runner
+        N, dev = sp.num_nodes, eng.device
+        self.eng = eng
+        self.Rb, self.N, self.maxw = Rb, N, run.max_blocks
+        T = Rb * N
+        self.n_dyn = 2 * T + Rb * self.maxw + Rb            # positions, slots, block tables, ctx
+        self.host = torch.zeros(self.n_dyn, dtype=torch.int32).pin_memory()
+        self.dyn = torch.zeros(self.n_dyn, dtype=torch.int32, device=dev)
+        self.cu = torch.arange(0, T + 1, N, dtype=torch.int32, device=dev)
+        self.tiles = torch.stack([torch.arange(Rb, dtype=torch.int32), torch.zeros(Rb, dtype=torch.int32)],
+                                 1).contiguous().to(dev)
+        self.tok = torch.zeros(Rb, N, dtype=torch.long, device=dev)
+        par = torch.full((Rb, N), -1, dtype=torch.int32)
+        par[:, 1:] = 0
+        self.par = par.to(dev)
+        o = 0
+        self.d_pos = self.dyn[o:o + T]
+        o += T
+        self.d_slots = self.dyn[o:o + T]
+        o += T
+        self.d_bt = self.dyn[o:o + Rb * self.maxw].view(Rb, self.maxw)
+        o += Rb * self.maxw
+        self.d_ctx = self.dyn[o:o + Rb]
+        self._fill_padding(0)
+        self.dyn.copy_(self.host)
+        self.graph = None
+        self._capture()
+
+    def _fill_padding(self, R: int) -> None:
+        """Rows >= R: a valid dummy tree on scratch page 0 (position 0.., context N)."""
+        T, N, Rb, maxw = self.Rb * self.N, self.N, self.Rb, self.maxw
+        h = self.host.numpy()
+        if R >= Rb:
+            return
+        h[R * N:T] = np.tile(np.arange(N, dtype=np.int32), Rb - R)                               # positions
+        h[T + R * N:2 * T] = np.arange(N, dtype=np.int32)[None].repeat(Rb - R, 0).ravel() % \
+            self.eng.pool.block_size                                                              # slots in page 0
+        bt0 = 2 * T
+        h[bt0 + R * maxw:bt0 + Rb * maxw] = 0
+        h[bt0 + Rb * maxw + R:bt0 + Rb * maxw + Rb] = N
+
+    def _body(self):
+        eng = self.eng
+        anc, depth = ops.tree_mask(self.par)
+        meta = AttnMeta(positions=self.d_pos, slot_mapping=self.d_slots, num_decode=0,
+                        num_prefill_tokens=self.Rb * self.N, pre_block_tables=self.d_bt, pre_cu_seqlens=self.cu,
+                        pre_context_lens=self.d_ctx, pre_tiles=self.tiles, tree_mask=anc, tree_n=self.N)
+        logits, feats = eng._forward_capture(meta, self.tok.view(-1))
+        tgt = logits.argmax(dim=-1).view(self.Rb, self.N)
+        acc, path, toks = ops.tree_verify(self.par, self.tok, tgt, anc, depth, eng.spec.depth + 1)
+        return acc, path, toks, feats
+
+    @torch.inference_mode()
+    def _capture(self) -> None:
+        eng = self.eng
+        eng.model.kv_cache = eng.pool.kv
+        s = torch.cuda.Stream(device=eng.device)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self._body()                                   # warm-up (lazy inits outside capture)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize(eng.device)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, pool=eng._graph_pool):
+            self.out = self._body()
+
+    def run(self, R: int, tok: torch.Tensor, par: torch.Tensor, pos, slots, brows, ctx):
+        T, N, maxw = self.Rb * self.N, self.N, self.maxw
+        h = self.host.numpy()
+        h[:R * N] = pos
+        h[T:T + R * N] = slots
+        bt0 = 2 * T
+        h[bt0:bt0 + R * maxw] = 0
+        for i, blk in enumerate(brows):
+            h[bt0 + i * maxw: bt0 + i * maxw + len(blk)] = blk
+        h[bt0 + self.Rb * maxw: bt0 + self.Rb * maxw + R] = ctx
+        self._fill_padding(R)
+        self.dyn.copy_(self.host, non_blocking=True)
+        self.tok[:R].copy_(tok)
+        self.par[:R].copy_(par)
+        if R < self.Rb:
+            self.tok[R:].zero_()
+        self.graph.replay()
+        acc, path, toks, feats = self.out
+        return acc[:R], path[:R], toks[:R], feats[:R * N]
+
+
 class SpecEngine(LLMEngine):
     """``LLMEngine`` with EAGLE-3 tree speculation for greedy requests."""
 
@@ -226,6 +328,19 @@ class SpecEngine(LLMEngine):
         self.oracle: Optional[dict] = None
         self.oracle_accept = 1.0
         self._oracle_rng = np.random.default_rng(0)
+        self._vgraphs: dict = {}
+        self._graph_pool = torch.cuda.graph_pool_handle() if self.device.type == "cuda" else None
+
+    def _verify_graph(self, R: int) -> Optional[_VerifyGraph]:
+        if not (self.spec.graphs and self.device.type == "cuda"):
+            return None
+        Rb = next((b for b in VERIFY_BUCKETS if b >= R), None)
+        if Rb is None:
+            return None
+        g = self._vgraphs.get(Rb)
+        if g is None:
+            g = self._vgraphs[Rb] = _VerifyGraph(self, Rb)
+        return g
 
     # ------------------------------------------------------------------ helpers
     def _eligible(self, r: Request) -> bool:
@@ -396,7 +511,6 @@ class SpecEngine(LLMEngine):
         self.spec_stats["draft_s"] += time.perf_counter() - td
         tv = time.perf_counter()
         # ---- 3) target verify over all N tree nodes
-        anc, depth = ops.tree_mask(par)
         vpos, vslots, vctx, vcu = [], [], [], [0]
         for i, r in enumerate(reqs):
             n = int(n_vec[i])
@@ -406,10 +520,15 @@ class SpecEngine(LLMEngine):
             vslots.extend((blk[sl // bs] * bs + sl % bs).tolist())
             vctx.append(n - 1 + N)
             vcu.append(vcu[-1] + N)
-        vm = _varlen_meta(run, vpos, vslots, brows, vcu, vctx, dev, tree_mask=anc, tree_n=N)
-        logits, feats = self._forward_capture(vm, tok.view(-1))
-        tgt = logits.argmax(dim=-1).view(R, N)
-        acc, path, toks = ops.tree_verify(par, tok, tgt, anc, depth, D + 1)
+        vg = self._verify_graph(R)
+        if vg is not None:
+            acc, path, toks, feats = vg.run(R, tok, par, vpos, vslots, brows, vctx)
+        else:
+            anc, depth = ops.tree_mask(par)
+            vm = _varlen_meta(run, vpos, vslots, brows, vcu, vctx, dev, tree_mask=anc, tree_n=N)
+            logits, feats = self._forward_capture(vm, tok.view(-1))
+            tgt = logits.argmax(dim=-1).view(R, N)
+            acc, path, toks = ops.tree_verify(par, tok, tgt, anc, depth, D + 1)
         acc_h = acc.cpu().tolist()
         path_h = path.cpu().numpy()
         toks_h = toks.cpu().numpy()

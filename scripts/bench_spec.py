@@ -46,11 +46,21 @@ def main():
     ap.add_argument("--train-seqs", type=int, default=64)
     ap.add_argument("--random-seqs", type=int, default=192)
     ap.add_argument("--oracle-accept", type=float, nargs="*", default=[0.6, 0.8, 1.0])
+    ap.add_argument("--target", default="random", choices=["random", "peaked"],
+                    help="random: plain random init (near-flat logits: greedy choices sit on bf16 near-ties, so "
+                         "kernel-order noise flips them and acceptance collapses); peaked: the LM head is a "
+                         "permuted copy of the embedding / sqrt(H), so the next token is a confident function "
+                         "of the current one, like a trained model's top-1 margins (same FLOPs and shapes)")
+    ap.add_argument("--no-verify-graph", action="store_true", help="eager verify pass (A/B for the hipGraph)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     cfg = EngineConfig(model=a.model, device="cuda", max_num_seqs=64, max_num_batched_tokens=8192,
                        max_model_len=2048, kv_fraction=0.5)
-    spec = SpecEngine(cfg, SpecConfig(depth=a.depth, width=a.width, topk=a.topk))
+    spec = SpecEngine(cfg, SpecConfig(depth=a.depth, width=a.width, topk=a.topk, graphs=not a.no_verify_graph))
+    if a.target == "peaked":
+        m = spec.model
+        perm = torch.randperm(m.embed.shape[0], generator=torch.Generator().manual_seed(7)).to(m.embed.device)
+        m.lm_head.copy_(m.embed.index_select(0, perm) / m.cfg.hidden_size ** 0.5)
     t0 = time.perf_counter()
     info = train_draft(spec, steps=a.train_steps, batch=16, prompt_len=64, gen_len=192, num_seqs=a.train_seqs,
                        random_seqs=a.random_seqs, log=lambda m: print(m, flush=True))
@@ -100,7 +110,8 @@ def main():
                                    "identical": [r.output for r in rs] == ref}
         print(json.dumps(row), flush=True)
         rows.append(row)
-    res = {"model": a.model, "tree": {"depth": a.depth, "width": a.width, "topk": a.topk},
+    res = {"model": a.model, "tree": {"depth": a.depth, "width": a.width, "topk": a.topk}, "target": a.target,
+           "verify_graph": not a.no_verify_graph,
            "prompt_len": a.prompt_len, "output_len": a.output_len, "draft_training": info, "rows": rows,
            "data": "synthetic prompts, random-init target, self-distilled draft"}
     print(json.dumps(res))

@@ -37,6 +37,12 @@ for s in $STEPS; do
     sweep70b) for c in 256 384 512; do run sweep70b_c$c 900 python bench.py --steps 40 --warmup 10 --concurrency $c --json-out gpurun_out/sweep70b_c$c.json; done ;;
     sweep70b_mbt) run sweep70b_c384_mbt8k 900 python bench.py --steps 40 --warmup 10 --concurrency 384 --max-batched-tokens 8192 --json-out gpurun_out/sweep70b_c384_mbt8k.json ;;
     spec8b) run spec8b 900 python scripts/bench_spec.py --out gpurun_out/spec8b.json ;;
+    spec8b_peaked) run spec8b_peaked 900 python scripts/bench_spec.py --batch 1 4 16 --target peaked --train-steps 1500 --random-seqs 1024 --out gpurun_out/spec8b_peaked.json ;;
+    pytest_spec) run pytest_spec 300 python -u -m pytest tests/test_spec.py -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    spec8b_peaked_eager) run spec8b_peaked_eager 900 python scripts/bench_spec.py --batch 1 4 16 --target peaked --train-steps 1500 --random-seqs 1024 --no-verify-graph --out gpurun_out/spec8b_peaked_eager.json ;;
+    skinny_test) run skinny_test 300 python -u -m pytest tests/test_kernels_gpu.py -k skinny -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    skinny_bench) run skinny_bench 600 python scripts/skinny_bench.py --nw 0 4 8 16 --out gpurun_out/skinny_bench.json ;;
+    declat) run declat 600 python scripts/decode_latency.py --out gpurun_out/declat.json && DGI_SKINNY_MAX_M=0 run declat_blaslt 600 python scripts/decode_latency.py --out gpurun_out/declat_blaslt.json ;;
     bench70b_long) run bench70b_long 1200 python bench.py --steps 200 --warmup 20 --json-out gpurun_out/bench70b_long.json ;;
   esac
 done

@@ -158,6 +158,23 @@ def test_silu_mul(T, I):
     torch.testing.assert_close(ops.silu_mul(gu).float(), ops.silu_mul_ref(gu).float(), atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("M", [1, 3, 16, 17, 32])
+@pytest.mark.parametrize("N,K,nw", [(6144, 4096, 0), (4096, 14336, 0), (1152, 896 + 128, 16), (256, 512, 4),
+                                    (512, 1024, 8)])
+def test_skinny_gemm(M, N, K, nw):
+    x = _bf(M, K)
+    w = _bf(N, K, scale=0.05)
+    b = _bf(N)
+    ref = (x.float() @ w.float().t() + b.float())
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    torch.ops.dgi.skinny_gemm(out, x, w, b, nw)
+    torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=2e-2)
+    # strided activation rows (a view into a wider buffer), no bias, via ops.linear
+    xs = _bf(M, K + 64)[:, :K]
+    y = ops.linear(xs, w)
+    torch.testing.assert_close(y.float(), xs.float() @ w.float().t(), atol=3e-2, rtol=2e-2)
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_sample_greedy_and_topk(dtype):
     B, V = 7, 128256

@@ -80,6 +80,33 @@ def test_spec_gpu_greedy_trajectory():
     assert se.acceptance()["tokens_per_step"] > 1.3
 
 
+@pytest.mark.gpu
+def test_spec_verify_graph_matches_eager():
+    """The hipGraph verify pass (static buffers, padded batch bucket) gives the
+    same tokens and acceptance as the eager verify pass, bit for bit."""
+    import dataclasses
+    spec = SpecConfig(depth=4, width=3, topk=4)
+    base, sg = _engines("llama-tiny-hd128", "cuda", spec)
+    se = SpecEngine(EngineConfig(model="llama-tiny-hd128", device="cuda", max_num_seqs=8, max_num_batched_tokens=256,
+                                 max_model_len=512, use_graphs=False), dataclasses.replace(spec, graphs=False))
+    se.model.copy_from(base.model)
+    sp = SamplingParams(max_tokens=24, temperature=0.0, ignore_eos=True)
+    prompts = _prompts(3, 1000)                        # R=3 -> bucket 4 with one padding row
+    ref = [r.output for r in base.generate(prompts, sp)]
+    outs = []
+    for eng in (sg, se):
+        eng.oracle, eng.oracle_accept = {}, 0.7
+        rs = [eng.add_request(p, sp) for p in prompts]
+        for r, o in zip(rs, ref):
+            eng.oracle[r.rid] = o
+        while eng.has_unfinished():
+            eng.step()
+        outs.append(([r.output for r in rs], eng.spec_stats["accepted"]))
+    assert sg._vgraphs and not se._vgraphs
+    assert outs[0] == outs[1]
+    assert outs[0][1] > 0
+
+
 # ------------------------------------------------------------------ reference-compatible API
 def test_compat_config_output_defaults():
     from worker.engines.speculative import SpeculativeConfig, SpeculativeOutput
