@@ -174,13 +174,13 @@ void silu_mul(at::Tensor out, const at::Tensor& gu) {
 }
 
 void skinny_gemm(at::Tensor out, const at::Tensor& x, const at::Tensor& w,
-                 const c10::optional<at::Tensor>& bias, int64_t nw) {
+                 const c10::optional<at::Tensor>& bias, int64_t cfg) {
   check_bf16(out, "out"); check_bf16(x, "x"); check_bf16(w, "w");
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "skinny_gemm: 2-D operands");
   TORCH_CHECK(x.stride(1) == 1 && out.stride(1) == 1 && w.is_contiguous(), "skinny_gemm: row-major operands");
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
   TORCH_CHECK(w.size(1) == K && out.size(0) == M && out.size(1) == N, "skinny_gemm: shape mismatch");
-  TORCH_CHECK(M <= 32 && K % 64 == 0 && N % 16 == 0 && x.stride(0) % 8 == 0, "skinny_gemm: M<=32, K%64, N%16");
+  TORCH_CHECK(M <= 32 && K % 1024 == 0 && N % 16 == 0 && x.stride(0) % 8 == 0, "skinny_gemm: M<=32, K%1024, N%16");
   const void* b = nullptr;
   if (bias.has_value()) {
     check_bf16(*bias, "bias");
@@ -188,7 +188,7 @@ void skinny_gemm(at::Tensor out, const at::Tensor& x, const at::Tensor& w,
     b = bias->data_ptr();
   }
   check_rc(dgi_skinny_gemm(x.data_ptr(), (int)x.stride(0), w.data_ptr(), b, out.data_ptr(), (int)out.stride(0),
-                           (int)M, (int)N, (int)K, (int)nw, cur_stream()),
+                           (int)M, (int)N, (int)K, (int)cfg, cur_stream()),
            "skinny_gemm");
 }
 
@@ -306,7 +306,7 @@ TORCH_LIBRARY(dgi, m) {
         "Tensor cu_seqlens_q, Tensor context_lens, Tensor tiles, int nh, int nkv, float scale, "
         "Tensor? tree_mask, int tree_n) -> ()");
   m.def("silu_mul(Tensor(a!) out, Tensor gu) -> ()");
-  m.def("skinny_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor? bias, int nw=0) -> ()");
+  m.def("skinny_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor? bias, int cfg=0) -> ()");
   m.def("sample(Tensor(a!) out, Tensor logits, Tensor? temperature, Tensor? seeds, int step) -> ()");
   m.def("topk(Tensor(a!) out_v, Tensor(b!) out_i, Tensor logits, int k) -> ()");
   m.def("kv_gather(Tensor(a!) buf, Tensor cache, Tensor ids) -> ()");

@@ -328,9 +328,18 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens,
 # Linear: weight-streaming MFMA kernel for decode-sized M, hipBLASLt otherwise
 # ----------------------------------------------------------------------------
 
-# Largest M the skinny kernel takes; above it hipBLASLt's tiles win (measured:
-# profiles/r1_skinny_gemm.md).  DGI_SKINNY_MAX_M=0 disables the kernel.
+# Where the skinny kernel beats hipBLASLt (profiles/r1_skinny_gemm.md, weights
+# streamed cold from HBM): K <= 4096 projections of 8B-class models at M <= 8
+# (1.3-2.1x on qkv / o / gate_up), and square 4096x4096 (o-proj) up to M = 32.
+# Larger K, the 128k-vocab head and every 70B shape stream at 4.5-5.7 TB/s in
+# hipBLASLt already.  DGI_SKINNY_MAX_M=0 disables the kernel.
 SKINNY_MAX_M = int(os.environ.get("DGI_SKINNY_MAX_M", "32"))
+
+
+def _use_skinny(M: int, N: int, K: int) -> bool:
+    if M > SKINNY_MAX_M or K % 1024 or N % 16 or K > 4096 or N > 32768:
+        return False
+    return M <= 8 or (N <= 4096 and M <= 32)
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
@@ -340,7 +349,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         return torch.nn.functional.linear(x, w, bias)
     M, K = x.shape
     N = w.shape[0]
-    if (x.is_cuda and M <= SKINNY_MAX_M and K % 64 == 0 and N % 16 == 0 and x.dtype == torch.bfloat16
+    if (x.is_cuda and _use_skinny(M, N, K) and x.dtype == torch.bfloat16
             and w.dtype == torch.bfloat16 and x.stride(1) == 1 and x.stride(0) % 8 == 0 and w.is_contiguous()):
         load_native(required=True)
         if out is None:

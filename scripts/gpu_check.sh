@@ -41,7 +41,7 @@ for s in $STEPS; do
     pytest_spec) run pytest_spec 300 python -u -m pytest tests/test_spec.py -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     spec8b_peaked_eager) run spec8b_peaked_eager 900 python scripts/bench_spec.py --batch 1 4 16 --target peaked --train-steps 1500 --random-seqs 1024 --no-verify-graph --out gpurun_out/spec8b_peaked_eager.json ;;
     skinny_test) run skinny_test 300 python -u -m pytest tests/test_kernels_gpu.py -k skinny -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
-    skinny_bench) run skinny_bench 600 python scripts/skinny_bench.py --nw 0 4 8 16 --out gpurun_out/skinny_bench.json ;;
+    skinny_bench) run skinny_bench 600 python scripts/skinny_bench.py --cfg 0 1 2 3 4 5 6 --out gpurun_out/skinny_bench.json ;;
     declat) run declat 600 python scripts/decode_latency.py --out gpurun_out/declat.json && DGI_SKINNY_MAX_M=0 run declat_blaslt 600 python scripts/decode_latency.py --out gpurun_out/declat_blaslt.json ;;
     bench70b_long) run bench70b_long 1200 python bench.py --steps 200 --warmup 20 --json-out gpurun_out/bench70b_long.json ;;
   esac

@@ -41,7 +41,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ms", type=int, nargs="+", default=[1, 2, 4, 8, 16, 32])
     ap.add_argument("--shapes", nargs="+", default=list(SHAPES))
-    ap.add_argument("--nw", type=int, nargs="+", default=[0])
+    ap.add_argument("--cfg", type=int, nargs="+", default=[0])
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
@@ -55,9 +55,9 @@ def main():
             x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
             out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
             impls = {"hipblaslt": lambda i: F.linear(x, ws[i % copies])}
-            for nw in a.nw:
-                impls[f"skinny_nw{nw}"] = (lambda nw_: lambda i: torch.ops.dgi.skinny_gemm(
-                    out, x, ws[i % copies], None, nw_))(nw)
+            for c in a.cfg:
+                impls[f"skinny_c{c}"] = (lambda c_: lambda i: torch.ops.dgi.skinny_gemm(
+                    out, x, ws[i % copies], None, c_))(c)
             ref = F.linear(x.float(), ws[0].float())
             torch.ops.dgi.skinny_gemm(out, x, ws[0], None, 0)
             err = (out.float() - ref).abs().max().item()
