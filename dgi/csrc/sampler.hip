@@ -28,6 +28,44 @@ __device__ __forceinline__ float load_logit<float>(const float* p, int i) { retu
 template <>
 __device__ __forceinline__ float load_logit<uint16_t>(const uint16_t* p, int i) { return bf16_to_f32(p[i]); }
 
+// Logits arrive as 16-byte vectors (8 bf16 or 4 fp32) when the row allows it:
+// one workgroup streams a 128k-vocab row (256 KB bf16) with 4 vectors in
+// flight per thread instead of 125 dependent 2-byte loads.
+template <typename T>
+__device__ __forceinline__ float vec_elem(const u32x4& v, int j);
+template <>
+__device__ __forceinline__ float vec_elem<float>(const u32x4& v, int j) { return __uint_as_float(v[j]); }
+template <>
+__device__ __forceinline__ float vec_elem<uint16_t>(const u32x4& v, int j) {
+  const uint32_t w = v[j >> 1];
+  return __uint_as_float((j & 1) ? (w & 0xffff0000u) : (w << 16));
+}
+
+template <typename T, typename F>
+__device__ __forceinline__ void scan_row(const T* lp, int V, int stride, F&& f) {
+  constexpr int E = 16 / sizeof(T);
+  const bool vec = (stride % E == 0) && ((reinterpret_cast<uintptr_t>(lp) & 15) == 0);
+  const int nvec = vec ? V / E : 0;
+  const int nt = blockDim.x;
+  for (int c0 = threadIdx.x; c0 < nvec; c0 += nt * 4) {
+    u32x4 buf[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = c0 + u * nt;
+      if (c < nvec) buf[u] = reinterpret_cast<const u32x4*>(lp)[c];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = c0 + u * nt;
+      if (c < nvec) {
+#pragma unroll
+        for (int j = 0; j < E; ++j) f(vec_elem<T>(buf[u], j), c * E + j);
+      }
+    }
+  }
+  for (int i = nvec * E + threadIdx.x; i < V; i += nt) f(load_logit<T>(lp, i), i);
+}
+
 template <typename T>
 __global__ __launch_bounds__(1024) void sample_kernel(const T* __restrict__ logits, int V, int stride,
                                                       const float* __restrict__ temperature,
@@ -41,14 +79,17 @@ __global__ __launch_bounds__(1024) void sample_kernel(const T* __restrict__ logi
   const uint32_t seed = seeds ? (uint32_t)(seeds[row] * 2654435761ull) ^ (uint32_t)(step * 40503u) : 0u;
   float best = -INFINITY;
   int best_i = 0x7fffffff;
-  for (int i = threadIdx.x; i < V; i += blockDim.x) {
-    float v = load_logit<T>(lp, i);
-    if (!greedy) {
+  if (greedy) {
+    scan_row<T>(lp, V, stride, [&](float v, int i) {
+      if (v > best || (v == best && i < best_i)) { best = v; best_i = i; }
+    });
+  } else {
+    scan_row<T>(lp, V, stride, [&](float v, int i) {
       const uint32_t h = hash32(seed ^ hash32((uint32_t)i + 0x9e3779b9u));
       const float u = ((h >> 8) + 0.5f) * (1.0f / 16777216.0f);
       v = v * inv_t - __logf(-__logf(u));
-    }
-    if (v > best || (v == best && i < best_i)) { best = v; best_i = i; }
+      if (v > best || (v == best && i < best_i)) { best = v; best_i = i; }
+    });
   }
   // wave reduce
 #pragma unroll
@@ -82,14 +123,13 @@ __global__ __launch_bounds__(256) void topk_kernel(const T* __restrict__ logits,
   int ti[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) { tv[k] = -INFINITY; ti[k] = 0x7fffffff; }
-  for (int i = threadIdx.x; i < V; i += 256) {
-    const float v = load_logit<T>(lp, i);
+  scan_row<T>(lp, V, stride, [&](float v, int i) {
     if (v > tv[K - 1]) {
       int k = K - 1;
       while (k > 0 && tv[k - 1] < v) { tv[k] = tv[k - 1]; ti[k] = ti[k - 1]; --k; }
       tv[k] = v; ti[k] = i;
     }
-  }
+  });
   __shared__ float sv[256 * 16];
   __shared__ int si[256 * 16];
   for (int k = 0; k < K; ++k) { sv[threadIdx.x * 16 + k] = tv[k]; si[threadIdx.x * 16 + k] = ti[k]; }

@@ -43,6 +43,7 @@ for s in $STEPS; do
     skinny_test) run skinny_test 300 python -u -m pytest tests/test_kernels_gpu.py -k skinny -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     skinny_bench) run skinny_bench 600 python scripts/skinny_bench.py --cfg 0 1 2 3 4 5 6 --out gpurun_out/skinny_bench.json ;;
     declat) run declat 600 python scripts/decode_latency.py --out gpurun_out/declat.json && DGI_SKINNY_MAX_M=0 run declat_blaslt 600 python scripts/decode_latency.py --out gpurun_out/declat_blaslt.json ;;
+    profdec) export TMPDIR=/tmp; run profdec 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profdec -o run --output-format csv -- python3 scripts/decode_latency.py --batch 1 --steps 200 ;;
     bench70b_long) run bench70b_long 1200 python bench.py --steps 200 --warmup 20 --json-out gpurun_out/bench70b_long.json ;;
   esac
 done

@@ -92,11 +92,13 @@ def test_node_server_generate_matches_engine(nproc):
             proc.wait()
 
 
-def test_worker_node_engine_attaches_and_generates():
-    """The worker's NodeLLMEngine launches a 2-rank node server and serves inference() through it."""
+@pytest.mark.parametrize("elastic", [False, True])
+def test_worker_node_engine_attaches_and_generates(elastic):
+    """The worker's NodeLLMEngine launches a 2-rank node server (directly, or
+    under the elastic supervisor) and serves inference() through it."""
     sys.path.insert(0, os.path.join(ROOT, "worker"))
     from engines import get_engine
-    eng = get_engine("mi355x-node")({"model_id": "llama-tiny", "gpus": 2, "max_num_seqs": 16,
+    eng = get_engine("mi355x-node")({"model_id": "llama-tiny", "gpus": 2, "max_num_seqs": 16, "elastic": elastic,
                                       "max_num_batched_tokens": 512, "max_model_len": 512, "startup_timeout": 240})
     eng.load_model()
     try:

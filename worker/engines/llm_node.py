@@ -9,7 +9,9 @@ the reference delegated to an external vLLM/SGLang server
 
 Config keys: ``node_url`` (attach) or ``gpus`` / ``device_ids`` / ``layout`` /
 ``port`` (launch), plus ``model_id``, ``max_num_seqs``,
-``max_num_batched_tokens``, ``max_model_len``.
+``max_num_batched_tokens``, ``max_model_len``.  ``elastic: true`` launches
+the node under ``dgi.serve.supervisor`` (rank loss -> re-plan on the
+surviving GPUs, in-flight requests resumed by re-prefill; ``max_restarts``).
 """
 from __future__ import annotations
 
@@ -57,14 +59,24 @@ class NodeLLMEngine(LLMBaseEngine):
                 "--max-batched-tokens", str(c.get("max_num_batched_tokens", 4096)),
                 "--max-model-len", str(c.get("max_model_len", 4096)),
                 "--layout", str(c.get("layout", "auto") if c.get("layout") not in (None, "single") else "auto")]
-        if n > 1:
+        env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if c.get("elastic"):
+            # the supervisor owns the ranks (and their device pinning) and serves the same HTTP surface
+            node = list(args[2:])          # drop "-m dgi.serve.node"
+            i = node.index("--port")
+            del node[i:i + 2]
+            cmd = [sys.executable, "-m", "dgi.serve.supervisor", "--nproc", str(n), "--port", str(port),
+                   "--max-restarts", str(c.get("max_restarts", 3))]
+            if c.get("device_ids"):
+                cmd += ["--gpus", ",".join(str(i) for i in ids)]
+            cmd += ["--"] + node
+        elif n > 1:
             cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
                    "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
         else:
             cmd = [sys.executable] + args
-        env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
-        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        if ids:
+        if ids and not c.get("elastic"):
             env["HIP_VISIBLE_DEVICES"] = ",".join(str(i) for i in ids)
         logger.info("launching node server: %s", " ".join(cmd))
         self.proc = subprocess.Popen(cmd, cwd=ROOT, env=env)
