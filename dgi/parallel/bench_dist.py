@@ -147,8 +147,11 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
     from dgi.parallel.pipeline import StageWorker
 
     if role == "prefill":
-        pcfg = EngineConfig(**{**cfg.__dict__, "max_num_seqs": 64})
-        srv = PrefillServer(pcfg, f, layout)
+        from dgi.parallel.plan import prefill_overflow_cap
+        lc = getattr(args, "prefill_local_cap", -1)
+        lc = prefill_overflow_cap(layout) if lc < 0 else lc
+        pcfg = EngineConfig(**{**cfg.__dict__, "max_num_seqs": 64 + lc})
+        srv = PrefillServer(pcfg, f, layout, local_cap=lc)
         phase = CtrlChannel(f, layout.decode_ranks[0], 4, tag="phase")
         vocab = srv.engine.model_cfg.vocab_size
         depth = max(2, args.max_batched_tokens // max(1, args.prompt_len))
@@ -171,7 +174,8 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
         f.barrier()
         el = time.perf_counter() - t0
         srv.finish()
-        return n, el, ttfts, {"migrated": srv.migrated, "migrate_s": round(srv.migrate_time, 3)}
+        return n, el, ttfts, {"migrated": srv.migrated, "migrate_s": round(srv.migrate_time, 3),
+                              "local_cap": lc, "local_tokens": srv.local_tokens}
 
     if role == "decode_driver":
         # single decode GPU: let it also serve local prompts with a slice of its pool

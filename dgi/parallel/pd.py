@@ -44,7 +44,7 @@ from dgi.parallel.plan import NodeLayout
 from dgi.sched.request import Request, SamplingParams, Status
 from dgi.utils.trace import mark, phase
 
-MSG_MIGRATE, MSG_CREDIT, MSG_DONE, MSG_FINISHED = 1, 2, 3, 4
+MSG_MIGRATE, MSG_CREDIT, MSG_DONE, MSG_FINISHED, MSG_TOKENS = 1, 2, 3, 4, 5
 REASONS = {0: None, 1: "length", 2: "stop"}
 CTRL = 8
 META_FIELDS = 11
@@ -64,11 +64,23 @@ def _req_meta(r: Request, nblocks: int) -> list:
 class PrefillServer:
     """One prefill rank."""
 
-    def __init__(self, cfg: EngineConfig, fabric: Fabric, layout: NodeLayout, seed_offset: int = 0):
+    def __init__(self, cfg: EngineConfig, fabric: Fabric, layout: NodeLayout, seed_offset: int = 0,
+                 local_cap: int = 0, report_tokens: bool = False):
         self.f = fabric
         self.layout = layout
         self.driver = layout.decode_ranks[0]
-        pcfg = EngineConfig(**{**cfg.__dict__, "device": str(fabric.device), "use_graphs": False})
+        # overflow decoding: when the decode side has no credit left, up to
+        # ``local_cap`` sequences stay on this rank and decode inside its mixed
+        # prefill+decode steps instead of the rank idling until credit returns
+        # (one decode GPU fed by 3+ prefill GPUs is decode-bound:
+        # profiles/r1_pd_capacity_70b.md).  ``report_tokens`` streams their
+        # tokens to the decode driver (node router) once per step.
+        self.local_cap = local_cap
+        self.local: set = set()
+        self.local_tokens = 0
+        self.report_tokens = report_tokens
+        pcfg = EngineConfig(**{**cfg.__dict__, "device": str(fabric.device),
+                               "use_graphs": bool(cfg.use_graphs and local_cap > 0)})
         self.engine = LLMEngine(pcfg)
         self.bs = self.engine.pool.block_size
         self.ch = CtrlChannel(fabric, self.driver, CTRL)
@@ -108,12 +120,16 @@ class PrefillServer:
         while self.pending:
             r = self.pending[0]
             need = _blocks_for(len(r.prompt) + r.params.max_tokens, self.bs)
-            if need > self.credit or self.seq_credit <= 0:
+            if need <= self.credit and self.seq_credit > 0:
+                self.credit -= need
+                self.seq_credit -= 1
+                r.spec_state = need  # credit reserved for this sequence
+            elif len(self.local) < self.local_cap:
+                r.spec_state = 0     # decoded here (overflow)
+                self.local.add(r.rid)
+            else:
                 break
-            self.credit -= need
-            self.seq_credit -= 1
             self.pending.popleft()
-            r.spec_state = need  # credit reserved for this sequence
             self.engine.scheduler.add(r)
             self.engine.requests[r.rid] = r
 
@@ -127,7 +143,19 @@ class PrefillServer:
             return []
         outs = self.engine.step()
         ready = []
+        report = []
         for o in outs:
+            if o.rid in self.local:
+                self.local_tokens += 1
+                if len(o.request.output) == 1 and o.request.ttft is not None:
+                    self.first_tokens += 1
+                    self.ttfts.append(o.request.ttft)
+                if o.finished:
+                    self.local.discard(o.rid)
+                if self.report_tokens:
+                    report += [int(o.rid), int(o.token),
+                               {"length": 1, "stop": 2}.get(o.finish_reason, 2) if o.finished else -1]
+                continue
             self.first_tokens += 1
             if o.request.ttft is not None:
                 self.ttfts.append(o.request.ttft)
@@ -141,6 +169,8 @@ class PrefillServer:
         if ready:
             with phase("migrate_send", reqs=len(ready)):
                 self._migrate(ready)
+        if report:
+            self.ch.send_var([MSG_TOKENS] + report)
         return outs
 
     def _migrate(self, reqs: list) -> None:
@@ -218,6 +248,7 @@ class DecodeDriver:
         self.arrivals: list = []   # migrated requests not yet reported (first token known)
         self.track_arrivals = False
         self.prefill_finished: list = []   # (rid, token, reason) of sequences done at their first token
+        self.remote_tokens: list = []      # (rid, token, reason|None) decoded on a prefill rank (overflow)
         self.refund = collections.Counter()
         self.refund_seqs = collections.Counter()
         self.done = set()
@@ -314,6 +345,12 @@ class DecodeDriver:
                 elif m[0] == MSG_FINISHED:
                     if self.track_arrivals:
                         self.prefill_finished.append((int(m[1]), int(m[2]), REASONS.get(int(m[3]))))
+                elif m[0] == MSG_TOKENS:
+                    if self.track_arrivals:
+                        for i in range(1, len(m) - 2, 3):
+                            code = int(m[i + 2])
+                            self.remote_tokens.append((int(m[i]), int(m[i + 1]),
+                                                       None if code < 0 else REASONS.get(code) or "stop"))
         self._admit_arrived()
 
     def step(self, poll: bool = True) -> list[StepOutput]:

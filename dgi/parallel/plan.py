@@ -100,3 +100,13 @@ def plan_node_layout(n_gpus: int, kind: str = "pdpp", prefill_ranks: Optional[in
     decode_stages = n_gpus - prefill_ranks
     k = "pdpp" if decode_stages > 1 else "pd"
     return NodeLayout(k, list(range(prefill_ranks)), list(range(prefill_ranks, n_gpus)))
+
+
+def prefill_overflow_cap(layout: NodeLayout, cap: int = 256) -> int:
+    """Sequences a prefill rank may decode itself while the decode side has no
+    credit (``PrefillServer(local_cap=...)``).  On for one decode GPU fed by 2+
+    prefill GPUs — that decode GPU saturates at ~4.6k tok/s on 70B while each
+    prefill GPU supplies ~2.5k (profiles/r1_pd_capacity_70b.md) — off where the
+    prefill side is the bottleneck (1 prefill GPU, or the 8-GPU 5P + 3-stage
+    decode pipeline)."""
+    return cap if layout.kind == "pd" and len(layout.prefill_ranks) >= 2 else 0

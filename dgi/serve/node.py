@@ -190,6 +190,17 @@ class Router:
                     self._finish(rid, reason)
                     self.load[p.dst] -= 1
             self.drv.prefill_finished.clear()
+            for rid, tok, reason in self.drv.remote_tokens:      # decoded on a prefill rank (overflow)
+                p = self.live.get(rid)
+                if p is None:
+                    continue
+                worked = True
+                if not p.tokens:
+                    self.load[p.dst] -= 1
+                self._emit(p, tok, reason is not None, reason)
+                if reason is not None:
+                    self._finish(rid, reason)
+            self.drv.remote_tokens.clear()
         return worked
 
     def serve_forever(self, stop: threading.Event) -> None:
@@ -286,10 +297,12 @@ def _prefill_loop(args, fabric, layout) -> None:
     from dgi.engine import EngineConfig
     from dgi.parallel.fabric import CtrlChannel
     from dgi.parallel.pd import PrefillServer
-    cfg = EngineConfig(model=args.model, device=str(fabric.device), max_num_seqs=64,
+    from dgi.parallel.plan import prefill_overflow_cap
+    cap = args.prefill_local_cap if args.prefill_local_cap >= 0 else prefill_overflow_cap(layout)
+    cfg = EngineConfig(model=args.model, device=str(fabric.device), max_num_seqs=64 + cap,
                        max_num_batched_tokens=args.max_batched_tokens, max_model_len=args.max_model_len,
-                       use_graphs=False, seed=args.seed)
-    srv = PrefillServer(cfg, fabric, layout)
+                       use_graphs=str(fabric.device).startswith("cuda") and not args.no_graphs, seed=args.seed)
+    srv = PrefillServer(cfg, fabric, layout, local_cap=cap, report_tokens=True)
     inbox = CtrlChannel(fabric, layout.decode_ranks[0], 1, tag="req")
     stopping = False
     while True:
@@ -319,6 +332,8 @@ def main(argv=None) -> int:
     ap.add_argument("--port", type=int, default=8100)
     ap.add_argument("--layout", default="auto")
     ap.add_argument("--prefill-ranks", type=int, default=0)
+    ap.add_argument("--prefill-local-cap", type=int, default=-1,
+                    help="sequences a prefill rank decodes itself when the decode side is full (-1 = auto)")
     ap.add_argument("--max-num-seqs", type=int, default=256)
     ap.add_argument("--max-batched-tokens", type=int, default=4096)
     ap.add_argument("--max-model-len", type=int, default=4096)

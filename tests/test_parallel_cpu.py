@@ -135,6 +135,44 @@ def _pd_body(rank, world):
     return None
 
 
+def _pd_overflow_body(rank, world):
+    """Decode side holds 2 sequences: the other prompts overflow into the
+    prefill rank's own decode (local_cap) and are reported back as tokens."""
+    import time as _t
+    from dgi.engine import EngineConfig
+    from dgi.parallel.fabric import Fabric
+    from dgi.parallel.pd import DecodeDriver, PrefillServer
+    from dgi.parallel.plan import NodeLayout
+    from dgi.sched.request import SamplingParams
+    f = Fabric()
+    cfg = EngineConfig(model=MODEL, device="cpu", num_blocks=128, max_num_seqs=8, max_model_len=256,
+                       max_num_batched_tokens=64, enable_prefix_caching=False)
+    layout = NodeLayout("pd", [0], [1])
+    sp = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
+    if rank == 0:
+        srv = PrefillServer(cfg, f, layout, local_cap=8, report_tokens=True)
+        reqs = [srv.submit(p, sp) for p in PROMPTS]
+        while srv.busy():
+            srv.step()
+        srv.finish()
+        return {"local": {tuple(r.prompt): r.output for r in reqs if len(r.output) > 1},
+                "migrated": srv.migrated, "local_tokens": srv.local_tokens}
+    from dataclasses import replace
+    drv = DecodeDriver(replace(cfg, max_num_seqs=2), f, layout)
+    drv.track_arrivals = True
+    done, remote = {}, {}
+    while not drv.all_prefill_done() or drv.engine.has_unfinished():
+        for o in drv.step():
+            if o.finished:
+                done[tuple(o.request.prompt)] = o.request.output
+        for rid, tok, reason in drv.remote_tokens:
+            remote.setdefault(rid, []).append((tok, reason))
+        drv.remote_tokens.clear()
+        _t.sleep(0.001)
+    drv.finish()
+    return {"decoded": done, "remote": remote}
+
+
 # ---------------------------------------------------------------------------- tests
 
 def test_layer_range_for_worker_covers_all_layers():
@@ -176,6 +214,19 @@ def test_pd_migration_matches_local_decode(world):
     ref = _reference_outputs()
     out = _spawn("_pd_body", world)
     assert out[1] == ref
+
+
+def test_pd_overflow_decodes_on_prefill_rank_when_decode_is_full():
+    ref = dict(zip(map(tuple, PROMPTS), _reference_outputs()))
+    out = _spawn("_pd_overflow_body", 2)
+    pre, dec = out[0], out[1]
+    assert pre["migrated"] >= 1 and len(pre["local"]) >= 1          # both paths taken
+    merged = {**dec["decoded"], **pre["local"]}
+    assert merged == ref
+    # every overflow token reached the decode driver (the node router's feed), last one with a reason
+    assert sorted(len(v) for v in dec["remote"].values()) == [6] * len(pre["local"])
+    assert all(v[-1][1] == "length" and all(r is None for _, r in v[:-1]) for v in dec["remote"].values())
+    assert pre["local_tokens"] == 6 * len(pre["local"])
 
 
 @pytest.mark.parametrize("npre,world", [(2, 4), (1, 4)])
