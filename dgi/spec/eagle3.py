@@ -309,6 +309,131 @@ class _VerifyGraph:
         return acc[:R], path[:R], toks[:R], feats[:R * N]
 
 
+class _DraftGraph:
+    """hipGraph of tree drafting (root top-k, then depths 2..D) for ``Rb`` sequences.
+
+    The per-depth metadata depends only on each sequence's length and block
+    table, never on what the draft proposes, so all depths' positions, KV
+    slots and context lengths are built on the host in one buffer and copied
+    once; the graph then runs every depth (ancestor masks, draft layer over
+    the chunk of tree nodes, top-k expansion, beam selection) without a host
+    round trip.  Inputs: root hidden states and last tokens; outputs: tree
+    tokens and parents.  Padding rows use the scratch page 0."""
+
+    def __init__(self, eng: "SpecEngine", Rb: int):
+        sp, run = eng.spec, eng.runner
+        self.eng, self.Rb, self.maxw = eng, Rb, run.max_blocks
+        self.W, self.D, self.K, self.N = sp.width, sp.depth, sp.topk, sp.num_nodes
+        dev = eng.device
+        H = eng.model_cfg.hidden_size
+        self.ms = [self.W * (d - 1) for d in range(2, self.D + 1)]
+        self.depth_np = np.concatenate([[0]] + [[d] * self.W for d in range(1, self.D + 1)]).astype(np.int64)
+        n_dyn = Rb * self.maxw + sum(2 * Rb * m + Rb for m in self.ms)
+        self.host = torch.zeros(n_dyn, dtype=torch.int32).pin_memory()
+        self.dyn = torch.zeros(n_dyn, dtype=torch.int32, device=dev)
+        o = 0
+        self.d_bt = self.dyn[o:o + Rb * self.maxw].view(Rb, self.maxw)
+        o += Rb * self.maxw
+        self.lv = []                     # per depth: (offset, m, pos, slots, ctx, cu, tiles)
+        tiles = torch.stack([torch.arange(Rb, dtype=torch.int32), torch.zeros(Rb, dtype=torch.int32)],
+                            1).contiguous().to(dev)
+        for m in self.ms:
+            pos = self.dyn[o:o + Rb * m]
+            slots = self.dyn[o + Rb * m:o + 2 * Rb * m]
+            ctx = self.dyn[o + 2 * Rb * m:o + 2 * Rb * m + Rb]
+            cu = torch.arange(0, Rb * m + 1, m, dtype=torch.int32, device=dev)
+            self.lv.append((o, m, pos, slots, ctx, cu, tiles))
+            o += 2 * Rb * m + Rb
+        self.g_root = torch.zeros(Rb, H, dtype=eng.cfg.dtype, device=dev)
+        self.last = torch.zeros(Rb, dtype=torch.long, device=dev)
+        self._fill(np.ones(Rb, np.int64), [[0]] * Rb)
+        self.dyn.copy_(self.host)
+        self._capture()
+
+    def _fill(self, n_vec, brows) -> None:
+        """Host metadata of every depth for sequences of length ``n_vec``."""
+        Rb, maxw, bs = self.Rb, self.maxw, self.eng.pool.block_size
+        h = self.host.numpy()
+        h[:Rb * maxw] = 0
+        for i, blk in enumerate(brows):
+            h[i * maxw: i * maxw + len(blk)] = blk
+        for o, m, *_ in self.lv:
+            ps = np.empty((Rb, m), np.int64)
+            sl = np.empty((Rb, m), np.int64)
+            for i in range(Rb):
+                n = int(n_vec[i]) if i < len(n_vec) else 1
+                blk = np.asarray(brows[i] if i < len(brows) else [0], np.int64)
+                ps[i] = n - 1 + self.depth_np[1:m + 1]
+                s_ = n + np.arange(m)
+                sl[i] = blk[np.minimum(s_ // bs, len(blk) - 1)] * bs + s_ % bs
+                if i >= len(brows):
+                    sl[i] = np.arange(m) % bs             # padding: scratch page 0
+            h[o:o + Rb * m] = ps.ravel()
+            h[o + Rb * m:o + 2 * Rb * m] = sl.ravel()
+            h[o + 2 * Rb * m:o + 2 * Rb * m + Rb] = [int(n_vec[i]) + m if i < len(n_vec) else 1 + m
+                                                     for i in range(Rb)]
+
+    def _body(self):
+        eng, dr = self.eng, self.eng.draft
+        Rb, W, D, K, N = self.Rb, self.W, self.D, self.K, self.N
+        dev = self.g_root.device
+        H = self.g_root.shape[1]
+        lp = dr.logprobs(self.g_root)
+        v1, t1 = ops.topk(lp, K)
+        tok = torch.zeros(Rb, N, dtype=torch.long, device=dev)
+        par = torch.full((Rb, N), -1, dtype=torch.int32, device=dev)
+        score = torch.zeros(Rb, N, dtype=torch.float32, device=dev)
+        G = torch.zeros(Rb, N, H, dtype=self.g_root.dtype, device=dev)
+        tok[:, 0] = self.last
+        G[:, 0] = self.g_root
+        tok[:, 1:W + 1] = t1[:, :W].long()
+        par[:, 1:W + 1] = 0
+        score[:, 1:W + 1] = v1[:, :W].float()
+        for d, (_, m, pos, slots, ctx, cu, tiles) in zip(range(2, D + 1), self.lv):
+            cpar = par[:, 1:m + 1] - 1
+            cpar = torch.where(cpar < 0, torch.full_like(cpar, -1), cpar)
+            anc, _ = ops.tree_mask(cpar.contiguous())
+            cm = AttnMeta(positions=pos, slot_mapping=slots, num_decode=0, num_prefill_tokens=Rb * m,
+                          pre_block_tables=self.d_bt, pre_cu_seqlens=cu, pre_context_lens=ctx, pre_tiles=tiles,
+                          tree_mask=anc, tree_n=m)
+            pidx = par[:, 1:m + 1].long()
+            hin = torch.gather(G, 1, pidx[:, :, None].expand(Rb, m, H)).reshape(Rb * m, H)
+            gc = dr.forward(tok[:, 1:m + 1].reshape(-1), hin, cm).view(Rb, m, H)
+            G[:, 1:m + 1] = gc
+            fr = torch.arange(m - W + 1, m + 1, device=dev)
+            lpf = dr.logprobs(gc[:, m - W:].reshape(Rb * W, H))
+            vf, tf = ops.topk(lpf, K)
+            cand = (score[:, fr][:, :, None] + vf.view(Rb, W, K).float()).view(Rb, W * K)
+            best, bi = torch.topk(cand, W, dim=1)
+            base = 1 + W * (d - 1)
+            tok[:, base: base + W] = torch.gather(tf.view(Rb, W * K).long(), 1, bi)
+            par[:, base: base + W] = fr[bi // K].int()
+            score[:, base: base + W] = best
+        return tok, par
+
+    @torch.inference_mode()
+    def _capture(self) -> None:
+        eng = self.eng
+        s = torch.cuda.Stream(device=eng.device)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self._body()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize(eng.device)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, pool=eng._graph_pool):
+            self.out = self._body()
+
+    def run(self, R: int, g_root: torch.Tensor, last: list, n_vec, brows):
+        self._fill(n_vec, brows)
+        self.dyn.copy_(self.host, non_blocking=True)
+        self.g_root[:R].copy_(g_root)
+        self.last[:R].copy_(torch.as_tensor(last, dtype=torch.long).pin_memory(), non_blocking=True)
+        self.graph.replay()
+        tok, par = self.out
+        return tok[:R], par[:R]
+
+
 class SpecEngine(LLMEngine):
     """``LLMEngine`` with EAGLE-3 tree speculation for greedy requests."""
 
@@ -329,7 +454,19 @@ class SpecEngine(LLMEngine):
         self.oracle_accept = 1.0
         self._oracle_rng = np.random.default_rng(0)
         self._vgraphs: dict = {}
+        self._dgraphs: dict = {}
         self._graph_pool = torch.cuda.graph_pool_handle() if self.device.type == "cuda" else None
+
+    def _draft_graph(self, R: int) -> Optional[_DraftGraph]:
+        if not (self.spec.graphs and self.device.type == "cuda" and self.spec.depth >= 2):
+            return None
+        Rb = next((b for b in VERIFY_BUCKETS if b >= R), None)
+        if Rb is None:
+            return None
+        g = self._dgraphs.get(Rb)
+        if g is None:
+            g = self._dgraphs[Rb] = _DraftGraph(self, Rb)
+        return g
 
     def _verify_graph(self, R: int) -> Optional[_VerifyGraph]:
         if not (self.spec.graphs and self.device.type == "cuda"):
@@ -464,48 +601,13 @@ class SpecEngine(LLMEngine):
         for r in reqs:
             r.spec_state.draft_len = r.total_len
         # ---- 2) tree drafting
-        lp = self.draft.logprobs(g_root)                         # [R, V]
-        v1, t1 = ops.topk(lp, K)
-        tok = torch.zeros(R, N, dtype=torch.long, device=dev)
-        par = torch.full((R, N), -1, dtype=torch.int32, device=dev)
-        score = torch.zeros(R, N, dtype=torch.float32, device=dev)
-        G = torch.zeros(R, N, H, dtype=g.dtype, device=dev)
-        tok[:, 0] = torch.tensor([r.all_tokens()[-1] for r in reqs], device=dev)
-        G[:, 0] = g_root
-        tok[:, 1:W + 1] = t1[:, :W].long()
-        par[:, 1:W + 1] = 0
-        score[:, 1:W + 1] = v1[:, :W].float()
         n_vec = np.asarray([r.total_len for r in reqs], np.int64)
         depth_np = np.concatenate([[0]] + [[d] * W for d in range(1, D + 1)])
-        for d in range(2, D + 1):
-            m = W * (d - 1)                                       # nodes 1..m (depths 1..d-1)
-            cpar = par[:, 1:m + 1] - 1                            # chunk-local parents (root -> -1)
-            cpar = torch.where(cpar < 0, torch.full_like(cpar, -1), cpar)
-            anc, _ = ops.tree_mask(cpar.contiguous())
-            cpos, cslots, cctx, ccu = [], [], [], [0]
-            for i, r in enumerate(reqs):
-                n = int(n_vec[i])
-                blk = np.asarray(r.blocks, np.int64)
-                ps = n - 1 + depth_np[1:m + 1]
-                sl = n + np.arange(m)
-                cpos.extend(ps.tolist())
-                cslots.extend((blk[sl // bs] * bs + sl % bs).tolist())
-                cctx.append(n + m)
-                ccu.append(ccu[-1] + m)
-            cm = _varlen_meta(run, cpos, cslots, brows, ccu, cctx, dev, tree_mask=anc, tree_n=m)
-            pidx = par[:, 1:m + 1].long()                          # parents of chunk nodes
-            hin = torch.gather(G, 1, pidx[:, :, None].expand(R, m, H)).reshape(R * m, H)
-            gc = self.draft.forward(tok[:, 1:m + 1].reshape(-1), hin, cm).view(R, m, H)
-            G[:, 1:m + 1] = gc
-            fr = torch.arange(m - W + 1, m + 1, device=dev)        # frontier = depth d-1 nodes
-            lpf = self.draft.logprobs(gc[:, m - W:].reshape(R * W, H))
-            vf, tf = ops.topk(lpf, K)                              # [R*W, K]
-            cand = (score[:, fr][:, :, None] + vf.view(R, W, K).float()).view(R, W * K)
-            best, bi = torch.topk(cand, W, dim=1)
-            base = 1 + W * (d - 1)
-            tok[:, base: base + W] = torch.gather(tf.view(R, W * K).long(), 1, bi)
-            par[:, base: base + W] = fr[bi // K].int()
-            score[:, base: base + W] = best
+        dg = self._draft_graph(R)
+        if dg is not None:
+            tok, par = dg.run(R, g_root, [r.all_tokens()[-1] for r in reqs], n_vec, brows)
+        else:
+            tok, par = self._draft_tree_eager(reqs, g_root, n_vec, depth_np, brows)
         if self.oracle:
             self._apply_oracle(reqs, tok, par, n_vec)
         self.spec_stats["draft_s"] += time.perf_counter() - td
@@ -580,6 +682,54 @@ class SpecEngine(LLMEngine):
         self.spec_stats["spec_steps"] += 1
         self.spec_stats["spec_rows"] += R
         return outs
+
+    def _draft_tree_eager(self, reqs, g_root, n_vec, depth_np, brows):
+        """Tree drafting, one host-built metadata copy per depth (CPU / no graphs)."""
+        W, D, K, N = self.spec.width, self.spec.depth, self.spec.topk, self.spec.num_nodes
+        R, H = g_root.shape
+        dev, run, bs = self.device, self.runner, self.pool.block_size
+        g = g_root
+        lp = self.draft.logprobs(g_root)                         # [R, V]
+        v1, t1 = ops.topk(lp, K)
+        tok = torch.zeros(R, N, dtype=torch.long, device=dev)
+        par = torch.full((R, N), -1, dtype=torch.int32, device=dev)
+        score = torch.zeros(R, N, dtype=torch.float32, device=dev)
+        G = torch.zeros(R, N, H, dtype=g.dtype, device=dev)
+        tok[:, 0] = torch.tensor([r.all_tokens()[-1] for r in reqs], device=dev)
+        G[:, 0] = g_root
+        tok[:, 1:W + 1] = t1[:, :W].long()
+        par[:, 1:W + 1] = 0
+        score[:, 1:W + 1] = v1[:, :W].float()
+        for d in range(2, D + 1):
+            m = W * (d - 1)                                       # nodes 1..m (depths 1..d-1)
+            cpar = par[:, 1:m + 1] - 1                            # chunk-local parents (root -> -1)
+            cpar = torch.where(cpar < 0, torch.full_like(cpar, -1), cpar)
+            anc, _ = ops.tree_mask(cpar.contiguous())
+            cpos, cslots, cctx, ccu = [], [], [], [0]
+            for i, r in enumerate(reqs):
+                n = int(n_vec[i])
+                blk = np.asarray(r.blocks, np.int64)
+                ps = n - 1 + depth_np[1:m + 1]
+                sl = n + np.arange(m)
+                cpos.extend(ps.tolist())
+                cslots.extend((blk[sl // bs] * bs + sl % bs).tolist())
+                cctx.append(n + m)
+                ccu.append(ccu[-1] + m)
+            cm = _varlen_meta(run, cpos, cslots, brows, ccu, cctx, dev, tree_mask=anc, tree_n=m)
+            pidx = par[:, 1:m + 1].long()                          # parents of chunk nodes
+            hin = torch.gather(G, 1, pidx[:, :, None].expand(R, m, H)).reshape(R * m, H)
+            gc = self.draft.forward(tok[:, 1:m + 1].reshape(-1), hin, cm).view(R, m, H)
+            G[:, 1:m + 1] = gc
+            fr = torch.arange(m - W + 1, m + 1, device=dev)        # frontier = depth d-1 nodes
+            lpf = self.draft.logprobs(gc[:, m - W:].reshape(R * W, H))
+            vf, tf = ops.topk(lpf, K)                              # [R*W, K]
+            cand = (score[:, fr][:, :, None] + vf.view(R, W, K).float()).view(R, W * K)
+            best, bi = torch.topk(cand, W, dim=1)
+            base = 1 + W * (d - 1)
+            tok[:, base: base + W] = torch.gather(tf.view(R, W * K).long(), 1, bi)
+            par[:, base: base + W] = fr[bi // K].int()
+            score[:, base: base + W] = best
+        return tok, par
 
     def _apply_oracle(self, reqs, tok, par, n_vec) -> None:
         W, D = self.spec.width, self.spec.depth
