@@ -10,7 +10,7 @@ using namespace dgi;
 
 template <int NC, bool ADD>
 __global__ __launch_bounds__(256) void rmsnorm_kernel(
-    uint16_t* __restrict__ out, uint16_t* __restrict__ x, uint16_t* __restrict__ residual,
+    uint16_t* out, uint16_t* x, uint16_t* __restrict__ residual,
     const uint16_t* __restrict__ w, int H, float eps) {
   const int row = blockIdx.x;
   const int tid = threadIdx.x;
@@ -20,17 +20,28 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(
   u32x4* orow = reinterpret_cast<u32x4*>(out + (size_t)row * H);
   const u32x4* wr = reinterpret_cast<const u32x4*>(w);
 
+  // every load of the row (x, residual, weight) is issued before any use, so a
+  // thread has 3*NC 16-byte loads in flight instead of one dependent chain
+  u32x4 xa[NC], ra[NC], wa[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int i = tid + c * 256;
+    if (i < nchunk) {
+      xa[c] = xr[i];
+      if (ADD) ra[c] = rr[i];
+      wa[c] = wr[i];
+    }
+  }
   float v[NC][8];
   float ss = 0.f;
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int i = tid + c * 256;
     if (i < nchunk) {
-      u32x4 a = xr[i];
-      unpack8(a, v[c]);
+      unpack8(xa[c], v[c]);
       if (ADD) {
         float r[8];
-        unpack8(rr[i], r);
+        unpack8(ra[c], r);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[c][j] += r[j];
         // The residual stream is kept in bf16 (what the next layer adds to).
@@ -53,7 +64,7 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(
     const int i = tid + c * 256;
     if (i < nchunk) {
       float wf[8];
-      unpack8(wr[i], wf);
+      unpack8(wa[c], wf);
       float o[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = v[c][j] * inv * wf[j];
