@@ -330,7 +330,8 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens,
 
 # Where the skinny kernel beats hipBLASLt (profiles/r1_skinny_gemm.md, weights
 # streamed cold from HBM): K <= 4096 projections of 8B-class models at M <= 8
-# (1.3-2.1x on qkv / o / gate_up), and square 4096x4096 (o-proj) up to M = 32.
+# (1.3-2.1x on qkv / o / gate_up), and square 4096x4096 (o-proj) up to M = 16
+# (at M = 32 the end-to-end decode step was no faster).
 # Larger K, the 128k-vocab head and every 70B shape stream at 4.5-5.7 TB/s in
 # hipBLASLt already.  DGI_SKINNY_MAX_M=0 disables the kernel.
 SKINNY_MAX_M = int(os.environ.get("DGI_SKINNY_MAX_M", "32"))
@@ -339,7 +340,7 @@ SKINNY_MAX_M = int(os.environ.get("DGI_SKINNY_MAX_M", "32"))
 def _use_skinny(M: int, N: int, K: int) -> bool:
     if M > SKINNY_MAX_M or K % 1024 or N % 16 or K > 4096 or N > 32768:
         return False
-    return M <= 8 or (N <= 4096 and M <= 32)
+    return M <= 8 or (N <= 4096 and M <= 16)
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
