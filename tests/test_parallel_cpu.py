@@ -112,7 +112,8 @@ def _pd_body(rank, world):
     sp = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
     if rank in layout.prefill_ranks:
         srv = PrefillServer(cfg, f, layout)
-        for i, p in enumerate(PROMPTS):
+        nlocal = int(os.environ.get("DGI_TEST_LOCAL", "0"))
+        for i, p in enumerate(PROMPTS[:len(PROMPTS) - nlocal]):
             if i % npre == rank:
                 srv.submit(p, sp)
         while srv.busy():
@@ -120,7 +121,10 @@ def _pd_body(rank, world):
         srv.finish()
         return "prefill"
     if rank == layout.decode_ranks[0]:
-        drv = DecodeDriver(cfg, f, layout)
+        nlocal = int(os.environ.get("DGI_TEST_LOCAL", "0"))
+        drv = DecodeDriver(cfg, f, layout, local_fraction=0.3 if nlocal else 0.0)
+        for p in PROMPTS[len(PROMPTS) - nlocal:]:          # served end to end on the decode side
+            assert drv.admit_local(p, sp) is not None
         done = {}
         while len(done) < len(PROMPTS):
             for o in drv.step():
@@ -227,6 +231,22 @@ def test_pd_overflow_decodes_on_prefill_rank_when_decode_is_full():
     assert sorted(len(v) for v in dec["remote"].values()) == [6] * len(pre["local"])
     assert all(v[-1][1] == "length" and all(r is None for _, r in v[:-1]) for v in dec["remote"].values())
     assert pre["local_tokens"] == 6 * len(pre["local"])
+
+
+def test_pdpp_decode_pipeline_also_serves_local_prompts(monkeypatch):
+    """The decode pipeline's driver admits prompts of its own (prefilled through
+    the pipeline) next to migrated sequences; every output equals local decoding."""
+    model = "llama-tiny-hd128"
+    monkeypatch.setenv("DGI_TEST_MODEL", model)
+    monkeypatch.setenv("DGI_TEST_PREFILL", "1")
+    monkeypatch.setenv("DGI_TEST_LOCAL", "2")
+    from dgi.engine import EngineConfig, LLMEngine
+    from dgi.sched.request import SamplingParams
+    e = LLMEngine(EngineConfig(model=model, device="cpu", num_blocks=128, max_num_seqs=8, max_model_len=256,
+                               max_num_batched_tokens=64, enable_prefix_caching=False))
+    ref = [r.output for r in e.generate(PROMPTS, SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True))]
+    out = _spawn("_pd_body", 3)
+    assert out[1] == ref
 
 
 @pytest.mark.parametrize("npre,world", [(2, 4), (1, 4)])
