@@ -184,9 +184,10 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
             # one prefill GPU leaves the decode GPU ~half idle (2.5k of ~4.6k tok/s): fill it with
             # local prompts; with 3+ prefill GPUs the decode GPU is the bottleneck already.  The
             # 8-GPU 3-stage decode pipeline has ~20% headroom over its 5 prefill GPUs (15k vs 12.4k
-            # tok/s, profiles/r1_pd_capacity_70b.md): a tenth of its pool serves local prompts
+            # tok/s, profiles/r1_pd_capacity_70b.md); local prompts there (--decode-local-frac) add
+            # prefill chunks to its microbatches and are off until measured on a whole node
             npre = len(layout.prefill_ranks)
-            local_frac = {1: 0.35, 2: 0.15}.get(npre, 0.0) if layout.kind == "pd" else 0.1
+            local_frac = {1: 0.35, 2: 0.15}.get(npre, 0.0) if layout.kind == "pd" else 0.0
         drv = DecodeDriver(cfg, f, layout, local_fraction=local_frac)
         phases = [CtrlChannel(f, p, 4, tag="phase") for p in layout.prefill_ranks]
         vocab = drv.engine.model_cfg.vocab_size
