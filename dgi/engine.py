@@ -110,6 +110,15 @@ class LLMEngine:
         self.requests: dict = {}
         self.stats = {"steps": 0, "prefill_tokens": 0, "decode_tokens": 0, "generated": 0,
                       "finished": 0, "step_time": 0.0}
+        # MLP row padding measured on this GPU (hipBLASLt kernel-selection cliffs, dgi.runtime.gemm_pad)
+        self.mlp_pad_table = None
+        if self.device.type == "cuda" and getattr(self.model, "mlp_pad", None) is None:
+            from dgi.runtime.gemm_pad import build_for_model
+            t1 = time.perf_counter()
+            self.mlp_pad_table = build_for_model(self.model, cfg.max_num_batched_tokens)
+            if self.mlp_pad_table is not None:
+                self.model.mlp_pad = self.mlp_pad_table.pad
+                self.mlp_pad_seconds = time.perf_counter() - t1
 
     # ------------------------------------------------------------------ API
     def add_request(self, prompt_ids: list[int], params: Optional[SamplingParams] = None, rid=None,

@@ -69,6 +69,9 @@ class LlamaModel:
         # tensor parallelism: in-place sum of partial outputs across the TP group
         # after the row-parallel O and down projections (dgi.parallel.tensor)
         self.reduce = None
+        # MLP row padding (dgi.runtime.gemm_pad): T -> rows to run gate_up/down on
+        self.mlp_pad = None
+        self._pad_buf: Optional[torch.Tensor] = None
         if init == "random":
             self._init_random(seed)
         elif init == "empty":
@@ -209,9 +212,24 @@ class LlamaModel:
                               tree_mask=meta.tree_mask, tree_n=meta.tree_n, out=out[nd:])
         return out
 
+    def _mlp_rows(self, T: int, like: torch.Tensor) -> int:
+        """Padded MLP row count for a T-row step, and the o-proj buffer it needs."""
+        if self.mlp_pad is None or not like.is_cuda or torch.cuda.is_current_stream_capturing():
+            return T
+        Mp = self.mlp_pad(T)
+        if Mp <= T:
+            return T
+        buf = self._pad_buf
+        if buf is None or buf.shape[0] < Mp or buf.dtype != like.dtype or buf.device != like.device:
+            buf = self._pad_buf = torch.empty(max(Mp, 4096), like.shape[1], dtype=like.dtype, device=like.device)
+        buf[T:Mp].zero_()       # pad rows: zeros in, ignored out
+        return Mp
+
     def forward_layers(self, h: torch.Tensor, meta: AttnMeta, residual: Optional[torch.Tensor] = None):
         c = self.cfg
         eps = c.rms_eps
+        T = h.shape[0]
+        Mp = self._mlp_rows(T, h) if self.layers else T
         for i, L in enumerate(self.layers):
             if residual is None:
                 residual = h
@@ -220,13 +238,21 @@ class LlamaModel:
                 ops.fused_add_rmsnorm(h, residual, L.in_norm, eps)
             qkv = ops.linear(h, L.qkv, L.qkv_bias)
             attn = self.attention(i, qkv, meta)
-            h = ops.linear(attn, L.o)
+            if Mp > T:
+                # o-proj writes the first T rows of the padded MLP input
+                h = torch.matmul(attn, L.o.t(), out=self._pad_buf[:T])
+            else:
+                h = ops.linear(attn, L.o)
             if self.reduce is not None:
                 self.reduce(h)
             ops.fused_add_rmsnorm(h, residual, L.post_norm, eps)
-            gu = ops.linear(h, L.gate_up)
-            act = ops.silu_mul(gu)
-            h = ops.linear(act, L.down)
+            if Mp > T:
+                act = ops.silu_mul(ops.linear(self._pad_buf[:Mp], L.gate_up))
+                h = ops.linear(act, L.down)[:T]
+            else:
+                gu = ops.linear(h, L.gate_up)
+                act = ops.silu_mul(gu)
+                h = ops.linear(act, L.down)
             if self.reduce is not None:
                 self.reduce(h)
             if self.capture_layers and (self.layer_start + i) in self.capture_layers:

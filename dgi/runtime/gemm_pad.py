@@ -1,0 +1,88 @@
+"""Row padding for the MLP GEMMs from a table measured on this GPU at start-up.
+
+hipBLASLt picks its kernel from (M, N, K), and on MI355X the choice has
+cliffs: for the Llama-3-70B down-projection (N 8192, K 28672) M = 1792 runs
+in 755 us while M = 1800 runs in 621 us; the QKV GEMM takes 301 us at
+M = 1700 and 243 us at M = 1800 (profiles/r1_gemm_m_sweep_70b.md).  A serving
+step's row count is whatever the scheduler packed, so it lands on both sides
+of those cliffs.
+
+The MLP is row-independent, so its rows can be padded for free as far as
+correctness goes: ``MlpPadTable.measure`` times gate_up + SiLU·mul + down for
+every multiple of ``step`` rows up to the token budget, and ``pad(T)`` returns
+the row count (a multiple of ``step``, at most ``max_grow`` larger than T)
+with the lowest measured time.  ``LlamaModel.forward_layers`` then lets the
+o-projection write into a padded buffer and runs the MLP on the padded rows.
+"""
+from __future__ import annotations
+
+import bisect
+import os
+from typing import Optional
+
+import torch
+
+
+class MlpPadTable:
+    def __init__(self, grid: list, times: list, step: int, max_grow: float = 0.15):
+        self.grid = list(grid)
+        self.times = list(times)
+        self.step = step
+        self.max_grow = max_grow
+        self._cache: dict = {}
+
+    @classmethod
+    def measure(cls, gate_up: torch.Tensor, down: torch.Tensor, m_min: int = 512, m_max: int = 4096,
+                step: int = 32, reps: int = 3) -> "MlpPadTable":
+        from dgi import ops
+        H = gate_up.shape[1]
+        x = torch.randn(m_max, H, device=gate_up.device, dtype=gate_up.dtype) * 0.1
+        grid = list(range(m_min, m_max + 1, step))
+        times = []
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+        def mlp(m):
+            ops.linear(ops.silu_mul(ops.linear(x[:m], gate_up)), down)
+
+        for m in grid:
+            mlp(m)
+            best = float("inf")
+            for _ in range(reps):
+                e0.record()
+                mlp(m)
+                e1.record()
+                e1.synchronize()
+                best = min(best, e0.elapsed_time(e1))
+            times.append(best)
+        return cls(grid, times, step)
+
+    def pad(self, T: int) -> int:
+        """Rows to run the MLP on for a step of ``T`` rows (``T`` when the table has no say)."""
+        r = self._cache.get(T)
+        if r is not None:
+            return r
+        r = T
+        if self.grid and self.grid[0] <= T <= self.grid[-1]:
+            i = bisect.bisect_left(self.grid, T)            # first grid row count >= T
+            j = i
+            best = i
+            while j < len(self.grid) and self.grid[j] <= T * (1 + self.max_grow):
+                if self.times[j] < self.times[best]:
+                    best = j
+                j += 1
+            r = self.grid[best]
+        self._cache[T] = r
+        return r
+
+
+def build_for_model(model, m_max: int, step: int = 32) -> Optional[MlpPadTable]:
+    """Measure the table for ``model``'s MLP shape on its device (None when off / not applicable)."""
+    if os.environ.get("DGI_MLP_PAD", "1") == "0":
+        return None
+    layers = getattr(model, "layers", None)
+    if not layers or not torch.cuda.is_available():
+        return None
+    L = layers[0]
+    if L.gate_up.device.type != "cuda" or m_max < 1024:
+        return None
+    return MlpPadTable.measure(L.gate_up, L.down, m_max=m_max, step=step)

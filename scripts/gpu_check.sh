@@ -45,6 +45,8 @@ for s in $STEPS; do
     declat) run declat 600 python scripts/decode_latency.py --out gpurun_out/declat.json && DGI_SKINNY_MAX_M=0 run declat_blaslt 600 python scripts/decode_latency.py --out gpurun_out/declat_blaslt.json ;;
     profdec) export TMPDIR=/tmp; run profdec 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profdec -o run --output-format csv -- python3 scripts/decode_latency.py --batch 1 --steps 200 ;;
     spec8b_cfg3) run spec8b_cfg3 900 python scripts/bench_spec.py --batch 1 8 32 --target peaked --train-steps 1500 --random-seqs 1024 --out gpurun_out/spec8b_cfg3.json ;;
+    padtable) run padtable 600 python scripts/mlp_pad_table.py --model llama3-70b --out gpurun_out/mlp_pad_70b.json ;;
+    bench70b_nopad) DGI_MLP_PAD=0 run bench70b_nopad 1200 python bench.py --steps 30 --warmup 5 --json-out gpurun_out/bench70b_nopad.json ;;
     bench70b_long) run bench70b_long 1200 python bench.py --steps 200 --warmup 20 --json-out gpurun_out/bench70b_long.json ;;
   esac
 done

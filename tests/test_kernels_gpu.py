@@ -297,3 +297,25 @@ def test_glm_engine_gpu_matches_cpu():
                                 max_num_batched_tokens=256, use_graphs=False), model_cfg=mc, model=cpu_model)
     cpu = [r.output for r in ce.generate(prompts, sp)]
     assert sum(a[:2] == b[:2] for a, b in zip(gpu, cpu)) >= 2, (gpu, cpu)
+
+
+def test_mlp_row_padding_matches_unpadded():
+    """Padding the MLP rows (o-proj into a padded buffer, gate_up/down on extra
+    zero rows) leaves every real row's result unchanged."""
+    from dgi.engine import EngineConfig, LLMEngine
+    from dgi.sched.request import SamplingParams
+    e = LLMEngine(EngineConfig(model="llama-tiny-hd128", device=DEV, max_num_seqs=8, max_num_batched_tokens=2048,
+                               max_model_len=1024, use_graphs=False))
+    tab = e.mlp_pad_table
+    assert tab is not None
+    for T in (512, 700, 1500, 2048):
+        p = tab.pad(T)
+        assert T <= p <= T * 1.15 + 32 and p % 32 == 0
+    g = torch.Generator().manual_seed(11)
+    prompts = [torch.randint(5, 1000, (n,), generator=g).tolist() for n in (130, 257, 301, 90)]
+    sp = SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True)
+    e.model.mlp_pad = None
+    ref = [r.output for r in e.generate(prompts, sp)]
+    e.model.mlp_pad = lambda T: T + 40 if T >= 64 else T
+    out = [r.output for r in e.generate(prompts, sp)]
+    assert out == ref
