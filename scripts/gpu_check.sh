@@ -47,6 +47,7 @@ for s in $STEPS; do
     spec8b_cfg3) run spec8b_cfg3 900 python scripts/bench_spec.py --batch 1 8 32 --target peaked --train-steps 1500 --random-seqs 1024 --out gpurun_out/spec8b_cfg3.json ;;
     padtable) run padtable 600 python scripts/mlp_pad_table.py --model llama3-70b --out gpurun_out/mlp_pad_70b.json ;;
     bench70b_nopad) DGI_MLP_PAD=0 run bench70b_nopad 1200 python bench.py --steps 30 --warmup 5 --json-out gpurun_out/bench70b_nopad.json ;;
+    pdcap_mbt) run pdcap_mbt 1000 python scripts/pd_capacity.py --mbt 3072,3584,4096,4608,5120,6144 --decode "" --out gpurun_out/pdcap_mbt.jsonl ;;
     bench70b_long) run bench70b_long 1200 python bench.py --steps 200 --warmup 20 --json-out gpurun_out/bench70b_long.json ;;
   esac
 done
