@@ -146,3 +146,23 @@ def test_direct_server_mounts_metrics_routes():
     w.engines["llm"] = object()
     assert c.get("/ready").json()["status"] == "ready"
     time.sleep(0)
+
+
+@pytest.mark.parametrize("name,layout,backend,prefill", [
+    ("config.example.yaml", "pdpp", "mi355x", 5),
+    ("config.8gb.yaml", "single", "mi355x", None),
+    ("config.2gb.yaml", "single", "native", None),
+])
+def test_shipped_example_configs_load(monkeypatch, name, layout, backend, prefill):
+    """The example configs shipped next to the worker (reference worker/config*.yaml) parse and wire up."""
+    import os
+    from worker.config import load_config
+    for k in list(os.environ):
+        if k.startswith(("GPU_", "DGI_")):
+            monkeypatch.delenv(k, raising=False)
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "worker")
+    cfg = load_config(os.path.join(root, name))
+    llm = cfg.engine_config("llm")
+    assert llm["layout"] == layout
+    assert llm["backend"] == backend
+    assert llm.get("prefill_ranks") == prefill

@@ -253,7 +253,10 @@ def main(argv: Optional[List[str]] = None) -> int:
     c.add_argument("--non-interactive", action="store_true")
     c.add_argument("--set", action="append", metavar="KEY=VALUE")
     c.set_defaults(fn=cmd_configure)
-    sub.add_parser("start", help="start the worker").set_defaults(fn=cmd_start)
+    st = sub.add_parser("start", help="start the worker")
+    # reference bug E-27: `gpu-worker start -c config.yaml` was rejected; accept it after the subcommand too
+    st.add_argument("-c", "--config", dest="start_config", default=None)
+    st.set_defaults(fn=cmd_start)
     sub.add_parser("status", help="show registration / server status").set_defaults(fn=cmd_status)
     s = sub.add_parser("set", help="set a config value (dotted key)")
     s.add_argument("key")
@@ -266,6 +269,8 @@ def main(argv: Optional[List[str]] = None) -> int:
     b.add_argument("--prompt-chars", type=int, default=200)
     b.set_defaults(fn=cmd_bench)
     a = ap.parse_args(argv)
+    if getattr(a, "start_config", None):
+        a.config = a.start_config
     return a.fn(a)
 
 
