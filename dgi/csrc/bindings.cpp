@@ -29,7 +29,9 @@ int dgi_silu_mul(const void* gu, void* out, int T, int I, hipStream_t s);
 int dgi_skinny_gemm(const void* x, int ldx, const void* w, const void* bias, void* y, int ldy, int M,
                     int N, int K, int nw, hipStream_t s);
 int dgi_sample(const void* logits, int is_bf16, int B, int V, int stride, const float* temperature,
-               const long long* seeds, long long step, long long* out, hipStream_t s);
+               const long long* seeds, long long step, const float* thresh, long long* out, hipStream_t s);
+int dgi_topkp_threshold(const void* logits, int is_bf16, int B, int V, int stride, const float* temperature,
+                        const long long* top_k, const float* top_p, float* thresh, hipStream_t s);
 int dgi_topk(const void* logits, int is_bf16, int B, int V, int stride, int K, float* out_v,
              long long* out_i, hipStream_t s);
 int dgi_kv_gather(const void* cache, const int* ids, int n, int LK, int num_blocks, int page_elems,
@@ -193,7 +195,7 @@ void skinny_gemm(at::Tensor out, const at::Tensor& x, const at::Tensor& w,
 }
 
 void sample(at::Tensor out, const at::Tensor& logits, const c10::optional<at::Tensor>& temperature,
-            const c10::optional<at::Tensor>& seeds, int64_t step) {
+            const c10::optional<at::Tensor>& seeds, int64_t step, const c10::optional<at::Tensor>& thresh) {
   check_dev(logits, "logits");
   TORCH_CHECK(out.scalar_type() == at::kLong && out.is_contiguous());
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1);
@@ -210,10 +212,34 @@ void sample(at::Tensor out, const at::Tensor& logits, const c10::optional<at::Te
     TORCH_CHECK(seeds->scalar_type() == at::kLong && seeds->numel() >= B);
     sp = reinterpret_cast<const long long*>(seeds->data_ptr<int64_t>());
   }
+  const float* thp = nullptr;
+  if (thresh.has_value() && thresh->defined()) {
+    TORCH_CHECK(thresh->scalar_type() == at::kFloat && thresh->numel() >= B && thresh->is_contiguous());
+    thp = thresh->data_ptr<float>();
+  }
   check_rc(dgi_sample(logits.data_ptr(), logits.scalar_type() == at::kBFloat16, B,
-                      (int)logits.size(1), (int)logits.stride(0), tp, sp, step,
+                      (int)logits.size(1), (int)logits.stride(0), tp, sp, step, thp,
                       reinterpret_cast<long long*>(out.data_ptr<int64_t>()), cur_stream()),
            "sample");
+}
+
+void topkp_threshold(at::Tensor thresh, const at::Tensor& logits, const at::Tensor& temperature,
+                     const at::Tensor& top_k, const at::Tensor& top_p) {
+  check_dev(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1);
+  TORCH_CHECK(logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat);
+  const int B = (int)logits.size(0);
+  TORCH_CHECK(thresh.scalar_type() == at::kFloat && thresh.is_contiguous() && thresh.numel() >= B);
+  TORCH_CHECK(temperature.scalar_type() == at::kFloat && temperature.is_contiguous() && temperature.numel() >= B);
+  TORCH_CHECK(top_k.scalar_type() == at::kLong && top_k.is_contiguous() && top_k.numel() >= B);
+  TORCH_CHECK(top_p.scalar_type() == at::kFloat && top_p.is_contiguous() && top_p.numel() >= B);
+  TORCH_CHECK(thresh.device() == logits.device() && temperature.device() == logits.device() &&
+              top_k.device() == logits.device() && top_p.device() == logits.device());
+  check_rc(dgi_topkp_threshold(logits.data_ptr(), logits.scalar_type() == at::kBFloat16, B, (int)logits.size(1),
+                               (int)logits.stride(0), temperature.data_ptr<float>(),
+                               reinterpret_cast<const long long*>(top_k.data_ptr<int64_t>()),
+                               top_p.data_ptr<float>(), thresh.data_ptr<float>(), cur_stream()),
+           "topkp_threshold");
 }
 
 void topk(at::Tensor out_v, at::Tensor out_i, const at::Tensor& logits, int64_t k) {
@@ -307,7 +333,10 @@ TORCH_LIBRARY(dgi, m) {
         "Tensor? tree_mask, int tree_n) -> ()");
   m.def("silu_mul(Tensor(a!) out, Tensor gu) -> ()");
   m.def("skinny_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor? bias, int cfg=0) -> ()");
-  m.def("sample(Tensor(a!) out, Tensor logits, Tensor? temperature, Tensor? seeds, int step) -> ()");
+  m.def("sample(Tensor(a!) out, Tensor logits, Tensor? temperature, Tensor? seeds, int step, "
+        "Tensor? thresh=None) -> ()");
+  m.def("topkp_threshold(Tensor(a!) thresh, Tensor logits, Tensor temperature, Tensor top_k, "
+        "Tensor top_p) -> ()");
   m.def("topk(Tensor(a!) out_v, Tensor(b!) out_i, Tensor logits, int k) -> ()");
   m.def("kv_gather(Tensor(a!) buf, Tensor cache, Tensor ids) -> ()");
   m.def("kv_scatter(Tensor(a!) cache, Tensor ids, Tensor buf) -> ()");
@@ -327,6 +356,7 @@ TORCH_LIBRARY_IMPL(dgi, CUDA, m) {
   m.impl("skinny_gemm", &skinny_gemm);
   m.impl("sample", &sample);
   m.impl("topk", &topk);
+  m.impl("topkp_threshold", &topkp_threshold);
   m.impl("kv_gather", &kv_gather);
   m.impl("kv_scatter", &kv_scatter);
   m.impl("kv_copy", &kv_copy);

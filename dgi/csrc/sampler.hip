@@ -70,7 +70,8 @@ template <typename T>
 __global__ __launch_bounds__(1024) void sample_kernel(const T* __restrict__ logits, int V, int stride,
                                                       const float* __restrict__ temperature,
                                                       const long long* __restrict__ seeds,
-                                                      long long step, long long* __restrict__ out) {
+                                                      long long step, const float* __restrict__ thresh,
+                                                      long long* __restrict__ out) {
   const int row = blockIdx.x;
   const T* lp = logits + (size_t)row * stride;
   const float temp = temperature ? temperature[row] : 0.f;
@@ -84,7 +85,9 @@ __global__ __launch_bounds__(1024) void sample_kernel(const T* __restrict__ logi
       if (v > best || (v == best && i < best_i)) { best = v; best_i = i; }
     });
   } else {
+    const float th = thresh ? thresh[row] : -INFINITY;
     scan_row<T>(lp, V, stride, [&](float v, int i) {
+      if (v < th) return;  // outside the top-k / top-p set
       const uint32_t h = hash32(seed ^ hash32((uint32_t)i + 0x9e3779b9u));
       const float u = ((h >> 8) + 0.5f) * (1.0f / 16777216.0f);
       v = v * inv_t - __logf(-__logf(u));
@@ -156,16 +159,145 @@ __global__ __launch_bounds__(256) void topk_kernel(const T* __restrict__ logits,
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// top-k / top-p (nucleus) cut as one logit threshold per row.
+//
+// With u > t "strictly greater", an element v is kept iff
+//   #{u > v} < top_k   and   sum_{u > v} exp((u - max) / T) <= top_p * Z
+// (HF order: temperature, then top-k, then top-p).  Both sides are monotone in
+// v, so the kept set is {v >= v*}.  v* is bracketed by a 16-way interval search
+// over [min, max]: every pass streams the row once and evaluates the count and
+// mass above 16 candidate cuts in registers (no sort, no atomics, no
+// materialised softmax), so a 128k-vocab row costs NPASS + 2 L2-resident scans.
+// The sampler then skips v < thresh.  Ties at the cut are all kept; when the
+// final interval still holds several distinct values (fp32 logits closer than
+// range / 16^NPASS) the cut keeps all of them — a superset by construction.
+constexpr int NCUT = 16;
+constexpr int NPASS = 6;
+
+template <int N>
+__device__ __forceinline__ void block_sum(float (&v)[N], float* red /* [16][N] */) {
+#pragma unroll
+  for (int j = 0; j < N; ++j)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v[j] += __shfl_xor(v[j], o, 64);
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int j = 0; j < N; ++j) red[w * N + j] = v[j];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    float a = 0.f;
+    for (int k = 0; k < nw; ++k) a += red[k * N + j];
+    v[j] = a;
+  }
+}
+
+__device__ __forceinline__ float block_minmax(float v, bool is_max, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float u = __shfl_xor(v, o, 64);
+    v = is_max ? fmaxf(v, u) : fminf(v, u);
+  }
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  float a = red[0];
+  for (int k = 1; k < nw; ++k) a = is_max ? fmaxf(a, red[k]) : fminf(a, red[k]);
+  return a;
+}
+
+template <typename T>
+__global__ __launch_bounds__(1024) void topkp_thresh_kernel(const T* __restrict__ logits, int V, int stride,
+                                                            const float* __restrict__ temperature,
+                                                            const long long* __restrict__ top_k,
+                                                            const float* __restrict__ top_p,
+                                                            float* __restrict__ thresh) {
+  __shared__ float red[16 * (2 * NCUT + 1)];
+  const int row = blockIdx.x;
+  const T* lp = logits + (size_t)row * stride;
+  const float temp = temperature ? temperature[row] : 1.f;
+  const long long kraw = top_k ? top_k[row] : 0;
+  const float p = top_p ? top_p[row] : 1.f;
+  const long long kk = (kraw <= 0 || kraw > V) ? (long long)V : kraw;
+  if (temp <= 1e-5f || (kk >= V && p >= 1.f)) {  // greedy or no filter
+    if (threadIdx.x == 0) thresh[row] = -INFINITY;
+    return;
+  }
+  const float sc = 1.4426950408889634f / temp;  // exp((u - max) / T) = exp2((u - max) * sc)
+
+  float vmax = -INFINITY, vmin = INFINITY;
+  scan_row<T>(lp, V, stride, [&](float v, int) {
+    if (v > -INFINITY && v < INFINITY) { vmax = fmaxf(vmax, v); vmin = fminf(vmin, v); }
+  });
+  vmax = block_minmax(vmax, true, red);
+  vmin = block_minmax(vmin, false, red);
+  if (!(vmax > vmin)) {  // constant (or empty) row: nothing to cut
+    if (threadIdx.x == 0) thresh[row] = -INFINITY;
+    return;
+  }
+  float lo = vmin, hi = vmax, pz = 0.f;
+  for (int pass = 0; pass < NPASS; ++pass) {
+    const float step = (hi - lo) * (1.f / NCUT);
+    float acc[2 * NCUT + 1];  // counts | masses | Z
+#pragma unroll
+    for (int j = 0; j < 2 * NCUT + 1; ++j) acc[j] = 0.f;
+    float z = 0.f;
+    scan_row<T>(lp, V, stride, [&](float v, int) {
+      if (pass == 0 && v > -INFINITY && v < INFINITY) z += exp2f((v - vmax) * sc);
+      if (!(v > lo)) return;  // never above any cut of this pass (and not -inf / NaN)
+      const float e = exp2f((fminf(v, vmax) - vmax) * sc);
+#pragma unroll
+      for (int j = 0; j < NCUT; ++j) {
+        const bool gt = v > lo + step * j;
+        acc[j] += gt ? 1.f : 0.f;
+        acc[NCUT + j] += gt ? e : 0.f;
+      }
+    });
+    acc[2 * NCUT] = z;
+    block_sum<2 * NCUT + 1>(acc, red);
+    if (pass == 0) {
+      pz = p * acc[2 * NCUT];
+      // cut 0 is vmin itself: if it passes, every finite element is kept
+      if (acc[0] < (float)kk && acc[NCUT] <= pz) {
+        if (threadIdx.x == 0) thresh[row] = -INFINITY;
+        return;
+      }
+    }
+    int jl = 0;  // largest failing cut (cut 0 == lo always fails)
+#pragma unroll
+    for (int j = 1; j < NCUT; ++j)
+      if (!(acc[j] < (float)kk && acc[NCUT + j] <= pz)) jl = j;
+    const float nlo = lo + step * jl;
+    hi = (jl == NCUT - 1) ? hi : lo + step * (jl + 1);
+    lo = nlo;
+    if (!(hi > lo)) break;
+  }
+  // v* = smallest element value in (lo, hi]
+  float vs = INFINITY;
+  scan_row<T>(lp, V, stride, [&](float v, int) {
+    if (v > lo && v <= hi) vs = fminf(vs, v);
+  });
+  vs = block_minmax(vs, false, red);
+  if (threadIdx.x == 0) thresh[row] = vs < INFINITY ? vs : hi;
+}
+
 }  // namespace
 
 extern "C" int dgi_sample(const void* logits, int is_bf16, int B, int V, int stride,
                           const float* temperature, const long long* seeds, long long step,
-                          long long* out, hipStream_t s) {
+                          const float* thresh, long long* out, hipStream_t s) {
   if (B == 0) return 0;
   if (is_bf16)
-    sample_kernel<uint16_t><<<B, 1024, 0, s>>>((const uint16_t*)logits, V, stride, temperature, seeds, step, out);
+    sample_kernel<uint16_t><<<B, 1024, 0, s>>>((const uint16_t*)logits, V, stride, temperature, seeds, step,
+                                               thresh, out);
   else
-    sample_kernel<float><<<B, 1024, 0, s>>>((const float*)logits, V, stride, temperature, seeds, step, out);
+    sample_kernel<float><<<B, 1024, 0, s>>>((const float*)logits, V, stride, temperature, seeds, step, thresh,
+                                            out);
   DGI_CHECK_LAUNCH();
   return 0;
 }
@@ -178,6 +310,21 @@ extern "C" int dgi_topk(const void* logits, int is_bf16, int B, int V, int strid
     topk_kernel<uint16_t><<<B, 256, 0, s>>>((const uint16_t*)logits, V, stride, K, out_v, out_i);
   else
     topk_kernel<float><<<B, 256, 0, s>>>((const float*)logits, V, stride, K, out_v, out_i);
+  DGI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dgi_topkp_threshold(const void* logits, int is_bf16, int B, int V, int stride,
+                                   const float* temperature, const long long* top_k, const float* top_p,
+                                   float* thresh, hipStream_t s) {
+  if (B == 0) return 0;
+  if (V < 1) return -2;
+  if (is_bf16)
+    topkp_thresh_kernel<uint16_t><<<B, 1024, 0, s>>>((const uint16_t*)logits, V, stride, temperature, top_k,
+                                                     top_p, thresh);
+  else
+    topkp_thresh_kernel<float><<<B, 1024, 0, s>>>((const float*)logits, V, stride, temperature, top_k, top_p,
+                                                  thresh);
   DGI_CHECK_LAUNCH();
   return 0;
 }

@@ -387,30 +387,67 @@ def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tens
 # Sampling
 # ----------------------------------------------------------------------------
 
-def apply_top_k_top_p(logits: torch.Tensor, top_k: torch.Tensor, top_p: torch.Tensor) -> torch.Tensor:
-    """Mask logits outside top-k / nucleus top-p (rows with k<=0 / p>=1 untouched)."""
+def topkp_threshold(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,
+                    top_p: torch.Tensor) -> torch.Tensor:
+    """Per-row logit cut for top-k / top-p: keep ``logits >= thresh`` (fp32 [B]).
+
+    HF order (temperature, then top-k, then nucleus): element v is kept iff
+    ``#{u > v} < top_k`` and ``sum_{u > v} softmax(u / T) <= top_p``.  Ties at the
+    cut are kept.  Rows that are greedy (T <= 1e-5) or unfiltered (top_k <= 0 and
+    top_p >= 1) get -inf.  Native path: one HIP kernel (sampler.hip, interval
+    search with register-resident counters; no sort)."""
+    B, V = logits.shape
+    if _native(logits):
+        th = torch.empty(B, dtype=torch.float32, device=logits.device)
+        torch.ops.dgi.topkp_threshold(th, logits, temperature.float().contiguous(), top_k.long().contiguous(),
+                                      top_p.float().contiguous())
+        return th
     lf = logits.float()
-    sorted_l, idx = lf.sort(dim=-1, descending=True)
-    V = lf.shape[-1]
-    ranks = torch.arange(V, device=lf.device)[None, :]
-    k = torch.where(top_k > 0, top_k, torch.full_like(top_k, V))
-    mask = ranks >= k[:, None]
-    probs = torch.softmax(sorted_l, dim=-1)
-    cum = probs.cumsum(-1) - probs
-    mask |= cum > top_p[:, None]
-    sorted_l = sorted_l.masked_fill(mask, float("-inf"))
-    return torch.empty_like(lf).scatter_(-1, idx, sorted_l)
+    s, _ = lf.sort(dim=-1, descending=True)
+    t = temperature.float().clamp(min=1e-5)[:, None]
+    fin = torch.isfinite(s)
+    e = torch.where(fin, torch.exp((s - s[:, :1]) / t), torch.zeros_like(s))
+    cum_excl = e.cumsum(-1) - e
+    asc = s.flip(-1).contiguous()
+    cnt_gt = V - torch.searchsorted(asc, s, right=True)              # #{u > v}
+    mass_gt = cum_excl.gather(-1, cnt_gt.clamp(max=V - 1))           # sum over u > v
+    k = torch.where(top_k > 0, top_k.long().clamp(max=V), torch.full_like(top_k.long(), V))
+    ok = (cnt_gt < k[:, None]) & (mass_gt <= top_p.float()[:, None] * e.sum(-1, keepdim=True)) & fin
+    last = ok.sum(-1) - 1                                            # kept prefix of the sorted row
+    th = s.gather(-1, last.clamp(min=0)[:, None]).squeeze(-1)
+    keep_all = ok.sum(-1) == fin.sum(-1)                             # every finite logit survives
+    off = (temperature <= 1e-5) | ((top_k <= 0) & (top_p >= 1.0)) | keep_all
+    return torch.where(off.to(th.device), torch.full_like(th, float("-inf")), th)
+
+
+def apply_top_k_top_p(logits: torch.Tensor, top_k: torch.Tensor, top_p: torch.Tensor,
+                      temperature: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Mask (to -inf) the logits outside the top-k / top-p set (see ``topkp_threshold``)."""
+    if temperature is None:
+        temperature = torch.ones(logits.shape[0], device=logits.device)
+    th = topkp_threshold(logits, temperature, top_k, top_p)
+    lf = logits.float()
+    return lf.masked_fill(lf < th[:, None], float("-inf"))
 
 
 def sample(logits: torch.Tensor, temperature: Optional[torch.Tensor] = None,
-           seeds: Optional[torch.Tensor] = None, step: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Greedy (temperature 0) or Gumbel-max sampling per row; returns int64 token ids."""
+           seeds: Optional[torch.Tensor] = None, step: int = 0, out: Optional[torch.Tensor] = None,
+           top_k: Optional[torch.Tensor] = None, top_p: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Greedy (temperature 0) or Gumbel-max sampling per row; returns int64 token ids.
+
+    With ``top_k`` / ``top_p`` the draw is restricted to ``topkp_threshold``'s set
+    (on GPU: a threshold kernel + the threshold-aware sampler, no sort and no
+    masked copy of the logits)."""
     B = logits.shape[0]
+    filt = top_k is not None and top_p is not None and temperature is not None
     if _native(logits):
         if out is None:
             out = torch.empty(B, dtype=torch.long, device=logits.device)
-        torch.ops.dgi.sample(out, logits, temperature, seeds, step)
+        th = topkp_threshold(logits, temperature, top_k, top_p) if filt else None
+        torch.ops.dgi.sample(out, logits, temperature, seeds, step, th)
         return out
+    if filt:
+        logits = apply_top_k_top_p(logits, top_k, top_p, temperature)
     lf = logits.float()
     if temperature is None or bool((temperature <= 1e-5).all()):
         r = lf.argmax(-1)

@@ -176,7 +176,7 @@ class ModelRunner:
 
     def sample_rows(self, logits, temps, seeds, filt=None):
         if filt is not None:
-            logits = ops.apply_top_k_top_p(logits, *filt)
+            return ops.sample(logits, temps, seeds, 0, top_k=filt[0], top_p=filt[1])
         return ops.sample(logits, temps, seeds, 0)
 
     def _sample(self, logits, reqs):
@@ -184,7 +184,7 @@ class ModelRunner:
         if any(r.params.needs_filter for r in reqs):
             tk = torch.tensor([r.params.top_k if not r.params.greedy else 0 for r in reqs], device=logits.device)
             tp = torch.tensor([r.params.top_p if not r.params.greedy else 1.0 for r in reqs], device=logits.device)
-            logits = ops.apply_top_k_top_p(logits, tk, tp)
+            return ops.sample(logits, temps, seeds, self.step_id, top_k=tk, top_p=tp)
         return ops.sample(logits, temps, seeds, self.step_id)
 
     @torch.inference_mode()

@@ -319,3 +319,46 @@ def test_mlp_row_padding_matches_unpadded():
     e.model.mlp_pad = lambda T: T + 40 if T >= 64 else T
     out = [r.output for r in e.generate(prompts, sp)]
     assert out == ref
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_topkp_threshold_kernel_matches_reference(dtype):
+    B, V = 24, 128256
+    g = torch.Generator(device="cpu").manual_seed(5)
+    logits = (torch.randn(B, V, generator=g) * 3).to(dtype)
+    logits[7, 1000:] = float("-inf")                       # masked vocab tail
+    logits[5] = 1.0                                        # constant row
+    temps = torch.tensor([0.0, 1.0, 0.7, 1.5] * 6)
+    ks = torch.tensor([0, 50, 1, 2000, 0, 50] * 4)
+    ps = torch.tensor([0.9, 1.0, 0.95, 0.5, 0.8, 0.999] * 4)
+    ref = ops.topkp_threshold(logits, temps, ks, ps)       # CPU reference (sort based)
+    lg = logits.to(DEV)
+    th = ops.topkp_threshold(lg, temps.to(DEV), ks.to(DEV), ps.to(DEV)).cpu()
+    kept_ref = (logits.float() >= ref[:, None]).sum(-1)
+    kept = (logits.float() >= th[:, None]).sum(-1)
+    for b in range(B):
+        # same set up to fp32 summation order at the nucleus boundary
+        assert abs(int(kept[b]) - int(kept_ref[b])) <= max(2, int(0.002 * int(kept_ref[b]))), \
+            (b, int(kept[b]), int(kept_ref[b]), float(th[b]), float(ref[b]))
+    # sampling stays inside the cut; unfiltered rows match the plain sampler
+    seeds = torch.arange(B, device=DEV)
+    out = ops.sample(lg, temps.to(DEV), seeds, 3, top_k=ks.to(DEV), top_p=ps.to(DEV))
+    picked = lg.float().gather(1, out[:, None]).squeeze(1).cpu()
+    assert bool((picked >= th).all())
+    off = torch.zeros(B, dtype=torch.long, device=DEV), torch.ones(B, device=DEV)
+    a = ops.sample(lg, temps.to(DEV), seeds, 3, top_k=off[0], top_p=off[1])
+    assert torch.equal(a, ops.sample(lg, temps.to(DEV), seeds, 3))
+
+
+def test_topkp_sampling_distribution():
+    V = 8
+    probs = torch.tensor([0.4, 0.3, 0.2, 0.05, 0.05, 0, 0, 0]) + 1e-9
+    logits = torch.log(probs)[None].repeat(8192, 1).to(DEV)
+    temps = torch.ones(8192, device=DEV)
+    seeds = torch.arange(8192, device=DEV)
+    ks = torch.full((8192,), 0, dtype=torch.long, device=DEV)
+    ps = torch.full((8192,), 0.6, device=DEV)               # nucleus = {0, 1} (0.4 <= 0.6 < 0.7)
+    out = ops.sample(logits, temps, seeds, 1, top_k=ks, top_p=ps).cpu()
+    freq = torch.bincount(out, minlength=V).float() / 8192
+    assert freq[2:].sum() == 0
+    assert abs(freq[0] - 4 / 7) < 0.03

@@ -1,5 +1,7 @@
 """CPU behaviour of dgi.ops: reference implementations (the GPU tests' oracles)
 and the dispatch rules that decide which native kernel a GPU call takes."""
+import math
+
 import torch
 import torch.nn.functional as F
 
@@ -50,3 +52,46 @@ def test_tree_mask_reference_marks_ancestors_and_depth():
     for n, s in want.items():
         row = int(anc[0, n])
         assert {i for i in range(5) if row >> i & 1} == s
+
+
+def _brute_threshold(row, T, k, p):
+    """Literal per-element definition of the top-k / top-p keep rule."""
+    vals = [float(v) for v in row]
+    z = sum(math.exp((v - max(vals)) / T) for v in vals)
+    kept = [v for v in vals
+            if sum(1 for u in vals if u > v) < k
+            and sum(math.exp((u - max(vals)) / T) for u in vals if u > v) <= p * z]
+    return min(kept) if len(kept) < len(vals) else float("-inf")
+
+
+def test_topkp_threshold_reference_matches_definition():
+    g = torch.Generator().manual_seed(0)
+    logits = torch.randn(6, 40, generator=g) * 2
+    logits[3, :10] = logits[3, 10]        # ties straddling the cut
+    temps = torch.tensor([1.0, 0.7, 1.3, 1.0, 0.5, 2.0])
+    ks = torch.tensor([5, 0, 12, 3, 40, 0])
+    ps = torch.tensor([1.0, 0.9, 0.5, 0.8, 0.95, 1.0])
+    th = ops.topkp_threshold(logits, temps, ks, ps)
+    for b in range(6):
+        k = int(ks[b]) if int(ks[b]) > 0 else 10 ** 9
+        want = _brute_threshold(logits[b].tolist(), float(temps[b]), k, float(ps[b]))
+        if b == 5:
+            want = float("-inf")                # top_k off and top_p = 1: no filter
+        assert float(th[b]) == want, (b, float(th[b]), want)
+    # top_k alone keeps exactly k distinct values; masking and greedy rows
+    masked = ops.apply_top_k_top_p(logits, ks, ps, temps)
+    assert int(torch.isfinite(masked[0]).sum()) == 5
+    th0 = ops.topkp_threshold(logits, torch.zeros(6), ks, ps)
+    assert torch.isinf(th0).all()
+
+
+def test_sample_with_filter_stays_inside_the_kept_set():
+    g = torch.Generator().manual_seed(1)
+    logits = torch.randn(16, 300, generator=g)
+    temps = torch.full((16,), 0.8)
+    ks = torch.full((16,), 7)
+    ps = torch.full((16,), 0.9)
+    th = ops.topkp_threshold(logits, temps, ks, ps)
+    out = ops.sample(logits, temps, torch.arange(16), 2, top_k=ks, top_p=ps)
+    picked = logits.gather(1, out[:, None]).squeeze(1)
+    assert bool((picked >= th).all())
