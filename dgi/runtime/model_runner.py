@@ -191,7 +191,7 @@ class ModelRunner:
     def execute(self, sb: ScheduledBatch) -> StepResult:
         self.step_id += 1
         if self.graphs is not None and not sb.prefill and sb.decode and \
-                len(sb.decode) <= self.graphs.max_bucket and not any(r.params.needs_filter for r in sb.decode):
+                len(sb.decode) <= self.graphs.max_bucket:
             toks = self.graphs.run(sb)
             return StepResult(toks, list(sb.decode))
         flat, hdr, sampled = self.build_host(sb)
@@ -230,6 +230,10 @@ class GraphRunner:
         self.ctx = torch.ones(maxb, dtype=torch.int32, device=dev)
         self.temps = torch.zeros(maxb, dtype=torch.float32, device=dev)
         self.seeds = torch.zeros(maxb, dtype=torch.long, device=dev)
+        # top-k / top-p ride in the graph too (threshold kernel; rows with
+        # k = 0, p = 1 exit after one store), so filtered requests stay captured
+        self.topk = torch.zeros(maxb, dtype=torch.long, device=dev)
+        self.topp = torch.ones(maxb, dtype=torch.float32, device=dev)
         self.step = torch.zeros(1, dtype=torch.long, device=dev)
         self.out = torch.zeros(maxb, dtype=torch.long, device=dev)
         self.host_in = torch.zeros(maxb * (4 + maxw), dtype=torch.int32).pin_memory()
@@ -245,7 +249,8 @@ class GraphRunner:
 
     def _body(self, b):
         logits = self.r.model.forward(self._meta(b), input_ids=self.ids[:b])
-        ops.sample(logits, self.temps[:b], self.seeds[:b], 0, out=self.out[:b])
+        ops.sample(logits, self.temps[:b], self.seeds[:b], 0, out=self.out[:b],
+                   top_k=self.topk[:b], top_p=self.topp[:b])
 
     @torch.inference_mode()
     def capture(self):
@@ -286,7 +291,12 @@ class GraphRunner:
         bt[:] = 0
         temps = np.zeros(b, np.float32)
         seeds = np.zeros(b, np.int64)
+        topk = np.zeros(b, np.int64)
+        topp = np.ones(b, np.float32)
         for i, rq in enumerate(sb.decode):
+            if rq.params.needs_filter:
+                topk[i] = max(0, rq.params.top_k)
+                topp[i] = rq.params.top_p
             p = rq.num_computed
             ids[i] = rq.output[-1]
             pos[i] = p
@@ -303,6 +313,8 @@ class GraphRunner:
         self.bt[:b].copy_(dev[4 * b:].view(b, maxw))
         self.temps[:b].copy_(torch.from_numpy(temps).pin_memory(), non_blocking=True)
         self.seeds[:b].copy_(torch.from_numpy(seeds).pin_memory(), non_blocking=True)
+        self.topk[:b].copy_(torch.from_numpy(topk).pin_memory(), non_blocking=True)
+        self.topp[:b].copy_(torch.from_numpy(topp).pin_memory(), non_blocking=True)
         self.graphs[b].replay()
         self.host_out[:b].copy_(self.out[:b], non_blocking=True)
         torch.cuda.current_stream().synchronize()

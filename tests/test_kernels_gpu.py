@@ -362,3 +362,23 @@ def test_topkp_sampling_distribution():
     freq = torch.bincount(out, minlength=V).float() / 8192
     assert freq[2:].sum() == 0
     assert abs(freq[0] - 4 / 7) < 0.03
+
+
+def test_graph_decode_with_top_k_one_matches_greedy():
+    """Filtered requests run inside the captured decode graph: temperature 1 with
+    top_k = 1 collapses to the argmax (up to bf16 ties at the max)."""
+    from dgi.engine import EngineConfig, LLMEngine
+    from dgi.models.config import get_config
+    from dgi.models.llama import LlamaModel
+    from dgi.sched.request import SamplingParams
+    mc = get_config("llama-tiny-hd128")
+    gm = LlamaModel(mc, "cuda", seed=11)
+    e = LLMEngine(EngineConfig(model="llama-tiny-hd128", device="cuda", num_blocks=256, max_num_seqs=8,
+                               max_model_len=512, max_num_batched_tokens=256, use_graphs=True),
+                  model_cfg=mc, model=gm)
+    prompts = [[1] + list(range(5, 5 + n)) for n in (6, 33, 90, 12)]
+    greedy = [r.output for r in e.generate(prompts, SamplingParams(max_tokens=10, temperature=0.0, ignore_eos=True))]
+    topk1 = [r.output for r in e.generate(prompts, SamplingParams(max_tokens=10, temperature=1.0, top_k=1,
+                                                                  top_p=1.0, ignore_eos=True))]
+    assert sum(a == b for a, b in zip(greedy, topk1)) >= 3, (greedy, topk1)
+    assert e.runner.graphs is not None and e.runner.graphs.captured
