@@ -169,7 +169,8 @@ __global__ __launch_bounds__(256) void topk_kernel(const T* __restrict__ logits,
 // v, so the kept set is {v >= v*}.  v* is bracketed by a 16-way interval search
 // over [min, max]: every pass streams the row once and evaluates the count and
 // mass above 16 candidate cuts in registers (no sort, no atomics, no
-// materialised softmax), so a 128k-vocab row costs NPASS + 2 L2-resident scans.
+// materialised softmax), so a 128k-vocab row costs at most NPASS + 2 L2-resident scans (bf16 rows
+// usually stop after 3 passes, once the interval is narrower than one bf16 ulp).
 // The sampler then skips v < thresh.  Ties at the cut are all kept; when the
 // final interval still holds several distinct values (fp32 logits closer than
 // range / 16^NPASS) the cut keeps all of them — a superset by construction.
@@ -229,6 +230,7 @@ __global__ __launch_bounds__(1024) void topkp_thresh_kernel(const T* __restrict_
     return;
   }
   const float sc = 1.4426950408889634f / temp;  // exp((u - max) / T) = exp2((u - max) * sc)
+  constexpr float kRel = sizeof(T) == 2 ? 1.f / 512.f : 1.f / 33554432.f;
 
   float vmax = -INFINITY, vmin = INFINITY;
   scan_row<T>(lp, V, stride, [&](float v, int) {
@@ -275,7 +277,9 @@ __global__ __launch_bounds__(1024) void topkp_thresh_kernel(const T* __restrict_
     const float nlo = lo + step * jl;
     hi = (jl == NCUT - 1) ? hi : lo + step * (jl + 1);
     lo = nlo;
-    if (!(hi > lo)) break;
+    // stop once (lo, hi] can hold at most one representable value of T
+    // (bf16: 8-bit mantissa, spacing >= |x| 2^-8 > width; fp32 rarely gets here)
+    if (!(hi > lo) || (hi - lo) < fminf(fabsf(lo), fabsf(hi)) * kRel) break;
   }
   // v* = smallest element value in (lo, hi]
   float vs = INFINITY;
