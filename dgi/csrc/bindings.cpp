@@ -205,16 +205,19 @@ void sample(at::Tensor out, const at::Tensor& logits, const c10::optional<at::Te
   const float* tp = nullptr;
   const long long* sp = nullptr;
   if (temperature.has_value() && temperature->defined()) {
-    TORCH_CHECK(temperature->scalar_type() == at::kFloat && temperature->numel() >= B);
+    TORCH_CHECK(temperature->scalar_type() == at::kFloat && temperature->numel() >= B &&
+                temperature->is_contiguous() && temperature->device() == logits.device());
     tp = temperature->data_ptr<float>();
   }
   if (seeds.has_value() && seeds->defined()) {
-    TORCH_CHECK(seeds->scalar_type() == at::kLong && seeds->numel() >= B);
+    TORCH_CHECK(seeds->scalar_type() == at::kLong && seeds->numel() >= B && seeds->is_contiguous() &&
+                seeds->device() == logits.device());
     sp = reinterpret_cast<const long long*>(seeds->data_ptr<int64_t>());
   }
   const float* thp = nullptr;
   if (thresh.has_value() && thresh->defined()) {
-    TORCH_CHECK(thresh->scalar_type() == at::kFloat && thresh->numel() >= B && thresh->is_contiguous());
+    TORCH_CHECK(thresh->scalar_type() == at::kFloat && thresh->numel() >= B && thresh->is_contiguous() &&
+                thresh->device() == logits.device());
     thp = thresh->data_ptr<float>();
   }
   check_rc(dgi_sample(logits.data_ptr(), logits.scalar_type() == at::kBFloat16, B,

@@ -5,8 +5,9 @@
 // reference samples inside HF generate / vLLM SamplingParams
 // (worker/engines/llm.py:62-69, worker/engines/llm_vllm.py:144-151) and
 // argmax/multinomial in speculative.py:444-449.
-// top-k / top-p filtering, when requested, is applied to the logits before
-// this kernel (rows with top_k/top_p disabled skip that pass entirely).
+// top-k / top-p filtering, when requested, is a per-row logit threshold
+// computed by topkp_thresh_kernel below; sample_kernel skips every element
+// under it (rows with top_k/top_p disabled get -inf and skip nothing).
 //
 // Also: per-row top-k (k <= 16) candidate extraction used by the EAGLE draft
 // tree builder (K13): each workgroup keeps a wave-level sorted list.
@@ -164,9 +165,11 @@ __global__ __launch_bounds__(256) void topk_kernel(const T* __restrict__ logits,
 // top-k / top-p (nucleus) cut as one logit threshold per row.
 //
 // With u > t "strictly greater", an element v is kept iff
-//   #{u > v} < top_k   and   sum_{u > v} exp((u - max) / T) <= top_p * Z
-// (HF order: temperature, then top-k, then top-p).  Both sides are monotone in
-// v, so the kept set is {v >= v*}.  v* is bracketed by a 16-way interval search
+//   #{u > v} < top_k   and   sum_{u > v} exp((u - max) / T) <= top_p * Z_k
+// (HF / vLLM order: temperature, then top-k, then top-p over the top-k
+// survivors renormalised: Z_k is the mass of {v : #{u > v} < top_k}, found by a
+// count-only search first).  Both sides are monotone in v, so the kept set is
+// {v >= v*}.  v* is bracketed by a 16-way interval search
 // over [min, max]: every pass streams the row once and evaluates the count and
 // mass above 16 candidate cuts in registers (no sort, no atomics, no
 // materialised softmax), so a 128k-vocab row costs at most NPASS + 2 L2-resident scans (bf16 rows
@@ -242,6 +245,42 @@ __global__ __launch_bounds__(1024) void topkp_thresh_kernel(const T* __restrict_
     if (threadIdx.x == 0) thresh[row] = -INFINITY;
     return;
   }
+  // ---- top-k cut (count-only interval search): the nucleus is renormalised over it
+  float kcut = -INFINITY;
+  if (kk < V) {
+    float lo = vmin, hi = vmax;
+    bool keep_all = false;
+    for (int pass = 0; pass < NPASS; ++pass) {
+      const float step = (hi - lo) * (1.f / NCUT);
+      float cnt[NCUT];
+#pragma unroll
+      for (int j = 0; j < NCUT; ++j) cnt[j] = 0.f;
+      scan_row<T>(lp, V, stride, [&](float v, int) {
+        if (!(v > lo)) return;
+#pragma unroll
+        for (int j = 0; j < NCUT; ++j) cnt[j] += v > lo + step * j ? 1.f : 0.f;
+      });
+      block_sum<NCUT>(cnt, red);
+      if (pass == 0 && cnt[0] < (float)kk) { keep_all = true; break; }   // top-k keeps every element
+      int jl = 0;
+#pragma unroll
+      for (int j = 1; j < NCUT; ++j)
+        if (!(cnt[j] < (float)kk)) jl = j;
+      const float nlo = lo + step * jl;
+      hi = (jl == NCUT - 1) ? hi : lo + step * (jl + 1);
+      lo = nlo;
+      if (!(hi > lo) || (hi - lo) < fminf(fabsf(lo), fabsf(hi)) * kRel) break;
+    }
+    if (!keep_all) {
+      float vk = INFINITY;
+      scan_row<T>(lp, V, stride, [&](float v, int) {
+        if (v > lo && v <= hi) vk = fminf(vk, v);
+      });
+      vk = block_minmax(vk, false, red);
+      kcut = vk < INFINITY ? vk : hi;
+    }
+  }
+
   float lo = vmin, hi = vmax, pz = 0.f;
   for (int pass = 0; pass < NPASS; ++pass) {
     const float step = (hi - lo) * (1.f / NCUT);
@@ -250,7 +289,7 @@ __global__ __launch_bounds__(1024) void topkp_thresh_kernel(const T* __restrict_
     for (int j = 0; j < 2 * NCUT + 1; ++j) acc[j] = 0.f;
     float z = 0.f;
     scan_row<T>(lp, V, stride, [&](float v, int) {
-      if (pass == 0 && v > -INFINITY && v < INFINITY) z += exp2f((v - vmax) * sc);
+      if (pass == 0 && v >= kcut && v < INFINITY) z += exp2f((v - vmax) * sc);   // Z_k
       if (!(v > lo)) return;  // never above any cut of this pass (and not -inf / NaN)
       const float e = exp2f((fminf(v, vmax) - vmax) * sc);
 #pragma unroll

@@ -391,11 +391,13 @@ def topkp_threshold(logits: torch.Tensor, temperature: torch.Tensor, top_k: torc
                     top_p: torch.Tensor) -> torch.Tensor:
     """Per-row logit cut for top-k / top-p: keep ``logits >= thresh`` (fp32 [B]).
 
-    HF order (temperature, then top-k, then nucleus): element v is kept iff
-    ``#{u > v} < top_k`` and ``sum_{u > v} softmax(u / T) <= top_p``.  Ties at the
-    cut are kept.  Rows that are greedy (T <= 1e-5) or unfiltered (top_k <= 0 and
-    top_p >= 1) get -inf.  Native path: one HIP kernel (sampler.hip, interval
-    search with register-resident counters; no sort)."""
+    HF / vLLM order (temperature, then top-k, then nucleus over the top-k
+    survivors, renormalised): element v is kept iff ``#{u > v} < top_k`` and
+    ``sum_{u > v} exp(u / T) <= top_p * Z_k`` where ``Z_k`` is the softmax mass of
+    the top-k set.  Ties at the cut are kept.  Rows that are greedy (T <= 1e-5)
+    or unfiltered (top_k <= 0 and top_p >= 1) get -inf.  Native path: one HIP
+    kernel (sampler.hip, interval searches with register-resident counters; no
+    sort)."""
     B, V = logits.shape
     if _native(logits):
         th = torch.empty(B, dtype=torch.float32, device=logits.device)
@@ -412,7 +414,9 @@ def topkp_threshold(logits: torch.Tensor, temperature: torch.Tensor, top_k: torc
     cnt_gt = V - torch.searchsorted(asc, s, right=True)              # #{u > v}
     mass_gt = cum_excl.gather(-1, cnt_gt.clamp(max=V - 1))           # sum over u > v
     k = torch.where(top_k > 0, top_k.long().clamp(max=V), torch.full_like(top_k.long(), V))
-    ok = (cnt_gt < k[:, None]) & (mass_gt <= top_p.float()[:, None] * e.sum(-1, keepdim=True)) & fin
+    in_k = (cnt_gt < k[:, None]) & fin
+    z_k = torch.where(in_k, e, torch.zeros_like(e)).sum(-1, keepdim=True)   # mass of the top-k survivors
+    ok = in_k & (mass_gt <= top_p.float()[:, None] * z_k)
     last = ok.sum(-1) - 1                                            # kept prefix of the sorted row
     th = s.gather(-1, last.clamp(min=0)[:, None]).squeeze(-1)
     keep_all = ok.sum(-1) == fin.sum(-1)                             # every finite logit survives

@@ -128,7 +128,7 @@ class PipelineEngine(LLMEngine):
         self.runner.step_id += 1
         flat, hdr, sampled = self.runner.build_host(sb)
         dev = self.runner.to_device(flat)
-        ids, meta, _temps, _seeds = self.runner.meta_from_device(dev, hdr)
+        ids, meta, _samp = self.runner.meta_from_device(dev, hdr)
         with torch.inference_mode():
             hidden = self.model.forward(meta, input_ids=ids)
         self.f.send(_hdr_tensor(hdr, KIND_FWD, self.f.device), self.next_rank)
@@ -292,7 +292,7 @@ class StageWorker:
             T = hdr[ModelRunner.H_T]
             hidden = torch.empty(T, H, dtype=self.pool.dtype, device=dev)
             f.recv(hidden, self.prev)
-            _ids, meta, temps, seeds = self.runner.meta_from_device(flat, hdr)
+            _ids, meta, samp = self.runner.meta_from_device(flat, hdr)
             with phase("stage_forward", rows=T):
                 out = self.model.forward(meta, hidden=hidden)
             self.steps += 1
@@ -301,7 +301,7 @@ class StageWorker:
                 toks = torch.zeros(self.mb_cap + 1, dtype=torch.long)
                 toks[0] = nlog
                 if nlog:
-                    toks[1: 1 + nlog] = ops.sample(out, temps, seeds, 0).cpu()
+                    toks[1: 1 + nlog] = samp.sample(out).cpu()
                 f.ctrl_send_tensor(toks, self.driver)
             else:
                 f.send(hb, self.next)

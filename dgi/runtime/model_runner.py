@@ -25,6 +25,18 @@ DEFAULT_BUCKETS = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256, 
 
 
 @dataclasses.dataclass
+class SamplingMeta:
+    """Per-row sampling parameters of one step, as device views of the step buffer."""
+    temps: torch.Tensor
+    seeds: torch.Tensor
+    top_k: Optional[torch.Tensor] = None     # None: no row of this step is filtered
+    top_p: Optional[torch.Tensor] = None
+
+    def sample(self, logits: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        return ops.sample(logits, self.temps, self.seeds, 0, out=out, top_k=self.top_k, top_p=self.top_p)
+
+
+@dataclasses.dataclass
 class StepResult:
     tokens: list          # sampled token per logits row (decode rows first, then sampled chunks)
     rows: list            # Request per sampled row
@@ -64,7 +76,7 @@ class ModelRunner:
     # ------------------------------------------------------------------ metadata
     # header layout (int64): the host-side shape of one step, shipped along
     # the pipeline so every stage rebuilds the same AttnMeta
-    H_LEN, H_T, H_NDP, H_NPRE, H_NB, H_MAXW, H_SPLITS, H_PART, H_NTILES, H_NLOG, H_STEP = range(1, 12)
+    H_LEN, H_T, H_NDP, H_NPRE, H_NB, H_MAXW, H_SPLITS, H_PART, H_NTILES, H_NLOG, H_STEP, H_FILT = range(1, 13)
     HEADER_SIZE = 16
 
     def build_host(self, sb: ScheduledBatch, pad_decode_to: int = 0):
@@ -120,8 +132,13 @@ class ModelRunner:
         lidx = np.asarray(logit_rows, np.int32)
         temps = np.asarray([r.params.temperature for r in sampled], np.float32).view(np.int32)
         seeds = np.asarray([(r.seed * 1000003 + self.step_id) & 0x7FFFFFFF for r in sampled], np.int32)
+        # top-k / top-p ride in the same flat buffer (one H2D copy; pipeline stages get them too)
+        filt = any(r.params.needs_filter for r in sampled)
+        topk = np.asarray([max(0, r.params.top_k) if r.params.needs_filter else 0 for r in sampled], np.int32)
+        topp = np.asarray([r.params.top_p if r.params.needs_filter else 1.0 for r in sampled],
+                          np.float32).view(np.int32)
         parts = [ids, pos, slots, dec_bt.ravel(), dec_ctx, pre_bt.ravel(), cu, pctx, tiles_np.ravel(), lidx,
-                 temps, seeds]
+                 temps, seeds, topk, topp]
         flat = np.concatenate(parts)
         max_ctx = int(dec_ctx.max()) if ndp else 1
         if self.is_cuda and ndp:
@@ -130,29 +147,33 @@ class ModelRunner:
             splits, part = 1, 1 << 20
         hdr = np.zeros(self.HEADER_SIZE, np.int64)
         hdr[[self.H_LEN, self.H_T, self.H_NDP, self.H_NPRE, self.H_NB, self.H_MAXW, self.H_SPLITS, self.H_PART,
-             self.H_NTILES, self.H_NLOG, self.H_STEP]] = [flat.size, T, ndp, npre, nb, maxw, splits, part,
-                                                          len(tiles), nlog, self.step_id]
+             self.H_NTILES, self.H_NLOG, self.H_STEP, self.H_FILT]] = [flat.size, T, ndp, npre, nb, maxw, splits,
+                                                                      part, len(tiles), nlog, self.step_id, int(filt)]
         return flat, hdr, sampled
 
     def meta_from_device(self, dev: torch.Tensor, hdr):
-        """Views of the device copy of ``flat`` -> (input ids, AttnMeta, temps, seeds)."""
+        """Views of the device copy of ``flat`` -> (input ids, AttnMeta, SamplingMeta)."""
         h = [int(x) for x in hdr]
         T, ndp, npre, nb, maxw = h[self.H_T], h[self.H_NDP], h[self.H_NPRE], h[self.H_NB], h[self.H_MAXW]
         ntiles, nlog = h[self.H_NTILES], h[self.H_NLOG]
-        sizes = [T, T, T, ndp * maxw, ndp, nb * maxw, nb + 1, nb, ntiles * 2, nlog, nlog, nlog]
+        sizes = [T, T, T, ndp * maxw, ndp, nb * maxw, nb + 1, nb, ntiles * 2, nlog, nlog, nlog, nlog, nlog]
         views = []
         o = 0
         for sz in sizes:
             views.append(dev[o: o + sz])
             o += sz
-        d_ids, d_pos, d_slots, d_dbt, d_dctx, d_pbt, d_cu, d_pctx, d_tiles, d_lidx, d_temps, d_seeds = views
+        (d_ids, d_pos, d_slots, d_dbt, d_dctx, d_pbt, d_cu, d_pctx, d_tiles, d_lidx, d_temps, d_seeds,
+         d_topk, d_topp) = views
         meta = AttnMeta(
             positions=d_pos, slot_mapping=d_slots, num_decode=ndp,
             dec_block_tables=d_dbt.view(ndp, maxw), dec_context_lens=d_dctx,
             dec_max_splits=h[self.H_SPLITS], dec_part_size=h[self.H_PART], dec_workspace=self.dec_ws,
             num_prefill_tokens=npre, pre_block_tables=d_pbt.view(nb, maxw), pre_cu_seqlens=d_cu,
             pre_context_lens=d_pctx, pre_tiles=d_tiles.view(-1, 2), logits_indices=d_lidx)
-        return d_ids, meta, d_temps.view(torch.float32), d_seeds.long()
+        samp = SamplingMeta(d_temps.view(torch.float32), d_seeds.long(),
+                            d_topk.long() if h[self.H_FILT] else None,
+                            d_topp.view(torch.float32) if h[self.H_FILT] else None)
+        return d_ids, meta, samp
 
     def to_device(self, flat: np.ndarray) -> torch.Tensor:
         host = torch.from_numpy(flat)
@@ -162,31 +183,10 @@ class ModelRunner:
 
     def build(self, sb: ScheduledBatch, pad_decode_to: int = 0):
         flat, hdr, sampled = self.build_host(sb, pad_decode_to)
-        ids, meta, _t, _s = self.meta_from_device(self.to_device(flat), hdr)
+        ids, meta, _samp = self.meta_from_device(self.to_device(flat), hdr)
         return ids, meta, sampled
 
     # ------------------------------------------------------------------ run
-    def sampling_tensors(self, reqs):
-        temps = torch.tensor([r.params.temperature for r in reqs], dtype=torch.float32)
-        seeds = torch.tensor([r.seed for r in reqs], dtype=torch.long)
-        if self.is_cuda:
-            temps = temps.pin_memory().to(self.device, non_blocking=True)
-            seeds = seeds.pin_memory().to(self.device, non_blocking=True)
-        return temps, seeds
-
-    def sample_rows(self, logits, temps, seeds, filt=None):
-        if filt is not None:
-            return ops.sample(logits, temps, seeds, 0, top_k=filt[0], top_p=filt[1])
-        return ops.sample(logits, temps, seeds, 0)
-
-    def _sample(self, logits, reqs):
-        temps, seeds = self.sampling_tensors(reqs)
-        if any(r.params.needs_filter for r in reqs):
-            tk = torch.tensor([r.params.top_k if not r.params.greedy else 0 for r in reqs], device=logits.device)
-            tp = torch.tensor([r.params.top_p if not r.params.greedy else 1.0 for r in reqs], device=logits.device)
-            return ops.sample(logits, temps, seeds, self.step_id, top_k=tk, top_p=tp)
-        return ops.sample(logits, temps, seeds, self.step_id)
-
     @torch.inference_mode()
     def execute(self, sb: ScheduledBatch) -> StepResult:
         self.step_id += 1
@@ -195,20 +195,11 @@ class ModelRunner:
             toks = self.graphs.run(sb)
             return StepResult(toks, list(sb.decode))
         flat, hdr, sampled = self.build_host(sb)
-        ids, meta, temps, seeds = self.meta_from_device(self.to_device(flat), hdr)
+        ids, meta, samp = self.meta_from_device(self.to_device(flat), hdr)
         logits = self.model.forward(meta, input_ids=ids)
         if not sampled:
             return StepResult([], [])
-        filt = None
-        if any(r.params.needs_filter for r in sampled):
-            filt = self.filter_tensors(sampled)
-        toks = self.sample_rows(logits, temps, seeds, filt)
-        return StepResult(toks.tolist(), sampled)
-
-    def filter_tensors(self, reqs):
-        tk = torch.tensor([r.params.top_k if not r.params.greedy else 0 for r in reqs], device=self.device)
-        tp = torch.tensor([r.params.top_p if not r.params.greedy else 1.0 for r in reqs], device=self.device)
-        return tk, tp
+        return StepResult(samp.sample(logits).tolist(), sampled)
 
 
 class GraphRunner:
@@ -236,7 +227,10 @@ class GraphRunner:
         self.topp = torch.ones(maxb, dtype=torch.float32, device=dev)
         self.step = torch.zeros(1, dtype=torch.long, device=dev)
         self.out = torch.zeros(maxb, dtype=torch.long, device=dev)
-        self.host_in = torch.zeros(maxb * (4 + maxw), dtype=torch.int32).pin_memory()
+        # one pinned staging buffer, one H2D copy per replay:
+        # ids | pos | slots | ctx | temps | seeds | topk | topp | block tables
+        self.NSEG = 8
+        self.host_in = torch.zeros(maxb * (self.NSEG + maxw), dtype=torch.int32).pin_memory()
         self.host_out = torch.zeros(maxb, dtype=torch.long).pin_memory()
         self.captured = False
 
@@ -278,21 +272,17 @@ class GraphRunner:
         r = self.r
         bs = r.bs
         maxw = r.max_blocks
+        S = self.NSEG
         h = self.host_in.numpy()
-        ids = h[:b]
-        pos = h[b: 2 * b]
-        slots = h[2 * b: 3 * b]
-        ctx = h[3 * b: 4 * b]
-        bt = h[4 * b: 4 * b + b * maxw].reshape(b, maxw)
-        ids[:] = 0
-        pos[:] = 0
-        slots[:] = 0
+        seg = h[: S * b].reshape(S, b)
+        ids, pos, slots, ctx = seg[0], seg[1], seg[2], seg[3]
+        temps, seeds, topk = seg[4].view(np.float32), seg[5], seg[6]
+        topp = seg[7].view(np.float32)
+        bt = h[S * b: S * b + b * maxw].reshape(b, maxw)
+        seg[:] = 0
         ctx[:] = 1
+        topp[:] = 1.0
         bt[:] = 0
-        temps = np.zeros(b, np.float32)
-        seeds = np.zeros(b, np.int64)
-        topk = np.zeros(b, np.int64)
-        topp = np.ones(b, np.float32)
         for i, rq in enumerate(sb.decode):
             if rq.params.needs_filter:
                 topk[i] = max(0, rq.params.top_k)
@@ -304,17 +294,18 @@ class GraphRunner:
             ctx[i] = p + 1
             bt[i, : len(rq.blocks)] = rq.blocks
             temps[i] = rq.params.temperature
-            seeds[i] = (rq.seed * 1000003 + r.step_id) & 0x7FFFFFFFFFFF
-        dev = self.host_in[: 4 * b + b * maxw].to(r.device, non_blocking=True)
-        self.ids[:b].copy_(dev[:b])
-        self.pos[:b].copy_(dev[b:2 * b])
-        self.slots[:b].copy_(dev[2 * b:3 * b])
-        self.ctx[:b].copy_(dev[3 * b:4 * b])
-        self.bt[:b].copy_(dev[4 * b:].view(b, maxw))
-        self.temps[:b].copy_(torch.from_numpy(temps).pin_memory(), non_blocking=True)
-        self.seeds[:b].copy_(torch.from_numpy(seeds).pin_memory(), non_blocking=True)
-        self.topk[:b].copy_(torch.from_numpy(topk).pin_memory(), non_blocking=True)
-        self.topp[:b].copy_(torch.from_numpy(topp).pin_memory(), non_blocking=True)
+            seeds[i] = (rq.seed * 1000003 + r.step_id) & 0x7FFFFFFF
+        dev = self.host_in[: S * b + b * maxw].to(r.device, non_blocking=True)
+        dseg = dev[: S * b].view(S, b)
+        self.ids[:b].copy_(dseg[0])
+        self.pos[:b].copy_(dseg[1])
+        self.slots[:b].copy_(dseg[2])
+        self.ctx[:b].copy_(dseg[3])
+        self.temps[:b].copy_(dseg[4].view(torch.float32))
+        self.seeds[:b].copy_(dseg[5])
+        self.topk[:b].copy_(dseg[6])
+        self.topp[:b].copy_(dseg[7].view(torch.float32))
+        self.bt[:b].copy_(dev[S * b:].view(b, maxw))
         self.graphs[b].replay()
         self.host_out[:b].copy_(self.out[:b], non_blocking=True)
         torch.cuda.current_stream().synchronize()

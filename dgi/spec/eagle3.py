@@ -533,7 +533,7 @@ class SpecEngine(LLMEngine):
         run = self.runner
         run.step_id += 1
         flat, hdr, sampled = run.build_host(sb)
-        ids, meta, temps, seeds = run.meta_from_device(run.to_device(flat), hdr)
+        ids, meta, samp = run.meta_from_device(run.to_device(flat), hdr)
         logits, feats = self._forward_capture(meta, ids)
         nd = len(sb.decode)
         row = nd
@@ -543,9 +543,7 @@ class SpecEngine(LLMEngine):
             row += c.length
         if not sampled:
             return self._apply(sb, [], [])
-        filt = run.filter_tensors(sampled) if any(r.params.needs_filter for r in sampled) else None
-        toks = run.sample_rows(logits, temps, seeds, filt).tolist()
-        return self._apply(sb, sampled, toks)
+        return self._apply(sb, sampled, samp.sample(logits).tolist())
 
     @torch.inference_mode()
     def _spec_step(self, reqs: list) -> list:

@@ -57,10 +57,10 @@ def test_tree_mask_reference_marks_ancestors_and_depth():
 def _brute_threshold(row, T, k, p):
     """Literal per-element definition of the top-k / top-p keep rule."""
     vals = [float(v) for v in row]
-    z = sum(math.exp((v - max(vals)) / T) for v in vals)
-    kept = [v for v in vals
-            if sum(1 for u in vals if u > v) < k
-            and sum(math.exp((u - max(vals)) / T) for u in vals if u > v) <= p * z]
+    in_k = [v for v in vals if sum(1 for u in vals if u > v) < k]
+    z_k = sum(math.exp((v - max(vals)) / T) for v in in_k)      # nucleus mass renormalised over top-k
+    kept = [v for v in in_k
+            if sum(math.exp((u - max(vals)) / T) for u in vals if u > v) <= p * z_k]
     return min(kept) if len(kept) < len(vals) else float("-inf")
 
 
@@ -95,3 +95,28 @@ def test_sample_with_filter_stays_inside_the_kept_set():
     out = ops.sample(logits, temps, torch.arange(16), 2, top_k=ks, top_p=ps)
     picked = logits.gather(1, out[:, None]).squeeze(1)
     assert bool((picked >= th).all())
+
+
+def test_topkp_matches_hf_topk_then_topp_warpers():
+    """Literal HF order: TopKLogitsWarper, then TopPLogitsWarper on the masked
+    (renormalised) scores.  The flat row is where renormalising matters: top-50
+    of 100 near-equal logits hold ~half the mass, so a full-vocab nucleus rule
+    would keep all 50 while HF keeps ~45."""
+    from transformers.generation.logits_process import TopKLogitsWarper, TopPLogitsWarper
+
+    g = torch.Generator().manual_seed(3)
+    logits = torch.randn(5, 100, generator=g) * 1.5
+    logits[0] = torch.linspace(0.0, 0.01, 100)          # flat row
+    temps = torch.tensor([1.0, 0.8, 1.0, 1.2, 0.6])
+    ks = torch.tensor([50, 50, 10, 0, 20])
+    ps = torch.tensor([0.9, 0.9, 0.5, 0.7, 0.99])
+    masked = ops.apply_top_k_top_p(logits, ks, ps, temps)
+    for b in range(5):
+        sc = (logits[b: b + 1] / temps[b]).double()
+        if int(ks[b]) > 0:
+            sc = TopKLogitsWarper(int(ks[b]))(None, sc)
+        sc = TopPLogitsWarper(float(ps[b]))(None, sc)
+        want = torch.isfinite(sc[0])
+        got = torch.isfinite(masked[b])
+        assert torch.equal(got, want), (b, int(got.sum()), int(want.sum()))
+    assert int(torch.isfinite(masked[0]).sum()) < 50
