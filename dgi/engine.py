@@ -41,6 +41,7 @@ class EngineConfig:
     layer_end: Optional[int] = None
     host_kv_gb: float = 0.0            # pinned host KV tier for evicted prefix pages (0 = off)
     graph_buckets: Optional[tuple] = None   # decode batch sizes captured as hipGraphs (None = defaults)
+    model_path: Optional[str] = None   # HF safetensors checkpoint dir (None: ``model`` if it is one, else random init)
 
 
 @dataclasses.dataclass
@@ -82,11 +83,15 @@ class LLMEngine:
             if self.device.index is None:
                 self.device = torch.device("cuda", torch.cuda.current_device())
             torch.cuda.set_device(self.device)
-        self.model_cfg = model_cfg or get_config(cfg.model)
+        self.checkpoint = None
+        if model is None:
+            from dgi.models.weights import resolve_checkpoint
+            self.checkpoint = resolve_checkpoint(cfg.model, cfg.model_path)
+        self.model_cfg = model_cfg or get_config(self.checkpoint or cfg.model)
         self.model_cfg.max_position = max(self.model_cfg.max_position, cfg.max_model_len)
         t0 = time.perf_counter()
         self.model = model or LlamaModel(self.model_cfg, self.device, cfg.dtype, cfg.layer_start, cfg.layer_end,
-                                         seed=cfg.seed)
+                                         seed=cfg.seed, checkpoint=self.checkpoint)
         if self.device.type == "cuda":
             torch.cuda.synchronize()
         self.load_seconds = time.perf_counter() - t0

@@ -50,7 +50,8 @@ class LlamaModel:
 
     def __init__(self, cfg: ModelConfig, device: torch.device | str = "cpu", dtype=torch.bfloat16,
                  layer_start: int = 0, layer_end: Optional[int] = None, has_embed: Optional[bool] = None,
-                 has_head: Optional[bool] = None, seed: int = 0, init: str = "random"):
+                 has_head: Optional[bool] = None, seed: int = 0, init: str = "random",
+                 checkpoint: Optional[str] = None):
         self.cfg = cfg
         self.device = torch.device(device)
         self.dtype = dtype
@@ -72,7 +73,13 @@ class LlamaModel:
         # MLP row padding (dgi.runtime.gemm_pad): T -> rows to run gate_up/down on
         self.mlp_pad = None
         self._pad_buf: Optional[torch.Tensor] = None
-        if init == "random":
+        self.load_info: Optional[dict] = None
+        if checkpoint:
+            # real weights: only this rank's layers / TP slices are read (dgi.models.weights)
+            from dgi.models.weights import load_checkpoint
+            self._init_empty()
+            self.load_info = load_checkpoint(self, checkpoint, getattr(self, "tp_rank", 0), getattr(self, "tp", 1))
+        elif init == "random":
             self._init_random(seed)
         elif init == "empty":
             self._init_empty()

@@ -434,6 +434,30 @@ def apply_top_k_top_p(logits: torch.Tensor, top_k: torch.Tensor, top_p: torch.Te
     return lf.masked_fill(lf < th[:, None], float("-inf"))
 
 
+_M32 = 0xFFFFFFFF
+
+
+def _hash32(x: torch.Tensor) -> torch.Tensor:
+    """sampler.hip ``hash32`` on int64 tensors holding uint32 values (products
+    wrap mod 2^64, so the low 32 bits are exact)."""
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & _M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & _M32
+    return x ^ (x >> 16)
+
+
+def gumbel_uniform(seeds: Optional[torch.Tensor], step: int, V: int, B: int) -> torch.Tensor:
+    """The per-(row, vocab id) uniforms the HIP sampler draws: a counter-based
+    hash of (row seed, step, token id), so a row's draw depends on its own seed
+    only (never on the batch it shares) and CPU and GPU pick the same tokens."""
+    sd = seeds.long().cpu() if seeds is not None else torch.zeros(B, dtype=torch.long)
+    row = ((sd * 2654435761) & _M32) ^ ((step * 40503) & _M32)
+    ids = _hash32((torch.arange(V, dtype=torch.long) + 0x9E3779B9) & _M32)
+    h = _hash32(row[:, None] ^ ids[None, :])
+    return ((h >> 8).float() + 0.5) * (1.0 / 16777216.0)
+
+
 def sample(logits: torch.Tensor, temperature: Optional[torch.Tensor] = None,
            seeds: Optional[torch.Tensor] = None, step: int = 0, out: Optional[torch.Tensor] = None,
            top_k: Optional[torch.Tensor] = None, top_p: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -456,11 +480,8 @@ def sample(logits: torch.Tensor, temperature: Optional[torch.Tensor] = None,
     if temperature is None or bool((temperature <= 1e-5).all()):
         r = lf.argmax(-1)
     else:
-        g = torch.Generator(device="cpu")
-        g.manual_seed(int(seeds[0]) * 1000003 + step if seeds is not None else step)
-        u = torch.rand(lf.shape, generator=g).clamp_(1e-10, 1.0)
         t = temperature.float().clamp(min=1e-5)
-        noisy = lf / t[:, None] - torch.log(-torch.log(u))
+        noisy = lf / t[:, None] - torch.log(-torch.log(gumbel_uniform(seeds, step, lf.shape[1], B)))
         r = torch.where(temperature <= 1e-5, lf.argmax(-1), noisy.argmax(-1))
     if out is not None:
         out.copy_(r)

@@ -96,11 +96,15 @@ class PipelineEngine(LLMEngine):
         self.f = fabric
         self.ranks = list(stage_ranks)
         assert self.ranks[0] == fabric.rank
-        mc = model_cfg or get_config(cfg.model)
+        from dgi.models.weights import resolve_checkpoint
+        ckpt = resolve_checkpoint(cfg.model, cfg.model_path)
+        mc = model_cfg or get_config(ckpt or cfg.model)
+        mc.max_position = max(mc.max_position, cfg.max_model_len)
         self.split = split or stage_split(mc, len(self.ranks))
         a, b = self.split[0]
         device = fabric.device
-        model = LlamaModel(mc, device, cfg.dtype, a, b, has_embed=True, has_head=len(self.ranks) == 1, seed=cfg.seed)
+        model = LlamaModel(mc, device, cfg.dtype, a, b, has_embed=True, has_head=len(self.ranks) == 1, seed=cfg.seed,
+                           checkpoint=ckpt)
         nb = stage_block_budget(mc, device, b - a, cfg)
         nb = agree_num_blocks(fabric, self.ranks, nb)
         pcfg = EngineConfig(**{**cfg.__dict__, "device": str(device), "layer_start": a, "layer_end": b,
@@ -234,7 +238,9 @@ class StageWorker:
         self.ranks = list(stage_ranks)
         self.idx = self.ranks.index(fabric.rank)
         assert self.idx > 0
-        mc = model_cfg or get_config(cfg.model)
+        from dgi.models.weights import resolve_checkpoint
+        ckpt = resolve_checkpoint(cfg.model, cfg.model_path)
+        mc = model_cfg or get_config(ckpt or cfg.model)
         mc.max_position = max(mc.max_position, cfg.max_model_len)
         self.mc = mc
         self.split = split or stage_split(mc, len(self.ranks))
@@ -244,7 +250,8 @@ class StageWorker:
         self.next = None if self.is_last else self.ranks[self.idx + 1]
         self.driver = self.ranks[0]
         dev = fabric.device
-        self.model = LlamaModel(mc, dev, cfg.dtype, a, b, has_embed=False, has_head=self.is_last, seed=cfg.seed)
+        self.model = LlamaModel(mc, dev, cfg.dtype, a, b, has_embed=False, has_head=self.is_last, seed=cfg.seed,
+                                checkpoint=ckpt)
         nb = stage_block_budget(mc, dev, b - a, cfg)
         nb = agree_num_blocks(fabric, self.ranks, nb)
         self.pool = BlockPool(nb, cfg.block_size, b - a, mc.num_kv_heads, mc.head_dim, cfg.dtype, dev)

@@ -44,11 +44,12 @@ class TPLlamaModel(LlamaModel):
     """Rank ``tp_rank`` of a ``tp``-way tensor-parallel Llama (weights bit-identical
     to the slices of the TP=1 random init)."""
 
-    def __init__(self, cfg: ModelConfig, device, dtype, tp_rank: int, tp: int, group=None, seed: int = 0):
+    def __init__(self, cfg: ModelConfig, device, dtype, tp_rank: int, tp: int, group=None, seed: int = 0,
+                 checkpoint: Optional[str] = None):
         self.full_cfg = cfg
         self.tp_rank, self.tp = tp_rank, tp
         self.group = group
-        super().__init__(tp_local_config(cfg, tp), device, dtype, seed=seed)
+        super().__init__(tp_local_config(cfg, tp), device, dtype, seed=seed, checkpoint=checkpoint)
         self.reduce = self._all_reduce if tp > 1 else None
 
     def _all_reduce(self, h: torch.Tensor) -> None:
@@ -98,12 +99,14 @@ class TPEngine(LLMEngine):
     """SPMD engine: one per TP rank, all fed the same requests in the same order."""
 
     def __init__(self, cfg: EngineConfig, tp_rank: int, tp: int, group=None, model_cfg: Optional[ModelConfig] = None):
-        full = model_cfg or get_config(cfg.model)
+        from dgi.models.weights import resolve_checkpoint
+        ckpt = resolve_checkpoint(cfg.model, cfg.model_path)
+        full = model_cfg or get_config(ckpt or cfg.model)
         full.max_position = max(full.max_position, cfg.max_model_len)
         dev = torch.device(cfg.device)
         if dev.type == "cuda" and dev.index is None:
             dev = torch.device("cuda", torch.cuda.current_device())
-        model = TPLlamaModel(full, dev, cfg.dtype, tp_rank, tp, group, seed=cfg.seed)
+        model = TPLlamaModel(full, dev, cfg.dtype, tp_rank, tp, group, seed=cfg.seed, checkpoint=ckpt)
         cfg = dataclasses.replace(cfg, device=str(dev))
         if tp > 1:
             # every rank must hold the same page count (block ids are shared): agree on the minimum

@@ -131,7 +131,7 @@ class ModelRunner:
         nlog = len(logit_rows)
         lidx = np.asarray(logit_rows, np.int32)
         temps = np.asarray([r.params.temperature for r in sampled], np.float32).view(np.int32)
-        seeds = np.asarray([(r.seed * 1000003 + self.step_id) & 0x7FFFFFFF for r in sampled], np.int32)
+        seeds = np.asarray([r.sample_seed() for r in sampled], np.int32)
         # top-k / top-p ride in the same flat buffer (one H2D copy; pipeline stages get them too)
         filt = any(r.params.needs_filter for r in sampled)
         topk = np.asarray([max(0, r.params.top_k) if r.params.needs_filter else 0 for r in sampled], np.int32)
@@ -294,7 +294,7 @@ class GraphRunner:
             ctx[i] = p + 1
             bt[i, : len(rq.blocks)] = rq.blocks
             temps[i] = rq.params.temperature
-            seeds[i] = (rq.seed * 1000003 + r.step_id) & 0x7FFFFFFF
+            seeds[i] = rq.sample_seed()
         dev = self.host_in[: S * b + b * maxw].to(r.device, non_blocking=True)
         dseg = dev[: S * b].view(S, b)
         self.ids[:b].copy_(dseg[0])

@@ -71,6 +71,13 @@ class Request:
     def all_tokens(self) -> list[int]:
         return self.prompt + self.output
 
+    def sample_seed(self) -> int:
+        """Seed of the next sampled token: a function of the request alone (its seed
+        and how many tokens it has produced), so a seeded request draws the same
+        tokens whatever the batching, the engine's step count or the parallel
+        layout (single GPU, pipeline, P/D, graph or eager)."""
+        return (self.seed * 1000003 + len(self.output)) & 0x7FFFFFFF
+
     @property
     def in_prefill(self) -> bool:
         return self.num_computed < self.prefill_target

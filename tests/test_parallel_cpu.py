@@ -26,13 +26,36 @@ def _free_port():
     return p
 
 
-def _reference_outputs(max_tokens=6):
-    from dgi.engine import EngineConfig, LLMEngine
+def _sp(i, max_tokens=6):
+    """Greedy by default; DGI_TEST_SAMPLED=1: seeded temperature + top-k + top-p
+    sampling (the draw is a function of the request's seed and position only,
+    so every layout must reproduce the single-process tokens exactly)."""
     from dgi.sched.request import SamplingParams
-    e = LLMEngine(EngineConfig(model=MODEL, device="cpu", num_blocks=128, max_num_seqs=8, max_model_len=256,
-                               max_num_batched_tokens=64, enable_prefix_caching=False))
-    return [r.output for r in e.generate(PROMPTS, SamplingParams(max_tokens=max_tokens, temperature=0.0,
-                                                                   ignore_eos=True))]
+    if os.environ.get("DGI_TEST_SAMPLED") == "1":
+        return SamplingParams(max_tokens=max_tokens, temperature=0.9, top_k=12, top_p=0.85, seed=4242 + i,
+                              ignore_eos=True)
+    return SamplingParams(max_tokens=max_tokens, temperature=0.0, ignore_eos=True)
+
+
+def _engine_cfg(model=None, **kw):
+    from dgi.engine import EngineConfig
+    ckpt = os.environ.get("DGI_TEST_CKPT") or None
+    base = dict(model=model or os.environ.get("DGI_TEST_MODEL", MODEL), model_path=ckpt, device="cpu",
+                num_blocks=128, max_num_seqs=8, max_model_len=256, max_num_batched_tokens=64,
+                enable_prefix_caching=False)
+    if ckpt:
+        base["dtype"] = torch.float32
+    base.update(kw)
+    return EngineConfig(**base)
+
+
+def _reference_outputs(max_tokens=6, model=None):
+    from dgi.engine import LLMEngine
+    e = LLMEngine(_engine_cfg(model))
+    reqs = [e.add_request(p, _sp(i, max_tokens)) for i, p in enumerate(PROMPTS)]
+    while e.has_unfinished():
+        e.step()
+    return [r.output for r in reqs]
 
 
 def _worker(rank, world, port, fn_name, q):
@@ -80,12 +103,11 @@ def _pp_body(rank, world):
     from dgi.parallel.pipeline import PipelineEngine, StageWorker
     from dgi.sched.request import SamplingParams
     f = Fabric()
-    cfg = EngineConfig(model=MODEL, device="cpu", num_blocks=128, max_num_seqs=8, max_model_len=256,
-                       max_num_batched_tokens=64, enable_prefix_caching=False)
+    cfg = _engine_cfg()
     ranks = list(range(world))
     if rank == 0:
         eng = PipelineEngine(cfg, f, ranks)
-        reqs = [eng.add_request(p, SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)) for p in PROMPTS]
+        reqs = [eng.add_request(p, _sp(i)) for i, p in enumerate(PROMPTS)]
         while eng.has_unfinished():
             eng.step()
         eng.stop_stages()
@@ -103,19 +125,16 @@ def _pd_body(rank, world):
     from dgi.parallel.plan import NodeLayout
     from dgi.sched.request import SamplingParams
     f = Fabric()
-    model = os.environ.get("DGI_TEST_MODEL", MODEL)
-    cfg = EngineConfig(model=model, device="cpu", num_blocks=128, max_num_seqs=8, max_model_len=256,
-                       max_num_batched_tokens=64, enable_prefix_caching=False)
+    cfg = _engine_cfg()
     # DGI_TEST_PREFILL prefill ranks, the rest a decode pipeline (1 stage = plain P/D)
     npre = int(os.environ.get("DGI_TEST_PREFILL", "1"))
     layout = NodeLayout("pd" if world - npre == 1 else "pdpp", list(range(npre)), list(range(npre, world)))
-    sp = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
     if rank in layout.prefill_ranks:
         srv = PrefillServer(cfg, f, layout)
         nlocal = int(os.environ.get("DGI_TEST_LOCAL", "0"))
         for i, p in enumerate(PROMPTS[:len(PROMPTS) - nlocal]):
             if i % npre == rank:
-                srv.submit(p, sp)
+                srv.submit(p, _sp(i))
         while srv.busy():
             srv.step()
         srv.finish()
@@ -123,8 +142,9 @@ def _pd_body(rank, world):
     if rank == layout.decode_ranks[0]:
         nlocal = int(os.environ.get("DGI_TEST_LOCAL", "0"))
         drv = DecodeDriver(cfg, f, layout, local_fraction=0.3 if nlocal else 0.0)
-        for p in PROMPTS[len(PROMPTS) - nlocal:]:          # served end to end on the decode side
-            assert drv.admit_local(p, sp) is not None
+        for i, p in enumerate(PROMPTS):
+            if i >= len(PROMPTS) - nlocal:                  # served end to end on the decode side
+                assert drv.admit_local(p, _sp(i)) is not None
         done = {}
         while len(done) < len(PROMPTS):
             for o in drv.step():
@@ -267,13 +287,13 @@ def test_pd_multi_prefill_and_three_stage_decode(npre, world, monkeypatch):
 
 
 def _tp_body(rank, world):
-    from dgi.engine import EngineConfig, LLMEngine
+    from dgi.engine import LLMEngine
     from dgi.parallel.tensor import TPEngine
     from dgi.sched.request import SamplingParams
-    cfg = EngineConfig(model="llama-tiny-tp", device="cpu", max_num_seqs=4, max_num_batched_tokens=128,
-                       max_model_len=256, use_graphs=False)
+    cfg = _engine_cfg("llama-tiny-tp", num_blocks=None, max_num_seqs=4, max_num_batched_tokens=128,
+                      use_graphs=False, enable_prefix_caching=True)
     g = torch.Generator().manual_seed(0)
-    prompts = [torch.randint(5, 1000, (n,), generator=g).tolist() for n in (9, 17, 30)]
+    prompts = [torch.randint(5, 500, (n,), generator=g).tolist() for n in (9, 17, 30)]
     sp = SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True)
     out = [r.output for r in TPEngine(cfg, rank, world).generate(prompts, sp)]
     if rank == 0:
@@ -283,6 +303,55 @@ def _tp_body(rank, world):
 
 
 def test_tensor_parallel_matches_single_process():
+    _spawn("_tp_body", 2)
+
+
+# ---------------------------------------------------------------------------- sampled requests / real weights
+def test_pipeline_sampled_top_k_top_p_matches_single_process(monkeypatch):
+    """temperature > 0 with top-k / top-p through a 2-stage pipeline: the last
+    stage applies each row's filters and draws with the row's own seed."""
+    monkeypatch.setenv("DGI_TEST_SAMPLED", "1")
+    ref = _reference_outputs()
+    assert ref != _greedy_reference()          # sampling actually changes the tokens
+    out = _spawn("_pp_body", 2)
+    assert out[0] == ref
+
+
+def test_pdpp_sampled_top_k_top_p_matches_single_process(monkeypatch):
+    monkeypatch.setenv("DGI_TEST_SAMPLED", "1")
+    monkeypatch.setenv("DGI_TEST_MODEL", "llama-tiny-hd128")
+    monkeypatch.setenv("DGI_TEST_PREFILL", "1")
+    ref = _reference_outputs(model="llama-tiny-hd128")
+    out = _spawn("_pd_body", 3)
+    assert out[1] == ref
+
+
+def _greedy_reference():
+    old = os.environ.pop("DGI_TEST_SAMPLED", None)
+    try:
+        return _reference_outputs()
+    finally:
+        if old is not None:
+            os.environ["DGI_TEST_SAMPLED"] = old
+
+
+@pytest.fixture
+def tiny_ckpt(tmp_path_factory):
+    from test_weights import save_tiny
+    d = str(tmp_path_factory.mktemp("ckpt"))
+    save_tiny("llama", d)
+    return d
+
+
+def test_pipeline_stages_load_disjoint_layers_from_checkpoint(tiny_ckpt, monkeypatch):
+    monkeypatch.setenv("DGI_TEST_CKPT", tiny_ckpt)
+    ref = _reference_outputs()
+    out = _spawn("_pp_body", 2)
+    assert out[0] == ref
+
+
+def test_tensor_parallel_loads_row_and_column_slices_from_checkpoint(tiny_ckpt, monkeypatch):
+    monkeypatch.setenv("DGI_TEST_CKPT", tiny_ckpt)
     _spawn("_tp_body", 2)
 
 

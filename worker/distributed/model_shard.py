@@ -70,16 +70,20 @@ class ModelShard(nn.Module):
     @classmethod
     def from_native(cls, model_id: str, start_layer: int, end_layer: int, device: str = "cuda",
                     dtype: torch.dtype = torch.bfloat16, seed: int = 0, num_blocks: int = 1024,
-                    block_size: int = 16) -> "ModelShard":
+                    block_size: int = 16, model_path: Optional[str] = None) -> "ModelShard":
+        """Native shard of layers [start, end): reads only those layers from a local
+        safetensors checkpoint when one exists (dgi.models.weights), else random init."""
         from dgi.kv.block_pool import BlockPool
         from dgi.models.config import get_config
         from dgi.models.llama import LlamaModel
-        mc = get_config(model_id)
+        from dgi.models.weights import resolve_checkpoint
+        ckpt = resolve_checkpoint(model_id, model_path)
+        mc = get_config(ckpt or model_id)
         shard = cls(model_id, start_layer, end_layer, device, dtype)
         shard.config = mc
         shard.is_first_shard = start_layer == 0
         shard.is_last_shard = end_layer == mc.num_layers
-        shard.native = LlamaModel(mc, device, dtype, start_layer, end_layer, seed=seed)
+        shard.native = LlamaModel(mc, device, dtype, start_layer, end_layer, seed=seed, checkpoint=ckpt)
         pool = BlockPool(num_blocks, block_size, max(1, end_layer - start_layer), mc.num_kv_heads, mc.head_dim,
                          dtype, device)
         shard.native.kv_cache = pool.kv

@@ -73,13 +73,27 @@ class NativeLLMEngine(LLMBaseEngine):
         from dgi.engine import EngineConfig, LLMEngine
         from dgi.models.config import get_config
 
+        from dgi.models.config import PRESETS
+        from dgi.models.weights import resolve_checkpoint
+
         c = _merged(self.config)
         model_id = c.get("model_id", "llama3-8b")
         device = c.get("device", "cuda" if torch.cuda.is_available() else "cpu")
-        mc = get_config(model_id)
+        # real weights when a local checkpoint exists (explicit model_path, a directory
+        # model_id, or an offline HF cache snapshot); random init only for the built-in
+        # benchmark presets or when explicitly allowed — never silently for a hub id
+        ckpt = resolve_checkpoint(model_id, c.get("model_path"))
+        if ckpt is None and model_id not in PRESETS and not c.get("allow_random_weights", False):
+            raise FileNotFoundError(
+                f"no local safetensors checkpoint for {model_id!r}: set engines.llm.model_path, or "
+                "allow_random_weights: true to serve random-init weights of that architecture")
+        if ckpt is None and model_id not in PRESETS:
+            logger.warning("serving RANDOM-INIT weights for %s (allow_random_weights)", model_id)
+        self.weights = ckpt or "random-init"
+        mc = get_config(ckpt or model_id)
         frac = c.get("mem_fraction_static", c.get("gpu_memory_utilization", c.get("kv_fraction", 0.9)))
         ecfg = EngineConfig(
-            model=model_id, device=device,
+            model=model_id, device=device, model_path=ckpt,
             max_num_seqs=int(c.get("max_running_requests", c.get("max_num_seqs", 256))),
             max_num_batched_tokens=int(c.get("chunked_prefill_size", c.get("max_num_batched_tokens", 8192))),
             max_model_len=int(c.get("context_length", c.get("max_model_len", 8192))),
@@ -102,7 +116,7 @@ class NativeLLMEngine(LLMBaseEngine):
                 self.engine.draft.load(load_file(sc["draft_path"], device=str(self.engine.device)))
         else:
             self.engine = LLMEngine(ecfg, model_cfg=mc)
-        self.tokenizer = load_tokenizer(c.get("tokenizer", model_id), vocab_size=mc.vocab_size,
+        self.tokenizer = load_tokenizer(c.get("tokenizer", ckpt or model_id), vocab_size=mc.vocab_size,
                                         bos=mc.bos_token_id, eos=mc.eos_token_id)
         self.device = device
         if c.get("warmup", False):
@@ -248,7 +262,8 @@ class NativeLLMEngine(LLMBaseEngine):
                          "streaming", "prefix_caching", "hipgraph_decode", "speculative_decoding"]
         if self.engine is not None:
             s["engine"] = {**self.engine.stats, **self.engine.scheduler.stats(),
-                           "model": self.engine.model_cfg.name, "num_blocks": self.engine.pool.num_blocks}
+                           "model": self.engine.model_cfg.name, "num_blocks": self.engine.pool.num_blocks,
+                           "weights": getattr(self, "weights", "random-init")}
         s["stats"] = dict(self.stats)
         return s
 
