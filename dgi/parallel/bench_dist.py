@@ -36,11 +36,17 @@ def _prompt(rng, n, vocab):
 def run_distributed(args, layout_kind: str, dist):
     f = Fabric()
     rank, world = f.rank, f.world
-    layout = plan_node_layout(world, layout_kind, getattr(args, "prefill_ranks", None) or None)
+    layout = plan_node_layout(world, layout_kind, getattr(args, "prefill_ranks", None) or None,
+                              decode_stages=getattr(args, "decode_stages", None) or None,
+                              decode_replicas=getattr(args, "decode_replicas", None) or None, model=args.model)
+    # every RCCL pair communicator up front (one tiny send/recv per pair, deadlock-free order)
+    t_pairs = f.connect_pairs(layout.p2p_pairs()) if layout.kind != "pp" else \
+        f.connect_pairs([(a, b) for a, b in zip(range(world), range(1, world))])
     # decode-side concurrency: one microbatch of 768 rows per decode stage keeps the
     # decode GEMMs out of the small-M regime (70B down-proj: 0.76 PF/s at M=512,
     # 1.28 at 1024); a single decode GPU is capped by its KV pool (credits) instead
-    conc = args.concurrency or (768 * len(layout.decode_ranks) if len(layout.decode_ranks) > 1 else 1024)
+    k = len(layout.decode_groups[0]) if layout.decode_groups else 1
+    conc = args.concurrency or (768 * k if k > 1 else 1024)
     # staged rehearsal: every rank shares one GPU, so each takes a slice of its memory
     kv_frac = float(os.environ.get("DGI_KV_FRACTION", 0.5 / world if f.staged else 0.9))
     cfg = EngineConfig(model=args.model, device=str(f.device), max_num_seqs=conc,
@@ -71,10 +77,21 @@ def run_distributed(args, layout_kind: str, dist):
     total = int(sum(x[0].item() for x in tl))
     el = max(x[1].item() for x in tl)
     all_ttfts = [v for o in obj for v in o["ttfts"]]
-    per_rank = [{k: v for k, v in o.items() if k != "ttfts"} for o in obj]
-    return total, el, all_ttfts, {"layout": {"kind": layout.kind, "prefill": layout.prefill_ranks,
-                                             "decode": layout.decode_ranks}, "concurrency": conc,
-                                  "ranks": per_rank}
+    all_tpots = [v for o in obj for v in o.get("tpots", [])]
+    per_rank = [{k: v for k, v in o.items() if k not in ("ttfts", "tpots")} for o in obj]
+    roles = {}
+    for o in per_rank:
+        r = roles.setdefault(o["role"], {"ranks": 0, "tokens": 0})
+        r["ranks"] += 1
+        r["tokens"] += int(o.get("tokens", 0))
+    for r in roles.values():
+        r["tok_s"] = round(r["tokens"] / el, 1) if el > 0 else 0.0
+    mig = [o["migration_ms_p50"] for o in per_rank if o.get("migration_ms_p50") is not None]
+    return total, el, all_ttfts, {"layout": {"kind": layout.kind, "describe": layout.describe(),
+                                             "prefill": layout.prefill_ranks, "decode_groups": layout.decode_groups},
+                                  "concurrency": conc, "pair_setup_s": round(t_pairs, 3), "roles": roles,
+                                  "migration_ms_p50": round(float(sorted(mig)[len(mig) // 2]), 3) if mig else None,
+                                  "tpots": all_tpots, "ranks": per_rank}
 
 
 # ---------------------------------------------------------------------------- layer pipeline only
@@ -139,26 +156,41 @@ def _run_pp(args, f, cfg, layout, role, sp, rng, conc):
     return 0, el, [], {"stage_steps": w.steps}
 
 
-# ---------------------------------------------------------------------------- P/D (+ decode pipeline)
+# ---------------------------------------------------------------------------- P/D (+ decode pipelines)
+
+def _tpots(reqs) -> list:
+    """Mean inter-token time (s) of each finished request with >= 2 tokens."""
+    out = []
+    for r in reqs:
+        tt = r.token_times
+        if len(tt) >= 2:
+            out.append((tt[-1] - tt[0]) / (len(tt) - 1))
+    return out
+
 
 def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
+    """P prefill ranks + R decode replicas.  The first replica's driver is the
+    clock: its productive steps are the benchmark steps, and it broadcasts the
+    phase boundaries (end of warm-up, end of the timed window) to every
+    prefill rank and every other replica driver."""
     from dgi.parallel.fabric import CtrlChannel
     from dgi.parallel.pd import DecodeDriver, PrefillServer
     from dgi.parallel.pipeline import StageWorker
+    from dgi.parallel.plan import decode_local_fraction, prefill_overflow_cap
 
+    clock = layout.drivers[0]
     if role == "prefill":
-        from dgi.parallel.plan import prefill_overflow_cap
         lc = getattr(args, "prefill_local_cap", -1)
-        lc = prefill_overflow_cap(layout) if lc < 0 else lc
+        lc = prefill_overflow_cap(layout, model=args.model) if lc < 0 else lc
         pcfg = EngineConfig(**{**cfg.__dict__, "max_num_seqs": 64 + lc})
         srv = PrefillServer(pcfg, f, layout, local_cap=lc)
-        phase = CtrlChannel(f, layout.decode_ranks[0], 4, tag="phase")
+        ph = CtrlChannel(f, clock, 4, tag="phase")
         vocab = srv.engine.model_cfg.vocab_size
         depth = max(2, args.max_batched_tokens // max(1, args.prompt_len))
 
         def serve_until_phase():
             n, ttfts = 0, []
-            while phase.poll() is None:
+            while ph.poll() is None:
                 while len(srv.pending) + len(srv.engine.scheduler.waiting) < depth:
                     srv.submit(_prompt(rng, args.prompt_len, vocab), sp)
                 before = len(srv.ttfts)
@@ -174,28 +206,37 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
         f.barrier()
         el = time.perf_counter() - t0
         srv.finish()
-        return n, el, ttfts, {"migrated": srv.migrated, "migrate_s": round(srv.migrate_time, 3),
-                              "local_cap": lc, "local_tokens": srv.local_tokens}
+        return n, el, ttfts, {"tokens": n, "migrated": srv.migrated, "migrate_s": round(srv.migrate_time, 3),
+                              "sent_GB": round(srv.sent_bytes / 1e9, 3), "local_cap": lc,
+                              "local_tokens": srv.local_tokens, "pd_scheduler": srv.pd_stats(),
+                              "migration_ms_p50": srv.pd_stats()["migration_ms_p50"]}
 
     if role == "decode_driver":
-        # single decode GPU: let it also serve local prompts with a slice of its pool
+        # a replica the prefill side cannot saturate also serves local prompts with a slice of its pool
         local_frac = float(getattr(args, "decode_local_frac", -1.0))
         if local_frac < 0:
-            # one prefill GPU leaves the decode GPU ~half idle (2.5k of ~4.6k tok/s): fill it with
-            # local prompts; with 3+ prefill GPUs the decode GPU is the bottleneck already.  The
-            # 8-GPU 3-stage decode pipeline has ~20% headroom over its 5 prefill GPUs (15k vs 12.4k
-            # tok/s, profiles/r1_pd_capacity_70b.md); local prompts there (--decode-local-frac) add
-            # prefill chunks to its microbatches and are off until measured on a whole node
-            npre = len(layout.prefill_ranks)
-            local_frac = {1: 0.35, 2: 0.15}.get(npre, 0.0) if layout.kind == "pd" else 0.0
+            local_frac = decode_local_fraction(layout, model=args.model)
         drv = DecodeDriver(cfg, f, layout, local_fraction=local_frac)
-        phases = [CtrlChannel(f, p, 4, tag="phase") for p in layout.prefill_ranks]
+        is_clock = f.rank == clock
+        others = [p for p in layout.prefill_ranks] + [d for d in layout.drivers if d != clock]
+        phases = [CtrlChannel(f, p, 4, tag="phase") for p in others] if is_clock else \
+            [CtrlChannel(f, clock, 4, tag="phase")]
         vocab = drv.engine.model_cfg.vocab_size
-        local_ttfts = []
+        local_ttfts, finished = [], []
 
         def top_local():
             while local_frac > 0 and drv.admit_local(_prompt(rng, args.prompt_len, vocab), sp) is not None:
                 pass
+
+        def one_step():
+            n = 0
+            for o in drv.step():
+                n += 1
+                if o.rid in drv.local_used and len(o.request.output) == 1:
+                    local_ttfts.append(o.request.ttft)
+                if o.finished:
+                    finished.append(o.request)
+            return n
 
         def run_steps(k):
             """k productive decode steps (idle polling while nothing has arrived does not count)."""
@@ -207,28 +248,41 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
                     if not drv.engine.has_unfinished():
                         time.sleep(0.0005)
                         continue
-                for o in drv.step():
-                    n += 1
-                    if o.rid in drv.local_used and len(o.request.output) == 1:
-                        local_ttfts.append(o.request.ttft)
+                n += one_step()
                 done += 1
             return n
 
-        ramp = args.ramp_steps if args.ramp_steps >= 0 else 2 * args.output_len
-        run_steps(ramp + args.warmup)
+        def run_until_phase():
+            n = 0
+            while phases[0].poll() is None:
+                top_local()
+                if not drv.engine.has_unfinished():
+                    drv.poll()
+                    if not drv.engine.has_unfinished():
+                        time.sleep(0.0005)
+                        continue
+                n += one_step()
+            return n
 
         def boundary():
-            for ph in phases:
-                ph.send([MSG_PHASE])
+            if is_clock:
+                for ph in phases:
+                    ph.send([MSG_PHASE])
             if hasattr(drv.engine, "pause_stages"):
                 drv.engine.pause_stages()
             torch.cuda.synchronize() if f.device.type == "cuda" else None
             f.barrier()
 
+        ramp = args.ramp_steps if args.ramp_steps >= 0 else 2 * args.output_len
+        if is_clock:
+            run_steps(ramp + args.warmup)
+        else:
+            run_until_phase()
         boundary()
         t0 = time.perf_counter()
         local_ttfts.clear()
-        n = run_steps(args.steps)
+        finished.clear()
+        n = run_steps(args.steps) if is_clock else run_until_phase()
         boundary()
         el = time.perf_counter() - t0
         running = len(drv.engine.scheduler.running)
@@ -237,11 +291,12 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
             drv.poll()
             time.sleep(0.001)
         drv.finish()
-        return n, el, list(local_ttfts), {"received": drv.received, "running_at_end": running,
-                                          "recv_GB": round(drv.recv_bytes / 1e9, 3), "local_fraction": local_frac}
+        return n, el, list(local_ttfts), {"tokens": n, "received": drv.received, "running_at_end": running,
+                                          "recv_GB": round(drv.recv_bytes / 1e9, 3), "local_fraction": local_frac,
+                                          "steps": drv.engine.stats["steps"], "tpots": _tpots(finished)}
 
-    # later decode pipeline stages
-    w = StageWorker(cfg, f, layout.decode_ranks)
+    # later stages of a decode pipeline replica
+    w = StageWorker(cfg, f, layout.group_of(f.rank))
     w.run()
     f.barrier()
     t0 = time.perf_counter()
@@ -250,4 +305,4 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
     f.barrier()
     el = time.perf_counter() - t0
     w.run()
-    return 0, el, [], {"stage_steps": w.steps}
+    return 0, el, [], {"tokens": 0, "stage_steps": w.steps}

@@ -123,6 +123,38 @@ class Fabric:
         if self.on_gpu:
             torch.cuda.current_stream().wait_stream(self.comm_stream)
 
+    def connect_pairs(self, pairs: list) -> float:
+        """Create every point-to-point communicator this rank will use NOW, with
+        one tiny send/recv per pair, so that RCCL set-up (and any failure of
+        it) happens at start-up instead of inside the first KV migration or
+        pipeline hop.  ``pairs`` must be the same sorted list on every rank
+        (``NodeLayout.p2p_pairs``): each rank walks its own pairs in that
+        global order and the first unfinished pair always has both ends ready,
+        so the walk cannot deadlock.  Returns the seconds it took."""
+        import time as _time
+        t0 = _time.perf_counter()
+        dev = self.device if (self.on_gpu or self.staged) else torch.device("cpu")
+        for a, b in pairs:
+            if self.rank not in (a, b):
+                continue
+            peer = b if self.rank == a else a
+            t = torch.full((1,), self.rank, dtype=torch.int64, device=dev)
+            r = torch.empty(1, dtype=torch.int64, device=dev)
+            if self.staged:
+                t, r = t.cpu(), r.cpu()
+            if self.rank == a:
+                dist.send(t, peer)
+                dist.recv(r, peer)
+            else:
+                dist.recv(r, peer)
+                dist.send(t, peer)
+            if int(r.item()) != peer:
+                raise RuntimeError(f"rank {self.rank}: pair warm-up with {peer} returned {int(r.item())}")
+        if self.on_gpu:
+            torch.cuda.synchronize(self.device)
+        self.pairs_connected = len([1 for a, b in pairs if self.rank in (a, b)])
+        return _time.perf_counter() - t0
+
     # ------------------------------------------------------------------ control (host, pollable)
     def ctrl_group(self):
         return self.ctrl

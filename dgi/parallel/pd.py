@@ -5,30 +5,39 @@ The reference's P/D path is an in-memory scheduler whose KV migration is
 SURVEY §3.5).  Here:
 
 * **Prefill ranks** (``PrefillServer``) run a prefill-only engine: full
-  model per GPU (Llama-3-70B bf16 fits in 288 GB), radix prefix cache,
-  batched/chunked prefill.  When a prompt completes, its first token is
-  sampled locally and its KV pages are packed per decode stage with the
-  ``kv_gather`` HIP kernel (that stage's layer slice, one contiguous
-  buffer); each slice goes straight to its stage with an RCCL send over
-  that pair's own xGMI link.  Request metadata rides the control store.
-* **Decode driver** (``DecodeDriver``) owns the decode engine — a single GPU
-  or stage 0 of a decode layer pipeline (``pdpp``).  It allocates pages,
-  posts its slice receive on a side stream (decode compute never waits on
-  a migration in flight), tells the later stages the page ids (they post
-  their own receives from the prefill rank), and admits the requests to
-  the next decode iteration once its slice has landed (``kv_scatter``).
-* **Flow control**: the decode driver grants block *credits* to each prefill
-  rank (gloo control group); a prefill rank admits a prompt only when it
-  holds credit for the whole sequence (prompt + max_tokens), and credits
-  flow back when sequences finish, so the decode pool can never run out
-  and nothing is ever preempted on the decode side.
+  model per GPU (Llama-3-70B bf16 fits in 288 GB), batched/chunked prefill.
+  When a prompt completes, its first token is sampled locally and its KV
+  pages are packed per decode stage with the ``kv_gather`` HIP kernel (that
+  stage's layer slice, one contiguous buffer); each slice goes straight to
+  its stage with an RCCL send over that pair's own xGMI link.  Request
+  metadata rides the control store.
+* **Decode replicas**: the node runs R decode replicas (``NodeLayout.
+  decode_groups``), each a whole-model decode GPU or a decode layer pipeline.
+  A replica's **driver** (``DecodeDriver``) allocates pages, posts its slice
+  receive on a side stream (decode compute never waits on a migration in
+  flight), tells its later stages the page ids (they post their own receives
+  from the prefill rank) and admits the requests once their slice landed.
+* **Placement**: each prefill rank runs a node-local instance of the
+  reference's ``PrefillDecodeScheduler`` (server/app/services/pd_scheduler.py
+  API, reference :274-323): every replica is a registered DECODE worker whose
+  KV headroom is the credit it granted this rank, and ``assign_job`` picks the
+  replica by bandwidth x headroom / (1 + active) at admission.  Migrations
+  are accounted through ``KVCacheMigrator.record``.
+* **Flow control**: every driver grants block *credits* to every prefill
+  rank; a prefill rank admits a prompt only when some replica holds credit
+  for the whole sequence (prompt + max_tokens), and credits flow back when
+  sequences finish, so no decode pool can run out and nothing is ever
+  preempted on the decode side.
 
-Control messages (int64[CTRL]) on the gloo group:
-  MIGRATE n_reqs total_blocks meta_len tok_len | CREDIT blocks | DONE
+Control messages (int64[CTRL]) on the rendezvous store:
+  MIGRATE n_reqs total_blocks meta_len tok_len | CREDIT blocks seqs | DONE |
+  FINISHED rid tok code | TOKENS (rid tok code)*
 """
 from __future__ import annotations
 
 import collections
+import importlib.util
+import os
 import time
 from typing import Optional
 
@@ -48,6 +57,36 @@ MSG_MIGRATE, MSG_CREDIT, MSG_DONE, MSG_FINISHED, MSG_TOKENS = 1, 2, 3, 4, 5
 REASONS = {0: None, 1: "length", 2: "stop"}
 CTRL = 8
 META_FIELDS = 11
+# per-GPU figures registered with the node-local P/D scheduler (MI355X: ~2.5 PF
+# dense bf16, 8 TB/s HBM3E); only their ratios matter for placement
+MI355X_TFLOPS = 2500.0
+MI355X_HBM_GBPS = 8000.0
+
+
+def pd_scheduler_module():
+    """The reference-compatible ``PrefillDecodeScheduler`` / ``KVCacheMigrator``
+    (server/app/services/pd_scheduler.py), imported without the server app."""
+    try:
+        from server.app.services import pd_scheduler as m   # repo root on sys.path
+        return m
+    except ImportError:
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        path = os.path.join(root, "server", "app", "services", "pd_scheduler.py")
+        spec = importlib.util.spec_from_file_location("dgi_pd_scheduler", path)
+        m = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(m)
+        return m
+
+
+def run_sync(coro):
+    """Drive a coroutine that never suspends (the scheduler's bookkeeping
+    methods) to completion without an event loop."""
+    try:
+        coro.send(None)
+    except StopIteration as e:
+        return e.value
+    coro.close()
+    raise RuntimeError("coroutine suspended outside an event loop")
 
 
 def _blocks_for(n_tokens: int, bs: int) -> int:
@@ -62,19 +101,23 @@ def _req_meta(r: Request, nblocks: int) -> list:
 
 
 class PrefillServer:
-    """One prefill rank."""
+    """One prefill rank: admits prompts against decode credit, prefills them and
+    migrates each finished prompt's KV to the decode replica chosen for it."""
 
     def __init__(self, cfg: EngineConfig, fabric: Fabric, layout: NodeLayout, seed_offset: int = 0,
-                 local_cap: int = 0, report_tokens: bool = False):
+                 local_cap: int = 0, report_tokens: bool = False, router: Optional[int] = None):
         self.f = fabric
         self.layout = layout
-        self.driver = layout.decode_ranks[0]
-        # overflow decoding: when the decode side has no credit left, up to
-        # ``local_cap`` sequences stay on this rank and decode inside its mixed
+        self.drivers = list(layout.drivers)
+        self.groups = {g[0]: list(g) for g in layout.decode_groups}
+        self.driver = self.drivers[0]
+        # overflow tokens / done-at-first-token reports go to the node router
+        self.router = self.drivers[0] if router is None else router
+        # overflow decoding: when no replica has credit left, up to ``local_cap``
+        # sequences stay on this rank and decode inside its mixed
         # prefill+decode steps instead of the rank idling until credit returns
-        # (one decode GPU fed by 3+ prefill GPUs is decode-bound:
-        # profiles/r1_pd_capacity_70b.md).  ``report_tokens`` streams their
-        # tokens to the decode driver (node router) once per step.
+        # (decode-bound layouts: profiles/r1_pd_capacity_70b.md).  ``report_tokens``
+        # streams their tokens to the router once per step.
         self.local_cap = local_cap
         self.local: set = set()
         self.local_tokens = 0
@@ -83,20 +126,36 @@ class PrefillServer:
                                "use_graphs": bool(cfg.use_graphs and local_cap > 0)})
         self.engine = LLMEngine(pcfg)
         self.bs = self.engine.pool.block_size
-        self.ch = CtrlChannel(fabric, self.driver, CTRL)
-        msg = self.ch.wait()  # initial credit grant
-        assert msg[0] == MSG_CREDIT
-        self.credit = int(msg[1])
-        self.seq_credit = int(msg[2])
+        self.ch = {d: CtrlChannel(fabric, d, CTRL) for d in self.drivers}
+        self.credit, self.seq_credit = {}, {}
+        for d in self.drivers:   # initial credit grant of every replica
+            msg = self.ch[d].wait()
+            assert msg[0] == MSG_CREDIT, msg
+            self.credit[d], self.seq_credit[d] = int(msg[1]), int(msg[2])
+        self.credit_total = dict(self.credit)
         self.pending: collections.deque = collections.deque()
+        self.target: dict = {}     # rid -> (driver, blocks reserved)
         self.migrated = 0
         self.migrate_time = 0.0
         self.sent_bytes = 0
-        # decode stages' layer ranges: each stage is sent its own slice of every page
+        # each replica's stages are sent their own layer slice of every page
         from dgi.parallel.pipeline import stage_split
-        self.split = stage_split(self.engine.model_cfg, len(layout.decode_ranks))
+        self.splits = {d: stage_split(self.engine.model_cfg, len(g)) for d, g in self.groups.items()}
         self.first_tokens = 0
         self.ttfts: list = []
+        # node-local P/D scheduler: replicas are DECODE workers, headroom = our credit
+        m = pd_scheduler_module()
+        self._pdm = m
+        self.pd = m.PrefillDecodeScheduler()
+        self.me = f"prefill-{fabric.rank}"
+        self.pd.register_worker(self.me, m.WorkerCapability(self.me, m.WorkerRole.PREFILL,
+                                                            compute_flops=MI355X_TFLOPS))
+        for d, g in self.groups.items():
+            self.pd.register_worker(str(d), m.WorkerCapability(
+                str(d), m.WorkerRole.DECODE, memory_bandwidth_gbps=MI355X_HBM_GBPS * len(g),
+                kv_cache_tokens_total=self.credit_total[d] * self.bs))
+        self.migrator = m.KVCacheMigrator(self.pd)
+        self.placed: dict = {d: collections.deque() for d in self.drivers}
 
     # ------------------------------------------------------------------ API
     def submit(self, prompt: list, params: SamplingParams, rid=None) -> Request:
@@ -108,25 +167,50 @@ class PrefillServer:
         return bool(self.pending) or self.engine.has_unfinished()
 
     def _poll_credit(self) -> None:
-        while True:
-            m = self.ch.poll()
-            if m is None:
-                break
-            if m[0] == MSG_CREDIT:
-                self.credit += int(m[1])
-                self.seq_credit += int(m[2])
+        for d, ch in self.ch.items():
+            while True:
+                m = ch.poll()
+                if m is None:
+                    break
+                if m[0] == MSG_CREDIT:
+                    self.credit[d] += int(m[1])
+                    self.seq_credit[d] += int(m[2])
+                    for _ in range(min(int(m[2]), len(self.placed[d]))):
+                        run_sync(self.pd.complete_job(self.placed[d].popleft(), self._pdm.JobPhase.DECODE))
+
+    def _pick(self, r: Request, need: int) -> Optional[int]:
+        """Replica for a prompt needing ``need`` blocks: the P/D scheduler's
+        decode placement over the replicas that hold enough of our credit."""
+        ok = {d: self.credit[d] >= need and self.seq_credit[d] > 0 for d in self.drivers}
+        if not any(ok.values()):
+            return None
+        for d in self.drivers:
+            tot = self.credit_total[d]
+            used = tot - self.credit[d] if ok[d] else tot
+            self.pd.update_worker_stats(str(d), {"kv_cache_tokens_used": used * self.bs,
+                                                 "kv_cache_tokens_total": tot * self.bs})
+        m = self._pdm
+        job = m.PendingJob(0.0, time.time(), str(r.rid), m.JobPhase.DECODE, len(r.prompt), r.params.max_tokens,
+                           kv_cache_key=f"kv:{r.rid}", kv_cache_worker=self.me)
+        a = run_sync(self.pd.assign_job(job))
+        d = int(a.worker_id)
+        if not ok.get(d):
+            run_sync(self.pd.complete_job(str(r.rid), m.JobPhase.DECODE))
+            return None
+        self.placed[d].append(str(r.rid))
+        return d
 
     def _admit(self) -> None:
         while self.pending:
             r = self.pending[0]
             need = _blocks_for(len(r.prompt) + r.params.max_tokens, self.bs)
-            if need <= self.credit and self.seq_credit > 0:
-                self.credit -= need
-                self.seq_credit -= 1
-                r.spec_state = need  # credit reserved for this sequence
+            d = self._pick(r, need)
+            if d is not None:
+                self.credit[d] -= need
+                self.seq_credit[d] -= 1
+                self.target[r.rid] = (d, need)
             elif len(self.local) < self.local_cap:
-                r.spec_state = 0     # decoded here (overflow)
-                self.local.add(r.rid)
+                self.local.add(r.rid)   # decoded here (overflow)
             else:
                 break
             self.pending.popleft()
@@ -159,79 +243,108 @@ class PrefillServer:
             self.first_tokens += 1
             if o.request.ttft is not None:
                 self.ttfts.append(o.request.ttft)
-            if o.finished:  # max_tokens == 1 or EOS at the first token
-                self.credit += int(o.request.spec_state or 0)
-                self.seq_credit += 1
+            if o.finished:  # max_tokens == 1 or EOS at the first token: nothing to migrate
+                d, need = self.target.pop(o.rid)
+                self.credit[d] += need
+                self.seq_credit[d] += 1
+                if self.placed[d] and str(o.rid) in self.placed[d]:
+                    self.placed[d].remove(str(o.rid))
+                    run_sync(self.pd.complete_job(str(o.rid), self._pdm.JobPhase.DECODE))
                 code = {"length": 1, "stop": 2}.get(o.finish_reason, 0)
-                self.ch.send([MSG_FINISHED, int(o.rid), int(o.token), code])
+                self.ch[self.router].send([MSG_FINISHED, int(o.rid), int(o.token), code])
             else:
                 ready.append(o.request)
         if ready:
             with phase("migrate_send", reqs=len(ready)):
                 self._migrate(ready)
         if report:
-            self.ch.send_var([MSG_TOKENS] + report)
+            self.ch[self.router].send_var([MSG_TOKENS] + report)
         return outs
 
     def _migrate(self, reqs: list) -> None:
-        """Hand finished prefills to the decode side.
+        """Hand finished prefills to their decode replicas.
 
         Request metadata (ids, sampling params, prompt tokens) travels on the
-        control store; each decode stage receives ONLY its own layer slice of
-        the pages, straight from this rank over its own xGMI link (no relay
-        through the decode driver)."""
-        t0 = time.perf_counter()
+        control store; each stage of the target replica receives ONLY its own
+        layer slice of the pages, straight from this rank over its own xGMI
+        link (no relay through the replica's driver)."""
         eng = self.engine
         dev = self.f.device
-        ids, meta, toks = [], [], []
+        by_d: dict = collections.defaultdict(list)
         for r in reqs:
-            nb = _blocks_for(r.num_computed, self.bs)
-            ids += r.blocks[:nb]
-            meta += _req_meta(r, nb) + [int(r.spec_state or 0)]
-            toks += r.prompt
-        ids_t = torch.tensor(ids, dtype=torch.int32, device=dev)
-        bufs = [ops.kv_gather(eng.pool.kv[a:b], ids_t) for a, b in self.split]
-        from dgi.parallel.fault import plan
-        if plan():
-            def corrupt():
-                bufs[0].view(-1)[: max(1, bufs[0].numel() // 64)] = float("nan")
-            plan().check(self.f.rank, self.migrated + 100000, corrupt=corrupt)
-        self.ch.send([MSG_MIGRATE, len(reqs), len(ids), len(meta), len(toks)])
-        self.ch.send_var(np.asarray(meta + toks, dtype=np.int64))
-        for rank, buf in zip(self.layout.decode_ranks, bufs):
-            self.f.send(buf, rank)
-        for r in reqs:
-            eng.scheduler.finish(r, "migrated")
-            eng.requests.pop(r.rid, None)
-        self.migrated += len(reqs)
-        self.sent_bytes += sum(b.numel() * b.element_size() for b in bufs)
-        self.migrate_time += time.perf_counter() - t0
+            by_d[self.target[r.rid][0]].append(r)
+        for d, rs in by_d.items():
+            t0 = time.perf_counter()
+            ids, meta, toks = [], [], []
+            for r in rs:
+                nb = _blocks_for(r.num_computed, self.bs)
+                ids += r.blocks[:nb]
+                meta += _req_meta(r, nb) + [int(self.target.pop(r.rid)[1])]
+                toks += r.prompt
+            ids_t = torch.tensor(ids, dtype=torch.int32, device=dev)
+            bufs = [ops.kv_gather(eng.pool.kv[a:b], ids_t) for a, b in self.splits[d]]
+            from dgi.parallel.fault import plan
+            if plan():
+                def corrupt():
+                    bufs[0].view(-1)[: max(1, bufs[0].numel() // 64)] = float("nan")
+                plan().check(self.f.rank, self.migrated + 100000, corrupt=corrupt)
+            self.ch[d].send([MSG_MIGRATE, len(rs), len(ids), len(meta), len(toks)])
+            self.ch[d].send_var(np.asarray(meta + toks, dtype=np.int64))
+            for rank, buf in zip(self.groups[d], bufs):
+                self.f.send(buf, rank)
+            for r in rs:
+                eng.scheduler.finish(r, "migrated")
+                eng.requests.pop(r.rid, None)
+            nbytes = sum(b.numel() * b.element_size() for b in bufs)
+            dt = time.perf_counter() - t0
+            self.migrator.record(f"kv:{rs[0].rid}", self.me, str(d), nbytes, dt * 1000.0)
+            self.migrated += len(rs)
+            self.sent_bytes += nbytes
+            self.migrate_time += dt
+
+    def pd_stats(self) -> dict:
+        st = self.pd.get_stats()
+        lat = self.migrator.latencies_ms
+        st["migration_ms_p50"] = round(float(np.median(lat)), 3) if lat else None
+        return st
 
     def finish(self) -> None:
-        """End of stream: the decode driver keeps receiving until it sees DONE."""
-        self.ch.send([MSG_DONE])
+        """End of stream: every replica driver keeps receiving until it sees DONE."""
+        for ch in self.ch.values():
+            ch.send([MSG_DONE])
         self.f.flush()
 
 
 class DecodeDriver:
-    """Decode side: single engine or stage 0 of the decode pipeline."""
+    """Driver of one decode replica: a single engine or stage 0 of a decode pipeline."""
 
     def __init__(self, cfg: EngineConfig, fabric: Fabric, layout: NodeLayout, credit_margin: float = 0.02,
-                 local_fraction: float = 0.0):
+                 local_fraction: float = 0.0, router: Optional[int] = None):
         self.f = fabric
         self.layout = layout
+        self.group = layout.group_of(fabric.rank)
+        assert self.group[0] == fabric.rank, "DecodeDriver runs on a replica's first rank"
         dcfg = EngineConfig(**{**cfg.__dict__, "device": str(fabric.device), "enable_prefix_caching": False})
-        if len(layout.decode_ranks) > 1:
-            self.engine = PipelineEngine(dcfg, fabric, layout.decode_ranks)
-            self.L_local = self.engine.model.num_local_layers
+        if len(self.group) > 1:
+            self.engine = PipelineEngine(dcfg, fabric, self.group)
         else:
             self.engine = LLMEngine(dcfg)
-            self.L_local = self.engine.model.num_local_layers
+        self.L_local = self.engine.model.num_local_layers
         mc = self.engine.model_cfg
         self.mc = mc
         self.bs = self.engine.pool.block_size
         self.prefill = list(layout.prefill_ranks)
         self.chans = {p: CtrlChannel(fabric, p, CTRL) for p in self.prefill}
+        # node router (serving): the other replicas' drivers forward their tokens to it
+        self.router = layout.drivers[0] if router is None else router
+        self.is_router = fabric.rank == self.router
+        self.fwd = None
+        self.fwd_in: dict = {}
+        if self.is_router:
+            self.fwd_in = {d: CtrlChannel(fabric, d, CTRL, tag="fwd") for d in layout.drivers if d != fabric.rank}
+        else:
+            self.fwd = CtrlChannel(fabric, self.router, CTRL, tag="fwd")
+        self.forward_tokens = False     # serving mode: stream outputs to the router
         free = self.engine.pool.num_free
         total = int(free * (1.0 - credit_margin - local_fraction))
         # hybrid decode: a slice of the pool serves prompts admitted locally (mixed
@@ -248,7 +361,7 @@ class DecodeDriver:
         self.arrivals: list = []   # migrated requests not yet reported (first token known)
         self.track_arrivals = False
         self.prefill_finished: list = []   # (rid, token, reason) of sequences done at their first token
-        self.remote_tokens: list = []      # (rid, token, reason|None) decoded on a prefill rank (overflow)
+        self.remote_tokens: list = []      # (rid, token, reason|None) from prefill ranks / other replicas
         self.refund = collections.Counter()
         self.refund_seqs = collections.Counter()
         self.done = set()
@@ -275,7 +388,6 @@ class DecodeDriver:
             self.engine.send_kv_notice(ids_t, p)
         self.inflight.append((p, rec, buf, ids, ids_t, meta, toks))
         self.recv_bytes += buf.numel() * buf.element_size()     # this stage's slice
-
     def _admit_arrived(self, block: bool = False) -> None:
         """Scatter every completed migration into the pool and admit its requests."""
         keep = []
@@ -347,11 +459,33 @@ class DecodeDriver:
                         self.prefill_finished.append((int(m[1]), int(m[2]), REASONS.get(int(m[3]))))
                 elif m[0] == MSG_TOKENS:
                     if self.track_arrivals:
-                        for i in range(1, len(m) - 2, 3):
-                            code = int(m[i + 2])
-                            self.remote_tokens.append((int(m[i]), int(m[i + 1]),
-                                                       None if code < 0 else REASONS.get(code) or "stop"))
+                        self._take_tokens(m)
+        for ch in self.fwd_in.values():      # router: tokens of the other replicas
+            while True:
+                m = ch.poll()
+                if m is None:
+                    break
+                if self.track_arrivals:
+                    self._take_tokens(m)
         self._admit_arrived()
+
+    def _take_tokens(self, m) -> None:
+        for i in range(1, len(m) - 2, 3):
+            code = int(m[i + 2])
+            self.remote_tokens.append((int(m[i]), int(m[i + 1]), None if code < 0 else REASONS.get(code) or "stop"))
+
+    def _forward(self, arrivals: list, outs: list) -> None:
+        """Non-router replicas: stream first tokens and step outputs to the router."""
+        msg = []
+        for r in arrivals:
+            msg += [int(r.user), int(r.output[0]), -1]
+        for o in outs:
+            if o.request.user is None:
+                continue
+            msg += [int(o.request.user), int(o.token),
+                    {"length": 1, "stop": 2}.get(o.finish_reason, 2) if o.finished else -1]
+        if msg:
+            self.fwd.send_var([MSG_TOKENS] + msg)
 
     def step(self, poll: bool = True) -> list[StepOutput]:
         """One decode iteration.  ``poll`` first takes in control messages and
@@ -359,6 +493,9 @@ class DecodeDriver:
         before the step poll themselves and pass ``poll=False``)."""
         if poll:
             self.poll()
+        arr = []
+        if self.forward_tokens and not self.is_router:
+            arr, self.arrivals = self.arrivals, []
         outs = self.engine.step() if self.engine.has_unfinished() else []
         for o in outs:
             if o.finished:
@@ -371,6 +508,8 @@ class DecodeDriver:
             self.chans[p].send([MSG_CREDIT, self.refund[p], self.refund_seqs[p]])
         self.refund.clear()
         self.refund_seqs.clear()
+        if self.forward_tokens and not self.is_router:
+            self._forward(arr, outs)
         return outs
 
     def all_prefill_done(self) -> bool:

@@ -56,57 +56,203 @@ def plan_layer_split(total_layers: int, stages: int, layer_cost: float = 1.0, em
 
 @dataclasses.dataclass
 class NodeLayout:
+    """How the GPUs of one node are assigned.
+
+    ``decode_groups`` lists the decode *replicas*: each is a list of ranks —
+    one rank (a whole-model decode GPU) or the stages of a decode layer
+    pipeline in order.  A flat list of ints is accepted as ONE group (the
+    pre-replica form).  Every prefill rank can migrate to every replica."""
     kind: str                      # single | dp | pp | pd | pdpp
     prefill_ranks: list
-    decode_ranks: list             # decode pipeline stages in order (len 1 = no PP)
-    replicas: int = 1
+    decode_groups: list            # [[driver, stage1, ...], ...]
+    replicas: int = 1              # dp: whole-model replicas
+
+    def __post_init__(self):
+        g = list(self.decode_groups)
+        if g and all(isinstance(x, int) for x in g):
+            g = [g]
+        self.decode_groups = [list(x) for x in g]
+
+    @property
+    def decode_ranks(self) -> list:
+        return [r for g in self.decode_groups for r in g]
+
+    @property
+    def drivers(self) -> list:
+        return [g[0] for g in self.decode_groups]
 
     @property
     def world(self) -> int:
         return len(self.prefill_ranks) + len(self.decode_ranks)
 
+    def group_of(self, rank: int) -> list:
+        for g in self.decode_groups:
+            if rank in g:
+                return g
+        raise KeyError(rank)
+
     def role(self, rank: int) -> str:
         if rank in self.prefill_ranks:
             return "prefill"
-        if self.decode_ranks and rank == self.decode_ranks[0]:
+        if rank in self.drivers:
             return "decode_driver"
         return "decode_stage"
 
+    def p2p_pairs(self) -> list:
+        """Every rank pair that moves device tensors: prefill -> each decode
+        rank (each stage receives its own KV layer slice) and adjacent stages
+        of each decode pipeline.  Sorted, so that eager communicator set-up in
+        this order cannot deadlock (``Fabric.connect_pairs``)."""
+        pairs = set()
+        for p in self.prefill_ranks:
+            for d in self.decode_ranks:
+                pairs.add((min(p, d), max(p, d)))
+        for g in self.decode_groups:
+            for a, b in zip(g, g[1:]):
+                pairs.add((min(a, b), max(a, b)))
+        return sorted(pairs)
+
+    def describe(self) -> str:
+        if self.kind in ("single", "dp", "pp"):
+            return f"{self.kind}{self.world if self.kind != 'dp' else self.replicas}"
+        gs = "+".join(f"pp{len(g)}" if len(g) > 1 else "1" for g in self.decode_groups)
+        return f"{len(self.prefill_ranks)}P+{len(self.decode_groups)}D[{gs}]"
+
+
+@dataclasses.dataclass
+class RoleCapacity:
+    """Per-role throughput of one model on one MI355X (output tok/s of a
+    512-in / 128-out load; ``scripts/pd_capacity.py`` measures it).
+
+    * ``prefill_tok_s``: decode demand one prefill-only GPU creates
+      (prompts/s x output_len);
+    * ``decode_tok_s[k]``: what one decode replica of k pipeline stages
+      emits (k GPUs, k microbatches);
+    * ``mixed_tok_s``: one GPU running mixed prefill+decode steps (DP / the
+      hybrid slack filler)."""
+    prefill_tok_s: float
+    decode_tok_s: dict
+    mixed_tok_s: float
+
+
+# Llama-3-70B, bf16, measured on one MI355X (profiles/r1_pd_capacity_70b.md;
+# mixed = driver BENCH_r01 1653 tok/s).  A 3-stage replica (~27 layers per
+# stage, 768-row microbatches) is 2/3 of the 40-layer stage time.
+CAPACITY = {
+    "llama3-70b": RoleCapacity(prefill_tok_s=19.3 * 128, decode_tok_s={1: 4600.0, 2: 11500.0, 3: 15000.0},
+                               mixed_tok_s=1653.0),
+}
+
+
+def estimate_layout(n_prefill: int, stages: int, replicas: int, cap: RoleCapacity, fill: bool = False) -> float:
+    """Node output tok/s of nP + replicas x (stages-deep decode) under ``cap``:
+    the slower side sets the rate.  ``fill`` adds the slack filler the
+    runtime uses (decode replicas admit local prompts; prefill ranks decode
+    overflow sequences) at the mixed-step rate — an upper bound."""
+    pre = n_prefill * cap.prefill_tok_s
+    dec = replicas * cap.decode_tok_s.get(stages, 0.0)
+    if pre <= 0 or dec <= 0:
+        return 0.0
+    base = min(pre, dec)
+    if not fill:
+        return base
+    if dec >= pre:
+        return base + (1.0 - pre / dec) * replicas * stages * cap.mixed_tok_s
+    return base + (1.0 - dec / pre) * n_prefill * cap.mixed_tok_s
+
+
+def choose_pd_layout(n_gpus: int, cap: RoleCapacity, max_stages: int = 3, prefer_pipeline: bool = True,
+                     tol: float = 0.03) -> tuple:
+    """(n_prefill, stages, replicas, est tok/s) with the highest disaggregated
+    rate (``estimate_layout`` without the filler); candidates within ``tol``
+    of the best are ranked by pipeline depth (deeper first when
+    ``prefer_pipeline``: more KV per GPU, bigger decode microbatches), then by
+    how little slack they leave."""
+    cands = []
+    for npre in range(1, n_gpus):
+        left = n_gpus - npre
+        for k in range(1, max_stages + 1):
+            if left % k or k not in cap.decode_tok_s:
+                continue
+            reps = left // k
+            est = estimate_layout(npre, k, reps, cap)
+            pre, dec = npre * cap.prefill_tok_s, reps * cap.decode_tok_s[k]
+            cands.append((est, k, npre, reps, abs(pre - dec) / max(pre, dec)))
+    top = max(c[0] for c in cands)
+    near = [c for c in cands if c[0] >= (1.0 - tol) * top]
+    near.sort(key=lambda c: ((-c[1] if prefer_pipeline else c[1]), c[4], -c[0]))
+    est, k, npre, reps, _ = near[0]
+    return npre, k, reps, est
+
+
+def _groups(first: int, stages: int, replicas: int) -> list:
+    return [list(range(first + i * stages, first + (i + 1) * stages)) for i in range(replicas)]
+
 
 def plan_node_layout(n_gpus: int, kind: str = "pdpp", prefill_ranks: Optional[int] = None,
-                     decode_stages: Optional[int] = None) -> NodeLayout:
-    """Default P:D split for prefill-heavy loads (512-in/128-out on 70B).
+                     decode_stages: Optional[int] = None, decode_replicas: Optional[int] = None,
+                     model: str = "llama3-70b") -> NodeLayout:
+    """Assign the node's GPUs to roles.
 
-    Measured on one MI355X (scripts/pd_capacity.py, profiles/r1_pd_capacity_70b.md):
-    a prefill GPU turns 19.3 prompts/s (4096-token steps) = 2.47k output tok/s of
-    decode demand; a full-model decode GPU steps 512 rows in 111 ms (4.6k tok/s,
-    KV-capped near 640 sequences); a 40-layer stage steps 512 / 1024 / 1536 rows
-    in 56 / 89 / 129 ms.  An S-stage decode pipeline with S microbatches of R
-    rows emits R / t_stage(R) tok/s: 2 stages top out near 11.9k, 3 stages
-    (~27 layers each) reach ~15k at R = 768.  So at 8 GPUs 5 prefill GPUs
-    (12.4k demand) feed a 3-stage decode pipeline; below 8, N-1 prefill GPUs
-    feed one decode GPU."""
+    ``pd``/``pdpp`` without explicit counts pick the split from the measured
+    per-role capacity table (``CAPACITY``, ``choose_pd_layout``): e.g. on
+    Llama-3-70B at 8 GPUs the estimate favours 5 prefill GPUs feeding one
+    3-stage decode pipeline (``pdpp``) or three whole-model decode GPUs
+    (``pd``); below 8, N-1 prefill GPUs feed one decode GPU.  Models without a
+    table entry fall back to N-1 prefill ranks + one decode GPU."""
     if n_gpus == 1 or kind == "single":
         return NodeLayout("single", [], [0])
     if kind == "pp":
         return NodeLayout("pp", [], list(range(n_gpus)))
     if kind == "dp":
         return NodeLayout("dp", [], [0], replicas=n_gpus)
-    if decode_stages is None:
-        decode_stages = 3 if (kind == "pdpp" and n_gpus >= 8) else 1
-    if prefill_ranks is None:
-        prefill_ranks = n_gpus - decode_stages
-    prefill_ranks = max(1, min(prefill_ranks, n_gpus - decode_stages))
-    decode_stages = n_gpus - prefill_ranks
-    k = "pdpp" if decode_stages > 1 else "pd"
-    return NodeLayout(k, list(range(prefill_ranks)), list(range(prefill_ranks, n_gpus)))
+    cap = CAPACITY.get(model)
+    if decode_stages is None and kind == "pd":
+        decode_stages = 1
+    if prefill_ranks is None and decode_replicas is None and cap is not None and \
+            (decode_stages is None or kind == "pd"):
+        npre, k, reps, _est = choose_pd_layout(n_gpus, cap, max_stages=decode_stages or 3,
+                                               prefer_pipeline=kind == "pdpp")
+    else:
+        k = decode_stages or (3 if (kind == "pdpp" and n_gpus >= 8) else 1)
+        reps = decode_replicas
+        npre = prefill_ranks
+        if npre is None:
+            reps = reps or 1
+            npre = n_gpus - k * reps
+        if reps is None:
+            reps = max(1, (n_gpus - npre) // k)
+    npre = max(1, min(npre, n_gpus - k))
+    reps = max(1, min(reps, (n_gpus - npre) // k))
+    npre = n_gpus - k * reps
+    groups = _groups(npre, k, reps)
+    return NodeLayout("pdpp" if k > 1 else "pd", list(range(npre)), groups)
 
 
-def prefill_overflow_cap(layout: NodeLayout, cap: int = 256) -> int:
+def prefill_overflow_cap(layout: NodeLayout, cap: int = 256, model: str = "llama3-70b") -> int:
     """Sequences a prefill rank may decode itself while the decode side has no
-    credit (``PrefillServer(local_cap=...)``).  On for one decode GPU fed by 2+
-    prefill GPUs — that decode GPU saturates at ~4.6k tok/s on 70B while each
-    prefill GPU supplies ~2.5k (profiles/r1_pd_capacity_70b.md) — off where the
-    prefill side is the bottleneck (1 prefill GPU, or the 8-GPU 5P + 3-stage
-    decode pipeline)."""
-    return cap if layout.kind == "pd" and len(layout.prefill_ranks) >= 2 else 0
+    credit (``PrefillServer(local_cap=...)``): on when the decode side is the
+    bottleneck of the capacity estimate (e.g. 70B with 3 prefill GPUs per
+    decode GPU: each prefill GPU supplies ~2.5k tok/s, a decode GPU absorbs
+    ~4.6k — profiles/r1_pd_capacity_70b.md)."""
+    c = CAPACITY.get(model)
+    if c is None:
+        return cap if layout.kind == "pd" and len(layout.prefill_ranks) >= 2 else 0
+    k = len(layout.decode_groups[0])
+    pre = len(layout.prefill_ranks) * c.prefill_tok_s
+    dec = len(layout.decode_groups) * c.decode_tok_s.get(k, 0.0)
+    return cap if pre > dec * 1.05 else 0
+
+
+def decode_local_fraction(layout: NodeLayout, model: str = "llama3-70b") -> float:
+    """Share of a decode replica's KV pool for prompts it admits itself (hybrid
+    decode) when the prefill side cannot saturate it."""
+    c = CAPACITY.get(model)
+    if c is None:
+        return {1: 0.35, 2: 0.15}.get(len(layout.prefill_ranks), 0.0) if layout.kind == "pd" else 0.0
+    k = len(layout.decode_groups[0])
+    pre = len(layout.prefill_ranks) * c.prefill_tok_s
+    dec = len(layout.decode_groups) * c.decode_tok_s.get(k, 0.0)
+    if dec <= pre * 1.05:
+        return 0.0
+    return round(min(0.5, 1.0 - pre / dec), 3)

@@ -6,12 +6,15 @@ serves on one GPU).  The layout is the benchmark's (``dgi.parallel.plan``):
 * ``single`` — one engine;
 * ``pd`` / ``pdpp`` — prefill ranks + a decode GPU or decode layer pipeline.
 
-The *router* lives on the decode driver rank (it sees every output): an
-HTTP front-end (FastAPI/uvicorn thread) queues requests; the router loop
-hands each prompt to the least-loaded prefill rank over a control channel
-(the rendezvous store), steps the decode engine, and resolves HTTP futures
-as tokens arrive.  The first token is sampled on the prefill rank and
-arrives with the migrated KV, so TTFT is measured at that arrival.
+The *router* lives on the first decode replica's driver: an HTTP front-end
+(FastAPI/uvicorn thread) queues requests; the router loop places each prompt
+on a prefill rank with a node-local ``PrefillDecodeScheduler`` (the
+reference's P/D scheduler API, server/app/services/pd_scheduler.py) over a
+control channel (the rendezvous store), steps its own decode replica, and
+resolves HTTP futures as tokens arrive — its own, and those the other decode
+replicas forward to it.  The first token is sampled on the prefill rank and
+arrives with the migrated KV, so TTFT is measured at that arrival.  The
+prefill ranks pick the decode replica of each request (pd.PrefillServer).
 
 This replaces the reference's per-request HTTP/gRPC hops between shard
 workers (worker/distributed/session.py:49-455, grpc_server.py:351-388) for
@@ -107,11 +110,18 @@ class Router:
             self.engine.warmup()
         else:
             from dgi.parallel.fabric import CtrlChannel
-            from dgi.parallel.pd import DecodeDriver
+            from dgi.parallel.pd import MI355X_TFLOPS, DecodeDriver, pd_scheduler_module
             self.drv = DecodeDriver(cfg, fabric, layout)
             self.drv.track_arrivals = True
             self.engine = self.drv.engine
             self.chans = {p: CtrlChannel(fabric, p, 1, tag="req") for p in layout.prefill_ranks}
+            # node-local P/D scheduler: prefill placement (flops / (1 + active prefill jobs))
+            m = pd_scheduler_module()
+            self._pdm = m
+            self.pd = m.PrefillDecodeScheduler()
+            for p in layout.prefill_ranks:
+                self.pd.register_worker(str(p), m.WorkerCapability(str(p), m.WorkerRole.PREFILL,
+                                                                   compute_flops=MI355X_TFLOPS))
         self.ready = threading.Event()
 
     # ------------------------------------------------------------------ request intake (HTTP thread)
@@ -148,10 +158,26 @@ class Router:
             if self.drv is None:
                 self.engine.add_request(p.prompt, p.params, rid=p.rid)
             else:
-                dst = min(self.chans, key=lambda r: self.load[r])
-                self.load[dst] += 1
-                p.dst = dst
-                self.chans[dst].send_var(encode_request(p.rid, p.prompt, p.params))
+                from dgi.parallel.pd import run_sync
+                m = self._pdm
+                run_sync(self.pd.submit_job(str(p.rid), len(p.prompt), p.params.max_tokens))
+                for job, a in run_sync(self.pd.get_batch(m.JobPhase.PREFILL, 64)):
+                    q = self.live.get(int(job.job_id))
+                    if q is None:
+                        continue
+                    dst = int(a.worker_id)
+                    self.load[dst] += 1
+                    q.dst = dst
+                    self.chans[dst].send_var(encode_request(q.rid, q.prompt, q.params))
+
+    def _prefill_done(self, p: "_Pending") -> None:
+        """First token arrived: the prompt's prefill job is complete."""
+        if self.drv is not None and p.dst >= 0:
+            from dgi.parallel.pd import run_sync
+            self.load[p.dst] -= 1
+            run_sync(self.pd.complete_job(str(p.rid), self._pdm.JobPhase.PREFILL,
+                                          (time.perf_counter() - p.t0) * 1000.0))
+            p.dst = -1
 
     def _finish(self, rid: int, reason: Optional[str]) -> None:
         p = self.live.pop(rid, None)
@@ -167,7 +193,7 @@ class Router:
             for r in self.drv.arrivals:            # first token, sampled on the prefill rank
                 p = self.live.get(r.user)
                 if p is not None:
-                    self.load[p.dst] -= 1
+                    self._prefill_done(p)
                     self._emit(p, r.output[0], False, None)
             self.drv.arrivals.clear()
             outs = self.drv.step(poll=False)
@@ -186,17 +212,18 @@ class Router:
             for rid, tok, reason in self.drv.prefill_finished:   # done at the first token
                 p = self.live.get(rid)
                 if p is not None:
+                    self._prefill_done(p)
                     self._emit(p, tok, True, reason)
                     self._finish(rid, reason)
-                    self.load[p.dst] -= 1
             self.drv.prefill_finished.clear()
-            for rid, tok, reason in self.drv.remote_tokens:      # decoded on a prefill rank (overflow)
+            # decoded on a prefill rank (overflow) or on another decode replica
+            for rid, tok, reason in self.drv.remote_tokens:
                 p = self.live.get(rid)
                 if p is None:
                     continue
                 worked = True
                 if not p.tokens:
-                    self.load[p.dst] -= 1
+                    self._prefill_done(p)
                 self._emit(p, tok, reason is not None, reason)
                 if reason is not None:
                     self._finish(rid, reason)
@@ -259,9 +286,13 @@ def build_app(router: Router, stop: threading.Event):
 
     @app.get("/stats")
     async def stats():
-        return {"requests": router.stats["requests"], "finished": router.stats["finished"],
-                "live": len(router.live), "engine": dict(router.engine.stats),
-                "scheduler": router.engine.scheduler.stats()}
+        out = {"requests": router.stats["requests"], "finished": router.stats["finished"],
+               "live": len(router.live), "engine": dict(router.engine.stats),
+               "scheduler": router.engine.scheduler.stats()}
+        if router.drv is not None:
+            out["pd_scheduler"] = router.pd.get_stats()
+            out["layout"] = router.layout.describe()
+        return out
 
     @app.post("/generate")
     async def generate(r: GenReq):
@@ -303,7 +334,7 @@ def _prefill_loop(args, fabric, layout) -> None:
                        max_num_batched_tokens=args.max_batched_tokens, max_model_len=args.max_model_len,
                        use_graphs=str(fabric.device).startswith("cuda") and not args.no_graphs, seed=args.seed)
     srv = PrefillServer(cfg, fabric, layout, local_cap=cap, report_tokens=True)
-    inbox = CtrlChannel(fabric, layout.decode_ranks[0], 1, tag="req")
+    inbox = CtrlChannel(fabric, layout.drivers[0], 1, tag="req")
     stopping = False
     while True:
         while True:
@@ -324,6 +355,28 @@ def _prefill_loop(args, fabric, layout) -> None:
     srv.finish()
 
 
+def _replica_loop(args, fabric, layout) -> None:
+    """Driver of a decode replica other than the router's: serve migrations,
+    forward every token to the router, stop once all prefill ranks are done."""
+    from dgi.engine import EngineConfig
+    from dgi.parallel.pd import DecodeDriver
+    cfg = EngineConfig(model=args.model, device=str(fabric.device), max_num_seqs=args.max_num_seqs,
+                       max_num_batched_tokens=args.max_batched_tokens, max_model_len=args.max_model_len,
+                       use_graphs=str(fabric.device).startswith("cuda") and not args.no_graphs, seed=args.seed)
+    drv = DecodeDriver(cfg, fabric, layout)
+    drv.track_arrivals = True
+    drv.forward_tokens = True
+    while True:
+        drv.poll()
+        if drv.engine.has_unfinished() or drv.arrivals:
+            drv.step(poll=False)
+        elif drv.all_prefill_done():
+            break
+        else:
+            time.sleep(0.001)
+    drv.finish()
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="llama3-8b")
@@ -332,6 +385,8 @@ def main(argv=None) -> int:
     ap.add_argument("--port", type=int, default=8100)
     ap.add_argument("--layout", default="auto")
     ap.add_argument("--prefill-ranks", type=int, default=0)
+    ap.add_argument("--decode-stages", type=int, default=0)
+    ap.add_argument("--decode-replicas", type=int, default=0)
     ap.add_argument("--prefill-local-cap", type=int, default=-1,
                     help="sequences a prefill rank decodes itself when the decode side is full (-1 = auto)")
     ap.add_argument("--max-num-seqs", type=int, default=256)
@@ -347,10 +402,16 @@ def main(argv=None) -> int:
         from dgi.parallel.plan import plan_node_layout
         fabric = Fabric()
         layout = plan_node_layout(world, "pdpp" if args.layout == "auto" else args.layout,
-                                  args.prefill_ranks or None)
+                                  args.prefill_ranks or None, decode_stages=args.decode_stages or None,
+                                  decode_replicas=args.decode_replicas or None, model=args.model)
+        fabric.connect_pairs(layout.p2p_pairs())
         role = layout.role(fabric.rank)
         if role == "prefill":
             _prefill_loop(args, fabric, layout)
+            fabric.close()
+            return 0
+        if role == "decode_driver" and fabric.rank != layout.drivers[0]:
+            _replica_loop(args, fabric, layout)
             fabric.close()
             return 0
         if role == "decode_stage":
@@ -359,7 +420,7 @@ def main(argv=None) -> int:
             cfg = EngineConfig(model=args.model, device=str(fabric.device), max_num_seqs=args.max_num_seqs,
                                max_num_batched_tokens=args.max_batched_tokens, max_model_len=args.max_model_len,
                                use_graphs=False, seed=args.seed, enable_prefix_caching=False)
-            w = StageWorker(cfg, fabric, layout.decode_ranks)
+            w = StageWorker(cfg, fabric, layout.group_of(fabric.rank))
             while w.run() != "stop":
                 pass
             fabric.close()

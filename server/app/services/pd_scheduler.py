@@ -249,6 +249,16 @@ class KVCacheMigrator:
         finally:
             self._pending_migrations.pop(mid, None)
 
+    def record(self, kv_cache_key: str, source_worker: str, target_worker: str, nbytes: int,
+               latency_ms: float) -> None:
+        """Account a migration a synchronous in-node transport already performed
+        (dgi.parallel.pd: RCCL page sends from a prefill rank to a decode replica)."""
+        self.scheduler._stats["migrations"] += 1
+        self.scheduler._stats["migration_bytes"] += int(nbytes)
+        self.latencies_ms.append(float(latency_ms))
+        if len(self.latencies_ms) > 4096:
+            del self.latencies_ms[:2048]
+
     async def _do_migrate(self, kv_cache_key: str, source_worker: str, target_worker: str) -> bool:
         t0 = time.perf_counter()
         try:

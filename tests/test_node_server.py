@@ -20,11 +20,11 @@ def _port():
     return p
 
 
-def _start(nproc, port, max_num_seqs=16):
+def _start(nproc, port, max_num_seqs=16, extra=()):
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
     env.pop("CUDA_VISIBLE_DEVICES", None)
     args = ["-m", "dgi.serve.node", "--model", "llama-tiny", "--port", str(port), "--max-model-len", "512",
-            "--max-num-seqs", str(max_num_seqs), "--max-batched-tokens", "512"]
+            "--max-num-seqs", str(max_num_seqs), "--max-batched-tokens", "512", *extra]
     if nproc > 1:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
                "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
@@ -56,16 +56,18 @@ def _reference(prompts, max_tokens):
                                                                    ignore_eos=True))]
 
 
-@pytest.mark.parametrize("nproc,max_num_seqs", [(1, 16), (2, 16), (3, 2)])
-def test_node_server_generate_matches_engine(nproc, max_num_seqs):
+@pytest.mark.parametrize("nproc,max_num_seqs,extra", [(1, 16, ()), (2, 16, ()), (3, 2, ()),
+                                                       (4, 16, ("--layout", "pd", "--prefill-ranks", "2"))])
+def test_node_server_generate_matches_engine(nproc, max_num_seqs, extra):
     """(3, 2): two prefill ranks, a decode rank that holds 2 sequences — the
     rest overflow into the prefill ranks' own decode and stream back through
-    the router."""
+    the router.  (4, pd, 2 prefill): two decode replicas; the second forwards
+    its tokens to the router on the first."""
     g = torch.Generator().manual_seed(3)
     prompts = [torch.randint(5, 500, (n,), generator=g).tolist() for n in (9, 23, 40)]
     ref = _reference(prompts, 8)
     port = _port()
-    proc = _start(nproc, port, max_num_seqs)
+    proc = _start(nproc, port, max_num_seqs, extra)
     url = f"http://127.0.0.1:{port}"
     try:
         _wait(url, proc)

@@ -126,9 +126,14 @@ def _pd_body(rank, world):
     from dgi.sched.request import SamplingParams
     f = Fabric()
     cfg = _engine_cfg()
-    # DGI_TEST_PREFILL prefill ranks, the rest a decode pipeline (1 stage = plain P/D)
+    # DGI_TEST_PREFILL prefill ranks; the rest DGI_TEST_REPLICAS decode replicas, each a
+    # decode pipeline over an equal share of the ranks (1 stage = a whole-model decode rank)
     npre = int(os.environ.get("DGI_TEST_PREFILL", "1"))
-    layout = NodeLayout("pd" if world - npre == 1 else "pdpp", list(range(npre)), list(range(npre, world)))
+    reps = int(os.environ.get("DGI_TEST_REPLICAS", "1"))
+    k = (world - npre) // reps
+    groups = [list(range(npre + i * k, npre + (i + 1) * k)) for i in range(reps)]
+    layout = NodeLayout("pd" if k == 1 else "pdpp", list(range(npre)), groups)
+    f.connect_pairs(layout.p2p_pairs())
     if rank in layout.prefill_ranks:
         srv = PrefillServer(cfg, f, layout)
         nlocal = int(os.environ.get("DGI_TEST_LOCAL", "0"))
@@ -139,21 +144,23 @@ def _pd_body(rank, world):
             srv.step()
         srv.finish()
         return "prefill"
-    if rank == layout.decode_ranks[0]:
-        nlocal = int(os.environ.get("DGI_TEST_LOCAL", "0"))
+    if rank in layout.drivers:
+        import time as _t
+        nlocal = int(os.environ.get("DGI_TEST_LOCAL", "0")) if rank == layout.drivers[0] else 0
         drv = DecodeDriver(cfg, f, layout, local_fraction=0.3 if nlocal else 0.0)
         for i, p in enumerate(PROMPTS):
             if i >= len(PROMPTS) - nlocal:                  # served end to end on the decode side
                 assert drv.admit_local(p, _sp(i)) is not None
         done = {}
-        while len(done) < len(PROMPTS):
+        while not drv.all_prefill_done() or drv.engine.has_unfinished():
             for o in drv.step():
                 if o.finished:
                     done[tuple(o.request.prompt)] = o.request.output
+            _t.sleep(0.001)
         drv.finish()
-        return [done[tuple(p)] for p in PROMPTS]
+        return done
     from dgi.parallel.pipeline import StageWorker
-    w = StageWorker(cfg, f, layout.decode_ranks)
+    w = StageWorker(cfg, f, layout.group_of(rank))
     w.run()
     f.flush()
     return None
@@ -199,6 +206,14 @@ def _pd_overflow_body(rank, world):
 
 # ---------------------------------------------------------------------------- tests
 
+def _merged(out, *drivers):
+    """Outputs per prompt, merged over the decode replicas' drivers."""
+    done = {}
+    for d in drivers:
+        done.update(out[d])
+    return [done[tuple(p)] for p in PROMPTS]
+
+
 def test_layer_range_for_worker_covers_all_layers():
     for L in (1, 7, 32, 80):
         for n in (1, 2, 3, 8):
@@ -223,7 +238,31 @@ def test_node_layout_defaults():
     assert plan_node_layout(1).kind == "single"
     assert plan_node_layout(2).kind == "pd"
     four = plan_node_layout(4)
-    assert four.kind == "pd" and len(four.prefill_ranks) == 3
+    assert four.kind == "pdpp" and four.decode_groups == [[2, 3]]
+    assert plan_node_layout(8, "pd").decode_groups == [[5], [6], [7]]
+    # explicit replica requests and legacy flat decode lists
+    lay = plan_node_layout(8, "pdpp", prefill_ranks=4, decode_stages=2)
+    assert lay.prefill_ranks == [0, 1, 2, 3] and lay.decode_groups == [[4, 5], [6, 7]] and lay.drivers == [4, 6]
+    assert lay.role(6) == "decode_driver" and lay.role(7) == "decode_stage" and lay.group_of(7) == [6, 7]
+    from dgi.parallel.plan import NodeLayout
+    assert NodeLayout("pdpp", [0], [1, 2]).decode_groups == [[1, 2]]
+    # every prefill rank talks to every decode rank, stages to their neighbour, sorted
+    assert lay.p2p_pairs() == sorted({(p, d) for p in range(4) for d in range(4, 8)} | {(4, 5), (6, 7)})
+    assert lay.describe() == "4P+2D[pp2+pp2]"
+
+
+def test_capacity_planner_balances_roles():
+    from dgi.parallel.plan import CAPACITY, RoleCapacity, choose_pd_layout, estimate_layout
+    cap = CAPACITY["llama3-70b"]
+    npre, k, reps, est = choose_pd_layout(8, cap)
+    assert npre + k * reps == 8 and est >= 0.97 * max(
+        estimate_layout(p, s, (8 - p) // s, cap) for p in range(1, 8) for s in (1, 2, 3) if (8 - p) % s == 0)
+    # a decode-heavy model (fast prefill, slow decode) gets more decode GPUs
+    slow = RoleCapacity(prefill_tok_s=10000.0, decode_tok_s={1: 2000.0}, mixed_tok_s=1500.0)
+    npre, k, reps, _ = choose_pd_layout(8, slow, max_stages=1)
+    assert reps > npre
+    # the slack filler never lowers the estimate
+    assert estimate_layout(5, 3, 1, cap, fill=True) >= estimate_layout(5, 3, 1, cap)
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -237,7 +276,7 @@ def test_pipeline_matches_single_process(world):
 def test_pd_migration_matches_local_decode(world):
     ref = _reference_outputs()
     out = _spawn("_pd_body", world)
-    assert out[1] == ref
+    assert _merged(out, 1) == ref
 
 
 def test_pd_overflow_decodes_on_prefill_rank_when_decode_is_full():
@@ -266,7 +305,7 @@ def test_pdpp_decode_pipeline_also_serves_local_prompts(monkeypatch):
                                max_num_batched_tokens=64, enable_prefix_caching=False))
     ref = [r.output for r in e.generate(PROMPTS, SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True))]
     out = _spawn("_pd_body", 3)
-    assert out[1] == ref
+    assert _merged(out, 1) == ref
 
 
 @pytest.mark.parametrize("npre,world", [(2, 4), (1, 4)])
@@ -283,7 +322,7 @@ def test_pd_multi_prefill_and_three_stage_decode(npre, world, monkeypatch):
                                max_num_batched_tokens=64, enable_prefix_caching=False))
     ref = [r.output for r in e.generate(PROMPTS, SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True))]
     out = _spawn("_pd_body", world)
-    assert out[npre] == ref
+    assert _merged(out, npre) == ref
 
 
 def _tp_body(rank, world):
@@ -323,7 +362,25 @@ def test_pdpp_sampled_top_k_top_p_matches_single_process(monkeypatch):
     monkeypatch.setenv("DGI_TEST_PREFILL", "1")
     ref = _reference_outputs(model="llama-tiny-hd128")
     out = _spawn("_pd_body", 3)
-    assert out[1] == ref
+    assert _merged(out, 1) == ref
+
+
+@pytest.mark.parametrize("npre,reps,world", [(2, 2, 4), (1, 2, 5)])
+def test_pd_decode_replicas_match_local_decode(npre, reps, world, monkeypatch):
+    """P prefill ranks feeding R decode replicas (2P+2D whole-model replicas;
+    1P + 2 x PP2 pipelines): each prompt is placed on a replica by the prefill
+    rank's node-local PrefillDecodeScheduler, seeded sampled outputs equal the
+    single-process ones, and both replicas get work."""
+    monkeypatch.setenv("DGI_TEST_MODEL", "llama-tiny-hd128")
+    monkeypatch.setenv("DGI_TEST_PREFILL", str(npre))
+    monkeypatch.setenv("DGI_TEST_REPLICAS", str(reps))
+    monkeypatch.setenv("DGI_TEST_SAMPLED", "1")
+    ref = _reference_outputs(model="llama-tiny-hd128")
+    out = _spawn("_pd_body", world)
+    k = (world - npre) // reps
+    drivers = [npre + i * k for i in range(reps)]
+    assert _merged(out, *drivers) == ref
+    assert all(len(out[d]) >= 1 for d in drivers)
 
 
 def _greedy_reference():
