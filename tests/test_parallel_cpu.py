@@ -40,7 +40,8 @@ def _sp(i, max_tokens=6):
 def _engine_cfg(model=None, **kw):
     from dgi.engine import EngineConfig
     ckpt = os.environ.get("DGI_TEST_CKPT") or None
-    base = dict(model=model or os.environ.get("DGI_TEST_MODEL", MODEL), model_path=ckpt, device="cpu",
+    base = dict(model=model or os.environ.get("DGI_TEST_MODEL", MODEL), model_path=ckpt,
+                device=os.environ.get("DGI_TEST_DEVICE", "cpu"),
                 num_blocks=128, max_num_seqs=8, max_model_len=256, max_num_batched_tokens=64,
                 enable_prefix_caching=False)
     if ckpt:
@@ -111,11 +112,12 @@ def _pp_body(rank, world):
         while eng.has_unfinished():
             eng.step()
         eng.stop_stages()
-        return [r.output for r in reqs]
+        return {"out": [r.output for r in reqs],
+                "replays": eng.sgraphs.replays if eng.sgraphs is not None else 0}
     w = StageWorker(cfg, f, ranks)
     assert w.run() == "stop"
     f.flush()
-    return None
+    return {"replays": w.sgraphs.replays if w.sgraphs is not None else 0}
 
 
 def _pd_body(rank, world):
@@ -269,7 +271,7 @@ def test_capacity_planner_balances_roles():
 def test_pipeline_matches_single_process(world):
     ref = _reference_outputs()
     out = _spawn("_pp_body", world)
-    assert out[0] == ref
+    assert out[0]["out"] == ref
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -353,7 +355,7 @@ def test_pipeline_sampled_top_k_top_p_matches_single_process(monkeypatch):
     ref = _reference_outputs()
     assert ref != _greedy_reference()          # sampling actually changes the tokens
     out = _spawn("_pp_body", 2)
-    assert out[0] == ref
+    assert out[0]["out"] == ref
 
 
 def test_pdpp_sampled_top_k_top_p_matches_single_process(monkeypatch):
@@ -404,7 +406,7 @@ def test_pipeline_stages_load_disjoint_layers_from_checkpoint(tiny_ckpt, monkeyp
     monkeypatch.setenv("DGI_TEST_CKPT", tiny_ckpt)
     ref = _reference_outputs()
     out = _spawn("_pp_body", 2)
-    assert out[0] == ref
+    assert out[0]["out"] == ref
 
 
 def test_tensor_parallel_loads_row_and_column_slices_from_checkpoint(tiny_ckpt, monkeypatch):
