@@ -233,6 +233,9 @@ class GraphRunner:
         self.host_in = torch.zeros(maxb * (self.NSEG + maxw), dtype=torch.int32).pin_memory()
         self.host_out = torch.zeros(maxb, dtype=torch.long).pin_memory()
         self.captured = False
+        # optional EAGLE-3 feature tap captured with the step: (layer ids, fuse fn) -> [b, H] per bucket
+        self.features = None
+        self.feats_out: dict = {}
 
     def _meta(self, b):
         r = self.r
@@ -242,7 +245,17 @@ class GraphRunner:
                         num_prefill_tokens=0, logits_indices=None)
 
     def _body(self, b):
-        logits = self.r.model.forward(self._meta(b), input_ids=self.ids[:b])
+        m = self.r.model
+        if self.features is not None:
+            layers, fuse = self.features
+            m.capture_layers, m.captured = tuple(layers), {}
+            try:
+                logits = m.forward(self._meta(b), input_ids=self.ids[:b])
+                self.feats_out[b] = fuse(torch.cat([m.captured[li] for li in layers], dim=-1))
+            finally:
+                m.capture_layers, m.captured = (), {}
+        else:
+            logits = m.forward(self._meta(b), input_ids=self.ids[:b])
         ops.sample(logits, self.temps[:b], self.seeds[:b], 0, out=self.out[:b],
                    top_k=self.topk[:b], top_p=self.topp[:b])
 
@@ -307,6 +320,11 @@ class GraphRunner:
         self.topp[:b].copy_(dseg[7].view(torch.float32))
         self.bt[:b].copy_(dev[S * b:].view(b, maxw))
         self.graphs[b].replay()
+        self.last_bucket = b
         self.host_out[:b].copy_(self.out[:b], non_blocking=True)
         torch.cuda.current_stream().synchronize()
         return self.host_out[:n].tolist()
+
+    def last_features(self, n: int) -> torch.Tensor:
+        """Fused EAGLE-3 features of the last replay's first ``n`` rows (feature tap on)."""
+        return self.feats_out[self.last_bucket][:n]

@@ -19,9 +19,26 @@ implementation whose hot paths run on the hand-written HIP kernels:
   greedy acceptance of the longest matching root path plus the bonus token
   by ``dgi_tree_verify``; accepted KV is compacted in place (slot copy).
 
-Greedy (temperature 0) requests speculate; sampled requests decode normally
-in the same engine.  Output is token-for-token identical to non-speculative
-greedy decoding (the target decides every token).
+* **Sampled requests** (temperature > 0, top-k / top-p) speculate too, with
+  *coupled* verification: every tree node gets the target's own sample for
+  its output position — the same Gumbel-max draw (request seed, output index)
+  non-speculative decoding makes — and a drafted child is accepted iff it
+  equals its parent's target sample.  Every emitted token is therefore
+  exactly the token plain sampled decoding would emit (lossless, not merely
+  equal in distribution), and the acceptance probability at a node is the
+  target mass of its drafted children — the most any lossless verifier can
+  accept for a fixed candidate set.  Greedy rows are the temperature-0 case.
+* **Adaptive depth** (reference ``_adapt_depth``, worker/engines/speculative.py:
+  456-463): the active tree depth moves down when the step's acceptance rate
+  is under ``min_accept_rate`` and up when it is over ``raise_accept_rate``.
+* **Auto-off**: the engine times speculative and plain steps per batch
+  bucket; when speculation costs more per generated token than plain
+  decoding it switches to plain hipGraph decode steps (which still tap the
+  EAGLE-3 features) and re-probes periodically, so it is never slower than
+  plain decoding for long.
+
+Output is token-for-token identical to non-speculative decoding (the target
+decides every token).
 """
 from __future__ import annotations
 
@@ -50,10 +67,18 @@ class SpecConfig:
     topk: int = 4             # children per frontier node K (<= 16, dgi_topk)
     feature_layers: Optional[tuple] = None  # default: (2, L//2, L-3)
     graphs: bool = True       # hipGraph-capture the tree verify pass per batch bucket (GPU)
+    adaptive_depth: bool = True       # reference SpeculativeConfig.adaptive_depth
+    min_accept_rate: float = 0.3      # reference SpeculativeConfig.min_accept_rate: shrink below it
+    raise_accept_rate: float = 0.7    # grow above it (reference _adapt_depth)
+    auto_off: bool = True             # fall back to plain decode while speculation is slower
+    probe_every: int = 48             # plain steps between speculation re-probes
 
     @property
     def num_nodes(self) -> int:
         return 1 + self.width * self.depth
+
+    def nodes(self, depth: int) -> int:
+        return 1 + self.width * depth
 
     def validate(self) -> None:
         if self.num_nodes > 64:
@@ -221,12 +246,18 @@ class _VerifyGraph:
     attention), argmax and ``tree_verify``.  Rows past the live batch are
     padding that reads/writes only the reserved scratch page 0."""
 
-    def __init__(self, eng: "SpecEngine", Rb: int):
+    def __init__(self, eng: "SpecEngine", Rb: int, depth: int):
         sp, run = eng.spec, eng.runner
-        N, dev = sp.num_nodes, eng.device
+        N, dev = sp.nodes(depth), eng.device
         self.eng = eng
+        self.depth = depth
         self.Rb, self.N, self.maxw = Rb, N, run.max_blocks
         T = Rb * N
+        # per-node sampling parameters of the coupled verification (temperature 0 = argmax)
+        self.temps = torch.zeros(T, dtype=torch.float32, device=dev)
+        self.seeds = torch.zeros(T, dtype=torch.long, device=dev)
+        self.topk = torch.zeros(T, dtype=torch.long, device=dev)
+        self.topp = torch.ones(T, dtype=torch.float32, device=dev)
         self.n_dyn = 2 * T + Rb * self.maxw + Rb            # positions, slots, block tables, ctx
         self.host = torch.zeros(self.n_dyn, dtype=torch.int32).pin_memory()
         self.dyn = torch.zeros(self.n_dyn, dtype=torch.int32, device=dev)
@@ -270,8 +301,8 @@ class _VerifyGraph:
                         num_prefill_tokens=self.Rb * self.N, pre_block_tables=self.d_bt, pre_cu_seqlens=self.cu,
                         pre_context_lens=self.d_ctx, pre_tiles=self.tiles, tree_mask=anc, tree_n=self.N)
         logits, feats = eng._forward_capture(meta, self.tok.view(-1))
-        tgt = logits.argmax(dim=-1).view(self.Rb, self.N)
-        acc, path, toks = ops.tree_verify(self.par, self.tok, tgt, anc, depth, eng.spec.depth + 1)
+        tgt = ops.sample(logits, self.temps, self.seeds, 0, top_k=self.topk, top_p=self.topp).view(self.Rb, self.N)
+        acc, path, toks = ops.tree_verify(self.par, self.tok, tgt, anc, depth, self.depth + 1)
         return acc, path, toks, feats
 
     @torch.inference_mode()
@@ -288,8 +319,16 @@ class _VerifyGraph:
         with torch.cuda.graph(self.graph, pool=eng._graph_pool):
             self.out = self._body()
 
-    def run(self, R: int, tok: torch.Tensor, par: torch.Tensor, pos, slots, brows, ctx):
+    def run(self, R: int, tok: torch.Tensor, par: torch.Tensor, pos, slots, brows, ctx, samp):
         T, N, maxw = self.Rb * self.N, self.N, self.maxw
+        temps, seeds, topk, topp = samp
+        n = R * N
+        self.temps[:n].copy_(temps, non_blocking=True)
+        self.seeds[:n].copy_(seeds, non_blocking=True)
+        self.topk[:n].copy_(topk, non_blocking=True)
+        self.topp[:n].copy_(topp, non_blocking=True)
+        if n < T:
+            self.temps[n:].zero_()
         h = self.host.numpy()
         h[:R * N] = pos
         h[T:T + R * N] = slots
@@ -320,10 +359,10 @@ class _DraftGraph:
     round trip.  Inputs: root hidden states and last tokens; outputs: tree
     tokens and parents.  Padding rows use the scratch page 0."""
 
-    def __init__(self, eng: "SpecEngine", Rb: int):
+    def __init__(self, eng: "SpecEngine", Rb: int, depth: int):
         sp, run = eng.spec, eng.runner
         self.eng, self.Rb, self.maxw = eng, Rb, run.max_blocks
-        self.W, self.D, self.K, self.N = sp.width, sp.depth, sp.topk, sp.num_nodes
+        self.W, self.D, self.K, self.N = sp.width, depth, sp.topk, sp.nodes(depth)
         dev = eng.device
         H = eng.model_cfg.hidden_size
         self.ms = [self.W * (d - 1) for d in range(2, self.D + 1)]
@@ -435,11 +474,10 @@ class _DraftGraph:
 
 
 class SpecEngine(LLMEngine):
-    """``LLMEngine`` with EAGLE-3 tree speculation for greedy requests."""
+    """``LLMEngine`` with EAGLE-3 tree speculation (greedy and sampled requests)."""
 
     def __init__(self, cfg: EngineConfig, spec: Optional[SpecConfig] = None, model_cfg: Optional[ModelConfig] = None,
                  model=None, draft: Optional[Eagle3Draft] = None):
-        cfg = dataclasses.replace(cfg, use_graphs=False)
         super().__init__(cfg, model_cfg, model)
         self.spec = spec or SpecConfig()
         self.spec.validate()
@@ -447,7 +485,7 @@ class SpecEngine(LLMEngine):
         self.feature_layers = tuple(self.spec.feature_layers or default_feature_layers(L))
         self.draft = draft or Eagle3Draft(self.model, self.pool.num_blocks, self.pool.block_size)
         self.spec_stats = {"spec_steps": 0, "spec_rows": 0, "accepted": 0, "spec_tokens": 0, "draft_s": 0.0,
-                           "verify_s": 0.0}
+                           "verify_s": 0.0, "plain_steps": 0, "switches_off": 0, "depth_changes": 0}
         # measurement aid: rid -> known greedy continuation; the depth-d node of
         # the first chain is replaced by it (kept with probability oracle_accept)
         self.oracle: Optional[dict] = None
@@ -456,16 +494,28 @@ class SpecEngine(LLMEngine):
         self._vgraphs: dict = {}
         self._dgraphs: dict = {}
         self._graph_pool = torch.cuda.graph_pool_handle() if self.device.type == "cuda" else None
+        # plain decode steps replay the engine's hipGraphs with the EAGLE-3 feature tap on
+        if self.runner.graphs is not None:
+            self.runner.graphs.features = (self.feature_layers, self.draft.fuse)
+        # adaptive depth + auto-off controller
+        self.cur_depth = self.spec.depth
+        self.spec_on = True
+        self._mode_steps = 0
+        self._probe = False
+        self._cost: dict = {}       # (mode, bucket) -> EMA seconds per generated token
+
+    def _bucket(self, R: int) -> int:
+        return next((b for b in VERIFY_BUCKETS if b >= R), VERIFY_BUCKETS[-1])
 
     def _draft_graph(self, R: int) -> Optional[_DraftGraph]:
-        if not (self.spec.graphs and self.device.type == "cuda" and self.spec.depth >= 2):
+        if not (self.spec.graphs and self.device.type == "cuda" and self.cur_depth >= 2):
             return None
         Rb = next((b for b in VERIFY_BUCKETS if b >= R), None)
         if Rb is None:
             return None
-        g = self._dgraphs.get(Rb)
+        g = self._dgraphs.get((Rb, self.cur_depth))
         if g is None:
-            g = self._dgraphs[Rb] = _DraftGraph(self, Rb)
+            g = self._dgraphs[(Rb, self.cur_depth)] = _DraftGraph(self, Rb, self.cur_depth)
         return g
 
     def _verify_graph(self, R: int) -> Optional[_VerifyGraph]:
@@ -474,14 +524,14 @@ class SpecEngine(LLMEngine):
         Rb = next((b for b in VERIFY_BUCKETS if b >= R), None)
         if Rb is None:
             return None
-        g = self._vgraphs.get(Rb)
+        g = self._vgraphs.get((Rb, self.cur_depth))
         if g is None:
-            g = self._vgraphs[Rb] = _VerifyGraph(self, Rb)
+            g = self._vgraphs[(Rb, self.cur_depth)] = _VerifyGraph(self, Rb, self.cur_depth)
         return g
 
     # ------------------------------------------------------------------ helpers
     def _eligible(self, r: Request) -> bool:
-        return r.params.greedy and not r.in_prefill and not r.busy
+        return not r.in_prefill and not r.busy
 
     def _state(self, r: Request) -> _SpecState:
         if r.spec_state is None:
@@ -503,16 +553,59 @@ class SpecEngine(LLMEngine):
     def _append_feats(self, r: Request, start: int, feats: torch.Tensor) -> None:
         st = self._state(r)
         if st.feat is None or st.feat_start + st.feat.shape[0] != start:
-            st.feat, st.feat_start = feats, start
+            st.feat, st.feat_start = feats.clone(), start
         else:
             st.feat = torch.cat([st.feat, feats])
+
+    # ------------------------------------------------------------------ controller
+    def _record(self, mode: str, R: int, seconds: float, tokens: int) -> None:
+        if tokens <= 0:
+            return
+        key = (mode, self._bucket(R))
+        c = seconds / tokens
+        old = self._cost.get(key)
+        self._cost[key] = c if old is None else 0.7 * old + 0.3 * c
+
+    def _adapt_depth(self, accept_rate: float) -> None:
+        """Reference semantics (worker/engines/speculative.py:456-463)."""
+        if not self.spec.adaptive_depth:
+            return
+        d = self.cur_depth
+        if accept_rate < self.spec.min_accept_rate:
+            d = max(1, d - 1)
+        elif accept_rate > self.spec.raise_accept_rate:
+            d = min(self.spec.depth, d + 1)
+        if d != self.cur_depth:
+            self.cur_depth = d
+            self.spec_stats["depth_changes"] += 1
+
+    def _control(self, R: int) -> None:
+        """Auto-off: after a few steps in a mode compare the measured cost per
+        generated token of speculation and plain decode at this batch bucket."""
+        if not self.spec.auto_off or R == 0:
+            return
+        self._mode_steps += 1
+        b = self._bucket(R)
+        cs, cp = self._cost.get(("spec", b)), self._cost.get(("plain", b))
+        if self.spec_on:
+            if self._mode_steps < 4:
+                return
+            if cp is None or cs is None or cs > cp:
+                # no plain reference yet (probe it), or speculation is the slower mode
+                self.spec_on, self._mode_steps = False, 0
+                self._probe = cp is None
+                if cs is not None and cp is not None:
+                    self.spec_stats["switches_off"] += 1
+        else:
+            if self._mode_steps >= (3 if self._probe else self.spec.probe_every):
+                self.spec_on, self._mode_steps, self._probe = True, 0, False
 
     # ------------------------------------------------------------------ step
     def step(self) -> list:
         t0 = time.perf_counter()
         self.model.kv_cache = self.pool.kv
         outs: list[StepOutput] = []
-        spec_reqs = [r for r in self.scheduler.running if self._eligible(r)]
+        spec_reqs = [r for r in self.scheduler.running if self._eligible(r)] if self.spec_on else []
         for r in spec_reqs:
             r.busy = True            # keep them out of the normal batch
         try:
@@ -521,10 +614,21 @@ class SpecEngine(LLMEngine):
             for r in spec_reqs:
                 r.busy = False
         if not sb.empty:
-            outs += self._normal_step(sb)
+            tn = time.perf_counter()
+            o = self._normal_step(sb)
+            outs += o
+            if not sb.prefill and not spec_reqs:
+                self._record("plain", len(sb.decode), time.perf_counter() - tn, len(o))
+                self.spec_stats["plain_steps"] += 1
+                self._control(len(sb.decode))
         live = [r for r in spec_reqs if r in self.scheduler.running and self._eligible(r)]
         if live:
-            outs += self._spec_step(live)
+            ts = time.perf_counter()
+            o = self._spec_step(live)
+            outs += o
+            if sb.empty:
+                self._record("spec", len(live), time.perf_counter() - ts, len(o))
+            self._control(len(live))
         self.stats["step_time"] += time.perf_counter() - t0
         return outs
 
@@ -532,23 +636,55 @@ class SpecEngine(LLMEngine):
     def _normal_step(self, sb) -> list:
         run = self.runner
         run.step_id += 1
+        g = run.graphs
+        if g is not None and not sb.prefill and sb.decode and len(sb.decode) <= g.max_bucket:
+            # plain decode: hipGraph replay with the feature tap
+            pos = [r.num_computed for r in sb.decode]
+            toks = g.run(sb)
+            feats = g.last_features(len(sb.decode))
+            for i, r in enumerate(sb.decode):
+                self._append_feats(r, pos[i], feats[i: i + 1])
+            return self._apply(sb, list(sb.decode), toks)
         flat, hdr, sampled = run.build_host(sb)
         ids, meta, samp = run.meta_from_device(run.to_device(flat), hdr)
         logits, feats = self._forward_capture(meta, ids)
         nd = len(sb.decode)
+        for i, r in enumerate(sb.decode):
+            self._append_feats(r, r.num_computed, feats[i: i + 1])
         row = nd
         for c in sb.prefill:
-            if c.req.params.greedy:
-                self._append_feats(c.req, c.start, feats[row: row + c.length])
+            self._append_feats(c.req, c.start, feats[row: row + c.length])
             row += c.length
         if not sampled:
             return self._apply(sb, [], [])
         return self._apply(sb, sampled, samp.sample(logits).tolist())
 
+    def _node_sampling(self, reqs: list, depth_np: np.ndarray):
+        """Per tree node (row-major [R, N]) temperature / seed / top-k / top-p of the
+        coupled verification: node of depth d samples output index len(output) + d
+        with the seed plain decoding uses for that index."""
+        R, N = len(reqs), len(depth_np)
+        temps = np.empty((R, N), np.float32)
+        seeds = np.empty((R, N), np.int64)
+        topk = np.zeros((R, N), np.int64)
+        topp = np.ones((R, N), np.float32)
+        for i, r in enumerate(reqs):
+            p = r.params
+            temps[i] = p.temperature
+            seeds[i] = (r.seed * 1000003 + len(r.output) + depth_np) & 0x7FFFFFFF
+            if p.needs_filter:
+                topk[i] = max(0, p.top_k)
+                topp[i] = p.top_p
+        out = [torch.from_numpy(x.ravel()) for x in (temps, seeds, topk, topp)]
+        if self.device.type == "cuda":
+            out = [x.pin_memory().to(self.device, non_blocking=True) for x in out]
+        return out
+
     @torch.inference_mode()
     def _spec_step(self, reqs: list) -> list:
         sp = self.spec
-        W, K, D, N = sp.width, sp.topk, sp.depth, sp.num_nodes
+        D = self.cur_depth
+        W, K, N = sp.width, sp.topk, sp.nodes(D)
         bs = self.pool.block_size
         dev = self.device
         run = self.runner
@@ -569,7 +705,6 @@ class SpecEngine(LLMEngine):
         # ---- 1) draft catch-up over committed positions [draft_len, n-1]
         pos, slots, cu, ctx, ids, feat_rows, brows = [], [], [0], [], [], [], []
         H = self.model_cfg.hidden_size
-        zero = torch.zeros(1, H, device=dev, dtype=self.cfg.dtype)
         for r in reqs:
             st = self._state(r)
             n = r.total_len
@@ -577,20 +712,14 @@ class SpecEngine(LLMEngine):
             p0 = min(st.draft_len, n - 1)
             blk = np.asarray(r.blocks, np.int64)
             ps = np.arange(p0, n)
-            pos.extend(ps.tolist())
-            slots.extend((blk[ps // bs] * bs + ps % bs).tolist())
+            pos.append(ps)
+            slots.append(blk[ps // bs] * bs + ps % bs)
             ids.extend(toks[p0:n])
             cu.append(cu[-1] + len(ps))
             ctx.append(n)
             brows.append(r.blocks)
-            # feature of position p-1 for every row p
-            for p in ps.tolist():
-                q = p - 1
-                if st.feat is not None and st.feat_start <= q < st.feat_start + st.feat.shape[0]:
-                    feat_rows.append(st.feat[q - st.feat_start: q - st.feat_start + 1])
-                else:
-                    feat_rows.append(zero)
-        meta = _varlen_meta(run, pos, slots, brows, cu, ctx, dev)
+            feat_rows.append(self._feature_rows(st, p0 - 1, n - 1, H))
+        meta = _varlen_meta(run, np.concatenate(pos), np.concatenate(slots), brows, cu, ctx, dev)
         d_ids = torch.tensor(ids, dtype=torch.long).pin_memory().to(dev, non_blocking=True) \
             if dev.type == "cuda" else torch.tensor(ids, dtype=torch.long)
         g = self.draft.forward(d_ids, torch.cat(feat_rows), meta)
@@ -600,34 +729,36 @@ class SpecEngine(LLMEngine):
             r.spec_state.draft_len = r.total_len
         # ---- 2) tree drafting
         n_vec = np.asarray([r.total_len for r in reqs], np.int64)
-        depth_np = np.concatenate([[0]] + [[d] * W for d in range(1, D + 1)])
+        depth_np = np.concatenate([[0]] + [[d] * W for d in range(1, D + 1)]).astype(np.int64)
         dg = self._draft_graph(R)
         if dg is not None:
             tok, par = dg.run(R, g_root, [r.all_tokens()[-1] for r in reqs], n_vec, brows)
         else:
-            tok, par = self._draft_tree_eager(reqs, g_root, n_vec, depth_np, brows)
+            tok, par = self._draft_tree_eager(reqs, g_root, n_vec, depth_np, brows, D)
         if self.oracle:
-            self._apply_oracle(reqs, tok, par, n_vec)
+            self._apply_oracle(reqs, tok, par, n_vec, D)
         self.spec_stats["draft_s"] += time.perf_counter() - td
         tv = time.perf_counter()
-        # ---- 3) target verify over all N tree nodes
+        # ---- 3) target verify over all N tree nodes (coupled sampling, greedy = temperature 0)
+        samp = self._node_sampling(reqs, depth_np)
         vpos, vslots, vctx, vcu = [], [], [], [0]
         for i, r in enumerate(reqs):
             n = int(n_vec[i])
             blk = np.asarray(r.blocks, np.int64)
-            vpos.extend((n - 1 + depth_np).tolist())
+            vpos.append(n - 1 + depth_np)
             sl = n - 1 + np.arange(N)
-            vslots.extend((blk[sl // bs] * bs + sl % bs).tolist())
+            vslots.append(blk[sl // bs] * bs + sl % bs)
             vctx.append(n - 1 + N)
             vcu.append(vcu[-1] + N)
+        vpos, vslots = np.concatenate(vpos), np.concatenate(vslots)
         vg = self._verify_graph(R)
         if vg is not None:
-            acc, path, toks, feats = vg.run(R, tok, par, vpos, vslots, brows, vctx)
+            acc, path, toks, feats = vg.run(R, tok, par, vpos, vslots, brows, vctx, samp)
         else:
             anc, depth = ops.tree_mask(par)
             vm = _varlen_meta(run, vpos, vslots, brows, vcu, vctx, dev, tree_mask=anc, tree_n=N)
             logits, feats = self._forward_capture(vm, tok.view(-1))
-            tgt = logits.argmax(dim=-1).view(R, N)
+            tgt = ops.sample(logits, samp[0], samp[1], 0, top_k=samp[2], top_p=samp[3]).view(R, N)
             acc, path, toks = ops.tree_verify(par, tok, tgt, anc, depth, D + 1)
         acc_h = acc.cpu().tolist()
         path_h = path.cpu().numpy()
@@ -679,11 +810,25 @@ class SpecEngine(LLMEngine):
                     break
         self.spec_stats["spec_steps"] += 1
         self.spec_stats["spec_rows"] += R
+        self._adapt_depth(sum(acc_h) / (R * D))
         return outs
 
-    def _draft_tree_eager(self, reqs, g_root, n_vec, depth_np, brows):
+    def _feature_rows(self, st: _SpecState, q0: int, q1: int, H: int) -> torch.Tensor:
+        """Fused target features of positions [q0, q1) (zeros where unknown)."""
+        n = q1 - q0
+        f = st.feat
+        if f is not None and st.feat_start <= q0 and q1 <= st.feat_start + f.shape[0]:
+            return f[q0 - st.feat_start: q1 - st.feat_start]
+        out = torch.zeros(n, H, dtype=self.cfg.dtype, device=self.device)
+        if f is not None:
+            lo, hi = max(q0, st.feat_start), min(q1, st.feat_start + f.shape[0])
+            if lo < hi:
+                out[lo - q0: hi - q0] = f[lo - st.feat_start: hi - st.feat_start]
+        return out
+
+    def _draft_tree_eager(self, reqs, g_root, n_vec, depth_np, brows, D):
         """Tree drafting, one host-built metadata copy per depth (CPU / no graphs)."""
-        W, D, K, N = self.spec.width, self.spec.depth, self.spec.topk, self.spec.num_nodes
+        W, K, N = self.spec.width, self.spec.topk, self.spec.nodes(D)
         R, H = g_root.shape
         dev, run, bs = self.device, self.runner, self.pool.block_size
         g = g_root
@@ -729,8 +874,8 @@ class SpecEngine(LLMEngine):
             score[:, base: base + W] = best
         return tok, par
 
-    def _apply_oracle(self, reqs, tok, par, n_vec) -> None:
-        W, D = self.spec.width, self.spec.depth
+    def _apply_oracle(self, reqs, tok, par, n_vec, D) -> None:
+        W = self.spec.width
         V = self.model_cfg.vocab_size
         rows = np.zeros((len(reqs), D), np.int64)
         for i, r in enumerate(reqs):
@@ -750,7 +895,8 @@ class SpecEngine(LLMEngine):
     def acceptance(self) -> dict:
         s = self.spec_stats
         rows = max(1, s["spec_rows"])
-        return {"mean_accepted": s["accepted"] / rows, "tokens_per_step": s["spec_tokens"] / rows, **s}
+        return {"mean_accepted": s["accepted"] / rows, "tokens_per_step": s["spec_tokens"] / rows,
+                "current_depth": self.cur_depth, "spec_on": self.spec_on, **s}
 
 
 # ---------------------------------------------------------------------------

@@ -52,11 +52,16 @@ def main():
                          "permuted copy of the embedding / sqrt(H), so the next token is a confident function "
                          "of the current one, like a trained model's top-1 margins (same FLOPs and shapes)")
     ap.add_argument("--no-verify-graph", action="store_true", help="eager verify pass (A/B for the hipGraph)")
+    ap.add_argument("--no-auto-off", action="store_true", help="always speculate (no plain-decode fallback)")
+    ap.add_argument("--no-adaptive", action="store_true", help="fixed tree depth")
+    ap.add_argument("--sampled", action="store_true",
+                    help="also run seeded temperature 0.8 / top-k 50 / top-p 0.9 requests (coupled verification)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     cfg = EngineConfig(model=a.model, device="cuda", max_num_seqs=64, max_num_batched_tokens=8192,
                        max_model_len=2048, kv_fraction=0.5)
-    spec = SpecEngine(cfg, SpecConfig(depth=a.depth, width=a.width, topk=a.topk, graphs=not a.no_verify_graph))
+    spec = SpecEngine(cfg, SpecConfig(depth=a.depth, width=a.width, topk=a.topk, graphs=not a.no_verify_graph,
+                                      auto_off=not a.no_auto_off, adaptive_depth=not a.no_adaptive))
     if a.target == "peaked":
         m = spec.model
         perm = torch.randperm(m.embed.shape[0], generator=torch.Generator().manual_seed(7)).to(m.embed.device)
@@ -87,6 +92,29 @@ def main():
                "tokens_per_step": round(acc["tokens_per_step"], 3), "identical": out == ref,
                "max_greedy_gap": round(gap, 4),
                "draft_s": round(acc["draft_s"], 3), "verify_s": round(acc["verify_s"], 3)}
+        row["controller"] = {k: acc[k] for k in ("current_depth", "spec_on", "plain_steps", "switches_off",
+                                                  "depth_changes")}
+        if a.sampled:
+            def spm(i):
+                return SamplingParams(max_tokens=a.output_len, temperature=0.8, top_k=50, top_p=0.9,
+                                      ignore_eos=True, seed=1000 + i)
+
+            def run(eng):
+                rs = [eng.add_request(pr, spm(i)) for i, pr in enumerate(prompts)]
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                while eng.has_unfinished():
+                    eng.step()
+                torch.cuda.synchronize()
+                return [r.output for r in rs], time.perf_counter() - t1
+            sref, ts_base = run(base)
+            spec.spec_stats.update(spec_steps=0, spec_rows=0, accepted=0, spec_tokens=0)
+            sout, ts_spec = run(spec)
+            sa = spec.acceptance()
+            row["sampled"] = {"plain_tok_s": round(toks / ts_base, 1), "spec_tok_s": round(toks / ts_spec, 1),
+                              "speedup": round(ts_base / ts_spec, 3), "mean_accepted": round(sa["mean_accepted"], 3),
+                              "token_agreement": round(sum(int(x == y) for o, q in zip(sout, sref)
+                                                           for x, y in zip(o, q)) / max(1, toks), 4)}
         # acceptance-controlled runs: the first tree chain is replaced by the known greedy
         # continuation, each token kept with probability p (ceiling / sensitivity of the machinery)
         for p in a.oracle_accept:
@@ -96,7 +124,8 @@ def main():
             rs = [spec.add_request(pr, sp) for pr in prompts]
             for r, o in zip(rs, ref):
                 reqs_rid[r.rid] = o
-            spec.spec_stats.update(spec_steps=0, spec_rows=0, accepted=0, spec_tokens=0, draft_s=0.0, verify_s=0.0)
+            spec.spec_stats.update(spec_steps=0, spec_rows=0, accepted=0, spec_tokens=0, draft_s=0.0, verify_s=0.0,
+                                   plain_steps=0)
             torch.cuda.synchronize()
             t1 = time.perf_counter()
             while spec.has_unfinished():
@@ -107,7 +136,9 @@ def main():
             ao = spec.acceptance()
             row[f"oracle_p{p}"] = {"tok_s": round(toks / t_o, 1), "speedup": round(t_base / t_o, 3),
                                    "mean_accepted": round(ao["mean_accepted"], 3),
-                                   "identical": [r.output for r in rs] == ref}
+                                   "identical": [r.output for r in rs] == ref,
+                                   "spec_steps": ao["spec_steps"], "plain_steps": ao["plain_steps"],
+                                   "depth": ao["current_depth"]}
         print(json.dumps(row), flush=True)
         rows.append(row)
     res = {"model": a.model, "tree": {"depth": a.depth, "width": a.width, "topk": a.topk}, "target": a.target,

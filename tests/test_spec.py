@@ -12,7 +12,8 @@ from dgi.sched.request import SamplingParams
 from dgi.spec.eagle3 import SpecConfig, SpecEngine, kv_slot_copy, train_draft
 
 
-def _engines(model="llama-tiny", device="cpu", spec=SpecConfig(depth=3, width=2, topk=3)):
+def _engines(model="llama-tiny", device="cpu", spec=None):
+    spec = spec or SpecConfig(depth=3, width=2, topk=3, auto_off=False, adaptive_depth=False)
     cfg = EngineConfig(model=model, device=device, max_num_seqs=8, max_num_batched_tokens=256, max_model_len=512,
                        use_graphs=False)
     base = LLMEngine(cfg)
@@ -53,6 +54,100 @@ def test_spec_mixed_greedy_and_sampled_requests():
     assert len(r1.output) == 10
 
 
+def _sampled(i, n=24):
+    return SamplingParams(max_tokens=n, temperature=0.9, top_k=20, top_p=0.9, ignore_eos=True, seed=100 + i)
+
+
+def _gen(eng, prompts, mk):
+    reqs = [eng.add_request(p, mk(i)) for i, p in enumerate(prompts)]
+    while eng.has_unfinished():
+        eng.step()
+    return [r.output for r in reqs]
+
+
+def test_spec_sampled_requests_are_identical_to_plain_sampling():
+    """Coupled verification: every tree node is checked against the target's own
+    seeded sample for that output index, so speculative sampled decoding emits
+    exactly the tokens plain sampled decoding emits."""
+    base, se = _engines()
+    train_draft(se, steps=60, batch=8, prompt_len=16, gen_len=48, num_seqs=16)
+    ref = _gen(base, _prompts(), _sampled)
+    se.spec_stats.update(spec_steps=0, spec_rows=0, accepted=0, spec_tokens=0)
+    assert _gen(se, _prompts(), _sampled) == ref
+    assert se.spec_stats["spec_steps"] > 0 and se.spec_stats["accepted"] > 0
+
+
+def test_sampler_distribution_chi_square():
+    """The Gumbel-max sampler (the draw plain and speculative decoding share)
+    follows softmax(logits / T) renormalised over the top-k / top-p set."""
+    from scipy.stats import chisquare
+
+    from dgi import ops
+    logits = torch.tensor([[2.0, 1.5, 1.0, 0.5, 0.0, -0.5, -1.0, -3.0]])
+    n = 20000
+    lg = logits.expand(n, -1).contiguous()
+    temps = torch.full((n,), 0.8)
+    seeds = torch.arange(n)
+    for k, p in ((0, 1.0), (5, 1.0), (0, 0.8)):
+        tk, tp = torch.full((n,), k), torch.full((n,), p)
+        out = ops.sample(lg, temps, seeds, 3, top_k=tk, top_p=tp)
+        kept = torch.isfinite(ops.apply_top_k_top_p(logits, tk[:1], tp[:1], temps[:1]))[0]
+        prob = torch.softmax(torch.where(kept, logits[0] / 0.8, torch.tensor(-float("inf"))), -1)
+        obs = torch.bincount(out, minlength=8).double()
+        assert int(obs[~kept].sum()) == 0
+        exp = prob[kept].double()
+        exp = (exp / exp.sum() * obs[kept].sum()).numpy()
+        stat, pval = chisquare(obs[kept].numpy(), exp)
+        assert pval > 1e-3, (k, p, stat, pval)
+
+
+def test_adaptive_depth_follows_acceptance():
+    """Reference _adapt_depth: depth shrinks under min_accept_rate, grows over 0.7."""
+    base, se = _engines(spec=SpecConfig(depth=4, width=2, topk=3, auto_off=False, adaptive_depth=True))
+    sp = SamplingParams(max_tokens=30, temperature=0.0, ignore_eos=True)
+    prompts = _prompts(2)
+    ref = [r.output for r in base.generate(prompts, sp)]
+    # oracle drafts that are always right: depth stays at the maximum
+    se.oracle, se.oracle_accept = {}, 1.0
+    reqs = [se.add_request(p, sp) for p in prompts]
+    for r, o in zip(reqs, ref):
+        se.oracle[r.rid] = o
+    while se.has_unfinished():
+        se.step()
+    assert [r.output for r in reqs] == ref and se.cur_depth == 4
+    # oracle drafts that are always wrong: depth falls to 1
+    se.oracle_accept = 0.0
+    reqs = [se.add_request(p, sp) for p in prompts]
+    for r, o in zip(reqs, ref):
+        se.oracle[r.rid] = o
+    while se.has_unfinished():
+        se.step()
+    assert [r.output for r in reqs] == ref and se.cur_depth == 1
+    assert se.spec_stats["depth_changes"] >= 3
+
+
+def test_auto_off_switches_to_plain_when_speculation_is_slower():
+    base, se = _engines(spec=SpecConfig(depth=3, width=2, topk=3, auto_off=True, adaptive_depth=False,
+                                        probe_every=12))
+    sp = SamplingParams(max_tokens=40, temperature=0.0, ignore_eos=True)
+    prompts = _prompts(2)
+    ref = [r.output for r in base.generate(prompts, sp)]
+    real = se._record
+    # make speculation look 3x as expensive per token as plain decoding
+
+    def rec(mode, R, seconds, tokens):
+        real(mode, R, seconds * (3.0 if mode == "spec" else 1.0) * tokens / max(1, tokens), tokens)
+    se._record = rec
+    reqs = [se.add_request(p, sp) for p in prompts]
+    modes = []
+    while se.has_unfinished():
+        se.step()
+        modes.append(se.spec_on)
+    assert [r.output for r in reqs] == ref                       # lossless in both modes
+    assert se.spec_stats["plain_steps"] > 0 and se.spec_stats["switches_off"] >= 1
+    assert modes.count(False) > modes.count(True)
+
+
 def test_kv_slot_copy():
     kv = torch.randn(3, 2, 5, 2, 4, 8)
     ref = kv.clone()
@@ -69,7 +164,8 @@ def test_spec_gpu_greedy_trajectory():
     kernel) and verification (prefill kernel) may order bf16 near-ties
     differently, so exact equality is checked via the teacher-forced gap."""
     from dgi.spec.eagle3 import greedy_gap
-    base, se = _engines("llama-tiny-hd128", "cuda", SpecConfig(depth=4, width=3, topk=4))
+    base, se = _engines("llama-tiny-hd128", "cuda", SpecConfig(depth=4, width=3, topk=4, auto_off=False,
+                                                               adaptive_depth=False))
     sp = SamplingParams(max_tokens=32, temperature=0.0, ignore_eos=True)
     prompts = _prompts(4, 1000)
     train_draft(se, steps=80, batch=8, prompt_len=32, gen_len=96, num_seqs=32, random_seqs=32)

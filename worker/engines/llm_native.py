@@ -108,8 +108,9 @@ class NativeLLMEngine(LLMBaseEngine):
             # EAGLE-3 tree speculation for greedy requests (dgi.spec.eagle3)
             from dgi.spec.eagle3 import SpecConfig, SpecEngine
             sc = spec if isinstance(spec, dict) else {}
-            self.engine = SpecEngine(ecfg, SpecConfig(**{k: sc[k] for k in ("depth", "width", "topk")
-                                                          if k in sc}),
+            keys = ("depth", "width", "topk", "adaptive_depth", "min_accept_rate", "raise_accept_rate",
+                    "auto_off", "probe_every")
+            self.engine = SpecEngine(ecfg, SpecConfig(**{k: sc[k] for k in keys if k in sc}),
                                      model_cfg=mc)
             if sc.get("draft_path"):
                 from safetensors.torch import load_file

@@ -46,7 +46,8 @@ class SpeculativeConfig:
         from dgi.spec.eagle3 import SpecConfig
         w = max(1, min(self.tree_width, 16))
         d = max(1, min(self.tree_depth, 63 // w))
-        return SpecConfig(depth=d, width=w, topk=max(w, min(16, w + 1)))
+        return SpecConfig(depth=d, width=w, topk=max(w, min(16, w + 1)), adaptive_depth=self.adaptive_depth,
+                          min_accept_rate=self.min_accept_rate)
 
 
 @dataclass
