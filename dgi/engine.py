@@ -113,6 +113,8 @@ class LLMEngine:
         self.runner = ModelRunner(self.model, self.pool, cfg.max_num_seqs, cfg.max_model_len,
                                   cfg.max_num_batched_tokens, cfg.use_graphs, **rkw)
         self.requests: dict = {}
+        # optional callback(ScheduledBatch) between scheduling and execution (P/D streaming)
+        self.pre_execute = None
         self.stats = {"steps": 0, "prefill_tokens": 0, "decode_tokens": 0, "generated": 0,
                       "finished": 0, "step_time": 0.0}
         # MLP row padding measured on this GPU (hipBLASLt kernel-selection cliffs, dgi.runtime.gemm_pad)
@@ -152,6 +154,8 @@ class LLMEngine:
             sb = self.scheduler.schedule()
         if sb.empty:
             return []
+        if self.pre_execute is not None:
+            self.pre_execute(sb)
         with phase("execute", decode=len(sb.decode), prefill=len(sb.prefill)):
             res = self.runner.execute(sb)
         with phase("apply"):

@@ -72,6 +72,9 @@ class LlamaModel:
         self.reduce = None
         # MLP row padding (dgi.runtime.gemm_pad): T -> rows to run gate_up/down on
         self.mlp_pad = None
+        # called with the global layer id once that layer's KV is in the cache
+        # (P/D layer-streamed migration sends finished layers while later ones compute)
+        self.layer_hook = None
         self._pad_buf: Optional[torch.Tensor] = None
         self.load_info: Optional[dict] = None
         if checkpoint:
@@ -264,6 +267,8 @@ class LlamaModel:
                 self.reduce(h)
             if self.capture_layers and (self.layer_start + i) in self.capture_layers:
                 self.captured[self.layer_start + i] = h + residual
+            if self.layer_hook is not None:
+                self.layer_hook(self.layer_start + i)
         return h, residual
 
     def embed_tokens(self, input_ids: torch.Tensor) -> torch.Tensor:

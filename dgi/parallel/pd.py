@@ -30,8 +30,17 @@ SURVEY §3.5).  Here:
   preempted on the decode side.
 
 Control messages (int64[CTRL]) on the rendezvous store:
-  MIGRATE n_reqs total_blocks meta_len tok_len | CREDIT blocks seqs | DONE |
-  FINISHED rid tok code | TOKENS (rid tok code)*
+  MIGRATE n_reqs total_blocks meta_len tok_len chunk_layers | CREDIT blocks seqs | DONE |
+  FINISHED rid tok code | TOKENS (rid tok code)* | FIRST n (tok code)*
+
+Layer-streamed migration (``stream_layers`` = C > 0): the
+prefill rank announces the prompts that finish in a step BEFORE it runs
+(MIGRATE, first tokens unknown), and a model layer hook sends each C-layer
+group of their pages (kv_gather on the compute stream -> RCCL send on the comm
+stream) as soon as the step's forward has written those layers, so the
+transfer overlaps the remaining layers' compute; the first tokens follow in a
+FIRST message once sampled.  The receiving stages post one receive per group
+into the matching layer slice of their buffer.
 """
 from __future__ import annotations
 
@@ -53,7 +62,7 @@ from dgi.parallel.plan import NodeLayout
 from dgi.sched.request import Request, SamplingParams, Status
 from dgi.utils.trace import mark, phase
 
-MSG_MIGRATE, MSG_CREDIT, MSG_DONE, MSG_FINISHED, MSG_TOKENS = 1, 2, 3, 4, 5
+MSG_MIGRATE, MSG_CREDIT, MSG_DONE, MSG_FINISHED, MSG_TOKENS, MSG_FIRST = 1, 2, 3, 4, 5, 6
 REASONS = {0: None, 1: "length", 2: "stop"}
 CTRL = 8
 META_FIELDS = 11
@@ -89,13 +98,21 @@ def run_sync(coro):
     raise RuntimeError("coroutine suspended outside an event loop")
 
 
+def layer_groups(n_layers: int, chunk: int) -> list:
+    """[a, b) layer groups a stage receives a migration in (chunk 0: all at once)."""
+    if chunk <= 0:
+        return [(0, n_layers)]
+    return [(a, min(n_layers, a + chunk)) for a in range(0, n_layers, chunk)]
+
+
 def _blocks_for(n_tokens: int, bs: int) -> int:
     return (n_tokens + bs - 1) // bs
 
 
-def _req_meta(r: Request, nblocks: int) -> list:
+def _req_meta(r: Request, nblocks: int, first: Optional[int] = None) -> list:
     p = r.params
-    return [int(r.rid) & 0x7FFFFFFF, 0, len(r.prompt), r.output[0], nblocks, p.max_tokens,
+    return [int(r.rid) & 0x7FFFFFFF, 0, len(r.prompt), r.output[0] if first is None else first, nblocks,
+            p.max_tokens,
             int(np.float32(p.temperature).view(np.int32)), int(r.seed) & 0x7FFFFFFF, int(p.ignore_eos), p.top_k,
             int(np.float32(p.top_p).view(np.int32))]
 
@@ -105,7 +122,8 @@ class PrefillServer:
     migrates each finished prompt's KV to the decode replica chosen for it."""
 
     def __init__(self, cfg: EngineConfig, fabric: Fabric, layout: NodeLayout, seed_offset: int = 0,
-                 local_cap: int = 0, report_tokens: bool = False, router: Optional[int] = None):
+                 local_cap: int = 0, report_tokens: bool = False, router: Optional[int] = None,
+                 stream_layers: int = 8):
         self.f = fabric
         self.layout = layout
         self.drivers = list(layout.drivers)
@@ -156,6 +174,21 @@ class PrefillServer:
                 kv_cache_tokens_total=self.credit_total[d] * self.bs))
         self.migrator = m.KVCacheMigrator(self.pd)
         self.placed: dict = {d: collections.deque() for d in self.drivers}
+        # layer-streamed migration: C-layer groups leave while later layers compute
+        self.stream_layers = int(stream_layers)
+        self._streams: list = []       # this step's (driver, reqs, ids_t, {end layer: [(stage, c0, c1)]})
+        self.streamed_bytes = 0
+        if self.stream_layers > 0:
+            self.engine.pre_execute = self._plan_stream
+
+    @staticmethod
+    def chunk_plan(split: list, C: int) -> list:
+        """(stage, c0, c1) layer groups of at most C layers inside each stage slice, in layer order."""
+        out = []
+        for si, (a, b) in enumerate(split):
+            for c0 in range(a, b, C):
+                out.append((si, c0, min(b, c0 + C)))
+        return out
 
     # ------------------------------------------------------------------ API
     def submit(self, prompt: list, params: SamplingParams, rid=None) -> Request:
@@ -217,6 +250,83 @@ class PrefillServer:
             self.engine.scheduler.add(r)
             self.engine.requests[r.rid] = r
 
+    # ------------------------------------------------------------------ layer-streamed migration
+    def _plan_stream(self, sb) -> None:
+        """Before a step runs: announce the prompts whose prefill completes in it
+        and arm the layer hook that ships their pages group by group."""
+        self._streams = []
+        fin = [c.req for c in sb.prefill if c.sample and c.req.rid not in self.local and c.req.rid in self.target]
+        if not fin:
+            return
+        dev = self.f.device
+        by_d: dict = collections.defaultdict(list)
+        for r in fin:
+            by_d[self.target[r.rid][0]].append(r)
+        hooks_any = False
+        for d, rs in by_d.items():
+            ids, meta, toks = [], [], []
+            for r in rs:
+                nb = _blocks_for(len(r.prompt), self.bs)
+                ids += r.blocks[:nb]
+                meta += _req_meta(r, nb, first=-1) + [int(self.target[r.rid][1])]
+                toks += r.prompt
+            ids_t = torch.tensor(ids, dtype=torch.int32, device=dev)
+            self.ch[d].send([MSG_MIGRATE, len(rs), len(ids), len(meta), len(toks), self.stream_layers])
+            self.ch[d].send_var(np.asarray(meta + toks, dtype=np.int64))
+            by_end: dict = collections.defaultdict(list)
+            for si, c0, c1 in self.chunk_plan(self.splits[d], self.stream_layers):
+                by_end[c1 - 1].append((si, c0, c1))
+            self._streams.append((d, rs, ids_t, by_end, time.perf_counter()))
+            hooks_any = True
+        if hooks_any:
+            self.engine.model.layer_hook = self._layer_done
+
+    def _layer_done(self, li: int) -> None:
+        kv = self.engine.pool.kv
+        for d, _rs, ids_t, by_end, _t0 in self._streams:
+            for si, c0, c1 in by_end.get(li, ()):
+                buf = ops.kv_gather(kv[c0:c1], ids_t)
+                self.f.send(buf, self.groups[d][si])
+                self.streamed_bytes += buf.numel() * buf.element_size()
+
+    def _finish_streams(self, outs) -> set:
+        """After the step: first tokens (and finish codes) of the streamed prompts."""
+        self.engine.model.layer_hook = None
+        done = set()
+        if not self._streams:
+            return done
+        by_rid = {o.rid: o for o in outs}
+        eng = self.engine
+        for d, rs, ids_t, by_end, t0 in self._streams:
+            msg = [MSG_FIRST, len(rs)]
+            nbytes = 0
+            for r in rs:
+                o = by_rid[r.rid]
+                code = {"length": 1, "stop": 2}.get(o.finish_reason, 2) if o.finished else -1
+                msg += [int(o.token), code]
+                _d, need = self.target.pop(r.rid)
+                nbytes += _blocks_for(len(r.prompt), self.bs)
+                if o.finished:        # done at the first token: the decode side frees its pages
+                    self.credit[d] += need
+                    self.seq_credit[d] += 1
+                    if str(r.rid) in self.placed[d]:
+                        self.placed[d].remove(str(r.rid))
+                        run_sync(self.pd.complete_job(str(r.rid), self._pdm.JobPhase.DECODE))
+                    self.ch[self.router].send([MSG_FINISHED, int(o.rid), int(o.token), max(0, code)])
+                else:
+                    eng.scheduler.finish(r, "migrated")
+                    eng.requests.pop(r.rid, None)
+                done.add(r.rid)
+            self.ch[d].send_var(msg)
+            dt = time.perf_counter() - t0
+            pb = nbytes * self.engine.pool.page_bytes()
+            self.migrator.record(f"kv:{rs[0].rid}", self.me, str(d), pb, dt * 1000.0)
+            self.migrated += sum(1 for r in rs if not by_rid[r.rid].finished)
+            self.sent_bytes += pb
+            self.migrate_time += dt
+        self._streams = []
+        return done
+
     def step(self) -> list[StepOutput]:
         from dgi.parallel.fault import plan
         if plan():
@@ -226,9 +336,15 @@ class PrefillServer:
         if not self.engine.has_unfinished():
             return []
         outs = self.engine.step()
+        streamed = self._finish_streams(outs)
         ready = []
         report = []
         for o in outs:
+            if o.rid in streamed:
+                self.first_tokens += 1
+                if o.request.ttft is not None:
+                    self.ttfts.append(o.request.ttft)
+                continue
             if o.rid in self.local:
                 self.local_tokens += 1
                 if len(o.request.output) == 1 and o.request.ttft is not None:
@@ -366,14 +482,17 @@ class DecodeDriver:
         self.refund_seqs = collections.Counter()
         self.done = set()
         self.inflight: list = []    # migrations whose pages are still on the wire
+        self.await_first: dict = {p: collections.deque() for p in self.prefill}
         self.received = 0
         self.recv_bytes = 0
 
     def _post_migration(self, p: int, msg) -> None:
         """Start receiving a migration from prefill rank ``p``: allocate pages,
-        post this stage's slice receive off the compute stream, tell the later
-        pipeline stages (which post their own receives from ``p``)."""
-        n_reqs, nblk, meta_len, tok_len = (int(x) for x in msg[1:5])
+        post this stage's slice receive(s) off the compute stream, tell the
+        later pipeline stages (which post their own receives from ``p``).  A
+        layer-streamed migration (chunk_layers > 0) arrives as one message per
+        layer group and waits for its FIRST message (the sampled first tokens)."""
+        n_reqs, nblk, meta_len, tok_len, chunk = (int(x) for x in msg[1:6])
         payload = self.chans[p].wait()
         meta = payload[:meta_len].reshape(n_reqs, META_FIELDS + 1).tolist()
         toks = payload[meta_len:meta_len + tok_len].tolist()
@@ -383,20 +502,38 @@ class DecodeDriver:
         mc = self.mc
         buf = torch.empty(self.L_local, 2, nblk, mc.num_kv_heads, self.bs, mc.head_dim, dtype=self.engine.pool.dtype,
                           device=dev)
-        rec = self.f.irecv_async(buf, p)
+        recs = [self.f.irecv_async(buf[a:b], p) for a, b in layer_groups(self.L_local, chunk)]
         if isinstance(self.engine, PipelineEngine):
-            self.engine.send_kv_notice(ids_t, p)
-        self.inflight.append((p, rec, buf, ids, ids_t, meta, toks))
+            self.engine.send_kv_notice(ids_t, p, chunk)
+        item = [p, recs, buf, ids, ids_t, meta, toks, chunk == 0]
+        self.inflight.append(item)
+        if chunk:
+            self.await_first[p].append(item)
         self.recv_bytes += buf.numel() * buf.element_size()     # this stage's slice
+
+    def _first(self, p: int, m) -> None:
+        """FIRST message of the oldest streamed migration from ``p``."""
+        item = self.await_first[p].popleft()
+        n = int(m[1])
+        for i in range(n):
+            item[5][i][3] = int(m[2 + 2 * i])           # first token
+            item[5][i][1] = int(m[3 + 2 * i])           # finish code (-1: keeps decoding)
+        item[7] = True
     def _admit_arrived(self, block: bool = False) -> None:
         """Scatter every completed migration into the pool and admit its requests."""
         keep = []
         for item in self.inflight:
-            p, rec, buf, ids, ids_t, meta, toks = item
-            if not (block or rec.ready()):
+            p, recs, buf, ids, ids_t, meta, toks, first_known = item
+            if block and not first_known:
+                while not item[7]:       # the FIRST message follows its MIGRATE on the same channel
+                    self._poll_ctrl(p)
+                    time.sleep(0.0005)
+                first_known = True
+            if not (first_known and (block or all(r.ready() for r in recs))):
                 keep.append(item)
                 continue
-            rec.complete()
+            for r in recs:
+                r.complete()
             mark("kv_migration_landed", len(meta))
             if self.f.on_gpu:
                 rs = self.f.recv_stream
@@ -414,7 +551,14 @@ class DecodeDriver:
         sch = self.engine.scheduler
         o = k = 0
         for m in meta:
-            rid, _, plen, first, nb, max_tok, tbits, seed, ign, topk, pbits, credit = m
+            rid, code, plen, first, nb, max_tok, tbits, seed, ign, topk, pbits, credit = m
+            if code > 0:
+                # streamed prompt that finished at its first token: release its pages
+                # (the prefill rank refunded the credit and reported it to the router)
+                self.engine.pool.free(ids[k:k + nb])
+                o += plen
+                k += nb
+                continue
             temp = float(np.int32(tbits).view(np.float32))
             top_p = float(np.int32(pbits).view(np.float32))
             sp = SamplingParams(max_tokens=max_tok, temperature=temp, top_p=top_p, top_k=topk,
@@ -444,22 +588,31 @@ class DecodeDriver:
         self.local_used[r.rid] = need
         return r
 
+    def _poll_ctrl(self, p: int) -> None:
+        ch = self.chans[p]
+        while True:
+            m = ch.poll()
+            if m is None:
+                break
+            self._handle(p, m)
+
+    def _handle(self, p: int, m) -> None:
+        if m[0] == MSG_MIGRATE:
+            self._post_migration(p, m)
+        elif m[0] == MSG_FIRST:
+            self._first(p, m)
+        elif m[0] == MSG_DONE:
+            self.done.add(p)
+        elif m[0] == MSG_FINISHED:
+            if self.track_arrivals:
+                self.prefill_finished.append((int(m[1]), int(m[2]), REASONS.get(int(m[3]))))
+        elif m[0] == MSG_TOKENS:
+            if self.track_arrivals:
+                self._take_tokens(m)
+
     def poll(self) -> None:
-        for p, ch in self.chans.items():
-            while True:
-                m = ch.poll()
-                if m is None:
-                    break
-                if m[0] == MSG_MIGRATE:
-                    self._post_migration(p, m)
-                elif m[0] == MSG_DONE:
-                    self.done.add(p)
-                elif m[0] == MSG_FINISHED:
-                    if self.track_arrivals:
-                        self.prefill_finished.append((int(m[1]), int(m[2]), REASONS.get(int(m[3]))))
-                elif m[0] == MSG_TOKENS:
-                    if self.track_arrivals:
-                        self._take_tokens(m)
+        for p in self.chans:
+            self._poll_ctrl(p)
         for ch in self.fwd_in.values():      # router: tokens of the other replicas
             while True:
                 m = ch.poll()

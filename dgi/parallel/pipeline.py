@@ -327,14 +327,16 @@ class PipelineEngine(LLMEngine):
         return outs
 
     # ------------------------------------------------------------------ control
-    def send_kv_notice(self, ids: torch.Tensor, src: int) -> None:
+    def send_kv_notice(self, ids: torch.Tensor, src: int, chunk: int = 0) -> None:
         """Tell later stages that pages ``ids`` of a P/D migration are on their
-        way from prefill rank ``src`` (each stage receives its own layer slice)."""
+        way from prefill rank ``src`` (each stage receives its own layer slice,
+        in ``chunk``-layer groups when the migration is layer-streamed)."""
         if self.next_rank is None:
             return
         hdr = np.zeros(HDR, np.int64)
         hdr[1] = ids.numel()
         hdr[2] = src
+        hdr[3] = chunk
         self.f.ctrl_send_tensor(_hdr_tensor(hdr, KIND_KV), self.next_rank)
         self.f.send(ids.to(self.f.device, torch.int32).contiguous(), self.next_rank)
 
@@ -367,16 +369,18 @@ class StageWorker:
         if f.on_gpu:
             rs = f.recv_stream
             rs.wait_stream(torch.cuda.current_stream())
-            for rec, buf, ids in self.kv_pending:
-                rec.complete()
+            for recs, buf, ids in self.kv_pending:
+                for rec in recs:
+                    rec.complete()
                 with torch.cuda.stream(rs):
                     ops.kv_scatter(self.pool.kv, ids, buf)
                 buf.record_stream(rs)
                 ids.record_stream(rs)
             torch.cuda.current_stream().wait_stream(rs)
         else:
-            for rec, buf, ids in self.kv_pending:
-                rec.complete()
+            for recs, buf, ids in self.kv_pending:
+                for rec in recs:
+                    rec.complete()
                 ops.kv_scatter(self.pool.kv, ids, buf)
         self.kv_pending = []
 
@@ -434,7 +438,7 @@ class StageWorker:
                 f.flush()
                 return "stop" if kind == KIND_STOP else "pause"
             if kind == KIND_KV:
-                n, src = hdr[1], hdr[2]
+                n, src, chunk = hdr[1], hdr[2], hdr[3]
                 ids = torch.empty(n, dtype=torch.int32, device=dev)
                 f.recv(ids, self.prev)
                 if self.next is not None:
@@ -442,7 +446,9 @@ class StageWorker:
                     f.send(ids, self.next)
                 buf = torch.empty(self.n_layers, 2, n, self.mc.num_kv_heads, self.pool.block_size, self.mc.head_dim,
                                   dtype=self.pool.dtype, device=dev)
-                self.kv_pending.append((f.irecv_async(buf, src), buf, ids))
+                from dgi.parallel.pd import layer_groups
+                self.kv_pending.append(([f.irecv_async(buf[a:b], src) for a, b in layer_groups(self.n_layers, chunk)],
+                                        buf, ids))
                 continue
             # KIND_FWD
             from dgi.parallel.fault import plan

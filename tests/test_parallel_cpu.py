@@ -137,7 +137,7 @@ def _pd_body(rank, world):
     layout = NodeLayout("pd" if k == 1 else "pdpp", list(range(npre)), groups)
     f.connect_pairs(layout.p2p_pairs())
     if rank in layout.prefill_ranks:
-        srv = PrefillServer(cfg, f, layout)
+        srv = PrefillServer(cfg, f, layout, stream_layers=int(os.environ.get("DGI_TEST_STREAM", "8")))
         nlocal = int(os.environ.get("DGI_TEST_LOCAL", "0"))
         for i, p in enumerate(PROMPTS[:len(PROMPTS) - nlocal]):
             if i % npre == rank:
@@ -145,7 +145,7 @@ def _pd_body(rank, world):
         while srv.busy():
             srv.step()
         srv.finish()
-        return "prefill"
+        return {"streamed": srv.streamed_bytes, "migrated": srv.migrated}
     if rank in layout.drivers:
         import time as _t
         nlocal = int(os.environ.get("DGI_TEST_LOCAL", "0")) if rank == layout.drivers[0] else 0
@@ -325,6 +325,23 @@ def test_pd_multi_prefill_and_three_stage_decode(npre, world, monkeypatch):
     ref = [r.output for r in e.generate(PROMPTS, SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True))]
     out = _spawn("_pd_body", world)
     assert _merged(out, npre) == ref
+
+
+@pytest.mark.parametrize("stream", [0, 1])
+def test_pd_layer_streamed_and_bulk_migration_match_local_decode(stream, monkeypatch):
+    """stream=1: every layer's pages leave the prefill rank as soon as the step
+    has written them (one receive per layer on each of the 2 decode stages);
+    stream=0: one bulk message per stage after the step.  Same outputs."""
+    model = "llama-tiny-hd128"
+    monkeypatch.setenv("DGI_TEST_MODEL", model)
+    monkeypatch.setenv("DGI_TEST_PREFILL", "1")
+    monkeypatch.setenv("DGI_TEST_STREAM", str(stream))
+    monkeypatch.setenv("DGI_TEST_SAMPLED", "1")
+    ref = _reference_outputs(model=model)
+    out = _spawn("_pd_body", 3)
+    assert _merged(out, 1) == ref
+    assert out[0]["migrated"] == len(PROMPTS)
+    assert (out[0]["streamed"] > 0) == (stream > 0)
 
 
 def _tp_body(rank, world):
