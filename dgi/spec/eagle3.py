@@ -191,12 +191,29 @@ class Eagle3Draft:
 
 
 class _SpecState:
-    __slots__ = ("draft_len", "feat_start", "feat")
+    __slots__ = ("draft_len", "feat_start", "_feat", "chunks", "n_chunked")
 
     def __init__(self, draft_len: int):
         self.draft_len = draft_len      # positions [0, draft_len) have draft KV
         self.feat_start = 0             # position of feat[0]
-        self.feat: Optional[torch.Tensor] = None   # fused target features [m, H]
+        self._feat: Optional[torch.Tensor] = None   # fused target features [m, H]
+        self.chunks: list = []          # appended rows not yet concatenated (plain decode steps)
+        self.n_chunked = 0
+
+    @property
+    def feat(self) -> Optional[torch.Tensor]:
+        if self.chunks:                 # one concatenation per spec step, not one per plain step
+            parts = ([self._feat] if self._feat is not None else []) + self.chunks
+            self._feat = torch.cat(parts)
+            self.chunks, self.n_chunked = [], 0
+        return self._feat
+
+    @feat.setter
+    def feat(self, v: Optional[torch.Tensor]) -> None:
+        self._feat, self.chunks, self.n_chunked = v, [], 0
+
+    def rows(self) -> int:
+        return (0 if self._feat is None else self._feat.shape[0]) + self.n_chunked
 
 
 def _varlen_meta(runner, positions, slots, block_rows, cu, ctx, device, tree_mask=None, tree_n=0,
@@ -551,11 +568,14 @@ class SpecEngine(LLMEngine):
         return logits, (self.draft.fuse(raw) if fuse else raw)
 
     def _append_feats(self, r: Request, start: int, feats: torch.Tensor) -> None:
+        """Record target features of positions [start, start + len(feats)).  ``feats``
+        must not alias a buffer that is rewritten later (callers clone once per step)."""
         st = self._state(r)
-        if st.feat is None or st.feat_start + st.feat.shape[0] != start:
-            st.feat, st.feat_start = feats.clone(), start
+        if st.rows() == 0 or st.feat_start + st.rows() != start:
+            st.feat, st.feat_start = feats, start
         else:
-            st.feat = torch.cat([st.feat, feats])
+            st.chunks.append(feats)
+            st.n_chunked += feats.shape[0]
 
     # ------------------------------------------------------------------ controller
     def _record(self, mode: str, R: int, seconds: float, tokens: int) -> None:
@@ -641,7 +661,7 @@ class SpecEngine(LLMEngine):
             # plain decode: hipGraph replay with the feature tap
             pos = [r.num_computed for r in sb.decode]
             toks = g.run(sb)
-            feats = g.last_features(len(sb.decode))
+            feats = g.last_features(len(sb.decode)).clone()     # one copy per step; rows are views of it
             for i, r in enumerate(sb.decode):
                 self._append_feats(r, pos[i], feats[i: i + 1])
             return self._apply(sb, list(sb.decode), toks)
