@@ -145,6 +145,20 @@ def get_admin_health_detailed(db: Session = Depends(get_db)):
             "stuck_jobs": int(stuck), "issues": issues, "timestamp": datetime.utcnow().isoformat()}
 
 
+# ---------------------------------------------------------------- P/D scheduler
+@router.get("/pd/stats")
+def get_pd_stats():
+    """Cluster P/D scheduler state (services/pd_runtime.py): queues, workers per role,
+    migrations; also exported as the ``queue_size{phase}`` gauges."""
+    from app.services.observability import MetricsCollector
+    from app.services.pd_runtime import coordinator
+    st = coordinator.stats()
+    mc = MetricsCollector(worker_id="control-plane")
+    mc.record_queue("prefill", st["prefill_queue_size"])
+    mc.record_queue("decode", st["decode_queue_size"])
+    return st
+
+
 # ---------------------------------------------------------------- workers
 @router.get("/workers")
 def list_workers(status: Optional[str] = None, region: Optional[str] = None, page: int = Query(1, ge=1),

@@ -19,6 +19,7 @@ from app.api.deps import lookup_api_key
 from app.db.database import get_db
 from app.models.models import Job, JobStatus, Worker, WorkerStatus
 from app.services.geo import detect_client_region
+from app.services.pd_runtime import coordinator
 from app.services.scheduler import SmartScheduler, get_region_distance
 from app.services.task_guarantee import TaskGuaranteeService
 
@@ -76,9 +77,14 @@ def _new_job(db: Session, payload: JobCreateRequest, client_ip, client_region, a
               client_ip=client_ip, client_region=client_region,
               enterprise_id=key.enterprise_id if key else None, api_key_id=key.id if key else None,
               status=JobStatus.QUEUED.value, created_at=datetime.utcnow())
+    pd = payload.type == "llm" and coordinator.wants_pd(payload.params)
+    if pd:
+        job.phase = "prefill"        # P/D job path (services/pd_runtime.py)
     db.add(job)
     db.commit()
     db.refresh(job)
+    if pd:
+        coordinator.on_created(job)
     return job
 
 

@@ -24,6 +24,7 @@ from app.api.deps import authenticate_worker, check_signature
 from app.db.database import get_db
 from app.models.models import Job, JobStatus, Worker, WorkerStatus
 from app.models.usage import Enterprise
+from app.services.pd_runtime import coordinator
 from app.services.reliability import ReliabilityService
 from app.services.scheduler import SmartScheduler
 from app.services.security import SecurityService
@@ -151,6 +152,7 @@ def register_worker(payload: WorkerRegisterRequest, db: Session = Depends(get_db
     ReliabilityService(db).start_session(w, commit=False)
     db.commit()
     db.refresh(w)
+    coordinator.sync_worker(w)
     return WorkerRegisterResponse(worker_id=str(w.id), token=token, refresh_token=refresh,
                                   signing_secret=w.signing_secret, token_expires_at=w.token_expires_at)
 
@@ -178,6 +180,7 @@ async def heartbeat(worker_id: str, payload: HeartbeatRequest, request: Request,
         w.extra_caps = {**(w.extra_caps or {}), "engine_stats": payload.engine_stats}
     ReliabilityService(db).update_score(w, "heartbeat", commit=False)
     db.commit()
+    coordinator.sync_worker(w, payload.engine_stats)
     changed = (w.config_version or 0) > payload.config_version
     action = "reload_config" if changed else None
     if SecurityService(db).should_refresh_token(w):
@@ -204,6 +207,8 @@ async def get_next_job(worker_id: str, request: Request, x_worker_token: Optiona
     w.current_job_id = job.id
     w.status = WorkerStatus.BUSY.value if _running(db, w.id) >= lc.max_concurrent_jobs else WorkerStatus.ONLINE.value
     db.commit()
+    if job.phase:
+        coordinator.on_assigned(job, w)
     return JobAssignment(job_id=str(job.id), type=job.type, params=job.params or {},
                          timeout_seconds=job.timeout_seconds, priority=job.priority)
 
@@ -220,6 +225,23 @@ async def complete_job(worker_id: str, job_id: str, payload: JobCompleteRequest,
         raise HTTPException(403, "Not authorized to complete this job")
     if job.status != JobStatus.RUNNING.value:
         return {"status": "ignored", "job_id": job_id, "job_status": job.status}
+    if job.phase == "prefill" and payload.success:
+        # P/D: the prefill phase is done -> the scheduler places the decode phase
+        live = {str(x) for x in db.execute(select(Worker.id).where(Worker.status.in_(
+            [WorkerStatus.ONLINE.value, WorkerStatus.BUSY.value]))).scalars()}
+        nxt = coordinator.on_prefill_done(job, w, payload.result, live=live | {str(w.id)})
+        job.phase, job.target_worker_id, job.params = "decode", nxt["target_worker_id"], nxt["params"]
+        job.status, job.worker_id, job.started_at = JobStatus.QUEUED.value, None, None
+        if w.current_job_id == job.id:
+            w.current_job_id = None
+        ReliabilityService(db).update_score(w, "job_completed", commit=False, latency_ms=payload.processing_time_ms)
+        db.commit()
+        return {"status": "ok", "job_id": job_id, "next_phase": "decode", "decode_worker": nxt["target_worker_id"]}
+    if job.phase:
+        if payload.success:
+            coordinator.on_decode_done(job, float(payload.processing_time_ms or 0))
+        else:
+            coordinator.on_failed(job)
     job.status = JobStatus.COMPLETED.value if payload.success else JobStatus.FAILED.value
     job.result, job.error = payload.result, payload.error
     job.completed_at = datetime.utcnow()

@@ -111,6 +111,8 @@ class Job(Base):
     enterprise_id: Mapped[str | None] = mapped_column(String(36))
     api_key_id: Mapped[str | None] = mapped_column(String(36))
     phase: Mapped[str | None] = mapped_column(String(16))   # P/D: prefill | decode
+    # P/D: the decode phase is pinned to the worker the P/D scheduler chose (services/pd_runtime.py)
+    target_worker_id: Mapped[str | None] = mapped_column(String(36), index=True)
     created_at: Mapped[datetime] = mapped_column(DateTime, default=datetime.utcnow, index=True)
     started_at: Mapped[datetime | None] = mapped_column(DateTime)
     completed_at: Mapped[datetime | None] = mapped_column(DateTime)

@@ -123,9 +123,13 @@ class SmartScheduler:
                           candidates: int = 8) -> Optional[Job]:
         if not supported_types:
             return None
-        q = (select(Job).where(Job.status == JobStatus.QUEUED.value, Job.type.in_(list(supported_types)))
+        q = (select(Job).where(Job.status == JobStatus.QUEUED.value, Job.type.in_(list(supported_types)),
+                               or_(Job.target_worker_id.is_(None), Job.target_worker_id == str(worker_id)))
              .order_by(Job.priority.desc(), Job.created_at.asc()).limit(candidates))
         jobs = list(self.db.execute(q).scalars())
+        if worker is not None and (worker.role or "hybrid") in ("prefill", "decode"):
+            # a P/D-phase job only goes to a worker of that role (or a hybrid one)
+            jobs = [j for j in jobs if not j.phase or j.phase == worker.role]
         if worker is not None and jobs:
             top = jobs[0].priority
             role = (worker.role or "hybrid")

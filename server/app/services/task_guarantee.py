@@ -54,6 +54,7 @@ class TaskGuaranteeService:
                 j.retry_count = (j.retry_count or 0) + 1
                 j.worker_id = None
                 j.started_at = None
+                j.target_worker_id = None      # a P/D decode pin dies with its worker
                 requeued += 1
             else:
                 j.status = JobStatus.FAILED.value
@@ -61,6 +62,12 @@ class TaskGuaranteeService:
                 j.completed_at = datetime.utcnow()
                 failed += 1
                 notify_job_done(j.id)
+        # unpin queued P/D decode phases waiting for this worker, and drop it from the P/D scheduler
+        for j in self.db.execute(select(Job).where(Job.target_worker_id == worker_id,
+                                                   Job.status == JobStatus.QUEUED.value)).scalars():
+            j.target_worker_id = None
+        from app.services.pd_runtime import coordinator
+        coordinator.drop_worker(worker_id)
         if w is not None:
             w.status = WorkerStatus.OFFLINE.value
             w.current_job_id = None

@@ -302,3 +302,61 @@ def test_api_no_worker_503_and_direct(client):
     wid, hdr, _ = _register(c, supports_direct=True, direct_url="http://10.0.0.5:8001")
     d = c.get("/api/v1/jobs/direct/nearest?job_type=llm").json()
     assert d["worker_id"] == wid and d["direct_url"].endswith(":8001")
+
+
+def test_api_pd_job_path_places_decode_by_scheduler(client):
+    """The cluster P/D path (reference pd_scheduler API, wired by services/pd_runtime):
+    a ``pd`` job is pulled by a prefill worker, its completion hands it to the
+    scheduler's decode placement, it is requeued pinned to the chosen decode
+    worker (with the KV source), only that worker can pull it, and the stats
+    endpoint reports the whole lifecycle."""
+    c = client
+    pre, hp, _ = _register(c, role="prefill", capabilities={"compute_flops": 2500.0})
+    dec1, hd1, _ = _register(c, role="decode", capabilities={"memory_bandwidth_gbps": 8000.0})
+    dec2, hd2, _ = _register(c, role="decode", capabilities={"memory_bandwidth_gbps": 2000.0})
+    # dec2 reports a nearly full KV cache: the scheduler must prefer dec1
+    c.post(f"/api/v1/workers/{dec2}/heartbeat", json={"status": "online",
+                                                       "engine_stats": {"num_blocks": 100, "used_blocks": 95}},
+           headers=hd2)
+    st0 = c.get("/api/v1/admin/pd/stats").json()
+    job_id = c.post("/api/v1/jobs", json={"type": "llm", "params": {"prompt": "hello", "max_tokens": 8,
+                                                                     "pd": True}}).json()["job_id"]
+    assert c.get("/api/v1/admin/pd/stats").json()["prefill_queue_size"] == st0["prefill_queue_size"] + 1
+    # decode workers do not take the prefill phase; the prefill worker does
+    assert c.get(f"/api/v1/workers/{dec1}/next-job", headers=hd1).json() is None
+    a = c.get(f"/api/v1/workers/{pre}/next-job", headers=hp).json()
+    assert a["job_id"] == job_id
+    r = c.post(f"/api/v1/workers/{pre}/jobs/{job_id}/complete",
+               json={"success": True, "result": {"response": "W", "first_token": "W", "kv_cache_key": "kv-1"},
+                     "processing_time_ms": 12}, headers=hp).json()
+    assert r["next_phase"] == "decode" and r["decode_worker"] == dec1
+    assert c.get(f"/api/v1/jobs/{job_id}").json()["status"] == "queued"
+    # pinned: the other decode worker cannot take it
+    assert c.get(f"/api/v1/workers/{dec2}/next-job", headers=hd2).json() is None
+    b = c.get(f"/api/v1/workers/{dec1}/next-job", headers=hd1).json()
+    assert b["job_id"] == job_id and b["params"]["pd_phase"] == "decode" and b["params"]["kv_source"] == pre
+    c.post(f"/api/v1/workers/{dec1}/jobs/{job_id}/complete",
+           json={"success": True, "result": {"response": "World", "usage": {"completion_tokens": 8}},
+                 "processing_time_ms": 30}, headers=hd1)
+    assert c.get(f"/api/v1/jobs/{job_id}").json()["status"] == "completed"
+    st = c.get("/api/v1/admin/pd/stats").json()
+    assert st["transitions"] == st0["transitions"] + 1 and st["decode_completed"] == st0["decode_completed"] + 1
+    assert st["migrations"] == st0["migrations"] + 1
+    assert st["prefill_workers"] >= 1 and st["decode_workers"] >= 2
+
+
+def test_worker_daemon_runs_pd_phases():
+    from worker.main import Worker as Daemon
+    d = Daemon.__new__(Daemon)
+    d.worker_id = "w1"
+    calls = []
+
+    def fake(job_type, params, job_id="direct"):
+        calls.append(dict(params))
+        return {"response": "tok" if params.get("max_tokens") == 1 else "full text", "usage": {}}
+    d._execute = fake
+    out = d.execute("llm", {"prompt": "x", "max_tokens": 16, "pd": True}, "j1")
+    assert out["phase"] == "prefill" and out["kv_cache_key"] == "w1:j1" and calls[-1]["max_tokens"] == 1
+    out = d.execute("llm", {"prompt": "x", "max_tokens": 16, "pd": True, "pd_phase": "decode", "kv_source": "p"},
+                    "j1")
+    assert out["phase"] == "decode" and out["response"] == "full text" and calls[-1]["max_tokens"] == 16

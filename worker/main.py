@@ -260,6 +260,26 @@ class Worker:
             self._batchers[job_type] = _JobBatcher(engine, b.max_batch_size, b.max_wait_ms)
 
     def execute(self, job_type: str, params: Dict[str, Any], job_id: str = "direct") -> Dict[str, Any]:
+        if job_type == "llm" and params.get("pd"):
+            return self._execute_pd(params, job_id)
+        return self._execute(job_type, params, job_id)
+
+    def _execute_pd(self, params: Dict[str, Any], job_id: str) -> Dict[str, Any]:
+        """Cluster P/D job (server services/pd_runtime.py).  Prefill phase: one
+        token, reported with the KV key the decode placement uses.  Decode phase:
+        the full completion on the worker the P/D scheduler chose; the KV cannot
+        cross nodes through this HTTP path, so the decode worker rebuilds it by
+        re-prefill (inside one MI355X node dgi migrates it over RCCL instead)."""
+        phase = params.get("pd_phase", "prefill")
+        if phase == "prefill":
+            out = self._execute("llm", {**params, "max_tokens": 1}, job_id)
+            return {**out, "phase": "prefill", "first_token": out.get("response", ""),
+                    "kv_cache_key": f"{self.worker_id}:{job_id}"}
+        out = self._execute("llm", {k: v for k, v in params.items() if k not in ("pd_phase", "first_token")},
+                            job_id)
+        return {**out, "phase": "decode", "kv_source": params.get("kv_source"), "reprefilled": True}
+
+    def _execute(self, job_type: str, params: Dict[str, Any], job_id: str = "direct") -> Dict[str, Any]:
         engine = self.engines.get(job_type)
         if engine is None:
             raise ValueError(f"No engine for type: {job_type}")
