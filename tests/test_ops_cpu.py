@@ -120,3 +120,19 @@ def test_topkp_matches_hf_topk_then_topp_warpers():
         got = torch.isfinite(masked[b])
         assert torch.equal(got, want), (b, int(got.sum()), int(want.sum()))
     assert int(torch.isfinite(masked[0]).sum()) < 50
+
+
+def test_running_set_is_an_ordered_o1_set():
+    from dgi.sched.request import Request, SamplingParams
+    from dgi.sched.scheduler import RunningSet
+    rs = RunningSet()
+    reqs = [Request([1, 2, 3], SamplingParams()) for _ in range(5)]
+    for r in reqs:
+        rs.append(r)
+    rs.remove(reqs[1])
+    rs.discard(reqs[1])
+    assert list(rs) == [reqs[0], reqs[2], reqs[3], reqs[4]] and len(rs) == 4
+    assert list(reversed(rs))[0] is reqs[4] and reqs[2] in rs and reqs[1] not in rs
+    for r in rs:                      # iteration is a snapshot: removal inside the loop is safe
+        rs.remove(r)
+    assert not rs
