@@ -126,3 +126,37 @@ def test_native_engine_refuses_silent_random_weights(tmp_path):
         assert st["engine"]["weights"] == str(tmp_path)
     finally:
         e.unload_model()
+
+
+def test_hf_shard_chain_keeps_kv_across_decode_steps(tmp_path):
+    """HF shards behind the gRPC/HTTP servicer keep a per-session KV cache
+    (the reference passed use_cache without past_key_values, E-6): a 2-shard
+    chain decoding token by token reproduces HF greedy generation, including a
+    multi-token chunk appended over an existing prefix."""
+    from worker.distributed.grpc_server import InferenceServicer
+    from worker.distributed.model_shard import ModelShard
+
+    model, _ = save_tiny("llama", str(tmp_path))
+    shards = [ModelShard.from_pretrained(str(tmp_path), a, b, device="cpu", dtype=torch.float32)
+              for a, b in ((0, 1), (1, 2))]
+    svcs = [InferenceServicer(s) for s in shards]
+    prompt = [1, 17, 99, 250, 3, 77, 401]
+    with torch.no_grad():
+        want = model.generate(torch.tensor([prompt]), max_new_tokens=6, do_sample=False, min_new_tokens=6,
+                              pad_token_id=0)[0].tolist()
+
+    def run(ids, pos):
+        x = torch.tensor([ids])
+        for sv in svcs:
+            x = sv._forward(sv._session("s"), x, pos)
+        with torch.inference_mode():
+            return int(shards[-1].get_logits(x)[0, -1].argmax())
+
+    # prefill the first 4 prompt tokens, then append the rest as one chunk, then decode
+    run(prompt[:4], 0)
+    tok = run(prompt[4:], 4)
+    out = list(prompt) + [tok]
+    for _ in range(5):
+        tok = run([tok], len(out) - 1)
+        out.append(tok)
+    assert out == want

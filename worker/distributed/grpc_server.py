@@ -33,11 +33,12 @@ logger = logging.getLogger(__name__)
 
 
 class _Session:
-    __slots__ = ("session_id", "blocks", "position", "created", "last", "tokens", "max_length")
+    __slots__ = ("session_id", "blocks", "position", "created", "last", "tokens", "max_length", "cache")
 
     def __init__(self, session_id: str, max_length: int = 4096):
         self.session_id = session_id
         self.blocks: List[int] = []
+        self.cache = None           # HF shards: per-session transformers Cache (KV kept across steps)
         self.position = 0
         self.created = time.time()
         self.last = self.created
@@ -105,9 +106,27 @@ class InferenceServicer:
             return self._native_forward(sess, x if torch.is_tensor(x) else torch.as_tensor(x), position)
         t = x if torch.is_tensor(x) else torch.as_tensor(x)
         dev = next(self.model_shard.parameters(), torch.empty(0)).device
-        pos_ids = torch.arange(position, position + t.shape[1], device=dev).unsqueeze(0)
+        S = t.shape[1]
+        pos_ids = torch.arange(position, position + S, device=dev).unsqueeze(0)
+        # stateful: the session's KV cache persists between Forward calls (the reference
+        # dropped it, E-6), so decode steps attend to the whole prefix
+        if sess.cache is None:
+            try:
+                from transformers import DynamicCache
+                sess.cache = DynamicCache()
+            except Exception:          # transformers missing: stateless fallback
+                sess.cache = None
+        mask = None
+        past = 0 if sess.cache is None else int(sess.cache.get_seq_length(self.model_shard.start_layer))
+        if sess.cache is not None and past > 0 and S > 1:
+            # chunk over an existing prefix: causal mask aligned to the end (SDPA's is_causal is top-left)
+            q = torch.arange(S, device=dev)[:, None] + past
+            k = torch.arange(past + S, device=dev)[None, :]
+            dt = next(self.model_shard.parameters(), torch.empty(0)).dtype
+            mask = torch.zeros(S, past + S, device=dev, dtype=dt).masked_fill(k > q, float("-inf"))[None, None]
         with torch.inference_mode():
-            out, _kv = self.model_shard.forward(t.to(dev), position_ids=pos_ids, use_cache=False)
+            out, _kv = self.model_shard.forward(t.to(dev), position_ids=pos_ids, past_key_values=sess.cache,
+                                                use_cache=sess.cache is not None, attention_mask=mask)
         return out
 
     async def _forward_to_next(self, output, position: int, session_id: str):

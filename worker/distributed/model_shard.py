@@ -146,7 +146,17 @@ class ModelShard(nn.Module):
                 extra["position_embeddings"] = self.rotary_emb(h, position_ids)
             except Exception:
                 pass
+        # transformers >= 4.5x: one Cache object shared by all layers (each attention
+        # updates its own layer_idx slot) — the shard keeps it per session, so decode
+        # steps attend to the whole history; legacy per-layer tuples otherwise
+        cache_obj = past_key_values if (past_key_values is not None and hasattr(past_key_values, "update")
+                                        and hasattr(past_key_values, "get_seq_length")) else None
         for i, layer in enumerate(self.layers):
+            if cache_obj is not None:
+                out = layer(h, attention_mask=attention_mask, position_ids=position_ids,
+                            past_key_values=cache_obj, use_cache=True, **extra)
+                h = out[0] if isinstance(out, tuple) else out
+                continue
             past = past_key_values[i] if past_key_values is not None and i < len(past_key_values) else None
             out = layer(h, position_ids=position_ids, past_key_value=past, use_cache=use_cache,
                         attention_mask=attention_mask, **extra)
@@ -158,6 +168,8 @@ class ModelShard(nn.Module):
                 h = out
         if self.is_last_shard and self.norm is not None:
             h = self.norm(h)
+        if cache_obj is not None:
+            return h, cache_obj
         return h, (new_kv if use_cache else None)
 
     def get_logits(self, hidden_states: torch.Tensor) -> torch.Tensor:
