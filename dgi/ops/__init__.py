@@ -52,6 +52,17 @@ def _warn_once(key: str, msg: str) -> None:
         warnings.warn(msg, RuntimeWarning, stacklevel=3)
 
 
+def _call(name: str, *args) -> None:
+    """Invoke a dgi HIP op; under DGI_DEBUG_SYNC=1 synchronize and name it on a fault."""
+    getattr(torch.ops.dgi, name)(*args)
+    if _DEBUG_SYNC:
+        from dgi.utils.debug import after_op
+        after_op(name, *args)
+
+
+_DEBUG_SYNC = os.environ.get("DGI_DEBUG_SYNC", "0") == "1"
+
+
 def native_available() -> bool:
     return load_native(False)
 
@@ -76,7 +87,7 @@ def rmsnorm_ref(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
 def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     if _native(x):
         out = torch.empty_like(x) if out is None else out
-        torch.ops.dgi.rmsnorm(out, x, w, eps)
+        _call("rmsnorm", out, x, w, eps)
         return out
     r = rmsnorm_ref(x, w, eps)
     if out is not None:
@@ -94,7 +105,7 @@ def fused_add_rmsnorm_ref(x: torch.Tensor, residual: torch.Tensor, w: torch.Tens
 def fused_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float) -> None:
     """residual <- x + residual; x <- rmsnorm(residual) * w (in place)."""
     if _native(x):
-        torch.ops.dgi.fused_add_rmsnorm(x, residual, w, eps)
+        _call("fused_add_rmsnorm", x, residual, w, eps)
     else:
         fused_add_rmsnorm_ref(x, residual, w, eps)
 
@@ -173,7 +184,7 @@ def rope_cache(qkv, positions, cos_sin, nh, nkv, hd, slot_mapping, k_cache, v_ca
     ``cos_sin`` is [max_pos, rd] (rd <= hd rotary dims); ``mode`` 0 = NeoX
     pairing (Llama, Qwen2), 1 = interleaved pairs (GLM-4, GPT-J)."""
     if _native(qkv):
-        torch.ops.dgi.rope_cache(qkv, positions, cos_sin, nh, nkv, hd, slot_mapping, k_cache, v_cache, mode)
+        _call("rope_cache", qkv, positions, cos_sin, nh, nkv, hd, slot_mapping, k_cache, v_cache, mode)
     else:
         rope_cache_ref(qkv, positions, cos_sin, nh, nkv, hd, slot_mapping, k_cache, v_cache, mode)
 
@@ -242,7 +253,7 @@ def paged_decode(q, k_cache, v_cache, block_tables, context_lens, nh, nkv, scale
         else:
             po = pl = torch.empty(0, dtype=torch.float32, device=q.device)
             part_size = max(128, ((part_size if part_size < (1 << 30) else 1 << 20) + 127) // 128 * 128)
-        torch.ops.dgi.paged_decode(out, q, k_cache, v_cache, block_tables, context_lens, po, pl,
+        _call("paged_decode", out, q, k_cache, v_cache, block_tables, context_lens, po, pl,
                                    nh, nkv, max_splits, part_size, scale)
         return out
     r = paged_decode_ref(q, k_cache, v_cache, block_tables, context_lens, nh, nkv, scale)
@@ -309,7 +320,7 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens,
         if tiles is None:
             tl = prefill_tiles(cu_seqlens_q.tolist())
             tiles = torch.tensor(tl if tl else [[0, 0]], dtype=torch.int32, device=q.device)[: len(tl)]
-        torch.ops.dgi.paged_prefill(out, q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens,
+        _call("paged_prefill", out, q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens,
                                     tiles, nh, nkv, scale, tree_mask, tree_n)
         return out
     r = paged_prefill_ref(q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens, nh, nkv, scale,
@@ -355,7 +366,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         load_native(required=True)
         if out is None:
             out = torch.empty(M, N, dtype=x.dtype, device=x.device)
-        torch.ops.dgi.skinny_gemm(out, x, w, bias, 0)
+        _call("skinny_gemm", out, x, w, bias, 0)
         return out
     r = torch.nn.functional.linear(x, w, bias)
     if out is not None:
@@ -374,7 +385,7 @@ def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tens
     if _native(gu):
         if out is None:
             out = torch.empty(*gu.shape[:-1], gu.shape[-1] // 2, dtype=gu.dtype, device=gu.device)
-        torch.ops.dgi.silu_mul(out, gu)
+        _call("silu_mul", out, gu)
         return out
     r = silu_mul_ref(gu)
     if out is not None:
@@ -401,7 +412,7 @@ def topkp_threshold(logits: torch.Tensor, temperature: torch.Tensor, top_k: torc
     B, V = logits.shape
     if _native(logits):
         th = torch.empty(B, dtype=torch.float32, device=logits.device)
-        torch.ops.dgi.topkp_threshold(th, logits, temperature.float().contiguous(), top_k.long().contiguous(),
+        _call("topkp_threshold", th, logits, temperature.float().contiguous(), top_k.long().contiguous(),
                                       top_p.float().contiguous())
         return th
     lf = logits.float()
@@ -472,7 +483,7 @@ def sample(logits: torch.Tensor, temperature: Optional[torch.Tensor] = None,
         if out is None:
             out = torch.empty(B, dtype=torch.long, device=logits.device)
         th = topkp_threshold(logits, temperature, top_k, top_p) if filt else None
-        torch.ops.dgi.sample(out, logits, temperature, seeds, step, th)
+        _call("sample", out, logits, temperature, seeds, step, th)
         return out
     if filt:
         logits = apply_top_k_top_p(logits, top_k, top_p, temperature)
@@ -495,7 +506,7 @@ def topk(logits: torch.Tensor, k: int):
         B = logits.shape[0]
         v = torch.empty(B, k, dtype=torch.float32, device=logits.device)
         i = torch.empty(B, k, dtype=torch.long, device=logits.device)
-        torch.ops.dgi.topk(v, i, logits, k)
+        _call("topk", v, i, logits, k)
         return v, i
     v, i = logits.float().topk(k, dim=-1)
     return v, i
@@ -511,7 +522,7 @@ def kv_gather(cache: torch.Tensor, ids: torch.Tensor, out: Optional[torch.Tensor
         if out is None:
             out = torch.empty(cache.shape[0], cache.shape[1], ids.numel(), *cache.shape[3:],
                               dtype=cache.dtype, device=cache.device)
-        torch.ops.dgi.kv_gather(out, cache, ids)
+        _call("kv_gather", out, cache, ids)
         return out
     r = cache[:, :, ids.long()]
     if out is not None:
@@ -522,7 +533,7 @@ def kv_gather(cache: torch.Tensor, ids: torch.Tensor, out: Optional[torch.Tensor
 
 def kv_scatter(cache: torch.Tensor, ids: torch.Tensor, buf: torch.Tensor) -> None:
     if _native(cache):
-        torch.ops.dgi.kv_scatter(cache, ids, buf)
+        _call("kv_scatter", cache, ids, buf)
     else:
         cache[:, :, ids.long()] = buf.view(cache.shape[0], cache.shape[1], ids.numel(), *cache.shape[3:])
 
@@ -530,7 +541,7 @@ def kv_scatter(cache: torch.Tensor, ids: torch.Tensor, buf: torch.Tensor) -> Non
 def kv_copy(cache: torch.Tensor, src: torch.Tensor, dst: torch.Tensor) -> None:
     """Copy pages src[i] -> dst[i] for every layer (src/dst sets must be disjoint)."""
     if _native(cache):
-        torch.ops.dgi.kv_copy(cache, src, dst)
+        _call("kv_copy", cache, src, dst)
     else:
         cache[:, :, dst.long()] = cache[:, :, src.long()]
 
@@ -566,7 +577,7 @@ def tree_mask(parent: torch.Tensor):
         B, N = parent.shape
         anc = torch.zeros(B, 64, dtype=torch.long, device=parent.device)
         depth = torch.empty(B, N, dtype=torch.int32, device=parent.device)
-        torch.ops.dgi.tree_mask(anc, depth, parent)
+        _call("tree_mask", anc, depth, parent)
         return anc, depth
     return tree_mask_ref(parent)
 
@@ -610,6 +621,6 @@ def tree_verify(parent, draft, target, anc, depth, max_path: int):
         acc = torch.empty(B, dtype=torch.int32, device=parent.device)
         path = torch.zeros(B, max_path, dtype=torch.int32, device=parent.device)
         toks = torch.zeros(B, max_path + 1, dtype=torch.long, device=parent.device)
-        torch.ops.dgi.tree_verify(acc, path, toks, parent, draft, target, anc, depth)
+        _call("tree_verify", acc, path, toks, parent, draft, target, anc, depth)
         return acc, path, toks
     return tree_verify_ref(parent, draft, target, anc, depth, max_path)

@@ -61,6 +61,9 @@ class Fabric:
         # queues behind a multi-hundred-MB transfer (see ``irecv_async``)
         self.recv_stream = torch.cuda.Stream(device=device) if self.on_gpu else None
         self._pending: list = []
+        # DGI_DEBUG_STREAMS=1: send buffers must not be rewritten while in flight (dgi.utils.debug)
+        from dgi.utils.debug import stream_checker
+        self.checker = stream_checker()
         # liveness watchdog over the rendezvous store (dgi.parallel.fault)
         self.watchdog = None
         if self.world > 1 and os.environ.get("DGI_WATCHDOG", "1") != "0":
@@ -72,7 +75,7 @@ class Fabric:
         """Ordered send on the data group; the compute stream is not blocked."""
         if self.staged:
             h = t.detach().cpu()
-            self._pending.append((dist.isend(h, dst), h))
+            self._pending.append((dist.isend(h, dst), h, None))
             self._reap()
             return
         if self.on_gpu:
@@ -80,11 +83,9 @@ class Fabric:
             with torch.cuda.stream(self.comm_stream):
                 self.comm_stream.wait_event(ev)
                 w = dist.isend(t, dst)
-            self._pending.append((w, t))
-            self._reap()
+            self._track(w, t)
         else:
-            self._pending.append((dist.isend(t, dst), t))
-            self._reap()
+            self._track(dist.isend(t, dst), t)
 
     def recv(self, t: torch.Tensor, src: int) -> torch.Tensor:
         """Blocking (stream-ordered on GPU) receive into ``t``."""
@@ -113,12 +114,28 @@ class Fabric:
             return AsyncRecv(self, w, t)
         return AsyncRecv(self, dist.irecv(t, src), t)
 
+    def _track(self, w, t: torch.Tensor) -> None:
+        rec = self.checker.on_send(t) if self.checker is not None else None
+        self._pending.append((w, t, rec))
+        self._reap()
+
+    def _done(self, rec) -> None:
+        if rec is not None:
+            self.checker.on_complete(rec)
+
     def _reap(self) -> None:
-        self._pending = [(w, t) for (w, t) in self._pending if not w.is_completed()]
+        keep = []
+        for w, t, rec in self._pending:
+            if w.is_completed():
+                self._done(rec)
+            else:
+                keep.append((w, t, rec))
+        self._pending = keep
 
     def flush(self) -> None:
-        for w, _t in self._pending:
+        for w, _t, rec in self._pending:
             w.wait()
+            self._done(rec)
         self._pending = []
         if self.on_gpu:
             torch.cuda.current_stream().wait_stream(self.comm_stream)
@@ -162,13 +179,13 @@ class Fabric:
     def ctrl_isend(self, arr: np.ndarray, dst: int):
         t = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.int64))
         w = dist.isend(t, dst, group=self.ctrl)
-        self._pending.append((w, t))
+        self._pending.append((w, t, None))
         return w
 
     def ctrl_send_tensor(self, t: torch.Tensor, dst: int) -> None:
         """Non-blocking host tensor send on the control group."""
         t = t.detach().cpu().contiguous()
-        self._pending.append((dist.isend(t, dst, group=self.ctrl), t))
+        self._pending.append((dist.isend(t, dst, group=self.ctrl), t, None))
 
     def ctrl_recv_tensor(self, t: torch.Tensor, src: int) -> torch.Tensor:
         dist.recv(t, src, group=self.ctrl)

@@ -2,6 +2,8 @@
 and the dispatch rules that decide which native kernel a GPU call takes."""
 import math
 
+import pytest
+
 import torch
 import torch.nn.functional as F
 
@@ -136,3 +138,27 @@ def test_running_set_is_an_ordered_o1_set():
     for r in rs:                      # iteration is a snapshot: removal inside the loop is safe
         rs.remove(r)
     assert not rs
+
+
+def test_debug_modes_are_opt_in(monkeypatch):
+    from dgi.utils import debug
+    monkeypatch.delenv("DGI_DEBUG_SYNC", raising=False)
+    monkeypatch.delenv("DGI_DEBUG_STREAMS", raising=False)
+    assert not debug.sync_enabled() and debug.stream_checker() is None
+    debug.after_op("noop")                         # no GPU / disabled: a no-op
+    monkeypatch.setenv("DGI_DEBUG_STREAMS", "1")
+    chk = debug.stream_checker()
+    t = torch.zeros(4)
+    rec = chk.on_send(t)
+    chk.on_complete(rec)                           # untouched buffer: fine
+    rec = chk.on_send(t)
+    t.add_(1)
+    with pytest.raises(debug.StreamOrderError):
+        chk.on_complete(rec)
+    monkeypatch.setenv("HIP_LAUNCH_BLOCKING", "0")
+    monkeypatch.setenv("DGI_DEBUG_SYNC", "0")
+    monkeypatch.setenv("AMD_SERIALIZE_KERNEL", "0")
+    monkeypatch.delenv("AMD_SERIALIZE_KERNEL")
+    debug.enable_serialized()
+    import os
+    assert os.environ["DGI_DEBUG_SYNC"] == "1" and os.environ["AMD_SERIALIZE_KERNEL"] == "3"

@@ -493,3 +493,32 @@ def test_watchdog_ends_survivor_of_dead_rank():
                 p.kill()
     assert codes[1] == 17
     assert codes[0] not in (0, None)   # the survivor was stopped by its watchdog, not left hanging
+
+
+def _reuse_body(rank, world):
+    """Rank 0 rewrites a send buffer before the transfer is known complete."""
+    import time as _t
+    from dgi.parallel.fabric import Fabric
+    from dgi.utils.debug import StreamOrderError
+    f = Fabric()
+    if rank == 0:
+        t = torch.arange(8, dtype=torch.float32)
+        f.send(t, 1)
+        t.add_(1.0)                    # the compute side reuses the buffer too early
+        try:
+            f.flush()
+        except StreamOrderError:
+            return {"caught": True, **f.checker.stats()}
+        return {"caught": False}
+    _t.sleep(0.5)
+    buf = torch.empty(8)
+    f.recv(buf, 0)
+    f.flush()
+    return {"stats": f.checker.stats()}
+
+
+def test_stream_order_checker_flags_send_buffer_reuse(monkeypatch):
+    monkeypatch.setenv("DGI_DEBUG_STREAMS", "1")
+    monkeypatch.setenv("DGI_WATCHDOG", "0")
+    out = _spawn("_reuse_body", 2)
+    assert out[0]["caught"] and out[0]["violations"] == 1 and out[0]["sends"] == 1
