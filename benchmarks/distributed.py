@@ -42,7 +42,12 @@ def main():
             str(a.warmup)]
     if a.concurrent:
         args += ["--concurrency", str(a.concurrent)]
-    res = {"pipeline": run_bench(a.workers, args)}
+    from results import from_bench_pipeline
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from dgi.models.config import get_config
+    raw = run_bench(a.workers, args)
+    res = {"pipeline": from_bench_pipeline(raw, a.workers, get_config(MODELS.get(a.model, a.model)).num_layers)
+           .to_dict(), "raw": {k: raw[k] for k in ("value", "ms_per_step", "config", "latency_ms") if k in raw}}
     if a.mode == "real":
         from single_worker import bench_http
         ns = argparse.Namespace(server_url=a.server_url, api_key=a.api_key, num_requests=a.num_requests,

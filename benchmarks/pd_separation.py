@@ -49,8 +49,14 @@ def main():
     a = ap.parse_args()
     if a.stress:
         a.concurrent = 512
+    from results import from_bench_pd
     modes = ["separated", "hybrid"] if a.compare else [a.mode]
-    out = {m: run(a, m) for m in modes}
+    out = {}
+    for m in modes:
+        raw = run(a, m)
+        pre, dec = (a.prefill_workers, a.decode_workers) if m == "separated" else \
+            (0, a.prefill_workers + a.decode_workers)
+        out[m] = from_bench_pd(raw, m, pre, dec).to_dict()
     for m, r in out.items():
         print(m, json.dumps(r))
     save(a.output, out)

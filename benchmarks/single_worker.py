@@ -1,8 +1,8 @@
 """Single-worker serving benchmark (reference benchmarks/single_worker.py, measured instead of never run).
 
-Closed-loop load against one engine: ``--num-requests`` requests, at most
-``--concurrent`` in flight, ``--max-tokens`` output each.  Reports output
-tok/s, TTFT p50/p95 and TPOT p50.  Backends:
+Closed-loop load against one engine: at most ``--concurrent`` requests in
+flight, ``--max-tokens`` output each; results are the reference's
+``BenchmarkResult`` records (benchmarks/results.py).  Backends:
 
 * ``mi355x`` / ``native`` — the dgi engine in-process (HIP kernels, hipGraph decode);
 * ``http`` — through the control plane + worker daemon at ``--server-url``
@@ -19,6 +19,7 @@ import threading
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
 def _pct(xs, q):
@@ -29,37 +30,17 @@ def _pct(xs, q):
 
 
 def bench_engine(a) -> dict:
-    import torch
-    from dgi.engine import EngineConfig, LLMEngine
-    from dgi.sched.request import SamplingParams
-    dev = "cuda" if torch.cuda.is_available() else "cpu"
-    eng = LLMEngine(EngineConfig(model=a.model, device=dev, max_num_seqs=max(a.concurrent, 1),
-                                 max_num_batched_tokens=a.max_batched_tokens, max_model_len=4096))
-    eng.warmup()
-    g = torch.Generator().manual_seed(0)
-    V = eng.model_cfg.vocab_size
-    prompts = [torch.randint(min(1000, V // 4), V, (a.prompt_length,), generator=g).tolist()
-               for _ in range(a.num_requests)]
-    sp = SamplingParams(max_tokens=a.max_tokens, temperature=0.0, ignore_eos=True)
-    pending = list(prompts)
-    live, done = [], []
-    t0 = time.perf_counter()
-    while pending or live:
-        while pending and len(live) < a.concurrent:
-            live.append(eng.add_request(pending.pop(), sp))
-        eng.step()
-        still = []
-        for r in live:
-            (done if r.finish_reason else still).append(r)
-        live = still
-    el = time.perf_counter() - t0
-    ttft = [r.ttft * 1000 for r in done]
-    tpot = [(r.token_times[-1] - r.token_times[0]) / max(1, len(r.token_times) - 1) * 1000 for r in done]
-    toks = sum(len(r.output) for r in done)
-    return {"backend": "mi355x", "model": a.model, "device": dev, "requests": len(done), "concurrent": a.concurrent,
-            "output_tok_s": round(toks / el, 1), "ttft_p50_ms": round(_pct(ttft, 0.5), 2),
-            "ttft_p95_ms": round(_pct(ttft, 0.95), 2), "tpot_p50_ms": round(_pct(tpot, 0.5), 2),
-            "seconds": round(el, 2)}
+    """The dgi engine under ``bench.py`` (closed loop at ``--concurrent``), as a
+    reference ``BenchmarkResult``."""
+    from _common import run_bench
+    from results import from_bench_single, gpu_stats
+    args = ["--model", a.model, "--layout", "single", "--concurrency", str(a.concurrent), "--prompt-len",
+            str(a.prompt_length), "--output-len", str(a.max_tokens), "--max-batched-tokens",
+            str(a.max_batched_tokens), "--steps", str(a.steps), "--warmup", str(a.warmup)]
+    res = run_bench(1, args)
+    out = from_bench_single(res, backend="mi355x", gpu=gpu_stats()).to_dict()
+    out["tpot_p50_ms"] = res.get("tpot_p50_ms")
+    return out
 
 
 def bench_http(a) -> dict:
@@ -93,9 +74,16 @@ def bench_http(a) -> dict:
     [t.start() for t in ths]
     [t.join() for t in ths]
     el = time.perf_counter() - t0
-    return {"backend": "http", "server": a.server_url, "requests": len(lat), "errors": errs,
-            "output_tok_s": round(toks[0] / el, 1), "latency_p50_ms": _pct(lat, 0.5),
-            "latency_p95_ms": _pct(lat, 0.95), "mean_latency_ms": statistics.mean(lat) if lat else None}
+    from results import BenchmarkResult
+    p = lambda q: float(_pct(lat, q) or 0.0)  # noqa: E731
+    mean = statistics.mean(lat) if lat else 0.0
+    # sync jobs return whole completions: TTFT through the pull path equals E2E here
+    return BenchmarkResult(backend="http", model_id=a.model, total_tokens=int(toks[0]), total_time_s=round(el, 3),
+                           tokens_per_second=round(toks[0] / el, 1) if el > 0 else 0.0, avg_ttft_ms=mean,
+                           p50_ttft_ms=p(0.5), p95_ttft_ms=p(0.95), p99_ttft_ms=p(0.99), avg_e2e_ms=mean,
+                           p50_e2e_ms=p(0.5), p95_e2e_ms=p(0.95), p99_e2e_ms=p(0.99), gpu_memory_used_gb=0.0,
+                           gpu_memory_total_gb=0.0, gpu_utilization_pct=0.0, avg_batch_size=float(a.concurrent),
+                           total_requests=len(lat)).to_dict() | {"errors": errs, "server": a.server_url}
 
 
 def main():
@@ -107,6 +95,8 @@ def main():
     ap.add_argument("--max-tokens", type=int, default=256)
     ap.add_argument("--prompt-length", type=int, default=128)
     ap.add_argument("--max-batched-tokens", type=int, default=8192)
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--server-url", default="http://localhost:8000")
     ap.add_argument("--api-key", default="")
     ap.add_argument("--output", default="benchmark_results.json")

@@ -44,7 +44,15 @@ def main():
     a = ap.parse_args()
     model = MODELS.get(a.model, a.model)
     depths = range(1, a.tree_depth + 1) if a.sweep_depth else [a.tree_depth]
-    res = {d: run(model, d, a.tree_width, a.max_tokens, a.train_steps) for d in depths}
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from results import from_spec_row
+    res = {}
+    for d in depths:
+        raw = run(model, d, a.tree_width, a.max_tokens, a.train_steps)
+        res[d] = [{"batch": row["batch"],
+                   "enabled": from_spec_row(row, model, d, a.tree_width, True, a.max_tokens).to_dict(),
+                   "disabled": from_spec_row(row, model, d, a.tree_width, False, a.max_tokens).to_dict()}
+                  for row in raw["rows"]]
     print(json.dumps(res, indent=2))
     with open(a.output, "w") as f:
         json.dump(res, f, indent=2)

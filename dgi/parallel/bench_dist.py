@@ -78,7 +78,8 @@ def run_distributed(args, layout_kind: str, dist):
     el = max(x[1].item() for x in tl)
     all_ttfts = [v for o in obj for v in o["ttfts"]]
     all_tpots = [v for o in obj for v in o.get("tpots", [])]
-    per_rank = [{k: v for k, v in o.items() if k not in ("ttfts", "tpots")} for o in obj]
+    all_e2es = [v for o in obj for v in o.get("e2es", [])]
+    per_rank = [{k: v for k, v in o.items() if k not in ("ttfts", "tpots", "e2es")} for o in obj]
     roles = {}
     for o in per_rank:
         r = roles.setdefault(o["role"], {"ranks": 0, "tokens": 0})
@@ -91,7 +92,7 @@ def run_distributed(args, layout_kind: str, dist):
                                              "prefill": layout.prefill_ranks, "decode_groups": layout.decode_groups},
                                   "concurrency": conc, "pair_setup_s": round(t_pairs, 3), "roles": roles,
                                   "migration_ms_p50": round(float(sorted(mig)[len(mig) // 2]), 3) if mig else None,
-                                  "tpots": all_tpots, "ranks": per_rank}
+                                  "tpots": all_tpots, "e2es": all_e2es, "ranks": per_rank}
 
 
 # ---------------------------------------------------------------------------- layer pipeline only
@@ -293,7 +294,9 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
         drv.finish()
         return n, el, list(local_ttfts), {"tokens": n, "received": drv.received, "running_at_end": running,
                                           "recv_GB": round(drv.recv_bytes / 1e9, 3), "local_fraction": local_frac,
-                                          "steps": drv.engine.stats["steps"], "tpots": _tpots(finished)}
+                                          "steps": drv.engine.stats["steps"], "tpots": _tpots(finished),
+                                          "e2es": [r.finish_time - r.arrival for r in finished
+                                                   if r.finish_time is not None]}
 
     # later stages of a decode pipeline replica
     w = StageWorker(cfg, f, layout.group_of(f.rank))

@@ -65,7 +65,7 @@ from dgi.utils.trace import mark, phase
 MSG_MIGRATE, MSG_CREDIT, MSG_DONE, MSG_FINISHED, MSG_TOKENS, MSG_FIRST = 1, 2, 3, 4, 5, 6
 REASONS = {0: None, 1: "length", 2: "stop"}
 CTRL = 8
-META_FIELDS = 11
+META_FIELDS = 12
 # per-GPU figures registered with the node-local P/D scheduler (MI355X: ~2.5 PF
 # dense bf16, 8 TB/s HBM3E); only their ratios matter for placement
 MI355X_TFLOPS = 2500.0
@@ -111,10 +111,11 @@ def _blocks_for(n_tokens: int, bs: int) -> int:
 
 def _req_meta(r: Request, nblocks: int, first: Optional[int] = None) -> list:
     p = r.params
+    age_us = int((time.perf_counter() - r.arrival) * 1e6)    # time since arrival on the prefill rank
     return [int(r.rid) & 0x7FFFFFFF, 0, len(r.prompt), r.output[0] if first is None else first, nblocks,
             p.max_tokens,
             int(np.float32(p.temperature).view(np.int32)), int(r.seed) & 0x7FFFFFFF, int(p.ignore_eos), p.top_k,
-            int(np.float32(p.top_p).view(np.int32))]
+            int(np.float32(p.top_p).view(np.int32)), age_us]
 
 
 class PrefillServer:
@@ -551,7 +552,7 @@ class DecodeDriver:
         sch = self.engine.scheduler
         o = k = 0
         for m in meta:
-            rid, code, plen, first, nb, max_tok, tbits, seed, ign, topk, pbits, credit = m
+            rid, code, plen, first, nb, max_tok, tbits, seed, ign, topk, pbits, age_us, credit = m
             if code > 0:
                 # streamed prompt that finished at its first token: release its pages
                 # (the prefill rank refunded the credit and reported it to the router)
@@ -568,6 +569,7 @@ class DecodeDriver:
             r.seed = seed
             r.output = [first]
             r.first_token_time = time.perf_counter()
+            r.arrival = r.first_token_time - age_us / 1e6     # ~ original arrival on the prefill rank
             o += plen
             sch.add_prefilled(r, ids[k:k + nb])
             self.engine.requests[r.rid] = r
