@@ -5,12 +5,17 @@ distributed.py:48-87, pd_separation.py:54-99, speculative.py:47-83); the
 converters are fed a bench.py JSON line / a bench_spec row of the shapes the
 GPU runs produce (profiles/), since bench.py itself needs a GPU."""
 import dataclasses
+import importlib.util
 import os
 import sys
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "benchmarks"))
-
-import results as R  # noqa: E402
+# loaded by path: putting benchmarks/ on sys.path would shadow worker's flat ``distributed`` package
+_spec = importlib.util.spec_from_file_location(
+    "bench_results", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "benchmarks",
+                                  "results.py"))
+R = importlib.util.module_from_spec(_spec)
+sys.modules["bench_results"] = R          # dataclasses resolve their module through sys.modules
+_spec.loader.exec_module(R)
 
 REF_FIELDS = {
     "BenchmarkResult": "backend model_id total_tokens total_time_s tokens_per_second avg_ttft_ms p50_ttft_ms "
