@@ -520,6 +520,9 @@ class SpecEngine(LLMEngine):
         self._mode_steps = 0
         self._probe = False
         self._cost: dict = {}       # (mode, bucket) -> EMA seconds per generated token
+        self._acc_ema: Optional[float] = None   # smoothed acceptance rate driving depth changes
+        self._acc_n = 0                          # steps behind it (at the current depth)
+        self._captured = False      # this step captured a hipGraph (its time is not a cost sample)
 
     def _bucket(self, R: int) -> int:
         return next((b for b in VERIFY_BUCKETS if b >= R), VERIFY_BUCKETS[-1])
@@ -533,6 +536,7 @@ class SpecEngine(LLMEngine):
         g = self._dgraphs.get((Rb, self.cur_depth))
         if g is None:
             g = self._dgraphs[(Rb, self.cur_depth)] = _DraftGraph(self, Rb, self.cur_depth)
+            self._captured = True
         return g
 
     def _verify_graph(self, R: int) -> Optional[_VerifyGraph]:
@@ -544,7 +548,32 @@ class SpecEngine(LLMEngine):
         g = self._vgraphs.get((Rb, self.cur_depth))
         if g is None:
             g = self._vgraphs[(Rb, self.cur_depth)] = _VerifyGraph(self, Rb, self.cur_depth)
+            self._captured = True
         return g
+
+    def warmup_spec(self, batches=(1,), depths=None) -> int:
+        """Capture the draft / verify hipGraphs of every (batch bucket, depth) the
+        adaptive controller can reach, so no capture lands in a serving step (a
+        capture inside a timed step also corrupts the auto-off cost estimate)."""
+        if not (self.spec.graphs and self.device.type == "cuda"):
+            return 0
+        keep, n = self.cur_depth, 0
+        try:
+            for R in batches:
+                for d in (depths or range(1, self.spec.depth + 1)):
+                    self.cur_depth = d
+                    n += int(self._verify_graph(R) is not None) + int(self._draft_graph(R) is not None)
+        finally:
+            self.cur_depth = keep
+            self._captured = False
+        return n
+
+    def reset_controller(self) -> None:
+        """Back to full depth, speculation on, no cost history."""
+        self.cur_depth, self.spec_on = self.spec.depth, True
+        self._mode_steps, self._probe = 0, False
+        self._cost.clear()
+        self._acc_ema, self._acc_n = None, 0
 
     # ------------------------------------------------------------------ helpers
     def _eligible(self, r: Request) -> bool:
@@ -587,16 +616,25 @@ class SpecEngine(LLMEngine):
         self._cost[key] = c if old is None else 0.7 * old + 0.3 * c
 
     def _adapt_depth(self, accept_rate: float) -> None:
-        """Reference semantics (worker/engines/speculative.py:456-463)."""
+        """Reference thresholds (worker/engines/speculative.py:456-463), applied to
+        an EMA of the per-step rate (the reference reacts to single steps, which
+        makes the depth — and with graphs, the captured graph — flip-flop); the
+        EMA restarts at every depth change since the rate depends on the depth."""
         if not self.spec.adaptive_depth:
             return
+        e = accept_rate if self._acc_ema is None else 0.6 * self._acc_ema + 0.4 * accept_rate
+        self._acc_ema = e
+        self._acc_n += 1
+        if self._acc_n < 2:
+            return
         d = self.cur_depth
-        if accept_rate < self.spec.min_accept_rate:
+        if e < self.spec.min_accept_rate:
             d = max(1, d - 1)
-        elif accept_rate > self.spec.raise_accept_rate:
+        elif e > self.spec.raise_accept_rate:
             d = min(self.spec.depth, d + 1)
         if d != self.cur_depth:
             self.cur_depth = d
+            self._acc_ema, self._acc_n = None, 0
             self.spec_stats["depth_changes"] += 1
 
     def _control(self, R: int) -> None:
@@ -610,11 +648,13 @@ class SpecEngine(LLMEngine):
         if self.spec_on:
             if self._mode_steps < 4:
                 return
-            if cp is None or cs is None or cs > cp:
+            if cs is None:
+                return               # no clean speculative sample yet (graph-capture steps)
+            if cp is None or cs > cp:
                 # no plain reference yet (probe it), or speculation is the slower mode
                 self.spec_on, self._mode_steps = False, 0
                 self._probe = cp is None
-                if cs is not None and cp is not None:
+                if cp is not None:
                     self.spec_stats["switches_off"] += 1
         else:
             if self._mode_steps >= (3 if self._probe else self.spec.probe_every):
@@ -644,9 +684,10 @@ class SpecEngine(LLMEngine):
         live = [r for r in spec_reqs if r in self.scheduler.running and self._eligible(r)]
         if live:
             ts = time.perf_counter()
+            self._captured = False
             o = self._spec_step(live)
             outs += o
-            if sb.empty:
+            if sb.empty and not self._captured:
                 self._record("spec", len(live), time.perf_counter() - ts, len(o))
             self._control(len(live))
         self.stats["step_time"] += time.perf_counter() - t0

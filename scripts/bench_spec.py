@@ -81,8 +81,11 @@ def main():
         sp = SamplingParams(max_tokens=a.output_len, temperature=0.0, ignore_eos=True)
         timed_generate(base, prompts, SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True))
         timed_generate(spec, prompts, SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True))
+        spec.warmup_spec([B])            # every depth the controller can reach, outside the timed runs
         ref, t_base = timed_generate(base, prompts, sp)
-        spec.spec_stats.update(spec_steps=0, spec_rows=0, accepted=0, spec_tokens=0, draft_s=0.0, verify_s=0.0)
+        spec.reset_controller()
+        spec.spec_stats.update(spec_steps=0, spec_rows=0, accepted=0, spec_tokens=0, draft_s=0.0, verify_s=0.0,
+                               plain_steps=0, switches_off=0, depth_changes=0)
         out, t_spec = timed_generate(spec, prompts, sp)
         acc = spec.acceptance()
         toks = B * a.output_len
@@ -108,6 +111,7 @@ def main():
                 torch.cuda.synchronize()
                 return [r.output for r in rs], time.perf_counter() - t1
             sref, ts_base = run(base)
+            spec.reset_controller()
             spec.spec_stats.update(spec_steps=0, spec_rows=0, accepted=0, spec_tokens=0)
             sout, ts_spec = run(spec)
             sa = spec.acceptance()
@@ -124,8 +128,9 @@ def main():
             rs = [spec.add_request(pr, sp) for pr in prompts]
             for r, o in zip(rs, ref):
                 reqs_rid[r.rid] = o
+            spec.reset_controller()
             spec.spec_stats.update(spec_steps=0, spec_rows=0, accepted=0, spec_tokens=0, draft_s=0.0, verify_s=0.0,
-                                   plain_steps=0)
+                                   plain_steps=0, switches_off=0, depth_changes=0)
             torch.cuda.synchronize()
             t1 = time.perf_counter()
             while spec.has_unfinished():

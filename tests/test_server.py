@@ -360,3 +360,83 @@ def test_worker_daemon_runs_pd_phases():
     out = d.execute("llm", {"prompt": "x", "max_tokens": 16, "pd": True, "pd_phase": "decode", "kv_source": "p"},
                     "j1")
     assert out["phase"] == "decode" and out["response"] == "full text" and calls[-1]["max_tokens"] == 16
+
+
+# ----------------------------------------------------------------- admin console
+def _spa_calls():
+    """(method, path template) of every admin API call in the SPA's script."""
+    import re
+    s = (ROOT / "server/static/admin/index.html").read_text()
+    calls = [("GET", m) for m in re.findall(r'get\(\s*[`"](/[^`"?]*)', s)]
+    calls += re.findall(r'call\("(GET|POST|PUT|DELETE)",\s*[`"](/[^`"?]*)', s)
+    norm = (lambda p: re.sub(r"\$\{[^}]*\}", "{x}", p) + ("{x}" if p.endswith("/") else ""))
+    return s, sorted(set((m, norm(p)) for m, p in calls))
+
+
+def test_admin_console_is_served_and_calls_only_real_routes(client):
+    import re
+    s, calls = _spa_calls()
+    r = client.get("/admin")
+    assert r.status_code == 200 and "MI355X Inference" in r.text
+    assert "cdn" not in s.lower() and "<script src" not in s          # self-contained, works offline
+    spec = client.get("/openapi.json").json()["paths"]
+    routes = [(m.upper(), path) for path, ops in spec.items() for m in ops if path.startswith("/api/v1/admin")]
+    assert routes
+
+    def known(method, path):
+        for m, tpl in routes:
+            rx = "^" + re.sub(r"\{[^}]+\}", "[^/]+", tpl) + "$"
+            if m == method and re.match(rx, "/api/v1/admin" + path.replace("{x}", "X")):
+                return True
+        return False
+    missing = [c for c in calls if not known(*c)]
+    assert not missing, missing
+    # the console covers every admin area: privacy, enterprises + keys, worker config, bills, usage, P/D
+    paths = {p for _, p in calls}
+    for need in ("/enterprises/{x}/privacy", "/enterprises/{x}/privacy/compliance",
+                 "/enterprises/{x}/privacy/retention-status", "/enterprises/{x}/privacy/cleanup",
+                 "/enterprises/{x}/privacy/export", "/enterprises/{x}/privacy/data", "/privacy/scheduled-cleanup",
+                 "/enterprises", "/enterprises/{x}/api-keys", "/workers/{x}/config", "/workers/{x}/usage",
+                 "/bills", "/bills/{x}", "/usage/records", "/pd/stats", "/health/detailed", "/dashboard/realtime"):
+        assert any(p == need or p.startswith(need) for p in paths), need
+    assert ("PUT", "/workers/{x}/config") in calls and ("DELETE", "/enterprises/{x}/privacy/data") in calls
+
+
+def test_admin_console_script_parses_and_reads_real_fields(client):
+    import re
+    import shutil
+    import subprocess
+    s, _ = _spa_calls()
+    js = re.search(r"<script>(.*)</script>", s, re.S).group(1)
+    if shutil.which("node"):
+        p = ROOT / "server/static/admin/.check.js"
+        try:
+            p.write_text(js)
+            out = subprocess.run(["node", "--check", str(p)], capture_output=True, text=True)
+            assert out.returncode == 0, out.stderr
+        finally:
+            p.unlink(missing_ok=True)
+    # the response fields the dashboard / worker / usage pages read
+    c = client
+    wid, hdr, _ = _register(c)
+    d = c.get("/api/v1/admin/dashboard").json()
+    assert {"online", "total"} <= set(d["workers"]) and {"jobs", "revenue", "gpu_hours"} <= set(d["today"])
+    rt = c.get("/api/v1/admin/dashboard/realtime").json()
+    assert {"busy", "details"} <= set(rt["workers"]) and {"running", "queued", "details"} <= set(rt["jobs"])
+    w = c.get(f"/api/v1/admin/workers/{wid}").json()
+    assert "load_control" in w["config"] and "version" in w["config"]
+    assert c.put(f"/api/v1/admin/workers/{wid}/config", json={"load_control": {"max_concurrent_jobs": 64}}
+                 ).json()["status"] == "ok"
+    assert c.get(f"/api/v1/admin/workers/{wid}").json()["config"]["load_control"]["max_concurrent_jobs"] == 64
+    u = c.get(f"/api/v1/admin/workers/{wid}/usage?days=30").json()
+    assert {"total_cost", "total_gpu_seconds"} <= set(u)
+    su = c.get("/api/v1/admin/usage/summary?group_by=day").json()
+    assert {"count", "cost", "gpu_hours"} <= set(su["totals"])
+    pd = c.get("/api/v1/admin/pd/stats").json()
+    assert {"prefill_queue_size", "decode_queue_size", "transitions", "migrations"} <= set(pd)
+    ent = c.post("/api/v1/admin/enterprises", json={"name": "Acme", "code": "acme"}).json()
+    c.post(f"/api/v1/admin/enterprises/{ent['id']}/api-keys", json={"name": "k"})
+    keys = c.get(f"/api/v1/admin/enterprises/{ent['id']}/api-keys").json()
+    assert isinstance(keys, list) and {"name", "key_prefix", "total_requests"} <= set(keys[0])
+    h = c.get("/api/v1/admin/health/detailed").json()
+    assert {"status", "database", "stale_workers", "stuck_jobs", "issues"} <= set(h)

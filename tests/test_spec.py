@@ -148,6 +148,32 @@ def test_auto_off_switches_to_plain_when_speculation_is_slower():
     assert modes.count(False) > modes.count(True)
 
 
+def test_controller_ignores_single_outliers_and_capture_steps():
+    """One low-acceptance step does not move the depth (EMA, >= 2 steps per depth);
+    a step that captured a graph is no cost sample, so it cannot switch speculation
+    off; reset_controller() restores full depth and forgets the costs."""
+    _, se = _engines(spec=SpecConfig(depth=4, width=2, topk=3, auto_off=True, adaptive_depth=True))
+    se._adapt_depth(0.9)
+    se._adapt_depth(0.0)                  # outlier: EMA 0.54, stays
+    assert se.cur_depth == 4
+    for _ in range(2):
+        se._adapt_depth(0.0)
+    assert se.cur_depth == 3 and se.spec_stats["depth_changes"] == 1
+    se._adapt_depth(0.0)                  # first sample at the new depth never moves it
+    assert se.cur_depth == 3
+    # auto-off: speculation steps without a clean cost sample keep speculation on
+    se._record("plain", 4, 0.010, 4)
+    for _ in range(6):
+        se._control(4)
+    assert se.spec_on
+    se._record("spec", 4, 0.030, 4)       # now measurably slower than plain
+    se._control(4)
+    assert not se.spec_on and se.spec_stats["switches_off"] == 1
+    se.reset_controller()
+    assert se.spec_on and se.cur_depth == 4 and not se._cost
+    assert se.warmup_spec([1, 2]) == 0    # CPU: no graphs to capture
+
+
 def test_kv_slot_copy():
     kv = torch.randn(3, 2, 5, 2, 4, 8)
     ref = kv.clone()

@@ -122,6 +122,10 @@ class NativeLLMEngine(LLMBaseEngine):
         self.device = device
         if c.get("warmup", False):
             self.engine.warmup()
+            if spec and hasattr(self.engine, "warmup_spec"):
+                # speculation graphs for the batch buckets this worker serves, at every depth
+                sb = (spec if isinstance(spec, dict) else {}).get("graph_batches", (1, 2, 4, 8))
+                self.engine.warmup_spec(tuple(sb))
         self._stop.clear()
         self._thread = threading.Thread(target=self._loop, name="dgi-engine", daemon=True)
         self._thread.start()
