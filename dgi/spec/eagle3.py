@@ -522,6 +522,9 @@ class SpecEngine(LLMEngine):
         self._cost: dict = {}       # (mode, bucket) -> EMA seconds per generated token
         self._acc_ema: Optional[float] = None   # smoothed acceptance rate driving depth changes
         self._acc_n = 0                          # steps behind it (at the current depth)
+        self._period = [0.0, 0, 0]               # clean spec samples this period: seconds, tokens, steps
+        self._backoff = 1                        # probe interval multiplier
+        self._probed = False                     # the current speculation period is a re-probe
         self._captured = False      # this step captured a hipGraph (its time is not a cost sample)
 
     def _bucket(self, R: int) -> int:
@@ -568,11 +571,14 @@ class SpecEngine(LLMEngine):
             self._captured = False
         return n
 
-    def reset_controller(self) -> None:
-        """Back to full depth, speculation on, no cost history."""
+    def reset_controller(self, keep_plain_costs: bool = False) -> None:
+        """Back to full depth, speculation on, no acceptance history.  Plain-decode
+        cost per bucket is a property of the hardware, not of the workload:
+        ``keep_plain_costs`` keeps it so a new workload needs no plain probe."""
         self.cur_depth, self.spec_on = self.spec.depth, True
-        self._mode_steps, self._probe = 0, False
-        self._cost.clear()
+        self._mode_steps, self._probe, self._probed, self._backoff = 0, False, False, 1
+        self._period = [0.0, 0, 0]
+        self._cost = {k: v for k, v in self._cost.items() if keep_plain_costs and k[0] == "plain"}
         self._acc_ema, self._acc_n = None, 0
 
     # ------------------------------------------------------------------ helpers
@@ -614,6 +620,10 @@ class SpecEngine(LLMEngine):
         c = seconds / tokens
         old = self._cost.get(key)
         self._cost[key] = c if old is None else 0.7 * old + 0.3 * c
+        if mode == "spec":           # this speculation period's own cost (acceptance changes between probes)
+            self._period[0] += seconds
+            self._period[1] += tokens
+            self._period[2] += 1
 
     def _adapt_depth(self, accept_rate: float) -> None:
         """Reference thresholds (worker/engines/speculative.py:456-463), applied to
@@ -638,26 +648,35 @@ class SpecEngine(LLMEngine):
             self.spec_stats["depth_changes"] += 1
 
     def _control(self, R: int) -> None:
-        """Auto-off: after a few steps in a mode compare the measured cost per
-        generated token of speculation and plain decode at this batch bucket."""
+        """Auto-off: compare this speculation period's measured cost per generated
+        token with plain decoding's at the same batch bucket.  Two clean samples
+        decide; a first period without a plain reference probes 3 plain steps.
+        Probes that keep losing back off exponentially (probe_every x 1, 2, 4, 8
+        plain steps), a winning probe resets the interval."""
         if not self.spec.auto_off or R == 0:
             return
         self._mode_steps += 1
-        b = self._bucket(R)
-        cs, cp = self._cost.get(("spec", b)), self._cost.get(("plain", b))
+        cp = self._cost.get(("plain", self._bucket(R)))
         if self.spec_on:
-            if self._mode_steps < 4:
+            secs, toks, n = self._period
+            if n < 2:
+                return               # fewer than 2 clean samples (graph-capture steps are not samples)
+            if cp is None:
+                self.spec_on, self._mode_steps, self._probe = False, 0, True
+            elif secs / toks > cp:
+                self.spec_on, self._mode_steps, self._probe = False, 0, False
+                self.spec_stats["switches_off"] += 1
+                if self._probed:
+                    self._backoff = min(8, self._backoff * 2)
+            else:
+                self._backoff = 1
+                self._period = [0.0, 0, 0]     # keep speculating; judge the next window afresh
                 return
-            if cs is None:
-                return               # no clean speculative sample yet (graph-capture steps)
-            if cp is None or cs > cp:
-                # no plain reference yet (probe it), or speculation is the slower mode
-                self.spec_on, self._mode_steps = False, 0
-                self._probe = cp is None
-                if cp is not None:
-                    self.spec_stats["switches_off"] += 1
+            self._period = [0.0, 0, 0]
         else:
-            if self._mode_steps >= (3 if self._probe else self.spec.probe_every):
+            wait = 3 if self._probe else self.spec.probe_every * self._backoff
+            if self._mode_steps >= wait:
+                self._probed = not self._probe
                 self.spec_on, self._mode_steps, self._probe = True, 0, False
 
     # ------------------------------------------------------------------ step

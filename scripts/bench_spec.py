@@ -128,7 +128,7 @@ def main():
             rs = [spec.add_request(pr, sp) for pr in prompts]
             for r, o in zip(rs, ref):
                 reqs_rid[r.rid] = o
-            spec.reset_controller()
+            spec.reset_controller(keep_plain_costs=True)     # plain cost per bucket is learned once per engine
             spec.spec_stats.update(spec_steps=0, spec_rows=0, accepted=0, spec_tokens=0, draft_s=0.0, verify_s=0.0,
                                    plain_steps=0, switches_off=0, depth_changes=0)
             torch.cuda.synchronize()

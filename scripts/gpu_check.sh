@@ -48,6 +48,7 @@ for s in $STEPS; do
     padtable) run padtable 600 python scripts/mlp_pad_table.py --model llama3-70b --out gpurun_out/mlp_pad_70b.json ;;
     bench70b_nopad) DGI_MLP_PAD=0 run bench70b_nopad 1200 python bench.py --steps 30 --warmup 5 --json-out gpurun_out/bench70b_nopad.json ;;
     pdcap_mbt) run pdcap_mbt 1000 python scripts/pd_capacity.py --mbt 3072,3584,4096,4608,5120,6144 --decode "" --out gpurun_out/pdcap_mbt.jsonl ;;
+    spec8b_ctl) run spec8b_ctl 900 python scripts/bench_spec.py --batch 1 4 16 --target peaked --train-steps 1500 --random-seqs 1024 --oracle-accept 0.6 1.0 --sampled --out gpurun_out/spec8b_ctl.json ;;
     bench70b_long) run bench70b_long 1200 python bench.py --steps 200 --warmup 20 --json-out gpurun_out/bench70b_long.json ;;
   esac
 done

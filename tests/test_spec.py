@@ -168,9 +168,27 @@ def test_controller_ignores_single_outliers_and_capture_steps():
     assert se.spec_on
     se._record("spec", 4, 0.030, 4)       # now measurably slower than plain
     se._control(4)
+    assert se.spec_on                     # one sample does not decide
+    se._record("spec", 4, 0.030, 4)
+    se._control(4)
     assert not se.spec_on and se.spec_stats["switches_off"] == 1
+    # losing re-probes back off: 48, then 96 plain steps
+    for wait in (48, 96):
+        for _ in range(wait - 1):
+            se._control(4)
+        assert not se.spec_on
+        se._control(4)
+        assert se.spec_on
+        se._record("spec", 4, 0.030, 4)
+        se._control(4)
+        se._record("spec", 4, 0.030, 4)
+        se._control(4)
+        assert not se.spec_on
+    assert se._backoff == 4
+    se.reset_controller(keep_plain_costs=True)
+    assert se.spec_on and se.cur_depth == 4 and list(se._cost) == [("plain", 4)]
     se.reset_controller()
-    assert se.spec_on and se.cur_depth == 4 and not se._cost
+    assert not se._cost
     assert se.warmup_spec([1, 2]) == 0    # CPU: no graphs to capture
 
 
