@@ -18,8 +18,8 @@ int dgi_rope_cache(void* qkv, int T, int qkv_stride, const int* positions, const
                    void* v_cache, int block_size, hipStream_t s);
 int dgi_paged_decode(const void* q, int q_stride, const void* k_cache, const void* v_cache,
                      const int* block_tables, int bt_stride, const int* context_lens, void* out,
-                     int out_stride, float* part_o, float* part_lse, int B, int nh, int nkv, int hd,
-                     int block_size, int max_splits, int part_size, float scale, hipStream_t s);
+                     int out_stride, float* part_o, float* part_lse, int* counters, int B, int nh, int nkv,
+                     int hd, int block_size, int max_splits, int part_size, float scale, hipStream_t s);
 int dgi_paged_prefill(const void* q, int q_stride, const void* k_cache, const void* v_cache,
                       const int* block_tables, int bt_stride, const int* cu_seqlens_q,
                       const int* context_lens, const int* tiles, int n_tiles, void* out,
@@ -28,6 +28,10 @@ int dgi_paged_prefill(const void* q, int q_stride, const void* k_cache, const vo
 int dgi_silu_mul(const void* gu, void* out, int T, int I, hipStream_t s);
 int dgi_skinny_gemm(const void* x, int ldx, const void* w, const void* bias, void* y, int ldy, int M,
                     int N, int K, int nw, hipStream_t s);
+int dgi_fused_skinny(const void* x, int ldx, const void* res, int ldr, void* res_out, const void* gamma,
+                     float eps, const void* w, const void* bias, void* y, int ldy, int M, int N, int K, int pro,
+                     int epi, const int* positions, const float* cos_sin, const int* slots, void* k_cache,
+                     void* v_cache, int nh, int nkv, int block_size, hipStream_t s);
 int dgi_sample(const void* logits, int is_bf16, int B, int V, int stride, const float* temperature,
                const long long* seeds, long long step, const float* thresh, long long* out, hipStream_t s);
 int dgi_topkp_threshold(const void* logits, int is_bf16, int B, int V, int stride, const float* temperature,
@@ -114,7 +118,8 @@ void rope_cache(at::Tensor qkv, const at::Tensor& positions, const at::Tensor& c
 void paged_decode(at::Tensor out, const at::Tensor& q, const at::Tensor& k_cache,
                   const at::Tensor& v_cache, const at::Tensor& block_tables,
                   const at::Tensor& context_lens, at::Tensor part_o, at::Tensor part_lse,
-                  int64_t nh, int64_t nkv, int64_t max_splits, int64_t part_size, double scale) {
+                  int64_t nh, int64_t nkv, int64_t max_splits, int64_t part_size, double scale,
+                  const c10::optional<at::Tensor>& counters) {
   check_bf16(out, "out"); check_bf16(q, "q"); check_bf16(k_cache, "k_cache"); check_bf16(v_cache, "v_cache");
   check_i32(block_tables, "block_tables"); check_i32(context_lens, "context_lens");
   TORCH_CHECK(q.dim() == 2 && q.stride(1) == 1 && out.dim() == 2 && out.stride(1) == 1);
@@ -128,11 +133,17 @@ void paged_decode(at::Tensor out, const at::Tensor& q, const at::Tensor& k_cache
     TORCH_CHECK(part_o.numel() >= (int64_t)B * nh * max_splits * hd);
     TORCH_CHECK(part_lse.numel() >= (int64_t)B * nh * max_splits);
   }
+  int* cnt = nullptr;
+  if (counters.has_value() && counters->defined() && max_splits > 1) {
+    check_i32(*counters, "counters");
+    TORCH_CHECK(counters->numel() >= (int64_t)B * nkv, "paged_decode: counters need B * nkv zeros");
+    cnt = counters->data_ptr<int>();
+  }
   check_rc(dgi_paged_decode(q.data_ptr(), (int)q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                             block_tables.data_ptr<int>(), (int)block_tables.stride(0),
                             context_lens.data_ptr<int>(), out.data_ptr(), (int)out.stride(0),
                             max_splits > 1 ? part_o.data_ptr<float>() : nullptr,
-                            max_splits > 1 ? part_lse.data_ptr<float>() : nullptr, B, (int)nh,
+                            max_splits > 1 ? part_lse.data_ptr<float>() : nullptr, cnt, B, (int)nh,
                             (int)nkv, hd, (int)k_cache.size(2), (int)max_splits, (int)part_size,
                             (float)scale, cur_stream()),
            "paged_decode");
@@ -192,6 +203,84 @@ void skinny_gemm(at::Tensor out, const at::Tensor& x, const at::Tensor& w,
   check_rc(dgi_skinny_gemm(x.data_ptr(), (int)x.stride(0), w.data_ptr(), b, out.data_ptr(), (int)out.stride(0),
                            (int)M, (int)N, (int)K, (int)cfg, cur_stream()),
            "skinny_gemm");
+}
+
+// Decode GEMM with fused RMSNorm prologue (pro 1: norm, 2: residual add + norm -> res_out) and
+// epilogue (epi 0: store, 1: SwiGLU over the [gate; up] rows, 2: RoPE + paged KV write).
+void fused_skinny(at::Tensor y, const at::Tensor& x, const c10::optional<at::Tensor>& res,
+                  const c10::optional<at::Tensor>& res_out, const c10::optional<at::Tensor>& gamma, double eps,
+                  const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t pro, int64_t epi,
+                  const c10::optional<at::Tensor>& positions, const c10::optional<at::Tensor>& cos_sin,
+                  const c10::optional<at::Tensor>& slots, const c10::optional<at::Tensor>& k_cache,
+                  const c10::optional<at::Tensor>& v_cache, int64_t nh, int64_t nkv) {
+  check_bf16(y, "y"); check_bf16(x, "x"); check_bf16(w, "w");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "fused_skinny: 2-D operands");
+  TORCH_CHECK(x.stride(1) == 1 && y.stride(1) == 1 && w.is_contiguous() && x.stride(0) % 8 == 0);
+  const int64_t M = x.size(0), K = x.size(1), R = w.size(0);
+  TORCH_CHECK(w.size(1) == K && y.size(0) == M && M <= 16 && K % 1024 == 0, "fused_skinny: M<=16, K%1024");
+  TORCH_CHECK(x.device() == w.device() && y.device() == w.device());
+  int64_t N = R;
+  if (epi == 1) {
+    TORCH_CHECK(R % 2 == 0 && y.size(1) == R / 2, "fused_skinny: SwiGLU output is [M, I] for [2I, K] weights");
+    N = R / 2;
+  } else {
+    TORCH_CHECK(y.size(1) == R, "fused_skinny: y must be [M, N]");
+  }
+  const void* rp = nullptr;
+  void* rop = nullptr;
+  int ldr = 0;
+  const void* gp = nullptr;
+  if (pro >= 1) {
+    TORCH_CHECK(gamma.has_value() && gamma->defined());
+    check_bf16(*gamma, "gamma");
+    TORCH_CHECK(gamma->is_contiguous() && gamma->numel() == K);
+    gp = gamma->data_ptr();
+  }
+  if (pro == 2) {
+    TORCH_CHECK(res.has_value() && res_out.has_value() && res->defined() && res_out->defined());
+    check_bf16(*res, "res"); check_bf16(*res_out, "res_out");
+    TORCH_CHECK(res->sizes() == x.sizes() && res_out->sizes() == x.sizes() && res->stride(1) == 1 &&
+                res_out->stride(1) == 1 && res->stride(0) == res_out->stride(0) && res->stride(0) % 8 == 0);
+    TORCH_CHECK(res_out->data_ptr() != res->data_ptr() && res_out->data_ptr() != x.data_ptr(),
+                "fused_skinny: res_out must not alias x or res");
+    rp = res->data_ptr();
+    rop = res_out->data_ptr();
+    ldr = (int)res->stride(0);
+  }
+  const void* b = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    check_bf16(*bias, "bias");
+    TORCH_CHECK(bias->is_contiguous() && bias->numel() == R);
+    b = bias->data_ptr();
+  }
+  const int* pos = nullptr;
+  const float* cs = nullptr;
+  const int* sl = nullptr;
+  void* kc = nullptr;
+  void* vc = nullptr;
+  int bsz = 16;
+  if (epi == 2) {
+    TORCH_CHECK(positions.has_value() && cos_sin.has_value() && slots.has_value() && k_cache.has_value() &&
+                v_cache.has_value());
+    check_i32(*positions, "positions"); check_i32(*slots, "slots");
+    check_bf16(*k_cache, "k_cache"); check_bf16(*v_cache, "v_cache");
+    TORCH_CHECK(positions->numel() >= M && slots->numel() >= M);
+    TORCH_CHECK(cos_sin->scalar_type() == at::kFloat && cos_sin->is_contiguous() && cos_sin->dim() == 2 &&
+                cos_sin->size(1) == 128, "fused_skinny: RoPE epilogue needs full 128-dim rotary");
+    TORCH_CHECK(k_cache->is_contiguous() && v_cache->is_contiguous() && k_cache->dim() == 4 &&
+                k_cache->size(1) == nkv && k_cache->size(3) == 128 && v_cache->sizes() == k_cache->sizes());
+    TORCH_CHECK(R == (nh + 2 * nkv) * 128);
+    pos = positions->data_ptr<int>();
+    cs = cos_sin->data_ptr<float>();
+    sl = slots->data_ptr<int>();
+    kc = k_cache->data_ptr();
+    vc = v_cache->data_ptr();
+    bsz = (int)k_cache->size(2);
+  }
+  check_rc(dgi_fused_skinny(x.data_ptr(), (int)x.stride(0), rp, ldr, rop, gp, (float)eps, w.data_ptr(), b,
+                            y.data_ptr(), (int)y.stride(0), (int)M, (int)N, (int)K, (int)pro, (int)epi, pos, cs,
+                            sl, kc, vc, (int)nh, (int)nkv, bsz, cur_stream()),
+           "fused_skinny");
 }
 
 void sample(at::Tensor out, const at::Tensor& logits, const c10::optional<at::Tensor>& temperature,
@@ -330,12 +419,15 @@ TORCH_LIBRARY(dgi, m) {
         "Tensor slot_mapping, Tensor(b!) k_cache, Tensor(c!) v_cache, int mode=0) -> ()");
   m.def("paged_decode(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor context_lens, Tensor(b!) part_o, Tensor(c!) part_lse, int nh, int nkv, int max_splits, "
-        "int part_size, float scale) -> ()");
+        "int part_size, float scale, Tensor(d!)? counters=None) -> ()");
   m.def("paged_prefill(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor cu_seqlens_q, Tensor context_lens, Tensor tiles, int nh, int nkv, float scale, "
         "Tensor? tree_mask, int tree_n) -> ()");
   m.def("silu_mul(Tensor(a!) out, Tensor gu) -> ()");
   m.def("skinny_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor? bias, int cfg=0) -> ()");
+  m.def("fused_skinny(Tensor(a!) y, Tensor x, Tensor? res, Tensor(b!)? res_out, Tensor? gamma, float eps, "
+        "Tensor w, Tensor? bias, int pro, int epi, Tensor? positions, Tensor? cos_sin, Tensor? slots, "
+        "Tensor(c!)? k_cache, Tensor(d!)? v_cache, int nh=0, int nkv=0) -> ()");
   m.def("sample(Tensor(a!) out, Tensor logits, Tensor? temperature, Tensor? seeds, int step, "
         "Tensor? thresh=None) -> ()");
   m.def("topkp_threshold(Tensor(a!) thresh, Tensor logits, Tensor temperature, Tensor top_k, "
@@ -357,6 +449,7 @@ TORCH_LIBRARY_IMPL(dgi, CUDA, m) {
   m.impl("paged_prefill", &paged_prefill);
   m.impl("silu_mul", &silu_mul);
   m.impl("skinny_gemm", &skinny_gemm);
+  m.impl("fused_skinny", &fused_skinny);
   m.impl("sample", &sample);
   m.impl("topk", &topk);
   m.impl("topkp_threshold", &topkp_threshold);

@@ -39,8 +39,8 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
     const uint16_t* __restrict__ q, int q_stride, const uint16_t* __restrict__ k_cache,
     const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ context_lens, uint16_t* __restrict__ out, int out_stride,
-    float* __restrict__ part_o, float* __restrict__ part_lse, int max_splits, int nh, int nkv,
-    int bs_log2, int part_size, float scale_log2) {
+    float* __restrict__ part_o, float* __restrict__ part_lse, int* __restrict__ counters, int max_splits, int nh,
+    int nkv, int bs_log2, int part_size, float scale_log2) {
   constexpr int KS = HD / 32;   // k-steps of the QK^T product
   constexpr int NC = HD / 16;   // 16-wide dim blocks of the PV product
   constexpr int VCH = HD / 8;   // 16-byte chunks per V row
@@ -51,10 +51,22 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
   const int h = blockIdx.y;
   const int b = blockIdx.z;
   const int ctx = context_lens[b];
-  const int start = split * part_size;
+  // part_size <= 0: device-side split plan from this sequence's own context —
+  // up to max_splits parts of at least -part_size tokens (32-token multiples),
+  // so a graph captured for the longest context does not leave short ones
+  // with idle workgroups or a needless reduce
+  int nsplit, part;
+  if (part_size > 0) {
+    part = part_size;
+    nsplit = (ctx + part - 1) / part;
+  } else {
+    nsplit = max(1, min(max_splits, (ctx + (-part_size) - 1) / (-part_size)));
+    part = (((ctx + nsplit - 1) / nsplit) + 31) & ~31;
+    nsplit = (ctx + part - 1) / part;
+  }
+  const int start = split * part;
   if (start >= ctx) return;
-  const int end = min(start + part_size, ctx);
-  const int nsplit = (ctx + part_size - 1) / part_size;
+  const int end = min(start + part, ctx);
   const int G = nh / nkv;
   const int bs = 1 << bs_log2;
 
@@ -224,6 +236,35 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
       if (d == 0) part_lse[pi] = M + log2f(L);
     }
   }
+  if (nsplit == 1 || counters == nullptr) return;
+  // ---- fused split reduce: the last of the nsplit workgroups of (b, kv-head)
+  // combines all partials (release: fence before the ticket; acquire: fence after)
+  __shared__ int s_last;
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) {
+    const int ticket = atomicAdd(&counters[b * nkv + h], 1);
+    s_last = ticket == nsplit - 1;
+    if (s_last) counters[b * nkv + h] = 0;  // ready for the next launch (stream-ordered)
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  for (int idx = tid; idx < G * HD; idx += 256) {
+    const int qq = idx / HD;
+    const int d = idx - qq * HD;
+    const int head = h * G + qq;
+    const size_t base = ((size_t)b * nh + head) * max_splits;
+    float M = -1e30f;
+    for (int sp = 0; sp < nsplit; ++sp) M = fmaxf(M, __builtin_nontemporal_load(part_lse + base + sp));
+    float W = 0.f, acc = 0.f;
+    for (int sp = 0; sp < nsplit; ++sp) {
+      const float wgt = exp2f(__builtin_nontemporal_load(part_lse + base + sp) - M);
+      W += wgt;
+      acc += wgt * __builtin_nontemporal_load(part_o + (base + sp) * HD + d);
+    }
+    out[(size_t)b * out_stride + head * HD + d] = f32_to_bf16(acc / W);
+  }
 }
 
 template <int HD>
@@ -234,7 +275,14 @@ __global__ __launch_bounds__(HD) void decode_reduce_kernel(
   const int b = blockIdx.x;
   const int head = blockIdx.y;
   const int ctx = context_lens[b];
-  const int nsplit = (ctx + part_size - 1) / part_size;
+  int nsplit;
+  if (part_size > 0) {
+    nsplit = (ctx + part_size - 1) / part_size;
+  } else {  // same device-side plan as the attention kernel
+    nsplit = max(1, min(max_splits, (ctx + (-part_size) - 1) / (-part_size)));
+    const int part = (((ctx + nsplit - 1) / nsplit) + 31) & ~31;
+    nsplit = (ctx + part - 1) / part;
+  }
   if (nsplit <= 1) return;
   const size_t base = ((size_t)b * nh + head) * max_splits;
   float M = -1e30f;
@@ -253,11 +301,13 @@ __global__ __launch_bounds__(HD) void decode_reduce_kernel(
 extern "C" int dgi_paged_decode(const void* q, int q_stride, const void* k_cache,
                                 const void* v_cache, const int* block_tables, int bt_stride,
                                 const int* context_lens, void* out, int out_stride, float* part_o,
-                                float* part_lse, int B, int nh, int nkv, int hd, int block_size,
+                                float* part_lse, int* counters, int B, int nh, int nkv, int hd, int block_size,
                                 int max_splits, int part_size, float scale, hipStream_t s) {
   if (B == 0) return 0;
   if (nh % nkv || nh / nkv > 16) return -2;
-  if (part_size % 128) return -3;
+  // fixed parts: multiples of 128 tokens; dynamic (part_size <= 0): minimum part a multiple of 32
+  if ((part_size > 0 && part_size % 128) || (part_size <= 0 && (part_size == 0 || (-part_size) % 32))) return -3;
+  if (max_splits <= 1) counters = nullptr;
   int bs_log2 = 0;
   while ((1 << bs_log2) < block_size) ++bs_log2;
   if ((1 << bs_log2) != block_size) return -4;
@@ -268,9 +318,9 @@ extern "C" int dgi_paged_decode(const void* q, int q_stride, const void* k_cache
     paged_decode_kernel<128><<<grid, 256, lds, s>>>(
         (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,
         block_tables, bt_stride, context_lens, (uint16_t*)out, out_stride, part_o, part_lse,
-        max_splits, nh, nkv, bs_log2, part_size, scale_log2);
+        counters, max_splits, nh, nkv, bs_log2, part_size, scale_log2);
     DGI_CHECK_LAUNCH();
-    if (max_splits > 1) {
+    if (max_splits > 1 && counters == nullptr) {
       decode_reduce_kernel<128><<<dim3(B, nh), 128, 0, s>>>(part_o, part_lse, context_lens,
                                                             (uint16_t*)out, out_stride, max_splits,
                                                             nh, part_size);
@@ -281,9 +331,9 @@ extern "C" int dgi_paged_decode(const void* q, int q_stride, const void* k_cache
     paged_decode_kernel<64><<<grid, 256, lds, s>>>(
         (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,
         block_tables, bt_stride, context_lens, (uint16_t*)out, out_stride, part_o, part_lse,
-        max_splits, nh, nkv, bs_log2, part_size, scale_log2);
+        counters, max_splits, nh, nkv, bs_log2, part_size, scale_log2);
     DGI_CHECK_LAUNCH();
-    if (max_splits > 1) {
+    if (max_splits > 1 && counters == nullptr) {
       decode_reduce_kernel<64><<<dim3(B, nh), 64, 0, s>>>(part_o, part_lse, context_lens,
                                                           (uint16_t*)out, out_stride, max_splits,
                                                           nh, part_size);

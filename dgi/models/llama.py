@@ -67,6 +67,7 @@ class LlamaModel:
         # EAGLE-3 feature taps: global layer ids whose output residual stream is kept
         self.capture_layers: tuple = ()
         self.captured: dict = {}
+        self.force_fused = False
         # tensor parallelism: in-place sum of partial outputs across the TP group
         # after the row-parallel O and down projections (dgi.parallel.tensor)
         self.reduce = None
@@ -203,12 +204,13 @@ class LlamaModel:
         return n
 
     # ------------------------------------------------------------------ forward
-    def attention(self, li: int, qkv: torch.Tensor, meta: AttnMeta) -> torch.Tensor:
+    def attention(self, li: int, qkv: torch.Tensor, meta: AttnMeta, rope: bool = True) -> torch.Tensor:
         c = self.cfg
         kc = self.kv_cache[li, 0]
         vc = self.kv_cache[li, 1]
-        ops.rope_cache(qkv, meta.positions, self.cos_sin, c.num_heads, c.num_kv_heads, c.head_dim,
-                       meta.slot_mapping, kc, vc, self.rope_mode)
+        if rope:       # else the qkv GEMM epilogue already rotated q/k and wrote the cache
+            ops.rope_cache(qkv, meta.positions, self.cos_sin, c.num_heads, c.num_kv_heads, c.head_dim,
+                           meta.slot_mapping, kc, vc, self.rope_mode)
         T = qkv.shape[0]
         out = torch.empty(T, c.q_size, device=qkv.device, dtype=qkv.dtype)
         nd = meta.num_decode
@@ -235,10 +237,59 @@ class LlamaModel:
         buf[T:Mp].zero_()       # pad rows: zeros in, ignored out
         return Mp
 
+    def _fused_decode(self, h: torch.Tensor, meta: AttnMeta) -> bool:
+        if meta.num_prefill_tokens != 0 or not ops.fused_decode_ok(h.shape[0], self.cfg.hidden_size):
+            return False
+        # force_fused: run the fused composition through the reference ops on CPU (tests)
+        return (h.is_cuda and h.dtype == torch.bfloat16) or self.force_fused
+
+    def _forward_layers_fused(self, h: torch.Tensor, meta: AttnMeta, residual: Optional[torch.Tensor]):
+        """Pure-decode layers with M <= 16 rows: 5 kernels per layer instead of 9.
+
+        qkv: RMSNorm (+ residual add) prologue and RoPE + paged-KV epilogue fused
+        into the weight-streaming GEMM; gate_up: RMSNorm prologue + SwiGLU
+        epilogue (ops.fused_skinny, dgi/csrc/fused_decode.hip).  The residual
+        stream ping-pongs between fresh buffers (the prologue reads the old one
+        while workgroup 0 writes the new)."""
+        c = self.cfg
+        eps = c.rms_eps
+        T = h.shape[0]
+        rope_epi = self.rope_mode == 0 and c.head_dim == 128 and self.cos_sin.shape[1] == 128
+        for i, L in enumerate(self.layers):
+            kc, vc = self.kv_cache[i, 0], self.kv_cache[i, 1]
+            qkv = torch.empty(T, L.qkv.shape[0], dtype=h.dtype, device=h.device)
+            if residual is None:
+                pro, res_out, new_res = 1, None, h
+            else:
+                res_out = torch.empty_like(h)
+                pro, new_res = 2, res_out
+            ops.fused_skinny(qkv, h, residual, res_out, L.in_norm, eps, L.qkv, L.qkv_bias, pro,
+                             2 if rope_epi else 0, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc,
+                             c.num_heads, c.num_kv_heads)
+            residual = new_res
+            attn = self.attention(i, qkv, meta, rope=not rope_epi)
+            h = ops.linear(attn, L.o)
+            if self.reduce is not None:
+                self.reduce(h)
+            act = torch.empty(T, L.gate_up.shape[0] // 2, dtype=h.dtype, device=h.device)
+            res_out = torch.empty_like(h)
+            ops.fused_skinny(act, h, residual, res_out, L.post_norm, eps, L.gate_up, None, 2, 1)
+            residual = res_out
+            h = ops.linear(act, L.down)
+            if self.reduce is not None:
+                self.reduce(h)
+            if self.capture_layers and (self.layer_start + i) in self.capture_layers:
+                self.captured[self.layer_start + i] = h + residual
+            if self.layer_hook is not None:
+                self.layer_hook(self.layer_start + i)
+        return h, residual
+
     def forward_layers(self, h: torch.Tensor, meta: AttnMeta, residual: Optional[torch.Tensor] = None):
         c = self.cfg
         eps = c.rms_eps
         T = h.shape[0]
+        if self.layers and self._fused_decode(h, meta):
+            return self._forward_layers_fused(h, meta, residual)
         Mp = self._mlp_rows(T, h) if self.layers else T
         for i, L in enumerate(self.layers):
             if residual is None:

@@ -236,25 +236,33 @@ def paged_decode(q, k_cache, v_cache, block_tables, context_lens, nh, nkv, scale
                  max_splits: int = 1, part_size: int = 1 << 30, out=None, workspace=None) -> torch.Tensor:
     """Single-token attention for each row of ``q`` over its paged context.
 
-    ``max_splits``/``part_size`` must cover the longest context in the batch
-    (``decode_split_plan``); with ``max_splits > 1`` a workspace
-    ``(part_o[B*nh*splits*hd], part_lse[B*nh*splits])`` fp32 is required.
+    ``part_size > 0``: fixed parts; ``max_splits``/``part_size`` must cover the
+    longest context (``decode_split_plan``).  ``part_size <= 0``: device-side
+    plan per sequence — up to ``max_splits`` parts of at least ``-part_size``
+    tokens (what captured graphs use).  With ``max_splits > 1`` a workspace
+    ``(part_o[B*nh*splits*hd], part_lse[B*nh*splits][, counters[B*nkv] int32 zeros])``
+    is used; with counters the last workgroup of each (sequence, kv-head)
+    combines the splits (no reduce kernel).
     """
     if _native(q):
         hd = k_cache.shape[-1]
         B = q.shape[0]
         if out is None:
             out = torch.empty(B, nh * hd, dtype=q.dtype, device=q.device)
+        cnt = None
         if max_splits > 1:
             if workspace is None:
                 workspace = (torch.empty(B * nh * max_splits * hd, dtype=torch.float32, device=q.device),
-                             torch.empty(B * nh * max_splits, dtype=torch.float32, device=q.device))
-            po, pl = workspace
+                             torch.empty(B * nh * max_splits, dtype=torch.float32, device=q.device),
+                             torch.zeros(B * nkv, dtype=torch.int32, device=q.device))
+            po, pl = workspace[0], workspace[1]
+            cnt = workspace[2] if len(workspace) > 2 else None
         else:
             po = pl = torch.empty(0, dtype=torch.float32, device=q.device)
-            part_size = max(128, ((part_size if part_size < (1 << 30) else 1 << 20) + 127) // 128 * 128)
+            if part_size > 0:
+                part_size = max(128, ((part_size if part_size < (1 << 30) else 1 << 20) + 127) // 128 * 128)
         _call("paged_decode", out, q, k_cache, v_cache, block_tables, context_lens, po, pl,
-                                   nh, nkv, max_splits, part_size, scale)
+              nh, nkv, max_splits, part_size, scale, cnt)
         return out
     r = paged_decode_ref(q, k_cache, v_cache, block_tables, context_lens, nh, nkv, scale)
     if out is not None:
@@ -373,6 +381,54 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         out.copy_(r)
         return out
     return r
+
+
+# Fused decode GEMM (fused_decode.hip): RMSNorm prologue + SwiGLU / RoPE+KV epilogue.
+# Used for the qkv and gate_up projections of pure-decode steps with M <= 16 rows
+# where the weight-streaming kernel is the GEMM of choice (K <= 4096, like
+# _use_skinny).  DGI_FUSED_DECODE=0 disables, =force ignores the K limit.
+FUSED_DECODE = os.environ.get("DGI_FUSED_DECODE", "1")
+
+
+def fused_decode_ok(M: int, K: int) -> bool:
+    if FUSED_DECODE == "0" or not 0 < M <= 16 or K % 1024:
+        return False
+    return FUSED_DECODE == "force" or (K <= 4096 and M <= SKINNY_MAX_M)
+
+
+def fused_skinny_ref(y, x, res, res_out, gamma, eps, w, bias, pro, epi, positions=None, cos_sin=None,
+                     slots=None, k_cache=None, v_cache=None, nh=0, nkv=0):
+    """Unfused composition of the same ops (CPU reference / test oracle)."""
+    if pro == 2:
+        s_ = (x.float() + res.float()).to(x.dtype)
+        res_out.copy_(s_)
+        xin = s_
+    else:
+        xin = x
+    xn = rmsnorm_ref(xin, gamma, eps) if pro else xin
+    out = torch.nn.functional.linear(xn.float(), w.float(), None if bias is None else bias.float()).to(x.dtype)
+    if epi == 1:
+        out = silu_mul_ref(out)
+    elif epi == 2:
+        rope_cache_ref(out, positions[: out.shape[0]], cos_sin, nh, nkv, 128, slots[: out.shape[0]], k_cache,
+                       v_cache, 0)
+    y.copy_(out)
+    return y
+
+
+def fused_skinny(y, x, res, res_out, gamma, eps, w, bias, pro: int, epi: int, positions=None, cos_sin=None,
+                 slots=None, k_cache=None, v_cache=None, nh: int = 0, nkv: int = 0):
+    """y = epi(rmsnorm_pro(x [+ res]) @ w.T + bias); pro 2 also writes res_out = x + res.
+
+    epi 0 stores [M, N]; epi 1 is SwiGLU over w = [gate; up] (y is [M, I]);
+    epi 2 applies NeoX RoPE to the q/k heads of a fused qkv output and writes k/v
+    into the paged cache at ``slots`` (head_dim 128, full rotary)."""
+    if _native(x):
+        _call("fused_skinny", y, x, res, res_out, gamma, eps, w, bias, pro, epi, positions, cos_sin, slots,
+              k_cache, v_cache, nh, nkv)
+        return y
+    return fused_skinny_ref(y, x, res, res_out, gamma, eps, w, bias, pro, epi, positions, cos_sin, slots,
+                            k_cache, v_cache, nh, nkv)
 
 
 def silu_mul_ref(gu: torch.Tensor) -> torch.Tensor:

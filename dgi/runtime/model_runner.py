@@ -12,6 +12,7 @@
 from __future__ import annotations
 
 import dataclasses
+import os
 from typing import Optional
 
 import numpy as np
@@ -67,8 +68,11 @@ class ModelRunner:
         maxb = max(max_num_seqs, max(graph_buckets) if graph_buckets else 1)
         self.dec_ws = None
         if self.is_cuda:
+            # partial O / log-sum-exp per split + one ticket counter per (sequence, kv-head)
+            # for the in-kernel split reduce (the counters return to 0 after every launch)
             self.dec_ws = (torch.empty(maxb * nh * self.ws_splits * hd, dtype=torch.float32, device=self.device),
-                           torch.empty(maxb * nh * self.ws_splits, dtype=torch.float32, device=self.device))
+                           torch.empty(maxb * nh * self.ws_splits, dtype=torch.float32, device=self.device),
+                           torch.zeros(maxb * model.cfg.num_kv_heads, dtype=torch.int32, device=self.device))
         self.graphs = None
         if use_graphs and self.is_cuda and model.has_head:
             self.graphs = GraphRunner(self, [b for b in graph_buckets if b <= max_num_seqs])
@@ -237,11 +241,25 @@ class GraphRunner:
         self.features = None
         self.feats_out: dict = {}
 
+    def split_plan(self, b: int) -> tuple:
+        """(max_splits, part_size) captured for bucket ``b``.  Dynamic (the
+        default): the kernel splits each sequence's own context into up to
+        ~4 workgroups per CU worth of parts of >= 64 tokens, so one graph serves
+        every context length without idle splits; DGI_DECODE_DYNAMIC=0 keeps the
+        fixed max_model_len / part_size plan."""
+        r = self.r
+        if os.environ.get("DGI_DECODE_DYNAMIC", "1") == "0":
+            return r.graph_splits, r.graph_part
+        nkv = r.model.cfg.num_kv_heads
+        want = max(1, -(-4 * r.num_cus // max(1, b * nkv)))
+        return min(r.ws_splits, want), -64
+
     def _meta(self, b):
         r = self.r
+        splits, part = self.split_plan(b)
         return AttnMeta(positions=self.pos[:b], slot_mapping=self.slots[:b], num_decode=b,
                         dec_block_tables=self.bt[:b], dec_context_lens=self.ctx[:b],
-                        dec_max_splits=r.graph_splits, dec_part_size=r.graph_part, dec_workspace=r.dec_ws,
+                        dec_max_splits=splits, dec_part_size=part, dec_workspace=r.dec_ws,
                         num_prefill_tokens=0, logits_indices=None)
 
     def _body(self, b):

@@ -526,6 +526,7 @@ class SpecEngine(LLMEngine):
         self._backoff = 1                        # probe interval multiplier
         self._probed = False                     # the current speculation period is a re-probe
         self._captured = False      # this step captured a hipGraph (its time is not a cost sample)
+        self.force_plain = False    # measurement aid: plain decode steps only (feature tap still on)
 
     def _bucket(self, R: int) -> int:
         return next((b for b in VERIFY_BUCKETS if b >= R), VERIFY_BUCKETS[-1])
@@ -684,7 +685,8 @@ class SpecEngine(LLMEngine):
         t0 = time.perf_counter()
         self.model.kv_cache = self.pool.kv
         outs: list[StepOutput] = []
-        spec_reqs = [r for r in self.scheduler.running if self._eligible(r)] if self.spec_on else []
+        spec_reqs = [r for r in self.scheduler.running if self._eligible(r)] \
+            if self.spec_on and not self.force_plain else []
         for r in spec_reqs:
             r.busy = True            # keep them out of the normal batch
         try:

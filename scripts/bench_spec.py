@@ -119,6 +119,13 @@ def main():
                               "speedup": round(ts_base / ts_spec, 3), "mean_accepted": round(sa["mean_accepted"], 3),
                               "token_agreement": round(sum(int(x == y) for o, q in zip(sout, sref)
                                                            for x, y in zip(o, q)) / max(1, toks), 4)}
+        # the feature-tapped plain path alone (what auto-off falls back to)
+        spec.force_plain = True
+        _, t_tap = timed_generate(spec, prompts, sp)
+        spec.force_plain = False
+        row["tapped_plain"] = {"tok_s": round(toks / t_tap, 1), "vs_plain": round(t_base / t_tap, 3)}
+        _, t_base2 = timed_generate(base, prompts, sp)
+        row["plain_rerun_tok_s"] = round(toks / t_base2, 1)
         # acceptance-controlled runs: the first tree chain is replaced by the known greedy
         # continuation, each token kept with probability p (ceiling / sensitivity of the machinery)
         for p in a.oracle_accept:

@@ -108,6 +108,19 @@ def test_paged_decode(nh, nkv, hd, ctx_lens):
     # fixed part 128 with many splits (graph style: empty splits exit)
     out3 = ops.paged_decode(qkv, kc, vc, bt, ctx, nh, nkv, scale, (max(ctx_lens) + 127) // 128 + 3, 128)
     torch.testing.assert_close(out3.float(), ref.float(), atol=2e-2, rtol=2e-2)
+    # separate reduce kernel (no ticket counters in the workspace)
+    ws2 = (torch.empty(B * nh * splits * hd, device=DEV), torch.empty(B * nh * splits, device=DEV))
+    out4 = ops.paged_decode(qkv, kc, vc, bt, ctx, nh, nkv, scale, splits, part, workspace=ws2)
+    torch.testing.assert_close(out4.float(), ref.float(), atol=2e-2, rtol=2e-2)
+    # device-side dynamic plan (graphs): up to S parts of >= 64 tokens, in-kernel reduce;
+    # the ticket counters must be back to zero after every launch
+    for S in (1, 3, 16, 64):
+        ws = (torch.empty(B * nh * S * hd, device=DEV), torch.empty(B * nh * S, device=DEV),
+              torch.zeros(B * nkv, dtype=torch.int32, device=DEV))
+        for _ in range(2):
+            out5 = ops.paged_decode(qkv, kc, vc, bt, ctx, nh, nkv, scale, S, -64, workspace=ws)
+            torch.testing.assert_close(out5.float(), ref.float(), atol=2e-2, rtol=2e-2)
+        assert int(ws[2].abs().sum()) == 0
 
 
 @pytest.mark.parametrize("nh,nkv", [(32, 8), (64, 8), (8, 1), (28, 4)])
@@ -396,3 +409,79 @@ def test_graph_decode_with_top_k_one_matches_greedy():
                                                                   top_p=1.0, ignore_eos=True))]
     assert sum(a == b for a, b in zip(greedy, topk1)) >= 3, (greedy, topk1)
     assert e.runner.graphs is not None and e.runner.graphs.captured
+
+
+@pytest.mark.parametrize("pro,epi", [(0, 0), (1, 0), (2, 0), (2, 1), (1, 2), (2, 2)])
+@pytest.mark.parametrize("M", [1, 5, 16])
+def test_fused_skinny_matches_reference(pro, epi, M):
+    """Fused decode GEMM (RMSNorm prologue, SwiGLU / RoPE+KV epilogue) vs the
+    unfused reference ops in fp32 on the same bf16 inputs."""
+    torch.manual_seed(M * 10 + pro * 3 + epi)
+    K = 4096
+    nh, nkv, bs, nb = 32, 8, 16, 64
+    if epi == 2:
+        R = (nh + 2 * nkv) * 128
+    elif epi == 1:
+        R = 2 * 1024
+    else:
+        R = 2048
+    x = (torch.randn(M, K, device=DEV) * 0.5).bfloat16()
+    res = (torch.randn(M, K, device=DEV)).bfloat16() if pro == 2 else None
+    gamma = (1 + 0.1 * torch.randn(K, device=DEV)).bfloat16() if pro else None
+    w = (torch.randn(R, K, device=DEV) * 0.02).bfloat16()
+    bias = (torch.randn(R, device=DEV) * 0.1).bfloat16() if epi != 1 else None
+    N = R // 2 if epi == 1 else R
+    pos = torch.randint(0, 1000, (M,), device=DEV, dtype=torch.int32)
+    inv = 1.0 / (10000 ** (torch.arange(0, 64, device=DEV).float() / 64))
+    ang = torch.arange(2048, device=DEV).float()[:, None] * inv[None]
+    cos_sin = torch.cat([ang.cos(), ang.sin()], dim=1).contiguous()
+    slots = torch.randperm(nb * bs, device=DEV)[:M].int()
+    if M > 2:
+        slots[1] = -1                      # padding row: no cache write
+    kc = torch.zeros(nb, nkv, bs, 128, device=DEV, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    kc_r, vc_r = kc.clone(), vc.clone()
+    y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    y_r = torch.empty_like(y)
+    ro = torch.empty_like(x) if pro == 2 else None
+    ro_r = torch.empty_like(x) if pro == 2 else None
+    ops.fused_skinny(y, x, res, ro, gamma, 1e-5, w, bias, pro, epi, pos, cos_sin, slots, kc, vc, nh, nkv)
+    ops.fused_skinny_ref(y_r, x, res, ro_r, gamma, 1e-5, w, bias, pro, epi, pos, cos_sin, slots, kc_r, vc_r,
+                         nh, nkv)
+    torch.cuda.synchronize()
+    if pro == 2:
+        assert torch.equal(ro, ro_r)
+    scale = float(y_r.float().abs().max()) + 1e-3
+    assert float((y.float() - y_r.float()).abs().max()) <= 0.02 * scale, float((y.float() - y_r.float()).abs().max())
+    if epi == 2:
+        for a_, b_ in ((kc, kc_r), (vc, vc_r)):
+            s2 = float(b_.float().abs().max()) + 1e-3
+            assert float((a_.float() - b_.float()).abs().max()) <= 0.02 * s2
+        if M > 2:
+            assert int((kc.view(-1, 128).abs().sum(1) > 0).sum()) == (M - 1) * nkv
+
+
+def test_fused_decode_model_matches_unfused():
+    """Engine decode with the fused layer path vs the unfused kernels (same GPU weights)."""
+    from dgi.engine import EngineConfig, LLMEngine
+    from dgi.models.config import get_config
+    from dgi.models.llama import LlamaModel
+    from dgi.sched.request import SamplingParams
+    mc = get_config("llama-tiny-hd128")
+    src = LlamaModel(mc, "cpu", seed=4)
+    prompts = [[1] + list(range(3, 3 + n)) for n in (5, 40, 130, 7)]
+    sp = SamplingParams(max_tokens=16, temperature=0.0, ignore_eos=True)
+    outs = []
+    old = ops.FUSED_DECODE
+    try:
+        for mode in ("0", "1"):
+            ops.FUSED_DECODE = mode
+            gm = LlamaModel(mc, "cuda", init="empty").copy_from(src)
+            e = LLMEngine(EngineConfig(model="llama-tiny-hd128", device="cuda", num_blocks=256, max_num_seqs=8,
+                                       max_model_len=512, max_num_batched_tokens=256, use_graphs=True),
+                          model_cfg=mc, model=gm)
+            outs.append([r.output for r in e.generate(prompts, sp)])
+    finally:
+        ops.FUSED_DECODE = old
+    agree = sum(a == b for a, b in zip(*outs))
+    assert agree >= 3, outs                # bf16 norm summation order may flip a near-tie

@@ -162,3 +162,44 @@ def test_debug_modes_are_opt_in(monkeypatch):
     debug.enable_serialized()
     import os
     assert os.environ["DGI_DEBUG_SYNC"] == "1" and os.environ["AMD_SERIALIZE_KERNEL"] == "3"
+
+
+def test_fused_decode_layers_match_unfused_on_cpu():
+    """The fused decode layer wiring (norm prologue, ping-pong residual, RoPE/KV and
+    SwiGLU epilogues) computes exactly the unfused layer on the reference ops."""
+    from dgi.engine import EngineConfig, LLMEngine
+    from dgi.models.config import get_config
+    from dgi.models.llama import LlamaModel
+    from dgi.sched.request import SamplingParams
+    for name in ("llama-tiny-hd128", "qwen-tiny", "glm-tiny"):
+        mc = get_config(name)
+        outs, logits = [], []
+        for fused in (False, True):
+            m = LlamaModel(mc, "cpu", torch.float32, seed=11)
+            m.force_fused = fused
+            calls = []
+            real_fused = m._forward_layers_fused
+
+            def count(*a, real_fused=real_fused, calls=calls):
+                calls.append(1)
+                return real_fused(*a)
+            m._forward_layers_fused = count
+            e = LLMEngine(EngineConfig(model=name, device="cpu", dtype=torch.float32, num_blocks=64, max_num_seqs=4,
+                                       max_model_len=256, max_num_batched_tokens=64, use_graphs=False,
+                                       enable_prefix_caching=False), model_cfg=mc, model=m)
+            got = []
+            orig = m.compute_logits
+
+            def spy(h, r, idx, orig=orig, got=got):
+                o = orig(h, r, idx)
+                got.append(o.detach().clone())
+                return o
+            m.compute_logits = spy
+            reqs = e.generate([[1, 5, 9, 300, 17], [1, 2, 3]], SamplingParams(max_tokens=6, temperature=0.0,
+                                                                              ignore_eos=True))
+            outs.append([r.output for r in reqs])
+            logits.append(got)
+            assert (len(calls) >= 5) == fused, (name, fused, len(calls))
+        assert outs[0] == outs[1], name
+        for a, b in zip(*logits):
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
