@@ -31,7 +31,7 @@ int dgi_skinny_gemm(const void* x, int ldx, const void* w, const void* bias, voi
 int dgi_fused_skinny(const void* x, int ldx, const void* res, int ldr, void* res_out, const void* gamma,
                      float eps, const void* w, const void* bias, void* y, int ldy, int M, int N, int K, int pro,
                      int epi, const int* positions, const float* cos_sin, const int* slots, void* k_cache,
-                     void* v_cache, int nh, int nkv, int block_size, hipStream_t s);
+                     void* v_cache, int nh, int nkv, int block_size, int cfg, hipStream_t s);
 int dgi_sample(const void* logits, int is_bf16, int B, int V, int stride, const float* temperature,
                const long long* seeds, long long step, const float* thresh, long long* out, hipStream_t s);
 int dgi_topkp_threshold(const void* logits, int is_bf16, int B, int V, int stride, const float* temperature,
@@ -212,7 +212,7 @@ void fused_skinny(at::Tensor y, const at::Tensor& x, const c10::optional<at::Ten
                   const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t pro, int64_t epi,
                   const c10::optional<at::Tensor>& positions, const c10::optional<at::Tensor>& cos_sin,
                   const c10::optional<at::Tensor>& slots, const c10::optional<at::Tensor>& k_cache,
-                  const c10::optional<at::Tensor>& v_cache, int64_t nh, int64_t nkv) {
+                  const c10::optional<at::Tensor>& v_cache, int64_t nh, int64_t nkv, int64_t cfg) {
   check_bf16(y, "y"); check_bf16(x, "x"); check_bf16(w, "w");
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "fused_skinny: 2-D operands");
   TORCH_CHECK(x.stride(1) == 1 && y.stride(1) == 1 && w.is_contiguous() && x.stride(0) % 8 == 0);
@@ -279,7 +279,7 @@ void fused_skinny(at::Tensor y, const at::Tensor& x, const c10::optional<at::Ten
   }
   check_rc(dgi_fused_skinny(x.data_ptr(), (int)x.stride(0), rp, ldr, rop, gp, (float)eps, w.data_ptr(), b,
                             y.data_ptr(), (int)y.stride(0), (int)M, (int)N, (int)K, (int)pro, (int)epi, pos, cs,
-                            sl, kc, vc, (int)nh, (int)nkv, bsz, cur_stream()),
+                            sl, kc, vc, (int)nh, (int)nkv, bsz, (int)cfg, cur_stream()),
            "fused_skinny");
 }
 
@@ -427,7 +427,7 @@ TORCH_LIBRARY(dgi, m) {
   m.def("skinny_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor? bias, int cfg=0) -> ()");
   m.def("fused_skinny(Tensor(a!) y, Tensor x, Tensor? res, Tensor(b!)? res_out, Tensor? gamma, float eps, "
         "Tensor w, Tensor? bias, int pro, int epi, Tensor? positions, Tensor? cos_sin, Tensor? slots, "
-        "Tensor(c!)? k_cache, Tensor(d!)? v_cache, int nh=0, int nkv=0) -> ()");
+        "Tensor(c!)? k_cache, Tensor(d!)? v_cache, int nh=0, int nkv=0, int cfg=0) -> ()");
   m.def("sample(Tensor(a!) out, Tensor logits, Tensor? temperature, Tensor? seeds, int step, "
         "Tensor? thresh=None) -> ()");
   m.def("topkp_threshold(Tensor(a!) thresh, Tensor logits, Tensor temperature, Tensor top_k, "

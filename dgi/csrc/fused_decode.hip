@@ -12,9 +12,10 @@
 //  prologue PRO (the GEMM input is the normalised residual stream):
 //    1: x = rmsnorm(h) * gamma                   (first layer: residual = h)
 //    2: x = rmsnorm(h + res) * gamma, res_out = bf16(h + res)   (fused add)
-//    Every workgroup reduces the M <= 16 row norms itself (8 KB per row from
-//    L2, overlapped with its first weight loads) and normalises its own X
-//    fragments in registers, so no normalised copy of X ever goes to memory.
+//    Every workgroup stages the M <= 16 normalised rows in LDS itself (8-16 KB
+//    per row from L2, overlapped with its first weight loads) and feeds the
+//    MFMA A fragments from there, so no normalised copy of X goes to HBM and
+//    the norm costs M*K work per workgroup, not 16 MFMA rows per lane.
 //    Workgroup 0 writes res_out; res_out must not alias h or res (the other
 //    workgroups are still reading them).
 //  epilogue EPI on the pair:
@@ -34,6 +35,8 @@
 using namespace dgi;
 
 namespace {
+
+constexpr size_t kMaxStagedBytes = 136 * 1024;
 
 struct FusedArgs {
   const uint16_t* x;  // h [M, ldx]
@@ -58,33 +61,16 @@ struct FusedArgs {
   int nh, nkv, bs_log2;
 };
 
-template <int U, int PRO>
+template <int U>
 struct Frag {
   u32x4 w[U][2][2];
-  u32x4 x[U][2];
-  u32x4 r[U][PRO == 2 ? 2 : 1];
-  u32x4 gm[U][PRO ? 2 : 1];
 };
-
-template <int PRO>
-__device__ __forceinline__ u32x4 normalise(u32x4 x, u32x4 r, u32x4 gm, float inv) {
-  float v[8], g[8], o[8];
-  unpack8(x, v);
-  if (PRO == 2) {
-    float rr[8];
-    unpack8(r, rr);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] += rr[j];
-    unpack8(pack8(v), v);  // the residual stream is bf16
-  }
-  unpack8(gm, g);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = v[j] * inv * g[j];
-  return pack8(o);
-}
 
 template <int NW, int U, int PRO, int EPI>
 __global__ __launch_bounds__(NW * 64) void fused_skinny_kernel(FusedArgs a) {
+  // normalised X rows live in LDS for the whole kernel: [M][K + 8] bf16 (16-byte
+  // row pad keeps the 16-row fragment reads off one bank)
+  extern __shared__ __attribute__((aligned(16))) uint16_t xs[];
   __shared__ f32x4 red[NW][2][64];
   __shared__ float s_part[NW][16];
   __shared__ float s_inv[16];
@@ -94,6 +80,8 @@ __global__ __launch_bounds__(NW * 64) void fused_skinny_kernel(FusedArgs a) {
   const int r = lane & 15;
   const int g = lane >> 4;
   const int K = a.K;
+  const int M = a.M;
+  const int ldx = K + 8;
   const int bid = blockIdx.x;
   const int c0 = (bid / a.tpg) * a.gstride + (bid % a.tpg) * 16;
   const int c1 = c0 + a.pair_off;
@@ -101,12 +89,9 @@ __global__ __launch_bounds__(NW * 64) void fused_skinny_kernel(FusedArgs a) {
   const size_t lane_k = (size_t)g * 16 + (size_t)w * 64;
   const uint16_t* w0 = a.w + (size_t)(c0 + r) * K + lane_k;
   const uint16_t* w1 = a.w + (size_t)(c1 + r) * K + lane_k;
-  const bool xval = r < a.M;
-  const uint16_t* xrow = a.x + (size_t)(xval ? r : 0) * a.ldx + lane_k;
-  const uint16_t* rrow = PRO == 2 ? a.res + (size_t)(xval ? r : 0) * a.ldr + lane_k : nullptr;
-  const uint16_t* grow = PRO ? a.gamma + lane_k : nullptr;
+  const bool xval = r < M;
 
-  auto load = [&](Frag<U, PRO>& f, int grp) {
+  auto load = [&](Frag<U>& f, int grp) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const size_t off = ((size_t)grp * NW * U + (size_t)u * NW) * 64;
@@ -116,73 +101,75 @@ __global__ __launch_bounds__(NW * 64) void fused_skinny_kernel(FusedArgs a) {
       f.w[u][0][1] = __builtin_nontemporal_load(p0 + 1);
       f.w[u][1][0] = __builtin_nontemporal_load(p1);
       f.w[u][1][1] = __builtin_nontemporal_load(p1 + 1);
-      if (xval) {
-        const u32x4* px = reinterpret_cast<const u32x4*>(xrow + off);
-        f.x[u][0] = px[0];
-        f.x[u][1] = px[1];
-        if (PRO == 2) {
-          const u32x4* pr = reinterpret_cast<const u32x4*>(rrow + off);
-          f.r[u][0] = pr[0];
-          f.r[u][1] = pr[1];
-        }
-      } else {
-        f.x[u][0] = f.x[u][1] = u32x4{0u, 0u, 0u, 0u};
-        if (PRO == 2) f.r[u][0] = f.r[u][1] = u32x4{0u, 0u, 0u, 0u};
-      }
-      if (PRO) {
-        const u32x4* pg = reinterpret_cast<const u32x4*>(grow + off);
-        f.gm[u][0] = pg[0];
-        f.gm[u][1] = pg[1];
-      }
     }
   };
 
-  Frag<U, PRO> cur, nxt;
-  load(cur, 0);  // first weight group in flight during the norm reduction
+  Frag<U> cur, nxt;
+  load(cur, 0);  // first weight group in flight while X is staged
 
-  float inv = 0.f;
-  if (PRO) {
-    // ---- row norms: M rows x K, 8 elements per thread-chunk
-    const int nchunk = K >> 3;
-    for (int m = 0; m < a.M; ++m) {
-      float ss = 0.f;
-      for (int c = tid; c < nchunk; c += NW * 64) {
-        float v[8];
-        unpack8(reinterpret_cast<const u32x4*>(a.x + (size_t)m * a.ldx)[c], v);
-        if (PRO == 2) {
-          float rr[8];
-          unpack8(reinterpret_cast<const u32x4*>(a.res + (size_t)m * a.ldr)[c], rr);
+  // ---- stage X (residual add, norm) into LDS once per workgroup: only the
+  // M useful rows, spread over all threads (not 16 MFMA rows per lane)
+  const int nchunk = K >> 3;
+  for (int m = 0; m < M; ++m) {
+    float ss = 0.f;
+    for (int c = tid; c < nchunk; c += NW * 64) {
+      u32x4 p = reinterpret_cast<const u32x4*>(a.x + (size_t)m * a.ldx)[c];
+      if (PRO == 2) {
+        float v[8], rr[8];
+        unpack8(p, v);
+        unpack8(reinterpret_cast<const u32x4*>(a.res + (size_t)m * a.ldr)[c], rr);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] += rr[j];
-          const u32x4 p = pack8(v);
-          if (bid == 0) reinterpret_cast<u32x4*>(a.res_out + (size_t)m * a.ldr)[c] = p;
-          unpack8(p, v);
-        }
+        for (int j = 0; j < 8; ++j) v[j] += rr[j];
+        p = pack8(v);  // the residual stream is bf16
+        if (bid == 0) reinterpret_cast<u32x4*>(a.res_out + (size_t)m * a.ldr)[c] = p;
+      }
+      if (PRO) {
+        float v[8];
+        unpack8(p, v);
 #pragma unroll
         for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
       }
+      *reinterpret_cast<u32x4*>(xs + m * ldx + c * 8) = p;
+    }
+    if (PRO) {
       ss = wave_sum(ss);
       if (lane == 0) s_part[w][m] = ss;
     }
+  }
+  if (PRO) {
     __syncthreads();
-    if (tid < a.M) {
+    if (tid < M) {
       float t = 0.f;
 #pragma unroll
       for (int j = 0; j < NW; ++j) t += s_part[j][tid];
       s_inv[tid] = rsqrtf(t / (float)K + a.eps);
     }
     __syncthreads();
-    inv = xval ? s_inv[r] : 0.f;
+    // each thread rescales the chunks it staged itself (same (m, c) mapping)
+    for (int m = 0; m < M; ++m) {
+      const float inv = s_inv[m];
+      for (int c = tid; c < nchunk; c += NW * 64) {
+        float v[8], gm[8], o[8];
+        unpack8(*reinterpret_cast<const u32x4*>(xs + m * ldx + c * 8), v);
+        unpack8(reinterpret_cast<const u32x4*>(a.gamma)[c], gm);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = v[j] * inv * gm[j];
+        *reinterpret_cast<u32x4*>(xs + m * ldx + c * 8) = pack8(o);
+      }
+    }
   }
+  __syncthreads();
 
+  const uint16_t* xl = xs + (xval ? r : 0) * ldx + lane_k;
   f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-  auto compute = [&](const Frag<U, PRO>& f) {
+  auto compute = [&](const Frag<U>& f, int grp) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      u32x4 xa = f.x[u][0], xb = f.x[u][1];
-      if (PRO) {
-        xa = normalise<PRO>(xa, f.r[u][0], f.gm[u][0], inv);
-        xb = normalise<PRO>(xb, f.r[u][PRO == 2 ? 1 : 0], f.gm[u][1], inv);
+      const int off = (grp * NW * U + u * NW) * 64;
+      u32x4 xa = u32x4{0u, 0u, 0u, 0u}, xb = u32x4{0u, 0u, 0u, 0u};
+      if (xval) {
+        xa = *reinterpret_cast<const u32x4*>(xl + off);
+        xb = *reinterpret_cast<const u32x4*>(xl + off + 8);
       }
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
@@ -193,10 +180,10 @@ __global__ __launch_bounds__(NW * 64) void fused_skinny_kernel(FusedArgs a) {
   };
   for (int grp = 0; grp + 1 < ngroups; ++grp) {
     load(nxt, grp + 1);
-    compute(cur);
+    compute(cur, grp);
     cur = nxt;
   }
-  compute(cur);
+  compute(cur, ngroups - 1);
 
   red[w][0][lane] = acc[0];
   red[w][1][lane] = acc[1];
@@ -262,12 +249,29 @@ __global__ __launch_bounds__(NW * 64) void fused_skinny_kernel(FusedArgs a) {
   }
 }
 
-template <int PRO, int EPI>
-int launch(const FusedArgs& a, int nblocks, hipStream_t s) {
-  // 8 waves x 2 K-steps per group (the skinny kernel's best M <= 16 config)
-  fused_skinny_kernel<8, 2, PRO, EPI><<<dim3(nblocks), 512, 0, s>>>(a);
+template <int NW, int U, int PRO, int EPI>
+int launch_cfg(const FusedArgs& a, int nblocks, hipStream_t s) {
+  if ((a.K / 64) % (NW * U)) return -7;
+  const size_t lds = (size_t)a.M * (a.K + 8) * 2;
+  // static (reduce tiles + norm partials) + staged X must fit the 160 KB of LDS
+  const size_t lds_static = (size_t)NW * 2 * 64 * 16 + (size_t)NW * 16 * 4 + 16 * 4;
+  if (lds + lds_static > 160 * 1024) return -6;
+  fused_skinny_kernel<NW, U, PRO, EPI><<<dim3(nblocks), NW * 64, lds, s>>>(a);
   DGI_CHECK_LAUNCH();
   return 0;
+}
+
+// cfg: (waves per workgroup, K-steps per load group)
+template <int PRO, int EPI>
+int launch(const FusedArgs& a, int nblocks, int cfg, hipStream_t s) {
+  switch (cfg) {
+    case 0: case 1: return launch_cfg<8, 2, PRO, EPI>(a, nblocks, s);
+    case 2: return launch_cfg<4, 4, PRO, EPI>(a, nblocks, s);
+    case 3: return launch_cfg<16, 1, PRO, EPI>(a, nblocks, s);
+    case 4: return launch_cfg<8, 1, PRO, EPI>(a, nblocks, s);
+    case 5: return launch_cfg<4, 2, PRO, EPI>(a, nblocks, s);
+    default: return -5;
+  }
 }
 
 }  // namespace
@@ -279,10 +283,11 @@ extern "C" int dgi_fused_skinny(const void* x, int ldx, const void* res, int ldr
                                 const void* gamma, float eps, const void* w, const void* bias, void* y,
                                 int ldy, int M, int N, int K, int pro, int epi, const int* positions,
                                 const float* cos_sin, const int* slots, void* k_cache, void* v_cache, int nh,
-                                int nkv, int block_size, hipStream_t s) {
+                                int nkv, int block_size, int cfg, hipStream_t s) {
   if (M <= 0 || N <= 0) return 0;
   if (M > 16) return -2;
   if (K % 1024 || ldx % 8 || (pro == 2 && ldr % 8)) return -3;
+  if ((size_t)M * (K + 8) * 2 > kMaxStagedBytes) return -6;  // X must fit in LDS next to the reduce buffer
   FusedArgs a{(const uint16_t*)x, ldx, (const uint16_t*)res, ldr, (uint16_t*)res_out, (const uint16_t*)gamma,
               eps, (const uint16_t*)w, (const uint16_t*)bias, (uint16_t*)y, ldy, M, K, 1, 32, 16,
               positions, cos_sin, slots, (uint16_t*)k_cache, (uint16_t*)v_cache, nh, nkv, 0};
@@ -309,7 +314,7 @@ extern "C" int dgi_fused_skinny(const void* x, int ldx, const void* res, int ldr
     return -5;
   }
   if (pro < 0 || pro > 2) return -5;
-#define DGI_FS(P, E) if (pro == P && epi == E) return launch<P, E>(a, nblocks, s);
+#define DGI_FS(P, E) if (pro == P && epi == E) return launch<P, E>(a, nblocks, cfg, s);
   DGI_FS(0, 0) DGI_FS(1, 0) DGI_FS(2, 0)
   DGI_FS(0, 1) DGI_FS(1, 1) DGI_FS(2, 1)
   DGI_FS(0, 2) DGI_FS(1, 2) DGI_FS(2, 2)

@@ -237,44 +237,63 @@ class LlamaModel:
         buf[T:Mp].zero_()       # pad rows: zeros in, ignored out
         return Mp
 
-    def _fused_decode(self, h: torch.Tensor, meta: AttnMeta) -> bool:
-        if meta.num_prefill_tokens != 0 or not ops.fused_decode_ok(h.shape[0], self.cfg.hidden_size):
-            return False
+    def _fused_decode(self, h: torch.Tensor, meta: AttnMeta) -> tuple:
+        """(fuse qkv, fuse gate_up) for this step; (False, False) = unfused layers."""
+        if meta.num_prefill_tokens != 0:
+            return False, False
+        if not ((h.is_cuda and h.dtype == torch.bfloat16) or self.force_fused):
+            return False, False
+        T, H = h.shape[0], self.cfg.hidden_size
         # force_fused: run the fused composition through the reference ops on CPU (tests)
-        return (h.is_cuda and h.dtype == torch.bfloat16) or self.force_fused
+        if self.force_fused:
+            return True, True
+        return ops.fused_decode_ok(T, H, "qkv"), ops.fused_decode_ok(T, H, "gate_up")
 
-    def _forward_layers_fused(self, h: torch.Tensor, meta: AttnMeta, residual: Optional[torch.Tensor]):
-        """Pure-decode layers with M <= 16 rows: 5 kernels per layer instead of 9.
-
-        qkv: RMSNorm (+ residual add) prologue and RoPE + paged-KV epilogue fused
-        into the weight-streaming GEMM; gate_up: RMSNorm prologue + SwiGLU
-        epilogue (ops.fused_skinny, dgi/csrc/fused_decode.hip).  The residual
-        stream ping-pongs between fresh buffers (the prologue reads the old one
-        while workgroup 0 writes the new)."""
+    def _forward_layers_fused(self, h: torch.Tensor, meta: AttnMeta, residual: Optional[torch.Tensor],
+                              fuse_qkv: bool = True, fuse_gu: bool = True):
+        """Pure-decode layers with few rows: the qkv projection with its RMSNorm
+        (+ residual add) prologue and RoPE + paged-KV epilogue in one kernel, and
+        gate_up with RMSNorm prologue + SwiGLU epilogue (ops.fused_skinny,
+        dgi/csrc/fused_decode.hip) — 5 kernels per layer instead of 9 when both
+        are fused.  A fused prologue writes the updated residual to a fresh
+        buffer (the old one is still being read by other workgroups); the
+        unfused steps update it in place as forward_layers does."""
         c = self.cfg
         eps = c.rms_eps
         T = h.shape[0]
         rope_epi = self.rope_mode == 0 and c.head_dim == 128 and self.cos_sin.shape[1] == 128
         for i, L in enumerate(self.layers):
             kc, vc = self.kv_cache[i, 0], self.kv_cache[i, 1]
-            qkv = torch.empty(T, L.qkv.shape[0], dtype=h.dtype, device=h.device)
-            if residual is None:
-                pro, res_out, new_res = 1, None, h
+            if fuse_qkv:
+                qkv = torch.empty(T, L.qkv.shape[0], dtype=h.dtype, device=h.device)
+                if residual is None:
+                    pro, res_out, new_res = 1, None, h
+                else:
+                    res_out = torch.empty_like(h)
+                    pro, new_res = 2, res_out
+                ops.fused_skinny(qkv, h, residual, res_out, L.in_norm, eps, L.qkv, L.qkv_bias, pro,
+                                 2 if rope_epi else 0, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc,
+                                 c.num_heads, c.num_kv_heads)
+                residual = new_res
+                attn = self.attention(i, qkv, meta, rope=not rope_epi)
             else:
-                res_out = torch.empty_like(h)
-                pro, new_res = 2, res_out
-            ops.fused_skinny(qkv, h, residual, res_out, L.in_norm, eps, L.qkv, L.qkv_bias, pro,
-                             2 if rope_epi else 0, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc,
-                             c.num_heads, c.num_kv_heads)
-            residual = new_res
-            attn = self.attention(i, qkv, meta, rope=not rope_epi)
+                if residual is None:
+                    residual = h
+                    h = ops.rmsnorm(h, L.in_norm, eps)
+                else:
+                    ops.fused_add_rmsnorm(h, residual, L.in_norm, eps)
+                attn = self.attention(i, ops.linear(h, L.qkv, L.qkv_bias), meta)
             h = ops.linear(attn, L.o)
             if self.reduce is not None:
                 self.reduce(h)
-            act = torch.empty(T, L.gate_up.shape[0] // 2, dtype=h.dtype, device=h.device)
-            res_out = torch.empty_like(h)
-            ops.fused_skinny(act, h, residual, res_out, L.post_norm, eps, L.gate_up, None, 2, 1)
-            residual = res_out
+            if fuse_gu:
+                act = torch.empty(T, L.gate_up.shape[0] // 2, dtype=h.dtype, device=h.device)
+                res_out = torch.empty_like(h)
+                ops.fused_skinny(act, h, residual, res_out, L.post_norm, eps, L.gate_up, None, 2, 1)
+                residual = res_out
+            else:
+                ops.fused_add_rmsnorm(h, residual, L.post_norm, eps)
+                act = ops.silu_mul(ops.linear(h, L.gate_up))
             h = ops.linear(act, L.down)
             if self.reduce is not None:
                 self.reduce(h)
@@ -288,8 +307,10 @@ class LlamaModel:
         c = self.cfg
         eps = c.rms_eps
         T = h.shape[0]
-        if self.layers and self._fused_decode(h, meta):
-            return self._forward_layers_fused(h, meta, residual)
+        if self.layers:
+            fq, fg = self._fused_decode(h, meta)
+            if fq or fg:
+                return self._forward_layers_fused(h, meta, residual, fq, fg)
         Mp = self._mlp_rows(T, h) if self.layers else T
         for i, L in enumerate(self.layers):
             if residual is None:

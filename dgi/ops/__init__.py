@@ -384,16 +384,23 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
 
 
 # Fused decode GEMM (fused_decode.hip): RMSNorm prologue + SwiGLU / RoPE+KV epilogue.
-# Used for the qkv and gate_up projections of pure-decode steps with M <= 16 rows
-# where the weight-streaming kernel is the GEMM of choice (K <= 4096, like
-# _use_skinny).  DGI_FUSED_DECODE=0 disables, =force ignores the K limit.
+# Where it pays (profiles/r2_fused_decode_bench.md, hipGraph-timed, weights cold):
+# the qkv projection at M <= 4 (16 vs 20 us at M = 1 on 8B) and gate_up at M = 1;
+# above that the per-workgroup X staging outweighs the saved launches and the
+# unfused chain wins.  K <= 4096 (8B-class) like _use_skinny.
+# DGI_FUSED_DECODE=0 disables, =force uses it for every M <= 16 and K.
 FUSED_DECODE = os.environ.get("DGI_FUSED_DECODE", "1")
+FUSED_MAX_M = {"qkv": 4, "gate_up": 1}
+# launch config per projection (fused_decode.hip cfg: 0 = 8 waves x 2 K-steps, 4 = 8 x 1)
+FUSED_KIND_CFG = {"qkv": 0, "gate_up": 4}
 
 
-def fused_decode_ok(M: int, K: int) -> bool:
-    if FUSED_DECODE == "0" or not 0 < M <= 16 or K % 1024:
+def fused_decode_ok(M: int, K: int, kind: str = "qkv") -> bool:
+    if FUSED_DECODE == "0" or not 0 < M <= 16 or K % 1024 or M * (K + 8) * 2 > 136 * 1024:
         return False
-    return FUSED_DECODE == "force" or (K <= 4096 and M <= SKINNY_MAX_M)
+    if FUSED_DECODE == "force":
+        return True
+    return K <= 4096 and M <= min(SKINNY_MAX_M, FUSED_MAX_M.get(kind, 0))
 
 
 def fused_skinny_ref(y, x, res, res_out, gamma, eps, w, bias, pro, epi, positions=None, cos_sin=None,
@@ -416,16 +423,21 @@ def fused_skinny_ref(y, x, res, res_out, gamma, eps, w, bias, pro, epi, position
     return y
 
 
+FUSED_CFG = int(os.environ.get("DGI_FUSED_CFG", "-1"))      # >= 0 overrides FUSED_KIND_CFG
+
+
 def fused_skinny(y, x, res, res_out, gamma, eps, w, bias, pro: int, epi: int, positions=None, cos_sin=None,
-                 slots=None, k_cache=None, v_cache=None, nh: int = 0, nkv: int = 0):
+                 slots=None, k_cache=None, v_cache=None, nh: int = 0, nkv: int = 0, cfg: Optional[int] = None):
     """y = epi(rmsnorm_pro(x [+ res]) @ w.T + bias); pro 2 also writes res_out = x + res.
 
     epi 0 stores [M, N]; epi 1 is SwiGLU over w = [gate; up] (y is [M, I]);
     epi 2 applies NeoX RoPE to the q/k heads of a fused qkv output and writes k/v
     into the paged cache at ``slots`` (head_dim 128, full rotary)."""
     if _native(x):
+        if cfg is None:
+            cfg = FUSED_CFG if FUSED_CFG >= 0 else FUSED_KIND_CFG["gate_up" if epi == 1 else "qkv"]
         _call("fused_skinny", y, x, res, res_out, gamma, eps, w, bias, pro, epi, positions, cos_sin, slots,
-              k_cache, v_cache, nh, nkv)
+              k_cache, v_cache, nh, nkv, cfg)
         return y
     return fused_skinny_ref(y, x, res, res_out, gamma, eps, w, bias, pro, epi, positions, cos_sin, slots,
                             k_cache, v_cache, nh, nkv)

@@ -68,11 +68,13 @@ class ModelRunner:
         maxb = max(max_num_seqs, max(graph_buckets) if graph_buckets else 1)
         self.dec_ws = None
         if self.is_cuda:
-            # partial O / log-sum-exp per split + one ticket counter per (sequence, kv-head)
-            # for the in-kernel split reduce (the counters return to 0 after every launch)
+            # partial O / log-sum-exp per split (+ with DGI_DECODE_FUSED_REDUCE=1 one ticket counter
+            # per (sequence, kv-head) for the in-kernel split reduce; off by default: its
+            # device-scope fences write back L2 and cost more than the reduce kernel on MI355X)
             self.dec_ws = (torch.empty(maxb * nh * self.ws_splits * hd, dtype=torch.float32, device=self.device),
-                           torch.empty(maxb * nh * self.ws_splits, dtype=torch.float32, device=self.device),
-                           torch.zeros(maxb * model.cfg.num_kv_heads, dtype=torch.int32, device=self.device))
+                           torch.empty(maxb * nh * self.ws_splits, dtype=torch.float32, device=self.device))
+            if os.environ.get("DGI_DECODE_FUSED_REDUCE", "0") == "1":
+                self.dec_ws += (torch.zeros(maxb * model.cfg.num_kv_heads, dtype=torch.int32, device=self.device),)
         self.graphs = None
         if use_graphs and self.is_cuda and model.has_head:
             self.graphs = GraphRunner(self, [b for b in graph_buckets if b <= max_num_seqs])
@@ -252,7 +254,10 @@ class GraphRunner:
             return r.graph_splits, r.graph_part
         nkv = r.model.cfg.num_kv_heads
         want = max(1, -(-4 * r.num_cus // max(1, b * nkv)))
-        return min(r.ws_splits, want), -64
+        # minimum part: 128 tokens (one 32-token tile per wave) below batch 8, 64 above
+        # (profiles/r2_fused_decode_bench.md: best or within 0.3 us at ctx 256-4096)
+        mp = int(os.environ.get("DGI_DECODE_MIN_PART", "0")) or (128 if b < 8 else 64)
+        return min(r.ws_splits, want), -mp
 
     def _meta(self, b):
         r = self.r

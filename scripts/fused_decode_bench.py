@@ -1,0 +1,148 @@
+#!/usr/bin/env python3
+"""Microbenchmarks for the decode-step kernels, timed inside hipGraphs (as decode runs).
+
+* fused_skinny (norm prologue + SwiGLU / RoPE epilogue) per launch config vs the
+  unfused chain (rmsnorm + skinny/hipBLASLt GEMM + silu_mul / rope_cache);
+* paged decode attention: fixed r1 split plan + reduce kernel vs the device-side
+  plan (min part sizes) with the reduce kernel or the in-kernel ticket reduce.
+Weights are bf16 random, streamed cold (a buffer set larger than the 256 MB MALL
+is rotated through).
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from dgi import ops  # noqa: E402
+
+
+def graph_time(fn, reps=20, iters=10):
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn(0)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for i in range(reps):
+            fn(i)
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1000 / (iters * reps)
+
+
+def bench_gemms(H, I, nh, nkv, Ms, cfgs):
+    dev = "cuda"
+    bf = torch.bfloat16
+    nbuf = 6                       # 6 x (qkv + gate_up) > MALL: weights come from HBM
+    qkv_w = [torch.randn((nh + 2 * nkv) * 128, H, device=dev, dtype=bf) * 0.02 for _ in range(nbuf)]
+    gu_w = [torch.randn(2 * I, H, device=dev, dtype=bf) * 0.02 for _ in range(nbuf)]
+    gamma = torch.ones(H, device=dev, dtype=bf)
+    inv = 1.0 / (10000 ** (torch.arange(0, 64, device=dev).float() / 64))
+    ang = torch.arange(4096, device=dev).float()[:, None] * inv[None]
+    cs = torch.cat([ang.cos(), ang.sin()], 1).contiguous()
+    kc = torch.zeros(512, nkv, 16, 128, device=dev, dtype=bf)
+    vc = torch.zeros_like(kc)
+    rows = []
+    for M in Ms:
+        x = torch.randn(M, H, device=dev, dtype=bf)
+        res = torch.randn(M, H, device=dev, dtype=bf)
+        ro = torch.empty_like(x)
+        pos = torch.arange(100, 100 + M, device=dev, dtype=torch.int32)
+        slots = torch.arange(M, device=dev, dtype=torch.int32)
+        qkv = torch.empty(M, qkv_w[0].shape[0], device=dev, dtype=bf)
+        act = torch.empty(M, I, device=dev, dtype=bf)
+        row = {"M": M}
+        for cfg in cfgs:                  # eager first: a fault names its variant
+            for epi, (yy, ww) in ((2, (qkv, qkv_w[0])), (1, (act, gu_w[0]))):
+                print(f"eager M={M} cfg={cfg} epi={epi}", flush=True)
+                ops.fused_skinny(yy, x, res, ro, gamma, 1e-5, ww, None, 2, epi, pos, cs, slots, kc, vc, nh, nkv,
+                                 cfg=cfg)
+                torch.cuda.synchronize()
+        for cfg in cfgs:
+            row[f"qkv_fused_c{cfg}"] = round(graph_time(lambda i: ops.fused_skinny(
+                qkv, x, res, ro, gamma, 1e-5, qkv_w[i % nbuf], None, 2, 2, pos, cs, slots, kc, vc, nh, nkv,
+                cfg=cfg)), 2)
+            row[f"gu_fused_c{cfg}"] = round(graph_time(lambda i: ops.fused_skinny(
+                act, x, res, ro, gamma, 1e-5, gu_w[i % nbuf], None, 2, 1, cfg=cfg)), 2)
+
+        def unfused_qkv(i):
+            xx = x.clone()
+            rr = res.clone()
+            ops.fused_add_rmsnorm(xx, rr, gamma, 1e-5)
+            q = ops.linear(xx, qkv_w[i % nbuf])
+            ops.rope_cache(q, pos, cs, nh, nkv, 128, slots, kc, vc, 0)
+
+        def unfused_gu(i):
+            xx = x.clone()
+            rr = res.clone()
+            ops.fused_add_rmsnorm(xx, rr, gamma, 1e-5)
+            ops.silu_mul(ops.linear(xx, gu_w[i % nbuf]))
+        row["qkv_unfused"] = round(graph_time(unfused_qkv), 2)
+        row["gu_unfused"] = round(graph_time(unfused_gu), 2)
+        row["clone_x2"] = round(graph_time(lambda i: (x.clone(), res.clone())), 2)
+        print(json.dumps(row), flush=True)
+        rows.append(row)
+    return rows
+
+
+def bench_attn(nh, nkv, Bs, ctxs):
+    dev = "cuda"
+    bf = torch.bfloat16
+    bs = 16
+    rows = []
+    for B in Bs:
+        for ctx in ctxs:
+            nblk = B * ((ctx + bs - 1) // bs) + 4
+            kc = torch.randn(nblk, nkv, bs, 128, device=dev, dtype=bf)
+            vc = torch.randn_like(kc)
+            maxw = (ctx + bs - 1) // bs
+            bt = torch.arange(B * maxw, device=dev, dtype=torch.int32).view(B, maxw)
+            cl = torch.full((B,), ctx, device=dev, dtype=torch.int32)
+            q = torch.randn(B, (nh + 2 * nkv) * 128, device=dev, dtype=bf)
+            out = torch.empty(B, nh * 128, device=dev, dtype=bf)
+            S = 16
+            ws2 = (torch.empty(B * nh * S * 128, device=dev), torch.empty(B * nh * S, device=dev))
+            ws3 = ws2 + (torch.zeros(B * nkv, device=dev, dtype=torch.int32),)
+            sc = 1 / 128 ** 0.5
+            row = {"B": B, "ctx": ctx}
+            row["r1_fixed256"] = round(graph_time(lambda i: ops.paged_decode(
+                q, kc, vc, bt, cl, nh, nkv, sc, 8, 256, out=out, workspace=ws2)), 2)
+            want = max(1, -(-4 * 256 // (B * nkv)))
+            for mp in (32, 64, 128, 256):
+                row[f"dyn{mp}"] = round(graph_time(lambda i: ops.paged_decode(
+                    q, kc, vc, bt, cl, nh, nkv, sc, min(S, want), -mp, out=out, workspace=ws2)), 2)
+                row[f"dyn{mp}_ticket"] = round(graph_time(lambda i: ops.paged_decode(
+                    q, kc, vc, bt, cl, nh, nkv, sc, min(S, want), -mp, out=out, workspace=ws3)), 2)
+            print(json.dumps(row), flush=True)
+            rows.append(row)
+    return rows
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--cfgs", type=int, nargs="+", default=[0, 2, 3, 4, 5])
+    ap.add_argument("--skip-attn", action="store_true")
+    a = ap.parse_args()
+    res = {"gemm_8b": bench_gemms(4096, 14336, 32, 8, [1, 2, 4, 8, 16], a.cfgs)}
+    if not a.skip_attn:
+        res["attn_8b"] = bench_attn(32, 8, [1, 4, 16], [256, 384, 1024, 4096])
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

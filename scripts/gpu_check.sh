@@ -50,8 +50,9 @@ for s in $STEPS; do
     pdcap_mbt) run pdcap_mbt 1000 python scripts/pd_capacity.py --mbt 3072,3584,4096,4608,5120,6144 --decode "" --out gpurun_out/pdcap_mbt.jsonl ;;
     spec8b_ctl) run spec8b_ctl 900 python scripts/bench_spec.py --batch 1 4 16 --target peaked --train-steps 1500 --random-seqs 1024 --oracle-accept 0.6 1.0 --sampled --out gpurun_out/spec8b_ctl.json ;;
     fused_tests) run fused_tests 600 python -u -m pytest tests/test_kernels_gpu.py tests/test_gpu_hf_parity.py -k "fused or paged_decode or decode_matches or hf_parity" -x -v -p no:cacheprovider --timeout 200 --timeout-method thread ;;
-    declat_fused) run declat_fused 600 python scripts/decode_latency.py --batch 1 4 16 --out gpurun_out/declat_fused.json && DGI_FUSED_DECODE=0 run declat_unfused 600 python scripts/decode_latency.py --batch 1 4 16 --out gpurun_out/declat_unfused.json && DGI_FUSED_DECODE=0 DGI_DECODE_DYNAMIC=0 run declat_r1 600 python scripts/decode_latency.py --batch 1 4 16 --out gpurun_out/declat_r1.json ;;
+    declat_fused) run declat_fused 600 python scripts/decode_latency.py --batch 1 2 4 16 64 --out gpurun_out/declat_fused.json && DGI_FUSED_DECODE=0 run declat_unfused 600 python scripts/decode_latency.py --batch 1 2 4 16 64 --out gpurun_out/declat_unfused.json && DGI_FUSED_DECODE=0 DGI_DECODE_DYNAMIC=0 run declat_r1 600 python scripts/decode_latency.py --batch 1 2 4 16 64 --out gpurun_out/declat_r1.json ;;
     profdec_fused) export TMPDIR=/tmp; run profdec_fused 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profdec_fused -o run --output-format csv -- python3 scripts/decode_latency.py --batch 1 --steps 200 ;;
+    fdbench) run fdbench 600 python scripts/fused_decode_bench.py --out gpurun_out/fdbench.json ;;
     bench70b_long) run bench70b_long 1200 python bench.py --steps 200 --warmup 20 --json-out gpurun_out/bench70b_long.json ;;
   esac
 done

@@ -171,12 +171,15 @@ def test_fused_decode_layers_match_unfused_on_cpu():
     from dgi.models.config import get_config
     from dgi.models.llama import LlamaModel
     from dgi.sched.request import SamplingParams
-    for name in ("llama-tiny-hd128", "qwen-tiny", "glm-tiny"):
+    for name, mix in (("llama-tiny-hd128", (True, True)), ("qwen-tiny", (True, False)), ("glm-tiny", (True, True)),
+                      ("llama-tiny-hd128", (False, True))):
         mc = get_config(name)
         outs, logits = [], []
         for fused in (False, True):
             m = LlamaModel(mc, "cpu", torch.float32, seed=11)
             m.force_fused = fused
+            if fused:
+                m._fused_decode = lambda h, meta, mix=mix: mix if meta.num_prefill_tokens == 0 else (False, False)
             calls = []
             real_fused = m._forward_layers_fused
 
