@@ -23,16 +23,20 @@ __device__ __forceinline__ float bf16_to_f32(uint16_t v) {
   return __uint_as_float(((uint32_t)v) << 16);
 }
 
-// Round-to-nearest-even f32 -> bf16 (inputs here are finite activations).
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+
+// Round-to-nearest-even f32 -> bf16.  Written as a (vector) conversion so hipcc
+// emits gfx950's v_cvt_pk_bf16_f32 (one VALU op for two values) instead of the
+// 5-6 integer ops of a bit-manipulation RNE — the softmax / norm / epilogue
+// loops are VALU-issue-bound and pay for every op here.
 __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
+  return __builtin_bit_cast(uint16_t, (__bf16)f);
 }
 
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
-  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+  const f32x2v v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v));
 }
 
 // 16-byte vector = 8 bf16.
