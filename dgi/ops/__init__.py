@@ -384,15 +384,15 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
 
 
 # Fused decode GEMM (fused_decode.hip): RMSNorm prologue + SwiGLU / RoPE+KV epilogue.
-# Where it pays (profiles/r2_fused_decode_bench.md, hipGraph-timed, weights cold):
-# the qkv projection at M <= 4 (16 vs 20 us at M = 1 on 8B) and gate_up at M = 1;
+# Where it pays (profiles/r2_decode8b_fused.md, hipGraph-timed, weights cold):
+# the qkv projection at M <= 8 (15 vs 18 us at M = 1 on 8B) and gate_up at M <= 2;
 # above that the per-workgroup X staging outweighs the saved launches and the
 # unfused chain wins.  K <= 4096 (8B-class) like _use_skinny.
 # DGI_FUSED_DECODE=0 disables, =force uses it for every M <= 16 and K.
 FUSED_DECODE = os.environ.get("DGI_FUSED_DECODE", "1")
-FUSED_MAX_M = {"qkv": 4, "gate_up": 1}
-# launch config per projection (fused_decode.hip cfg: 0 = 8 waves x 2 K-steps, 4 = 8 x 1)
-FUSED_KIND_CFG = {"qkv": 0, "gate_up": 4}
+FUSED_MAX_M = {"qkv": 8, "gate_up": 2}
+# launch config per projection (fused_decode.hip cfg: 4 = 8 waves x 1 K-step, 5 = 4 waves x 2)
+FUSED_KIND_CFG = {"qkv": 4, "gate_up": 5}
 
 
 def fused_decode_ok(M: int, K: int, kind: str = "qkv") -> bool:
