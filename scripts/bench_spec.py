@@ -33,6 +33,16 @@ def timed_generate(eng, prompts, sp):
     return [r.output for r in reqs], time.perf_counter() - t0
 
 
+def median_run(fn, n):
+    """(result of the last run, median seconds) over n runs of fn() -> (result, seconds)."""
+    res, ts = None, []
+    for _ in range(max(1, n)):
+        res, t = fn()
+        ts.append(t)
+    ts.sort()
+    return res, ts[len(ts) // 2]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="llama3-8b")
@@ -45,6 +55,7 @@ def main():
     ap.add_argument("--train-steps", type=int, default=300)
     ap.add_argument("--train-seqs", type=int, default=64)
     ap.add_argument("--random-seqs", type=int, default=192)
+    ap.add_argument("--repeats", type=int, default=3, help="timed runs per measurement (median)")
     ap.add_argument("--oracle-accept", type=float, nargs="*", default=[0.6, 0.8, 1.0])
     ap.add_argument("--target", default="random", choices=["random", "peaked"],
                     help="random: plain random init (near-flat logits: greedy choices sit on bf16 near-ties, so "
@@ -82,11 +93,16 @@ def main():
         timed_generate(base, prompts, SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True))
         timed_generate(spec, prompts, SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True))
         spec.warmup_spec([B])            # every depth the controller can reach, outside the timed runs
-        ref, t_base = timed_generate(base, prompts, sp)
-        spec.reset_controller()
-        spec.spec_stats.update(spec_steps=0, spec_rows=0, accepted=0, spec_tokens=0, draft_s=0.0, verify_s=0.0,
-                               plain_steps=0, switches_off=0, depth_changes=0)
-        out, t_spec = timed_generate(spec, prompts, sp)
+        # every timed quantity is the median of --repeats runs (run-to-run spread of the
+        # plain engine alone is a few %, the size of the effects measured here)
+        ref, t_base = median_run(lambda: timed_generate(base, prompts, sp), a.repeats)
+
+        def spec_run():
+            spec.reset_controller()
+            spec.spec_stats.update(spec_steps=0, spec_rows=0, accepted=0, spec_tokens=0, draft_s=0.0, verify_s=0.0,
+                                   plain_steps=0, switches_off=0, depth_changes=0)
+            return timed_generate(spec, prompts, sp)
+        out, t_spec = median_run(spec_run, a.repeats)
         acc = spec.acceptance()
         toks = B * a.output_len
         gap = max(greedy_gap(spec, p, o) for p, o in zip(prompts, out))
@@ -121,34 +137,34 @@ def main():
                                                            for x, y in zip(o, q)) / max(1, toks), 4)}
         # the feature-tapped plain path alone (what auto-off falls back to)
         spec.force_plain = True
-        _, t_tap = timed_generate(spec, prompts, sp)
+        _, t_tap = median_run(lambda: timed_generate(spec, prompts, sp), a.repeats)
         spec.force_plain = False
         row["tapped_plain"] = {"tok_s": round(toks / t_tap, 1), "vs_plain": round(t_base / t_tap, 3)}
-        _, t_base2 = timed_generate(base, prompts, sp)
-        row["plain_rerun_tok_s"] = round(toks / t_base2, 1)
         # acceptance-controlled runs: the first tree chain is replaced by the known greedy
         # continuation, each token kept with probability p (ceiling / sensitivity of the machinery)
         for p in a.oracle_accept:
-            reqs_rid = {}
-            spec.oracle = reqs_rid
-            spec.oracle_accept = p
-            rs = [spec.add_request(pr, sp) for pr in prompts]
-            for r, o in zip(rs, ref):
-                reqs_rid[r.rid] = o
-            spec.reset_controller(keep_plain_costs=True)     # plain cost per bucket is learned once per engine
-            spec.spec_stats.update(spec_steps=0, spec_rows=0, accepted=0, spec_tokens=0, draft_s=0.0, verify_s=0.0,
-                                   plain_steps=0, switches_off=0, depth_changes=0)
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            while spec.has_unfinished():
-                spec.step()
-            torch.cuda.synchronize()
-            t_o = time.perf_counter() - t1
+            def oracle_run():
+                reqs_rid = {}
+                spec.oracle = reqs_rid
+                spec.oracle_accept = p
+                rs = [spec.add_request(pr, sp) for pr in prompts]
+                for r, o in zip(rs, ref):
+                    reqs_rid[r.rid] = o
+                spec.reset_controller(keep_plain_costs=True)     # plain cost per bucket is learned once per engine
+                spec.spec_stats.update(spec_steps=0, spec_rows=0, accepted=0, spec_tokens=0, draft_s=0.0,
+                                       verify_s=0.0, plain_steps=0, switches_off=0, depth_changes=0)
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                while spec.has_unfinished():
+                    spec.step()
+                torch.cuda.synchronize()
+                return [r.output for r in rs], time.perf_counter() - t1
+            o_out, t_o = median_run(oracle_run, a.repeats)
             spec.oracle = None
             ao = spec.acceptance()
             row[f"oracle_p{p}"] = {"tok_s": round(toks / t_o, 1), "speedup": round(t_base / t_o, 3),
                                    "mean_accepted": round(ao["mean_accepted"], 3),
-                                   "identical": [r.output for r in rs] == ref,
+                                   "identical": o_out == ref,
                                    "spec_steps": ao["spec_steps"], "plain_steps": ao["plain_steps"],
                                    "depth": ao["current_depth"]}
         print(json.dumps(row), flush=True)
