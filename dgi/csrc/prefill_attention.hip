@@ -28,16 +28,26 @@ using namespace dgi;
 
 namespace {
 
-__device__ __forceinline__ int k_off(int row, int ch) {  // element offset, HD=128
-  return row * 128 + (((ch) ^ (row & 15)) << 3);
+// Element offset of 16-byte chunk `ch` of LDS row `row`.
+// HD=128 (256-B rows): K chunk ^ (row & 15) — 16 consecutive rows at one chunk
+// hit 16 distinct slots (ds_read_b128); V chunk ^ ((row & 3) << 2) for the
+// transposed reads.  HD=64 (128-B rows, two rows per 64-bank line): row & 1
+// already picks the bank half, so K XORs (row >> 1) & 7 and V shifts rows
+// 2-3 of each 4-row block by 4 chunks.
+template <int HD>
+__device__ __forceinline__ int k_off(int row, int ch) {
+  if constexpr (HD == 128) return row * 128 + (((ch) ^ (row & 15)) << 3);
+  else return row * 64 + (((ch) ^ ((row >> 1) & 7)) << 3);
 }
+template <int HD>
 __device__ __forceinline__ int v_off(int row, int ch) {
-  return row * 128 + (((ch) ^ ((row & 3) << 2)) << 3);
+  if constexpr (HD == 128) return row * 128 + (((ch) ^ ((row & 3) << 2)) << 3);
+  else return row * 64 + (((ch) ^ (((row >> 1) & 1) << 2)) << 3);
 }
 
-constexpr int HD = 128;
 constexpr int KT = 64;  // keys per tile
 
+template <int HD>
 __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
     const uint16_t* __restrict__ q, int q_stride, const uint16_t* __restrict__ k_cache,
     const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
@@ -74,12 +84,16 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
   if (is_tree) tmask = tree_mask[(size_t)b * 64 + (my_row - tree_first)];
   const int tree_key0 = pos_base + tree_first;  // key index of tree node 0
 
+  constexpr int NS = HD / 16;   // k-steps of S^T = K Q^T
+  constexpr int ND = HD / 32;   // 32-dim blocks of O^T
+  constexpr int CH = HD / 8;    // 16-byte chunks per K/V row
+  constexpr int NP = KT * CH / 256;  // staging passes per tile (256 threads, one chunk each)
   // Q fragments (B operand): lane holds Q[row lr][16 s + 8 hh + j]
-  u32x4 qf[8];
+  u32x4 qf[NS];
   {
     const uint16_t* qp = q + (size_t)(q0 + (row_valid ? my_row : 0)) * q_stride + head * HD;
 #pragma unroll
-    for (int s = 0; s < 8; ++s)
+    for (int s = 0; s < NS; ++s)
       qf[s] = row_valid ? *reinterpret_cast<const u32x4*>(qp + 16 * s + 8 * hh) : u32x4{0, 0, 0, 0};
   }
 
@@ -87,9 +101,9 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
   const int kv_end = min(ctx, pos_base + last_row + 1);
 
   float m_run = -1e30f, l_run = 0.f;
-  f32x16 o[4];
+  f32x16 o[ND];
 #pragma unroll
-  for (int d = 0; d < 4; ++d)
+  for (int d = 0; d < ND; ++d)
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
 
@@ -98,12 +112,12 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
   // the global loads of tile i+1 are in flight while tile i is consumed from
   // LDS (1 workgroup per CU at this register budget, so latency must be hidden
   // inside the wave, not by occupancy).
-  u32x4 kr[4], vr[4];
+  u32x4 kr[NP], vr[NP];
   auto load_tile = [&](int kb0) {
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int row = p * 16 + (tid >> 4);
-      const int ch = tid & 15;
+    for (int p = 0; p < NP; ++p) {
+      const int row = p * (256 / CH) + tid / CH;
+      const int ch = tid % CH;
       const int key = min(kb0 + row, kv_end - 1);
       const int blk = bt[key >> bs_log2];
       const size_t base = ((size_t)blk * nkv + kvh) * head_stride + (size_t)(key & (bs - 1)) * HD + ch * 8;
@@ -120,11 +134,11 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
   for (int kb0 = 0; kb0 < kv_end; kb0 += KT) {
     __syncthreads();  // previous tile fully consumed
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int row = p * 16 + (tid >> 4);
-      const int ch = tid & 15;
-      *reinterpret_cast<u32x4*>(ks + k_off(row, ch)) = kr[p];
-      *reinterpret_cast<u32x4*>(vs + v_off(row, ch)) = vr[p];
+    for (int p = 0; p < NP; ++p) {
+      const int row = p * (256 / CH) + tid / CH;
+      const int ch = tid % CH;
+      *reinterpret_cast<u32x4*>(ks + k_off<HD>(row, ch)) = kr[p];
+      *reinterpret_cast<u32x4*>(vs + v_off<HD>(row, ch)) = vr[p];
     }
     __syncthreads();
     if (kb0 + KT < kv_end) load_tile(kb0 + KT);
@@ -137,8 +151,8 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
 #pragma unroll
       for (int r = 0; r < 16; ++r) sc[kb][r] = 0.f;
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const u32x4 a = *reinterpret_cast<const u32x4*>(ks + k_off(32 * kb + lr, 2 * s + hh));
+      for (int s = 0; s < NS; ++s) {
+        const u32x4 a = *reinterpret_cast<const u32x4*>(ks + k_off<HD>(32 * kb + lr, 2 * s + hh));
         sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a), as_bf16x8(qf[s]), sc[kb], 0, 0, 0);
       }
     }
@@ -174,7 +188,7 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
       const float alpha = exp2f(m_run - m_new);
       l_run *= alpha;
 #pragma unroll
-      for (int d = 0; d < 4; ++d) o[d] *= alpha;
+      for (int d = 0; d < ND; ++d) o[d] *= alpha;
       m_run = m_new;
     }
     float psum = 0.f;
@@ -213,13 +227,13 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) pf[jj] = pack_bf16x2(sc[kb][8 * s2 + 2 * jj], sc[kb][8 * s2 + 2 * jj + 1]);
 #pragma unroll
-        for (int d = 0; d < 4; ++d) {
+        for (int d = 0; d < ND; ++d) {
           const int col = 32 * d + 16 * (g16 & 1) + 4 * tp;
           const int r0 = 32 * kb + 16 * s2 + 4 * hh + tq;
           short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_short4*)(vs + v_off(r0, col >> 3) + (col & 7)));
+              (lds_short4*)(vs + v_off<HD>(r0, col >> 3) + (col & 7)));
           short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_short4*)(vs + v_off(r0 + 8, col >> 3) + (col & 7)));
+              (lds_short4*)(vs + v_off<HD>(r0 + 8, col >> 3) + (col & 7)));
           u32x4 vf;
           vf[0] = (uint32_t)(uint16_t)lo[0] | ((uint32_t)(uint16_t)lo[1] << 16);
           vf[1] = (uint32_t)(uint16_t)lo[2] | ((uint32_t)(uint16_t)lo[3] << 16);
@@ -234,7 +248,7 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
   const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
   uint16_t* op = out + (size_t)(q0 + my_row) * out_stride + head * HD;
 #pragma unroll
-  for (int d = 0; d < 4; ++d)
+  for (int d = 0; d < ND; ++d)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       const int dim = 32 * d + 8 * rr + 4 * hh;
@@ -255,17 +269,23 @@ extern "C" int dgi_paged_prefill(const void* q, int q_stride, const void* k_cach
                                  int block_size, float scale, const unsigned long long* tree_mask,
                                  int tree_n, hipStream_t s) {
   if (n_tiles == 0) return 0;
-  if (hd != 128) return -5;
+  if (hd != 128 && hd != 64) return -5;
   if (nh % nkv) return -2;
   if (tree_n > 64) return -6;
   int bs_log2 = 0;
   while ((1 << bs_log2) < block_size) ++bs_log2;
   if ((1 << bs_log2) != block_size) return -4;
   const float scale_log2 = scale * 1.4426950408889634f;
-  prefill_attn_kernel<<<dim3(n_tiles, nh), 256, 0, s>>>(
-      (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables,
-      bt_stride, cu_seqlens_q, context_lens, tiles, (uint16_t*)out, out_stride, nh, nkv, bs_log2,
-      scale_log2, tree_mask, tree_n);
+  if (hd == 128)
+    prefill_attn_kernel<128><<<dim3(n_tiles, nh), 256, 0, s>>>(
+        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables,
+        bt_stride, cu_seqlens_q, context_lens, tiles, (uint16_t*)out, out_stride, nh, nkv, bs_log2,
+        scale_log2, tree_mask, tree_n);
+  else
+    prefill_attn_kernel<64><<<dim3(n_tiles, nh), 256, 0, s>>>(
+        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables,
+        bt_stride, cu_seqlens_q, context_lens, tiles, (uint16_t*)out, out_stride, nh, nkv, bs_log2,
+        scale_log2, tree_mask, tree_n);
   DGI_CHECK_LAUNCH();
   return 0;
 }

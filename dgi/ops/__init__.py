@@ -318,8 +318,8 @@ def prefill_tiles(cu_seqlens_q: list[int], tile: int = 128) -> list[tuple[int, i
 def paged_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens, nh, nkv, scale,
                   tiles=None, tree_mask=None, tree_n: int = 0, out=None) -> torch.Tensor:
     """Causal varlen attention of packed queries over the paged KV (prefix + new)."""
-    if _native(q) and k_cache.shape[-1] != 128:
-        _warn_once("paged_prefill", f"head_dim {k_cache.shape[-1]}: the MFMA prefill kernel is built for 128; "
+    if _native(q) and k_cache.shape[-1] not in (64, 128):
+        _warn_once("paged_prefill", f"head_dim {k_cache.shape[-1]}: the MFMA prefill kernel is built for 64 / 128; "
                                     "using the PyTorch reference")
     elif _native(q):
         hd = k_cache.shape[-1]

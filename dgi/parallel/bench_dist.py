@@ -54,7 +54,8 @@ def run_distributed(args, layout_kind: str, dist):
                        max_model_len=max(2048, args.prompt_len + args.output_len + 64),
                        use_graphs=not args.no_graphs, seed=args.seed, enable_prefix_caching=False,
                        kv_fraction=kv_frac)
-    sp = SamplingParams(max_tokens=args.output_len, temperature=0.0, ignore_eos=True)
+    sp = SamplingParams(max_tokens=args.output_len, temperature=getattr(args, "temperature", 0.0),
+                        top_k=getattr(args, "top_k", 0), top_p=getattr(args, "top_p", 1.0), ignore_eos=True)
     rng = random.Random(777 + rank)
     role = layout.role(rank)
     try:

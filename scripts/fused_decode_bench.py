@@ -97,6 +97,29 @@ def bench_gemms(H, I, nh, nkv, Ms, cfgs):
     return rows
 
 
+def bench_plain(shapes, Ms):
+    """skinny_gemm launch configs vs hipBLASLt (torch.matmul) on plain decode projections."""
+    dev, bf = "cuda", torch.bfloat16
+    rows = []
+    for name, N, K in shapes:
+        nbuf = max(2, int(2.5e9 // (N * K * 2)))      # rotate > MALL worth of weights
+        ws = [torch.randn(N, K, device=dev, dtype=bf) * 0.02 for _ in range(nbuf)]
+        for M in Ms:
+            x = torch.randn(M, K, device=dev, dtype=bf)
+            y = torch.empty(M, N, device=dev, dtype=bf)
+            row = {"gemm": name, "M": M, "N": N, "K": K,
+                   "hipblaslt": round(graph_time(lambda i: torch.matmul(x, ws[i % nbuf].t(), out=y)), 2)}
+            for cfg in (1, 2, 3, 4, 5, 6):
+                try:
+                    row[f"skinny_c{cfg}"] = round(graph_time(
+                        lambda i: torch.ops.dgi.skinny_gemm(y, x, ws[i % nbuf], None, cfg)), 2)
+                except Exception as e:          # shape not supported by this config
+                    row[f"skinny_c{cfg}"] = None
+            print(json.dumps(row), flush=True)
+            rows.append(row)
+    return rows
+
+
 def bench_attn(nh, nkv, Bs, ctxs):
     dev = "cuda"
     bf = torch.bfloat16
@@ -135,7 +158,16 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--cfgs", type=int, nargs="+", default=[0, 2, 3, 4, 5])
     ap.add_argument("--skip-attn", action="store_true")
+    ap.add_argument("--plain", action="store_true", help="only the plain skinny-vs-hipBLASLt table")
     a = ap.parse_args()
+    if a.plain:
+        ops.load_native(required=True)
+        res = {"plain_8b": bench_plain([("down", 4096, 14336), ("o", 4096, 4096), ("qkv", 6144, 4096),
+                                        ("gate_up", 28672, 4096)], [1, 2, 4, 8, 16])}
+        if a.out:
+            with open(a.out, "w") as f:
+                json.dump(res, f, indent=1)
+        return
     res = {"gemm_8b": bench_gemms(4096, 14336, 32, 8, [1, 2, 4, 8, 16], a.cfgs)}
     if not a.skip_attn:
         res["attn_8b"] = bench_attn(32, 8, [1, 4, 16], [256, 384, 1024, 4096])

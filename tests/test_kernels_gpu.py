@@ -123,11 +123,12 @@ def test_paged_decode(nh, nkv, hd, ctx_lens):
         assert int(ws[2].abs().sum()) == 0
 
 
-@pytest.mark.parametrize("nh,nkv", [(32, 8), (64, 8), (8, 1), (28, 4)])
+@pytest.mark.parametrize("nh,nkv,hd", [(32, 8, 128), (64, 8, 128), (8, 1, 128), (28, 4, 128), (32, 8, 64),
+                                       (14, 2, 64)])
 @pytest.mark.parametrize("qlens,ctxs", [([5], [5]), ([130, 1, 64], [130, 40, 600]), ([512], [512]),
                                         ([300, 77], [1000, 77])])
-def test_paged_prefill(nh, nkv, qlens, ctxs):
-    hd, bs = 128, 16
+def test_paged_prefill(nh, nkv, hd, qlens, ctxs):
+    bs = 16
     maxw = 80
     nblocks = sum((c + bs - 1) // bs for c in ctxs) + 4
     kc, vc = _make_cache(nblocks, nkv, bs, hd)
