@@ -359,7 +359,13 @@ SKINNY_MAX_M = int(os.environ.get("DGI_SKINNY_MAX_M", "32"))
 def _use_skinny(M: int, N: int, K: int) -> bool:
     if M > SKINNY_MAX_M or K % 1024 or N % 16 or K > 4096 or N > 32768:
         return False
-    return M <= 8 or (N <= 4096 and M <= 16)
+    # wide projections (8B gate_up, N = 28672) stay ahead of hipBLASLt up to M = 16
+    # with the 16-wave config (profiles/r2_decode8b_fused.md, plain GEMM table)
+    return M <= 8 or (N <= 4096 and M <= 16) or (N >= 16384 and M <= 16)
+
+
+def _skinny_cfg(M: int, N: int) -> int:
+    return 5 if (M > 8 and N >= 16384) else 0
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
@@ -374,7 +380,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         load_native(required=True)
         if out is None:
             out = torch.empty(M, N, dtype=x.dtype, device=x.device)
-        _call("skinny_gemm", out, x, w, bias, 0)
+        _call("skinny_gemm", out, x, w, bias, _skinny_cfg(M, N))
         return out
     r = torch.nn.functional.linear(x, w, bias)
     if out is not None:
