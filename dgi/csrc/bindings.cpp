@@ -24,7 +24,7 @@ int dgi_paged_prefill(const void* q, int q_stride, const void* k_cache, const vo
                       const int* block_tables, int bt_stride, const int* cu_seqlens_q,
                       const int* context_lens, const int* tiles, int n_tiles, void* out,
                       int out_stride, int nh, int nkv, int hd, int block_size, float scale,
-                      const unsigned long long* tree_mask, int tree_n, hipStream_t s);
+                      const unsigned long long* tree_mask, int tree_n, int tile_rows, hipStream_t s);
 int dgi_silu_mul(const void* gu, void* out, int T, int I, hipStream_t s);
 int dgi_skinny_gemm(const void* x, int ldx, const void* w, const void* bias, void* y, int ldy, int M,
                     int N, int K, int nw, hipStream_t s);
@@ -153,7 +153,7 @@ void paged_prefill(at::Tensor out, const at::Tensor& q, const at::Tensor& k_cach
                    const at::Tensor& v_cache, const at::Tensor& block_tables,
                    const at::Tensor& cu_seqlens_q, const at::Tensor& context_lens,
                    const at::Tensor& tiles, int64_t nh, int64_t nkv, double scale,
-                   const c10::optional<at::Tensor>& tree_mask, int64_t tree_n) {
+                   const c10::optional<at::Tensor>& tree_mask, int64_t tree_n, int64_t tile_rows) {
   check_bf16(out, "out"); check_bf16(q, "q"); check_bf16(k_cache, "k_cache"); check_bf16(v_cache, "v_cache");
   check_i32(block_tables, "block_tables"); check_i32(cu_seqlens_q, "cu_seqlens_q");
   check_i32(context_lens, "context_lens"); check_i32(tiles, "tiles");
@@ -173,7 +173,7 @@ void paged_prefill(at::Tensor out, const at::Tensor& q, const at::Tensor& k_cach
                              cu_seqlens_q.data_ptr<int>(), context_lens.data_ptr<int>(),
                              tiles.data_ptr<int>(), (int)tiles.size(0), out.data_ptr(),
                              (int)out.stride(0), (int)nh, (int)nkv, hd, (int)k_cache.size(2),
-                             (float)scale, tm, (int)tree_n, cur_stream()),
+                             (float)scale, tm, (int)tree_n, (int)tile_rows, cur_stream()),
            "paged_prefill");
 }
 
@@ -422,7 +422,7 @@ TORCH_LIBRARY(dgi, m) {
         "int part_size, float scale, Tensor(d!)? counters=None) -> ()");
   m.def("paged_prefill(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor cu_seqlens_q, Tensor context_lens, Tensor tiles, int nh, int nkv, float scale, "
-        "Tensor? tree_mask, int tree_n) -> ()");
+        "Tensor? tree_mask, int tree_n, int tile_rows=128) -> ()");
   m.def("silu_mul(Tensor(a!) out, Tensor gu) -> ()");
   m.def("skinny_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor? bias, int cfg=0) -> ()");
   m.def("fused_skinny(Tensor(a!) y, Tensor x, Tensor? res, Tensor(b!)? res_out, Tensor? gamma, float eps, "

@@ -47,8 +47,11 @@ __device__ __forceinline__ int v_off(int row, int ch) {
 
 constexpr int KT = 64;  // keys per tile
 
-template <int HD>
-__global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
+// NW waves x 32 query rows per workgroup (one K/V tile staging shared by all of them):
+// NW = 4 -> 128-row tiles, 2 workgroups per CU; NW = 8 -> 256-row tiles, 1 per CU
+// (same 2 waves per SIMD, half the K/V staging per query row).
+template <int HD, int NW>
+__global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void prefill_attn_kernel(
     const uint16_t* __restrict__ q, int q_stride, const uint16_t* __restrict__ k_cache,
     const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_seqlens_q, const int* __restrict__ context_lens,
@@ -87,7 +90,8 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
   constexpr int NS = HD / 16;   // k-steps of S^T = K Q^T
   constexpr int ND = HD / 32;   // 32-dim blocks of O^T
   constexpr int CH = HD / 8;    // 16-byte chunks per K/V row
-  constexpr int NP = KT * CH / 256;  // staging passes per tile (256 threads, one chunk each)
+  constexpr int NT = NW * 64;        // threads
+  constexpr int NP = KT * CH / NT;   // staging passes per tile (one chunk per thread per pass)
   // Q fragments (B operand): lane holds Q[row lr][16 s + 8 hh + j]
   u32x4 qf[NS];
   {
@@ -97,7 +101,7 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
       qf[s] = row_valid ? *reinterpret_cast<const u32x4*>(qp + 16 * s + 8 * hh) : u32x4{0, 0, 0, 0};
   }
 
-  const int last_row = min(t0 + 128, qlen) - 1;
+  const int last_row = min(t0 + 32 * NW, qlen) - 1;
   const int kv_end = min(ctx, pos_base + last_row + 1);
 
   float m_run = -1e30f, l_run = 0.f;
@@ -116,7 +120,7 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
   auto load_tile = [&](int kb0) {
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
-      const int row = p * (256 / CH) + tid / CH;
+      const int row = p * (NT / CH) + tid / CH;
       const int ch = tid % CH;
       const int key = min(kb0 + row, kv_end - 1);
       const int blk = bt[key >> bs_log2];
@@ -131,18 +135,21 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
   // keys <= wave_first_pos are visible to every row of the wave
   const int wave_first_pos = pos_base + t0 + 32 * w;
   const bool wave_tree = tree_mask != nullptr && (t0 + 32 * w + 31 >= tree_first);
+  const bool wave_rows = t0 + 32 * w < qlen;
   for (int kb0 = 0; kb0 < kv_end; kb0 += KT) {
     __syncthreads();  // previous tile fully consumed
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
-      const int row = p * (256 / CH) + tid / CH;
+      const int row = p * (NT / CH) + tid / CH;
       const int ch = tid % CH;
       *reinterpret_cast<u32x4*>(ks + k_off<HD>(row, ch)) = kr[p];
       *reinterpret_cast<u32x4*>(vs + v_off<HD>(row, ch)) = vr[p];
     }
     __syncthreads();
     if (kb0 + KT < kv_end) load_tile(kb0 + KT);
-    if (kb0 > wave_last_pos) continue;  // whole tile above this wave's diagonal
+    // whole tile above this wave's diagonal, or no valid query row in this wave
+    // (it still stages K/V for the others)
+    if (kb0 > wave_last_pos || !wave_rows) continue;
 
     // ---- S^T = K Q^T for two 32-key blocks
     f32x16 sc[2];
@@ -261,13 +268,13 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
 
 }  // namespace
 
-// tiles: int32 [n_tiles, 2] = (sequence index, first query row of the 128-row tile)
+// tiles: int32 [n_tiles, 2] = (sequence index, first query row of the tile_rows-row tile)
 extern "C" int dgi_paged_prefill(const void* q, int q_stride, const void* k_cache,
                                  const void* v_cache, const int* block_tables, int bt_stride,
                                  const int* cu_seqlens_q, const int* context_lens, const int* tiles,
                                  int n_tiles, void* out, int out_stride, int nh, int nkv, int hd,
                                  int block_size, float scale, const unsigned long long* tree_mask,
-                                 int tree_n, hipStream_t s) {
+                                 int tree_n, int tile_rows, hipStream_t s) {
   if (n_tiles == 0) return 0;
   if (hd != 128 && hd != 64) return -5;
   if (nh % nkv) return -2;
@@ -276,16 +283,18 @@ extern "C" int dgi_paged_prefill(const void* q, int q_stride, const void* k_cach
   while ((1 << bs_log2) < block_size) ++bs_log2;
   if ((1 << bs_log2) != block_size) return -4;
   const float scale_log2 = scale * 1.4426950408889634f;
-  if (hd == 128)
-    prefill_attn_kernel<128><<<dim3(n_tiles, nh), 256, 0, s>>>(
-        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables,
-        bt_stride, cu_seqlens_q, context_lens, tiles, (uint16_t*)out, out_stride, nh, nkv, bs_log2,
-        scale_log2, tree_mask, tree_n);
-  else
-    prefill_attn_kernel<64><<<dim3(n_tiles, nh), 256, 0, s>>>(
-        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables,
-        bt_stride, cu_seqlens_q, context_lens, tiles, (uint16_t*)out, out_stride, nh, nkv, bs_log2,
-        scale_log2, tree_mask, tree_n);
+  if (tile_rows != 128 && tile_rows != 256) return -7;
+#define DGI_PREFILL(HDV, NWV)                                                                          \
+  prefill_attn_kernel<HDV, NWV><<<dim3(n_tiles, nh), NWV * 64, 0, s>>>(                                \
+      (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables,     \
+      bt_stride, cu_seqlens_q, context_lens, tiles, (uint16_t*)out, out_stride, nh, nkv, bs_log2,         \
+      scale_log2, tree_mask, tree_n)
+  if (hd == 128) {
+    if (tile_rows == 256) DGI_PREFILL(128, 8); else DGI_PREFILL(128, 4);
+  } else {
+    if (tile_rows == 256) DGI_PREFILL(64, 8); else DGI_PREFILL(64, 4);
+  }
+#undef DGI_PREFILL
   DGI_CHECK_LAUNCH();
   return 0;
 }

@@ -306,7 +306,14 @@ def paged_prefill_ref(q, k_cache, v_cache, block_tables, cu_seqlens_q, context_l
     return out
 
 
-def prefill_tiles(cu_seqlens_q: list[int], tile: int = 128) -> list[tuple[int, int]]:
+# query rows per prefill-attention workgroup: 128 (4 waves) or 256 (8 waves sharing
+# each staged K/V tile).  Every producer of ``tiles`` (model runner, EAGLE verify /
+# draft metadata, ops.paged_prefill) cuts sequences at this size.
+PREFILL_TILE = int(os.environ.get("DGI_PREFILL_TILE", "128"))
+
+
+def prefill_tiles(cu_seqlens_q: list[int], tile: int = 0) -> list[tuple[int, int]]:
+    tile = tile or PREFILL_TILE
     tiles = []
     for b in range(len(cu_seqlens_q) - 1):
         ql = cu_seqlens_q[b + 1] - cu_seqlens_q[b]
@@ -329,7 +336,7 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens,
             tl = prefill_tiles(cu_seqlens_q.tolist())
             tiles = torch.tensor(tl if tl else [[0, 0]], dtype=torch.int32, device=q.device)[: len(tl)]
         _call("paged_prefill", out, q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens,
-                                    tiles, nh, nkv, scale, tree_mask, tree_n)
+              tiles, nh, nkv, scale, tree_mask, tree_n, PREFILL_TILE)
         return out
     r = paged_prefill_ref(q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens, nh, nkv, scale,
                           tree_mask, tree_n)

@@ -131,7 +131,7 @@ class ModelRunner:
             row += c.length
         tiles = []
         for j in range(nb):
-            for t0 in range(0, int(cu[j + 1] - cu[j]), 128):
+            for t0 in range(0, int(cu[j + 1] - cu[j]), ops.PREFILL_TILE):
                 tiles.append((j, t0))
         tiles_np = np.asarray(tiles, np.int32).reshape(-1, 2)
         nlog = len(logit_rows)

@@ -224,7 +224,7 @@ def _varlen_meta(runner, positions, slots, block_rows, cu, ctx, device, tree_mas
     bt = np.zeros((nb, maxw), np.int32)
     for i, blk in enumerate(block_rows):
         bt[i, : len(blk)] = blk
-    tiles = [(j, t0) for j in range(nb) for t0 in range(0, int(cu[j + 1] - cu[j]), 128)]
+    tiles = [(j, t0) for j in range(nb) for t0 in range(0, int(cu[j + 1] - cu[j]), ops.PREFILL_TILE)]
     tiles_np = np.asarray(tiles, np.int32).reshape(-1, 2)
     parts = [np.asarray(positions, np.int32), np.asarray(slots, np.int32), bt.ravel(), np.asarray(cu, np.int32),
              np.asarray(ctx, np.int32), tiles_np.ravel()]
