@@ -652,6 +652,8 @@ class SpecEngine(LLMEngine):
         """Auto-off: compare this speculation period's measured cost per generated
         token with plain decoding's at the same batch bucket.  Two clean samples
         decide; a first period without a plain reference probes 3 plain steps.
+        Slower than plain: first step the tree one level shallower (adaptive
+        depth), and only at depth 1 fall back to plain decoding.
         Probes that keep losing back off exponentially (probe_every x 1, 2, 4, 8
         plain steps), a winning probe resets the interval."""
         if not self.spec.auto_off or R == 0:
@@ -664,6 +666,12 @@ class SpecEngine(LLMEngine):
                 return               # fewer than 2 clean samples (graph-capture steps are not samples)
             if cp is None:
                 self.spec_on, self._mode_steps, self._probe = False, 0, True
+            elif secs / toks > cp and self.spec.adaptive_depth and self.cur_depth > 1:
+                # slower than plain at this depth: a shallower tree costs less per step and
+                # wastes fewer rejected nodes — try it before giving up on speculation
+                self.cur_depth -= 1
+                self._acc_ema, self._acc_n = None, 0
+                self.spec_stats["depth_changes"] += 1
             elif secs / toks > cp:
                 self.spec_on, self._mode_steps, self._probe = False, 0, False
                 self.spec_stats["switches_off"] += 1

@@ -171,6 +171,15 @@ def test_controller_ignores_single_outliers_and_capture_steps():
     assert se.spec_on                     # one sample does not decide
     se._record("spec", 4, 0.030, 4)
     se._control(4)
+    # slower than plain at depth 3: a shallower tree is tried first
+    assert se.spec_on and se.cur_depth == 2 and se.spec_stats["switches_off"] == 0
+    for _ in range(2):
+        se._record("spec", 4, 0.030, 4)
+        se._control(4)
+    assert se.spec_on and se.cur_depth == 1
+    for _ in range(2):
+        se._record("spec", 4, 0.030, 4)
+        se._control(4)
     assert not se.spec_on and se.spec_stats["switches_off"] == 1
     # losing re-probes back off: 48, then 96 plain steps
     for wait in (48, 96):
