@@ -72,6 +72,8 @@ class SpecConfig:
     raise_accept_rate: float = 0.7    # grow above it (reference _adapt_depth)
     auto_off: bool = True             # fall back to plain decode while speculation is slower
     probe_every: int = 48             # plain steps between speculation re-probes
+    min_gain: float = 0.07            # speculation stays on only if >= 7 % cheaper per token than plain
+                                      # (its per-step host work and async tail are partly outside the timer)
 
     @property
     def num_nodes(self) -> int:
@@ -666,13 +668,13 @@ class SpecEngine(LLMEngine):
                 return               # fewer than 2 clean samples (graph-capture steps are not samples)
             if cp is None:
                 self.spec_on, self._mode_steps, self._probe = False, 0, True
-            elif secs / toks > cp and self.spec.adaptive_depth and self.cur_depth > 1:
+            elif secs / toks > cp * (1.0 - self.spec.min_gain) and self.spec.adaptive_depth and self.cur_depth > 1:
                 # slower than plain at this depth: a shallower tree costs less per step and
                 # wastes fewer rejected nodes — try it before giving up on speculation
                 self.cur_depth -= 1
                 self._acc_ema, self._acc_n = None, 0
                 self.spec_stats["depth_changes"] += 1
-            elif secs / toks > cp:
+            elif secs / toks > cp * (1.0 - self.spec.min_gain):
                 self.spec_on, self._mode_steps, self._probe = False, 0, False
                 self.spec_stats["switches_off"] += 1
                 if self._probed:

@@ -109,7 +109,7 @@ class NativeLLMEngine(LLMBaseEngine):
             from dgi.spec.eagle3 import SpecConfig, SpecEngine
             sc = spec if isinstance(spec, dict) else {}
             keys = ("depth", "width", "topk", "adaptive_depth", "min_accept_rate", "raise_accept_rate",
-                    "auto_off", "probe_every")
+                    "auto_off", "probe_every", "min_gain")
             self.engine = SpecEngine(ecfg, SpecConfig(**{k: sc[k] for k in keys if k in sc}),
                                      model_cfg=mc)
             if sc.get("draft_path"):
