@@ -705,21 +705,21 @@ class SpecEngine(LLMEngine):
             for r in spec_reqs:
                 r.busy = False
         if not sb.empty:
-            tn = time.perf_counter()
             o = self._normal_step(sb)
             outs += o
             if not sb.prefill and not spec_reqs:
-                self._record("plain", len(sb.decode), time.perf_counter() - tn, len(o))
+                # cost samples are whole steps (scheduling and host work included) in both
+                # modes, so neither mode's per-step overhead falls outside its timer
+                self._record("plain", len(sb.decode), time.perf_counter() - t0, len(o))
                 self.spec_stats["plain_steps"] += 1
                 self._control(len(sb.decode))
         live = [r for r in spec_reqs if r in self.scheduler.running and self._eligible(r)]
         if live:
-            ts = time.perf_counter()
             self._captured = False
             o = self._spec_step(live)
             outs += o
             if sb.empty and not self._captured:
-                self._record("spec", len(live), time.perf_counter() - ts, len(o))
+                self._record("spec", len(live), time.perf_counter() - t0, len(o))
             self._control(len(live))
         self.stats["step_time"] += time.perf_counter() - t0
         return outs
@@ -988,7 +988,10 @@ class SpecEngine(LLMEngine):
         s = self.spec_stats
         rows = max(1, s["spec_rows"])
         return {"mean_accepted": s["accepted"] / rows, "tokens_per_step": s["spec_tokens"] / rows,
-                "current_depth": self.cur_depth, "spec_on": self.spec_on, **s}
+                "current_depth": self.cur_depth, "spec_on": self.spec_on,
+                # the controller's per-bucket cost estimates (ms per generated token)
+                "cost_ms_per_token": {f"{m}@{b}": round(v * 1000, 4) for (m, b), v in sorted(self._cost.items())},
+                **s}
 
 
 # ---------------------------------------------------------------------------

@@ -166,7 +166,8 @@ def main():
                                    "mean_accepted": round(ao["mean_accepted"], 3),
                                    "identical": o_out == ref,
                                    "spec_steps": ao["spec_steps"], "plain_steps": ao["plain_steps"],
-                                   "depth": ao["current_depth"]}
+                                   "depth": ao["current_depth"], "costs": ao["cost_ms_per_token"],
+                                   "plain_ms_per_token": round(1000 * t_base / toks, 4)}
         print(json.dumps(row), flush=True)
         rows.append(row)
     res = {"model": a.model, "tree": {"depth": a.depth, "width": a.width, "topk": a.topk}, "target": a.target,
