@@ -521,7 +521,12 @@ class SpecEngine(LLMEngine):
         self.spec_on = True
         self._mode_steps = 0
         self._probe = False
-        self._cost: dict = {}       # (mode, bucket) -> EMA seconds per generated token
+        self._cost: dict = {}       # (mode, bucket) -> seconds per generated token (spec: EMA, plain: recent min)
+        self._plain_win: dict = {}  # (plain, bucket) -> last 16 plain cost samples
+        # step-time accounting by mode (seconds, steps): plain steps right after a speculative
+        # step vs after a plain one, and speculative steps
+        self.step_times = {"after_spec": [0.0, 0], "after_plain": [0.0, 0], "spec": [0.0, 0]}
+        self._last_mode = None
         self._acc_ema: Optional[float] = None   # smoothed acceptance rate driving depth changes
         self._acc_n = 0                          # steps behind it (at the current depth)
         self._period = [0.0, 0, 0]               # clean spec samples this period: seconds, tokens, steps
@@ -582,6 +587,8 @@ class SpecEngine(LLMEngine):
         self._mode_steps, self._probe, self._probed, self._backoff = 0, False, False, 1
         self._period = [0.0, 0, 0]
         self._cost = {k: v for k, v in self._cost.items() if keep_plain_costs and k[0] == "plain"}
+        if not keep_plain_costs:
+            self._plain_win = {}
         self._acc_ema, self._acc_n = None, 0
 
     # ------------------------------------------------------------------ helpers
@@ -621,8 +628,17 @@ class SpecEngine(LLMEngine):
             return
         key = (mode, self._bucket(R))
         c = seconds / tokens
-        old = self._cost.get(key)
-        self._cost[key] = c if old is None else 0.7 * old + 0.3 * c
+        if mode == "plain":
+            # plain decode cost at a bucket is a hardware property: keep the fastest of the
+            # recent samples (a one-off stall — a lazily captured graph, a pipeline tail — must
+            # not make speculation look cheaper than it is)
+            win = self._plain_win.setdefault(key, [])
+            win.append(c)
+            del win[:-16]
+            self._cost[key] = min(win)
+        else:
+            old = self._cost.get(key)
+            self._cost[key] = c if old is None else 0.7 * old + 0.3 * c
         if mode == "spec":           # this speculation period's own cost (acceptance changes between probes)
             self._period[0] += seconds
             self._period[1] += tokens
@@ -710,7 +726,12 @@ class SpecEngine(LLMEngine):
             if not sb.prefill and not spec_reqs:
                 # cost samples are whole steps (scheduling and host work included) in both
                 # modes, so neither mode's per-step overhead falls outside its timer
-                self._record("plain", len(sb.decode), time.perf_counter() - t0, len(o))
+                dt = time.perf_counter() - t0
+                self._record("plain", len(sb.decode), dt, len(o))
+                k = "after_spec" if self._last_mode == "spec" else "after_plain"
+                self.step_times[k][0] += dt
+                self.step_times[k][1] += 1
+                self._last_mode = "plain"
                 self.spec_stats["plain_steps"] += 1
                 self._control(len(sb.decode))
         live = [r for r in spec_reqs if r in self.scheduler.running and self._eligible(r)]
@@ -719,7 +740,11 @@ class SpecEngine(LLMEngine):
             o = self._spec_step(live)
             outs += o
             if sb.empty and not self._captured:
-                self._record("spec", len(live), time.perf_counter() - t0, len(o))
+                dt = time.perf_counter() - t0
+                self._record("spec", len(live), dt, len(o))
+                self.step_times["spec"][0] += dt
+                self.step_times["spec"][1] += 1
+            self._last_mode = "spec"
             self._control(len(live))
         self.stats["step_time"] += time.perf_counter() - t0
         return outs

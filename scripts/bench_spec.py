@@ -151,6 +151,7 @@ def main():
                 for r, o in zip(rs, ref):
                     reqs_rid[r.rid] = o
                 spec.reset_controller(keep_plain_costs=True)     # plain cost per bucket is learned once per engine
+                spec.step_times = {k: [0.0, 0] for k in spec.step_times}
                 spec.spec_stats.update(spec_steps=0, spec_rows=0, accepted=0, spec_tokens=0, draft_s=0.0,
                                        verify_s=0.0, plain_steps=0, switches_off=0, depth_changes=0)
                 torch.cuda.synchronize()
@@ -167,7 +168,9 @@ def main():
                                    "identical": o_out == ref,
                                    "spec_steps": ao["spec_steps"], "plain_steps": ao["plain_steps"],
                                    "depth": ao["current_depth"], "costs": ao["cost_ms_per_token"],
-                                   "plain_ms_per_token": round(1000 * t_base / toks, 4)}
+                                   "plain_ms_per_token": round(1000 * t_base / toks, 4),
+                                   "step_ms": {k: round(1000 * v[0] / max(1, v[1]), 3) for k, v in spec.step_times.items()},
+                                   "step_n": {k: v[1] for k, v in spec.step_times.items()}}
         print(json.dumps(row), flush=True)
         rows.append(row)
     res = {"model": a.model, "tree": {"depth": a.depth, "width": a.width, "topk": a.topk}, "target": a.target,
