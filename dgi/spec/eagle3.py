@@ -530,6 +530,7 @@ class SpecEngine(LLMEngine):
         self._acc_ema: Optional[float] = None   # smoothed acceptance rate driving depth changes
         self._acc_n = 0                          # steps behind it (at the current depth)
         self._period = [0.0, 0, 0]               # clean spec samples this period: seconds, tokens, steps
+        self._period_acc = [0, 0]                # accepted drafts, rows speculated this period
         self._backoff = 1                        # probe interval multiplier
         self._probed = False                     # the current speculation period is a re-probe
         self._captured = False      # this step captured a hipGraph (its time is not a cost sample)
@@ -586,6 +587,7 @@ class SpecEngine(LLMEngine):
         self.cur_depth, self.spec_on = self.spec.depth, True
         self._mode_steps, self._probe, self._probed, self._backoff = 0, False, False, 1
         self._period = [0.0, 0, 0]
+        self._period_acc = [0, 0]
         self._cost = {k: v for k, v in self._cost.items() if keep_plain_costs and k[0] == "plain"}
         if not keep_plain_costs:
             self._plain_win = {}
@@ -686,8 +688,10 @@ class SpecEngine(LLMEngine):
                 self.spec_on, self._mode_steps, self._probe = False, 0, True
             elif secs / toks > cp * (1.0 - self.spec.min_gain) and self.spec.adaptive_depth and self.cur_depth > 1:
                 # slower than plain at this depth: a shallower tree costs less per step and
-                # wastes fewer rejected nodes — try it before giving up on speculation
-                self.cur_depth -= 1
+                # wastes fewer rejected nodes — try it before giving up on speculation; jump
+                # straight to one level past the accepted length this period measured
+                acc_len = self._period_acc[0] / max(1, self._period_acc[1])
+                self.cur_depth = max(1, min(self.cur_depth - 1, int(math.ceil(acc_len)) + 1))
                 self._acc_ema, self._acc_n = None, 0
                 self.spec_stats["depth_changes"] += 1
             elif secs / toks > cp * (1.0 - self.spec.min_gain):
@@ -698,8 +702,10 @@ class SpecEngine(LLMEngine):
             else:
                 self._backoff = 1
                 self._period = [0.0, 0, 0]     # keep speculating; judge the next window afresh
+                self._period_acc = [0, 0]
                 return
             self._period = [0.0, 0, 0]
+            self._period_acc = [0, 0]
         else:
             wait = 3 if self._probe else self.spec.probe_every * self._backoff
             if self._mode_steps >= wait:
@@ -927,6 +933,8 @@ class SpecEngine(LLMEngine):
                     break
         self.spec_stats["spec_steps"] += 1
         self.spec_stats["spec_rows"] += R
+        self._period_acc[0] += sum(acc_h)
+        self._period_acc[1] += R
         self._adapt_depth(sum(acc_h) / (R * D))
         return outs
 

@@ -166,6 +166,7 @@ def test_controller_ignores_single_outliers_and_capture_steps():
     for _ in range(6):
         se._control(4)
     assert se.spec_on
+    se._period_acc = [8, 4]               # 2 drafts accepted per row: depth 3 is already long enough
     se._record("spec", 4, 0.030, 4)       # now measurably slower than plain
     se._control(4)
     assert se.spec_on                     # one sample does not decide
