@@ -28,6 +28,8 @@ int dgi_paged_prefill(const void* q, int q_stride, const void* k_cache, const vo
 int dgi_silu_mul(const void* gu, void* out, int T, int I, hipStream_t s);
 int dgi_skinny_gemm(const void* x, int ldx, const void* w, const void* bias, void* y, int ldy, int M,
                     int N, int K, int nw, hipStream_t s);
+int dgi_mfma_gemm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int epi,
+                  hipStream_t s);
 int dgi_fused_skinny(const void* x, int ldx, const void* res, int ldr, void* res_out, const void* gamma,
                      float eps, const void* w, const void* bias, void* y, int ldy, int M, int N, int K, int pro,
                      int epi, const int* positions, const float* cos_sin, const int* slots, void* k_cache,
@@ -203,6 +205,26 @@ void skinny_gemm(at::Tensor out, const at::Tensor& x, const at::Tensor& w,
   check_rc(dgi_skinny_gemm(x.data_ptr(), (int)x.stride(0), w.data_ptr(), b, out.data_ptr(), (int)out.stride(0),
                            (int)M, (int)N, (int)K, (int)cfg, cur_stream()),
            "skinny_gemm");
+}
+
+// LDS-tiled MFMA GEMM (prefill / mixed steps): epi 0 out = x w^T; epi 1 out = SwiGLU with w = [gate; up].
+void mfma_gemm(at::Tensor out, const at::Tensor& x, const at::Tensor& w, int64_t epi) {
+  check_bf16(out, "out"); check_bf16(x, "x"); check_bf16(w, "w");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "mfma_gemm: 2-D operands");
+  TORCH_CHECK(x.device() == w.device() && x.device() == out.device(), "mfma_gemm: operands on one device");
+  TORCH_CHECK(x.stride(1) == 1 && out.stride(1) == 1 && w.is_contiguous(), "mfma_gemm: row-major operands");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && out.size(0) == M, "mfma_gemm: shape mismatch");
+  TORCH_CHECK(epi == 0 || epi == 1, "mfma_gemm: epi 0 (store) or 1 (SwiGLU)");
+  TORCH_CHECK(out.size(1) == (epi == 1 ? N / 2 : N), "mfma_gemm: output columns");
+  TORCH_CHECK(N % 256 == 0 && K % 64 == 0 && x.stride(0) % 8 == 0 && out.stride(0) % 4 == 0,
+              "mfma_gemm: N%256, K%64, ldx%8, ldy%4");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0 &&
+              reinterpret_cast<uintptr_t>(out.data_ptr()) % 8 == 0, "mfma_gemm: operand alignment");
+  TORCH_CHECK((int64_t)M * x.stride(0) < (1LL << 31), "mfma_gemm: activation too large for 32-bit offsets");
+  check_rc(dgi_mfma_gemm(x.data_ptr(), (int)x.stride(0), w.data_ptr(), out.data_ptr(), (int)out.stride(0), (int)M,
+                         (int)N, (int)K, (int)epi, cur_stream()),
+           "mfma_gemm");
 }
 
 // Decode GEMM with fused RMSNorm prologue (pro 1: norm, 2: residual add + norm -> res_out) and
@@ -425,6 +447,7 @@ TORCH_LIBRARY(dgi, m) {
         "Tensor? tree_mask, int tree_n, int tile_rows=128) -> ()");
   m.def("silu_mul(Tensor(a!) out, Tensor gu) -> ()");
   m.def("skinny_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor? bias, int cfg=0) -> ()");
+  m.def("mfma_gemm(Tensor(a!) out, Tensor x, Tensor w, int epi=0) -> ()");
   m.def("fused_skinny(Tensor(a!) y, Tensor x, Tensor? res, Tensor(b!)? res_out, Tensor? gamma, float eps, "
         "Tensor w, Tensor? bias, int pro, int epi, Tensor? positions, Tensor? cos_sin, Tensor? slots, "
         "Tensor(c!)? k_cache, Tensor(d!)? v_cache, int nh=0, int nkv=0, int cfg=0) -> ()");
@@ -449,6 +472,7 @@ TORCH_LIBRARY_IMPL(dgi, CUDA, m) {
   m.impl("paged_prefill", &paged_prefill);
   m.impl("silu_mul", &silu_mul);
   m.impl("skinny_gemm", &skinny_gemm);
+  m.impl("mfma_gemm", &mfma_gemm);
   m.impl("fused_skinny", &fused_skinny);
   m.impl("sample", &sample);
   m.impl("topk", &topk);

@@ -1,0 +1,219 @@
+// dgi/csrc/mfma_gemm.hip — LDS-tiled MFMA GEMM for prefill / mixed-step projections
+// (SURVEY K3/K8/K11), with an optional fused SwiGLU epilogue.
+//
+//   epi 0:  Y[M, N]  = X[M, K] · W[N, K]^T
+//   epi 1:  Y[M, I]  = silu(X · Wg^T) * (X · Wu^T)   with W = [Wg; Wu] (2I x K, the
+//           layout of the model's fused gate_up weight)
+//
+// bf16 in/out, fp32 accumulate.  Written for gfx950 (CDNA4), one 512-thread
+// workgroup (8 waves) per CU:
+//
+//  * 256 x 256 output tile, K step 64, two LDS stages of X and W tiles
+//    (2 x 64 KB): the whole 160 KB LDS budget goes to one deep tile, so every
+//    staged byte feeds 256 MFMA columns;
+//  * global -> LDS by `global_load_lds_dwordx4` (16 B per lane, no VGPR
+//    round trip).  The LDS image is lane-linear (128-byte rows of 64 k), so
+//    the bank-conflict swizzle is applied to the per-lane SOURCE address:
+//    16-byte chunk c of row r holds logical k-chunk c ^ ((r >> 1) & 7), which
+//    makes every 16-lane ds_read_b128 group of a fragment read hit 16
+//    distinct bank slots;
+//  * wave tile 128 (M) x 64 (N): 8 x 4 accumulators of
+//    v_mfma_f32_16x16x32_bf16 with W as the A operand and X as the B
+//    operand, so each lane ends up with 4 consecutive output COLUMNS of one
+//    row (8-byte stores) — and, for SwiGLU, with the gate and up values of
+//    the same column in the same lane and register;
+//  * one barrier per K step (behind an explicit vmcnt(0): hipcc does not wait
+//    for global_load_lds before a barrier on its own): fragments of k-half 1 are read while the
+//    MFMAs of k-half 0 run, the barrier retires the next stage's loads and
+//    everyone's reads of the current stage, then the stage after next is
+//    issued into the stage just consumed while k-half 1's MFMAs run;
+//  * XCD-aware tile order: blocks that share an XCD (b % 8) take a
+//    contiguous run of tiles, M-fastest, so the 8 row tiles that reuse one
+//    W tile run side by side on one L2.
+//
+// Requirements (checked by the host): N % 256 == 0 (epi 1: I % 128 == 0),
+// K % 64 == 0, ldx % 8 == 0, ldy % 4 == 0.  Any M: rows past M are clamped
+// on load and skipped on store.
+#include "common.h"
+
+using namespace dgi;
+
+namespace {
+
+constexpr int kBM = 256;
+constexpr int kBK = 64;
+constexpr int kTileBytes = kBM * kBK * 2;      // 32 KB: one operand, one stage
+constexpr int kStageBytes = 2 * kTileBytes;    // X tile + W tile
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef const __attribute__((address_space(1))) void gbl_void_t;
+
+__device__ __forceinline__ void glds16(const uint16_t* src, char* lds) {
+  __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds, 16, 0, 0);
+}
+
+__device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
+
+template <int EPI>
+__global__ __launch_bounds__(512) void mfma_gemm_kernel(const uint16_t* __restrict__ X, int ldx,
+                                                         const uint16_t* __restrict__ W,
+                                                         uint16_t* __restrict__ Y, int ldy, int M, int I, int K,
+                                                         int tiles_m, int tiles_total) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * kStageBytes];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int wm = w >> 2, wn = w & 3;
+
+  // XCD-aware, bijective block -> tile map (blocks b and b + 8 share an XCD)
+  const int b = blockIdx.x;
+  const int xcd = b & 7, li = b >> 3;
+  const int q8 = tiles_total >> 3, r8 = tiles_total & 7;
+  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + li;
+  const int tm = t % tiles_m, tn = t / tiles_m;
+  const int m0 = tm * kBM;
+
+  // ---- staging map: lane-linear LDS image, swizzled global source
+  const int q = tid >> 3;                         // row within each 64-row slab
+  const int lc = (tid & 7) ^ ((tid >> 4) & 7);    // logical k-chunk this lane fetches
+  int xoff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = min(m0 + i * 64 + q, M - 1);
+    xoff[i] = r * ldx + lc * 8;
+  }
+  // W rows: epi 0 -> n0 + 64 i + q; epi 1 -> slab i = wave column i: 32 gate rows then the
+  // matching 32 up rows, so accumulator columns 0-1 (gate) pair with 2-3 (up) in one wave
+  int wrow0, wstep;
+  if (EPI == 1) {
+    wrow0 = tn * 128 + (q < 32 ? q : I + q - 32);
+    wstep = 32;
+  } else {
+    wrow0 = tn * 256 + q;
+    wstep = 64;
+  }
+  const uint16_t* wsrc = W + (size_t)wrow0 * K + lc * 8;
+  const size_t wslab = (size_t)wstep * K;
+  char* const lds_x = smem + w * 1024;               // + stage * kStageBytes + i * 8 KB
+  char* const lds_w = smem + kTileBytes + w * 1024;
+
+  auto issue = [&](int kt, int stage) {
+    const int k0 = kt * kBK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16(X + xoff[i] + k0, lds_x + stage * kStageBytes + i * 8192);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16(wsrc + i * wslab + k0, lds_w + stage * kStageBytes + i * 8192);
+  };
+
+  // ---- fragment read map (bytes inside one operand tile)
+  const int r16 = lane & 15;
+  const int sw = (lane >> 1) & 7;
+  const int ph0 = ((lane >> 4) ^ sw) * 16;           // k-half 0: chunks 0-3
+  const int ph1 = ((4 + (lane >> 4)) ^ sw) * 16;     // k-half 1: chunks 4-7
+  const int xbase = (wm * 128 + r16) * 128;
+  const int wbase = kTileBytes + (wn * 64 + r16) * 128;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 xa[8], wa[4], xb[8], wb[4];
+  auto read = [&](int stage, int ph, bf16x8* xf, bf16x8* wf) {
+    const char* s = smem + stage * kStageBytes;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wf[j] = *(const bf16x8*)(s + wbase + j * 2048 + ph);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) xf[i] = *(const bf16x8*)(s + xbase + i * 2048 + ph);
+  };
+  auto mma = [&](const bf16x8* xf, const bf16x8* wf) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+  };
+
+  const int nt = K / kBK;
+  issue(0, 0);
+  if (nt > 1) issue(1, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  read(0, ph0, xa, wa);
+  for (int kt = 0; kt < nt; ++kt) {
+    const int st = kt & 1;
+    read(st, ph1, xb, wb);
+    __builtin_amdgcn_s_setprio(1);
+    mma(xa, wa);
+    __builtin_amdgcn_s_setprio(0);
+    // next stage landed: hipcc does not count global_load_lds as an LDS write
+    // before a barrier, so the wave's own loads are retired explicitly
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();        // every wave's loads landed; every wave done reading this stage
+    if (kt + 2 < nt) issue(kt + 2, st);
+    if (kt + 1 < nt) read(st ^ 1, ph0, xa, wa);
+    __builtin_amdgcn_s_setprio(1);
+    mma(xb, wb);
+    __builtin_amdgcn_s_setprio(0);
+  }
+
+  // ---- epilogue: lane holds rows m = .. + (lane & 15), columns 4 (lane >> 4) + 0..3 of each 16x16 tile
+  const int c4 = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + r16;
+    if (m >= M) continue;
+    uint16_t* yrow = Y + (size_t)m * ldy;
+    if (EPI == 1) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const f32x4 g = acc[i][j], u = acc[i][j + 2];
+        const int n = tn * 128 + wn * 32 + j * 16 + c4;
+        uint2 v;
+        v.x = pack_bf16x2(silu(g[0]) * u[0], silu(g[1]) * u[1]);
+        v.y = pack_bf16x2(silu(g[2]) * u[2], silu(g[3]) * u[3]);
+        *(uint2*)(yrow + n) = v;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 a = acc[i][j];
+        const int n = tn * 256 + wn * 64 + j * 16 + c4;
+        uint2 v;
+        v.x = pack_bf16x2(a[0], a[1]);
+        v.y = pack_bf16x2(a[2], a[3]);
+        *(uint2*)(yrow + n) = v;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// epi 0: Y[M, N] = X W^T with N = rows of W; epi 1: Y[M, I] = SwiGLU with W = [gate; up] (2I rows).
+extern "C" int dgi_mfma_gemm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K,
+                             int epi, hipStream_t s) {
+  if (M <= 0) return 0;
+  if (K % kBK || ldx % 8 || ldy % 4) return -3;
+  int I = 0, tiles_n;
+  if (epi == 1) {
+    if (N % 256) return -3;
+    I = N / 2;
+    tiles_n = I / 128;
+  } else if (epi == 0) {
+    if (N % 256) return -3;
+    tiles_n = N / 256;
+  } else {
+    return -4;
+  }
+  const int tiles_m = (M + kBM - 1) / kBM;
+  const int total = tiles_m * tiles_n;
+  if (epi == 1)
+    mfma_gemm_kernel<1><<<dim3(total), 512, 0, s>>>((const uint16_t*)x, ldx, (const uint16_t*)w, (uint16_t*)y,
+                                                    ldy, M, I, K, tiles_m, total);
+  else
+    mfma_gemm_kernel<0><<<dim3(total), 512, 0, s>>>((const uint16_t*)x, ldx, (const uint16_t*)w, (uint16_t*)y,
+                                                    ldy, M, I, K, tiles_m, total);
+  DGI_CHECK_LAUNCH();
+  return 0;
+}

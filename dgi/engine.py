@@ -39,7 +39,8 @@ class EngineConfig:
     workspace_bytes: int = 8 << 30
     layer_start: int = 0
     layer_end: Optional[int] = None
-    host_kv_gb: float = 0.0            # pinned host KV tier for evicted prefix pages (0 = off)
+    host_kv_gb: float = 0.0            # pinned host KV tier: evicted prefix pages + swapped-out
+                                       # preempted sequences (0 = off, < 0 = auto-size: ``auto_host_kv_gb``)
     graph_buckets: Optional[tuple] = None   # decode batch sizes captured as hipGraphs (None = defaults)
     model_path: Optional[str] = None   # HF safetensors checkpoint dir (None: ``model`` if it is one, else random init)
 
@@ -75,6 +76,22 @@ def engine_block_budget(cfg: EngineConfig, mc: ModelConfig, n_local: int, device
     return max(2, min(nblocks, cap))
 
 
+def auto_host_kv_gb(pool: BlockPool, device: torch.device, pool_share: float = 0.5,
+                    ram_share: float = 0.25) -> float:
+    """Size of the pinned host KV tier when ``host_kv_gb < 0``: half the HBM KV
+    pool (on a 288 GB MI355X serving 70B that is ~55 GB per GPU, enough to hold
+    every sequence preempted in a burst), capped by this GPU's share of a quarter
+    of the host's available RAM (pinned pages cannot be swapped by the OS)."""
+    try:
+        import psutil
+        avail = psutil.virtual_memory().available
+    except Exception:   # pragma: no cover - psutil is optional
+        avail = 16 << 30
+    gpus = max(1, torch.cuda.device_count()) if device.type == "cuda" else 1
+    want = pool.page_bytes() * pool.num_blocks * pool_share
+    return min(want, avail * ram_share / gpus) / (1 << 30)
+
+
 class LLMEngine:
     def __init__(self, cfg: EngineConfig, model_cfg: Optional[ModelConfig] = None, model=None):
         self.cfg = cfg
@@ -103,12 +120,17 @@ class LLMEngine:
         self.scheduler = Scheduler(self.pool, SchedulerConfig(cfg.max_num_seqs, cfg.max_num_batched_tokens,
                                                               cfg.max_model_len, cfg.enable_prefix_caching))
         self.host_tier = None
-        if cfg.host_kv_gb > 0 and cfg.enable_prefix_caching:
+        host_gb = cfg.host_kv_gb
+        if host_gb < 0:      # auto: GPU engines only (CPU rehearsals have no HBM to relieve)
+            host_gb = auto_host_kv_gb(self.pool, self.device) if self.device.type == "cuda" else 0.0
+        if host_gb > 0:
             from dgi.kv.host_tier import HostKVTier
             from dgi.kv.radix_cache import RadixCache
-            cap = max(1, int(cfg.host_kv_gb * (1 << 30) // self.pool.page_bytes()))
+            cap = max(1, int(host_gb * (1 << 30) // self.pool.page_bytes()))
             self.host_tier = HostKVTier(self.pool, cap)
-            self.scheduler.radix = RadixCache(self.pool, self.host_tier)
+            self.scheduler.host_tier = self.host_tier
+            if cfg.enable_prefix_caching:
+                self.scheduler.radix = RadixCache(self.pool, self.host_tier)
         rkw = {"graph_buckets": tuple(cfg.graph_buckets)} if cfg.graph_buckets else {}
         self.runner = ModelRunner(self.model, self.pool, cfg.max_num_seqs, cfg.max_model_len,
                                   cfg.max_num_batched_tokens, cfg.use_graphs, **rkw)

@@ -475,6 +475,42 @@ def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tens
     return r
 
 
+def mfma_gemm_ref(x: torch.Tensor, w: torch.Tensor, epi: int = 0) -> torch.Tensor:
+    """fp32 reference of ``mfma_gemm``: x @ w.T, or SwiGLU over w = [gate; up]."""
+    y = x.float() @ w.float().t()
+    if epi == 1:
+        I = w.shape[0] // 2
+        y = torch.nn.functional.silu(y[:, :I]) * y[:, I:]
+    return y.to(x.dtype)
+
+
+def mfma_gemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    """Shapes/layouts the LDS-tiled MFMA GEMM kernel takes (dgi/csrc/mfma_gemm.hip)."""
+    return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 2
+            and x.stride(1) == 1 and x.stride(0) % 8 == 0 and w.is_contiguous() and w.shape[0] % 256 == 0
+            and x.shape[1] % 64 == 0 and x.data_ptr() % 16 == 0 and x.shape[0] * x.stride(0) < (1 << 31))
+
+
+def mfma_gemm(x: torch.Tensor, w: torch.Tensor, epi: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Hand-written LDS-tiled MFMA GEMM (256x256 tiles, global_load_lds
+    staging, XCD-aware tile order): ``epi`` 0 -> x @ w.T; 1 -> the fused
+    SwiGLU of the MLP, silu(x @ gate.T) * (x @ up.T) with w = [gate; up],
+    written once (no [M, 2I] intermediate and no separate silu_mul pass)."""
+    M = x.shape[0]
+    N = w.shape[0] // 2 if epi == 1 else w.shape[0]
+    if mfma_gemm_ok(x, w):
+        load_native(required=True)
+        if out is None:
+            out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+        _call("mfma_gemm", out, x, w, epi)
+        return out
+    r = mfma_gemm_ref(x, w, epi)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
 # ----------------------------------------------------------------------------
 # Sampling
 # ----------------------------------------------------------------------------

@@ -23,6 +23,35 @@ import torch
 import torch.distributed as dist
 
 
+def shared_gpu() -> bool:
+    """``DGI_SHARED_GPU=1``: several ranks share one GPU and still talk RCCL.
+
+    RCCL refuses two ranks on one device of one host ("Duplicate GPU
+    detected"); giving every rank its own ``NCCL_HOSTID`` makes each look like
+    a separate host, so the data plane runs RCCL's network transport over
+    loopback.  Slow, but every send/recv is a real RCCL kernel on a real
+    stream with RCCL's blocking semantics (a send waits for its matching
+    receive), which a gloo rehearsal cannot show: the rehearsal for the
+    8-GPU layouts on a one-GPU box."""
+    return os.environ.get("DGI_SHARED_GPU", "0") == "1"
+
+
+def local_device_index() -> int:
+    lr = int(os.environ.get("LOCAL_RANK", 0))
+    if shared_gpu():
+        return lr % max(1, torch.cuda.device_count())
+    return lr
+
+
+def prepare_rccl_env() -> None:
+    """Environment RCCL must see before its first communicator (call before
+    ``init_process_group('nccl')``)."""
+    if shared_gpu():
+        os.environ["NCCL_HOSTID"] = f"dgi-shared-rank{os.environ.get('RANK', '0')}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
+
+
 class Fabric:
     def __init__(self, backend: Optional[str] = None, device: Optional[torch.device] = None,
                  timeout_s: float = 1800.0):
@@ -32,7 +61,8 @@ class Fabric:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29511")
             if be == "nccl":
-                torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", 0)))
+                prepare_rccl_env()
+                torch.cuda.set_device(local_device_index())
             dist.init_process_group(be, timeout=datetime.timedelta(seconds=timeout_s))
             self.owns_pg = True
         self.rank = dist.get_rank()

@@ -8,8 +8,11 @@ step:
 
 1. every running sequence in the decode phase gets one token (a new KV page
    when it crosses a block boundary); if the pool is exhausted the most
-   recently admitted sequence is preempted (pages released, recomputed
-   later: its prefix is usually still in the radix cache);
+   recently admitted sequence is preempted.  With a pinned host KV tier
+   (``dgi.kv.host_tier``) its pages are swapped out (``kv_gather`` + async
+   DMA) and copied back when it is re-admitted, so no prefill is recomputed;
+   without one (or with the tier full) its pages are released and recomputed
+   later, usually from the radix cache;
 2. the remaining token budget (``max_num_batched_tokens``) is filled with
    prefill chunks — first unfinished chunks of running sequences, then new
    requests in FCFS/priority order, each admission starting from its longest
@@ -106,6 +109,9 @@ class Scheduler:
         self.running = RunningSet()
         self.radix: Optional[RadixCache] = RadixCache(pool) if cfg.enable_prefix_caching else None
         self.num_preemptions = 0
+        self.host_tier = None          # HostKVTier: swap preempted sequences out instead of recomputing
+        self.num_swapped_out = 0
+        self.num_swapped_in = 0
 
     # ------------------------------------------------------------------ queue
     def add(self, req: Request) -> None:
@@ -122,6 +128,9 @@ class Scheduler:
             for r in q:
                 if r.rid == rid:
                     q.remove(r)
+                    if r.swapped is not None:
+                        self.host_tier.release(r.swapped[0])
+                        r.swapped = None
                     self._release(r, cache=False)
                     r.status = Status.FINISHED
                     r.finish_reason = "abort"
@@ -149,14 +158,45 @@ class Scheduler:
 
     def _preempt(self, victim: Request) -> None:
         self.running.remove(victim)
-        self._release(victim, cache=True)
-        victim.num_computed = 0
+        n = victim.num_computed
+        nb = (n + self.bs - 1) // self.bs
+        tier = self.host_tier
+        if tier is not None and n > 0 and nb <= len(victim.blocks) and nb <= tier.num_free:
+            # swap out: the computed pages go to pinned host memory, nothing is recomputed
+            victim.swapped = (tier.spill(victim.blocks[:nb]), n)
+            self._release(victim, cache=False)
+            self.num_swapped_out += 1
+        else:
+            self._release(victim, cache=True)
+            victim.num_computed = 0
+            victim.prefill_target = victim.total_len
         victim.num_cached = 0
-        victim.prefill_target = victim.total_len
         victim.status = Status.WAITING
         victim.preempted += 1
         self.num_preemptions += 1
         self.waiting.appendleft(victim)
+
+    def _swap_in(self, req: Request) -> bool:
+        """Re-admit a swapped-out sequence: fresh pages, KV copied back from the
+        host tier (ordered on the compute stream before the next forward)."""
+        slots, n = req.swapped
+        nb = len(slots)
+        if nb > self.pool.num_free and not self.pool.can_allocate(nb):
+            return False
+        try:
+            blocks = self.pool.allocate(nb)
+        except OutOfBlocks:
+            return False
+        self.host_tier.restore(slots, blocks)
+        self.host_tier.release(slots)
+        req.swapped = None
+        req.blocks = blocks
+        req.radix_path = []
+        req.num_computed = n
+        req.status = Status.RUNNING
+        self.running.append(req)
+        self.num_swapped_in += 1
+        return True
 
     # ------------------------------------------------------------------ schedule
     def add_prefilled(self, req: Request, blocks: list[int]) -> None:
@@ -219,6 +259,12 @@ class Scheduler:
             n_seqs += 1
         while self.waiting and budget > 0 and len(self.running) < self.cfg.max_num_seqs and n_seqs < seq_cap:
             req = self.waiting[0]
+            if req.swapped is not None:
+                # back in the next step's batch (decode row or its remaining prefill chunk)
+                if not self._swap_in(req):
+                    break
+                self.waiting.popleft()
+                continue
             toks = req.all_tokens()
             target = req.prefill_target
             cached_blocks: list[int] = []
@@ -268,5 +314,7 @@ class Scheduler:
             "free_blocks": self.pool.num_free,
             "used_blocks": self.pool.num_used,
             "preemptions": self.num_preemptions,
+            "swapped_out": self.num_swapped_out,
+            "swapped_in": self.num_swapped_in,
             "prefix_hit_rate": self.radix.hit_rate() if self.radix else 0.0,
         }

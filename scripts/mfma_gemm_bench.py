@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Hand-written MFMA GEMM (dgi/csrc/mfma_gemm.hip) vs hipBLASLt on the Llama-3
+layer GEMMs at prefill / mixed-step row counts.
+
+For gate_up the comparison is the whole MLP front half: hipBLASLt GEMM +
+the separate silu_mul pass vs the kernel's fused SwiGLU epilogue (epi 1).
+Variants are timed in interleaved rounds in one process on the same random
+operands (uniform [-1, 1) activations, 0.02-scaled weights), median of the
+rounds; one JSON line per (shape, M).
+
+  python scripts/mfma_gemm_bench.py [shape-prefix]      GEMM_MS=1024,2048 ...
+"""
+import json
+import os
+import statistics
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from dgi import ops  # noqa: E402
+
+SHAPES = {  # name: (N, K)
+    "70b_qkv": (10240, 8192), "70b_o": (8192, 8192), "70b_gate_up": (57344, 8192), "70b_down": (8192, 28672),
+    "8b_qkv": (6144, 4096), "8b_o": (4096, 4096), "8b_gate_up": (28672, 4096), "8b_down": (4096, 14336),
+}
+MS = [int(x) for x in os.environ.get("GEMM_MS", "512,1024,1536,1792,2048,4096").split(",")]
+ROUNDS = int(os.environ.get("GEMM_ROUNDS", "7"))
+ITERS = int(os.environ.get("GEMM_ITERS", "10"))
+
+
+def timed(fn):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(ITERS):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) * 1e3 / ITERS
+
+
+def main():
+    ops.load_native(required=True)
+    for name, (N, K) in SHAPES.items():
+        if len(sys.argv) > 1 and not name.startswith(sys.argv[1]):
+            continue
+        w = (torch.rand(N, K, device="cuda") * 2 - 1).to(torch.bfloat16) * 0.02
+        for M in MS:
+            x = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+            fused = name.endswith("gate_up")
+            if fused:
+                variants = {
+                    "hipblaslt+silu_mul": lambda: ops.silu_mul(F.linear(x, w)),
+                    "mfma_swiglu": lambda: ops.mfma_gemm(x, w, 1),
+                    "mfma+silu_mul": lambda: ops.silu_mul(ops.mfma_gemm(x, w, 0)),
+                }
+            else:
+                variants = {"hipblaslt": lambda: F.linear(x, w), "mfma": lambda: ops.mfma_gemm(x, w, 0)}
+            for f in variants.values():
+                f()
+            torch.cuda.synchronize()
+            times = {k: [] for k in variants}
+            for _ in range(ROUNDS):
+                for k, f in variants.items():
+                    times[k].append(timed(f))
+            row = {"gemm": name, "M": M, "N": N, "K": K}
+            flops = 2 * M * N * K
+            for k, v in times.items():
+                us = statistics.median(v)
+                row[k + "_us"] = round(us, 1)
+                row[k + "_TFLOPs"] = round(flops / (us * 1e-6) / 1e12, 1)
+            base = "hipblaslt+silu_mul" if fused else "hipblaslt"
+            mine = "mfma_swiglu" if fused else "mfma"
+            row["speedup"] = round(row[base + "_us"] / row[mine + "_us"], 3)
+            print(json.dumps(row), flush=True)
+            del x
+        del w
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

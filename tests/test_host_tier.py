@@ -82,3 +82,45 @@ def test_host_tier_gpu_roundtrip():
     got, path = rc.match(toks + [1])
     torch.cuda.synchronize()
     assert torch.equal(pool.kv[:, :, got], want)
+
+
+@pytest.mark.parametrize("prefix_caching", [False, True])
+def test_preemption_swaps_to_host_tier_instead_of_recomputing(prefix_caching):
+    """A pool too small for every running sequence forces preemptions: with the
+    host tier the victims' pages are swapped out and back, the outputs equal an
+    unconstrained engine's, and no prompt token is prefilled twice."""
+    base = dict(model="llama-tiny", device="cpu", max_num_seqs=6, max_num_batched_tokens=256,
+                max_model_len=256, use_graphs=False, enable_prefix_caching=prefix_caching)
+    g = torch.Generator().manual_seed(3)
+    prompts = [torch.randint(5, 500, (20 + 3 * i,), generator=g).tolist() for i in range(6)]
+    sp = SamplingParams(max_tokens=24, temperature=0.0, ignore_eos=True)
+    big = LLMEngine(EngineConfig(**base, num_blocks=256))
+    want = [r.output for r in big.generate(prompts, sp)]
+    # 6 sequences x up to 59 tokens need ~22 pages of 16; 16 pages force preemption
+    eng = LLMEngine(EngineConfig(**base, num_blocks=17, host_kv_gb=0.05), model=big.model)
+    got = [r.output for r in eng.generate(prompts, sp)]
+    st = eng.scheduler.stats()
+    assert got == want
+    assert st["preemptions"] > 0 and st["swapped_out"] == st["preemptions"] == st["swapped_in"]
+    assert eng.stats["prefill_tokens"] == sum(len(p) for p in prompts)
+    if not prefix_caching:          # (the radix cache may keep evicted prefix pages there)
+        assert eng.host_tier.num_free == eng.host_tier.capacity
+
+
+def test_preemption_without_tier_recomputes():
+    base = dict(model="llama-tiny", device="cpu", max_num_seqs=6, max_num_batched_tokens=256,
+                max_model_len=256, use_graphs=False, enable_prefix_caching=False)
+    g = torch.Generator().manual_seed(3)
+    prompts = [torch.randint(5, 500, (20 + 3 * i,), generator=g).tolist() for i in range(6)]
+    sp = SamplingParams(max_tokens=24, temperature=0.0, ignore_eos=True)
+    eng = LLMEngine(EngineConfig(**base, num_blocks=17))
+    eng.generate(prompts, sp)
+    assert eng.scheduler.stats()["preemptions"] > 0
+    assert eng.stats["prefill_tokens"] > sum(len(p) for p in prompts)
+
+
+def test_auto_host_tier_size_is_half_the_pool_capped_by_ram():
+    from dgi.engine import auto_host_kv_gb
+    pool = _pool(nb=65)
+    gb = auto_host_kv_gb(pool, torch.device("cpu"))
+    assert 0 < gb <= pool.page_bytes() * 65 * 0.5 / (1 << 30) + 0.01

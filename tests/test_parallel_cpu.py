@@ -65,7 +65,12 @@ def _worker(rank, world, port, fn_name, q):
     torch.set_num_threads(1)
     try:
         import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        backend = os.environ.get("DGI_TEST_BACKEND", "gloo")
+        if backend == "nccl":       # DGI_SHARED_GPU=1: every rank on device 0, RCCL data plane
+            from dgi.parallel.fabric import local_device_index, prepare_rccl_env
+            prepare_rccl_env()
+            torch.cuda.set_device(local_device_index())
+        dist.init_process_group(backend, rank=rank, world_size=world)
         res = globals()[fn_name](rank, world)
         q.put((rank, "ok", res))
         dist.barrier()

@@ -51,3 +51,47 @@ def test_staged_pd_replicas_match_local_decode(staged, monkeypatch):
     out = tpc._spawn("_pd_body", 3, timeout=240)
     got = tpc._merged(out, 1, 2)
     assert _agree(got, ref) >= 0.75, (got, ref)
+
+
+# ---------------------------------------------------------------------------- RCCL on one GPU
+# DGI_SHARED_GPU=1 (dgi.parallel.fabric.shared_gpu): every rank on device 0 with
+# its own NCCL_HOSTID, so RCCL accepts the ranks and moves data over its
+# network transport.  Every send/recv is a real RCCL operation with RCCL's
+# blocking semantics (a send waits for its receive): the ordering bugs a gloo
+# rehearsal cannot show surface here as hangs, which the timeouts turn into
+# failures.
+
+@pytest.fixture
+def shared_rccl(monkeypatch):
+    monkeypatch.setenv("DGI_SHARED_GPU", "1")
+    monkeypatch.setenv("DGI_TEST_BACKEND", "nccl")
+    monkeypatch.setenv("DGI_TEST_DEVICE", "cuda")
+    monkeypatch.setenv("DGI_TEST_MODEL", "llama-tiny-hd128")
+    monkeypatch.setenv("DGI_WATCHDOG", "0")
+    monkeypatch.setenv("NCCL_SOCKET_IFNAME", "lo")
+
+
+@pytest.mark.parametrize("sampled", [False, True])
+def test_rccl_pipeline_on_shared_gpu(shared_rccl, monkeypatch, sampled):
+    if sampled:
+        monkeypatch.setenv("DGI_TEST_SAMPLED", "1")
+    ref = tpc._reference_outputs(model="llama-tiny-hd128")
+    out = tpc._spawn("_pp_body", 2, timeout=150)
+    assert out[0]["replays"] > 0 and out[1]["replays"] > 0
+    assert [len(x) for x in out[0]["out"]] == [len(x) for x in ref]
+    assert _agree(out[0]["out"], ref) >= 0.75, (out[0]["out"], ref)
+
+
+@pytest.mark.parametrize("replicas,world", [(2, 3), (1, 3)])
+def test_rccl_pd_on_shared_gpu(shared_rccl, monkeypatch, replicas, world):
+    """1 prefill rank + 2 whole-model decode replicas, and 1 prefill rank + one
+    2-stage decode pipeline (pdpp): KV migration, layer streaming and stage hops
+    all over RCCL."""
+    monkeypatch.setenv("DGI_TEST_PREFILL", "1")
+    monkeypatch.setenv("DGI_TEST_REPLICAS", str(replicas))
+    monkeypatch.setenv("DGI_TEST_SAMPLED", "1")
+    ref = tpc._reference_outputs(model="llama-tiny-hd128")
+    out = tpc._spawn("_pd_body", world, timeout=150)
+    drivers = [1, 2] if replicas == 2 else [1]
+    got = tpc._merged(out, *drivers)
+    assert _agree(got, ref) >= 0.75, (got, ref)

@@ -84,7 +84,8 @@ class NativeRuntimeConfig(BaseModel):
     graph_batch_buckets: List[int] = Field(
         default_factory=lambda: [int(x) for x in get_env("DGI_GRAPH_BATCH_BUCKETS", [], list)])
     kv_fraction: float = Field(default_factory=_env("DGI_KV_FRACTION", 0.9, float))
-    cpu_tier_gb: float = Field(default_factory=_env("DGI_CPU_TIER_GB", 0.0, float))
+    # pinned host KV tier (GB): < 0 = auto (half the HBM KV pool, capped by host RAM), 0 = off
+    cpu_tier_gb: float = Field(default_factory=_env("DGI_CPU_TIER_GB", -1.0, float))
     pp: int = Field(default_factory=_env("DGI_PP", 1, int))
     pd: Optional[str] = Field(default_factory=_env("DGI_PD", None))          # "P:D", e.g. "6:2"
     spec: Optional[str] = Field(default_factory=_env("DGI_SPEC", None))      # "eagle3"
