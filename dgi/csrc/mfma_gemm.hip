@@ -36,6 +36,8 @@
 // on load and skipped on store.
 #include "common.h"
 
+#include <type_traits>
+
 using namespace dgi;
 
 namespace {
@@ -54,7 +56,7 @@ __device__ __forceinline__ void glds16(const uint16_t* src, char* lds) {
 
 __device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
 
-template <int EPI>
+template <int EPI, int SCHED>
 __global__ __launch_bounds__(512) void mfma_gemm_kernel(const uint16_t* __restrict__ X, int ldx,
                                                          const uint16_t* __restrict__ W,
                                                          uint16_t* __restrict__ Y, int ldy, int M, int I, int K,
@@ -76,12 +78,8 @@ __global__ __launch_bounds__(512) void mfma_gemm_kernel(const uint16_t* __restri
   // ---- staging map: lane-linear LDS image, swizzled global source
   const int q = tid >> 3;                         // row within each 64-row slab
   const int lc = (tid & 7) ^ ((tid >> 4) & 7);    // logical k-chunk this lane fetches
-  int xoff[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = min(m0 + i * 64 + q, M - 1);
-    xoff[i] = r * ldx + lc * 8;
-  }
+  const int xq = m0 + q;                          // rows xq + 64 i (clamped to M - 1 at issue)
+  const uint16_t* const xsrc = X + lc * 8;
   // W rows: epi 0 -> n0 + 64 i + q; epi 1 -> slab i = wave column i: 32 gate rows then the
   // matching 32 up rows, so accumulator columns 0-1 (gate) pair with 2-3 (up) in one wave
   int wrow0, wstep;
@@ -100,7 +98,8 @@ __global__ __launch_bounds__(512) void mfma_gemm_kernel(const uint16_t* __restri
   auto issue = [&](int kt, int stage) {
     const int k0 = kt * kBK;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) glds16(X + xoff[i] + k0, lds_x + stage * kStageBytes + i * 8192);
+    for (int i = 0; i < 4; ++i)
+      glds16(xsrc + min(xq + i * 64, M - 1) * ldx + k0, lds_x + stage * kStageBytes + i * 8192);
 #pragma unroll
     for (int i = 0; i < 4; ++i) glds16(wsrc + i * wslab + k0, lds_w + stage * kStageBytes + i * 8192);
   };
@@ -140,21 +139,75 @@ __global__ __launch_bounds__(512) void mfma_gemm_kernel(const uint16_t* __restri
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   read(0, ph0, xa, wa);
-  for (int kt = 0; kt < nt; ++kt) {
-    const int st = kt & 1;
-    read(st, ph1, xb, wb);
-    __builtin_amdgcn_s_setprio(1);
-    mma(xa, wa);
-    __builtin_amdgcn_s_setprio(0);
-    // next stage landed: hipcc does not count global_load_lds as an LDS write
-    // before a barrier, so the wave's own loads are retired explicitly
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();        // every wave's loads landed; every wave done reading this stage
-    if (kt + 2 < nt) issue(kt + 2, st);
-    if (kt + 1 < nt) read(st ^ 1, ph0, xa, wa);
-    __builtin_amdgcn_s_setprio(1);
-    mma(xb, wb);
-    __builtin_amdgcn_s_setprio(0);
+  if (SCHED == 0) {
+    for (int kt = 0; kt < nt; ++kt) {
+      const int st = kt & 1;
+      read(st, ph1, xb, wb);
+      __builtin_amdgcn_s_setprio(1);
+      mma(xa, wa);
+      __builtin_amdgcn_s_setprio(0);
+      // next stage landed: hipcc does not count global_load_lds as an LDS write
+      // before a barrier, so the wave's own loads are retired explicitly
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();        // every wave's loads landed; every wave done reading this stage
+      if (kt + 2 < nt) issue(kt + 2, st);
+      if (kt + 1 < nt) read(st ^ 1, ph0, xa, wa);
+      __builtin_amdgcn_s_setprio(1);
+      mma(xb, wb);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  } else {
+    // Same schedule with the memory instructions spread between the MFMAs
+    // (sched_group_barrier): k-half 1's 12 fragment reads ride 2 MFMAs each,
+    // and after the barrier every global_load_lds and k-half 0 fragment read
+    // of the next step is paired with MFMAs instead of issuing as one burst.
+    // The loop is peeled so each body is one scheduling region (no s_setprio
+    // inside: it would split the region and pin the bursts in place).
+    auto body = [&](int kt, auto issue_next, auto read_next) {
+      const int st = kt & 1;
+      read(st, ph1, xb, wb);
+      mma(xa, wa);
+#pragma unroll
+      for (int i = 0; i < 12; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (decltype(issue_next)::value) issue(kt + 2, st);
+      if constexpr (decltype(read_next)::value) read(st ^ 1, ph0, xa, wa);
+      mma(xb, wb);
+      if constexpr (decltype(issue_next)::value) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 1);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 1);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 1);
+      } else if constexpr (decltype(read_next)::value) {
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 1);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 1);
+      }
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    int kt = 0;
+    for (; kt + 2 < nt; ++kt) body(kt, T_{}, T_{});
+    if (kt + 1 < nt) body(kt++, F_{}, T_{});
+    body(kt, F_{}, F_{});
   }
 
   // ---- epilogue: lane holds rows m = .. + (lane & 15), columns 4 (lane >> 4) + 0..3 of each 16x16 tile
@@ -188,32 +241,31 @@ __global__ __launch_bounds__(512) void mfma_gemm_kernel(const uint16_t* __restri
   }
 }
 
+template <int EPI, int SCHED>
+void launch(const void* x, int ldx, const void* w, void* y, int ldy, int M, int I, int K, int tiles_m, int total,
+            hipStream_t s) {
+  mfma_gemm_kernel<EPI, SCHED><<<dim3(total), 512, 0, s>>>((const uint16_t*)x, ldx, (const uint16_t*)w,
+                                                          (uint16_t*)y, ldy, M, I, K, tiles_m, total);
+}
+
 }  // namespace
 
-// epi 0: Y[M, N] = X W^T with N = rows of W; epi 1: Y[M, I] = SwiGLU with W = [gate; up] (2I rows).
+// epi & 1: 0 = Y[M, N] = X W^T with N = rows of W; 1 = Y[M, I] = SwiGLU with W = [gate; up] (2I rows).
+// epi >> 4: instruction schedule of the K loop (0 = compiler order, 1 = interleaved).
 extern "C" int dgi_mfma_gemm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K,
                              int epi, hipStream_t s) {
   if (M <= 0) return 0;
-  if (K % kBK || ldx % 8 || ldy % 4) return -3;
-  int I = 0, tiles_n;
-  if (epi == 1) {
-    if (N % 256) return -3;
-    I = N / 2;
-    tiles_n = I / 128;
-  } else if (epi == 0) {
-    if (N % 256) return -3;
-    tiles_n = N / 256;
-  } else {
-    return -4;
-  }
+  if (K % kBK || ldx % 8 || ldy % 4 || N % 256) return -3;
+  const int swiglu = epi & 15, sched = epi >> 4;
+  if (swiglu > 1 || sched > 1) return -4;
+  const int I = swiglu ? N / 2 : 0;
+  const int tiles_n = swiglu ? I / 128 : N / 256;
   const int tiles_m = (M + kBM - 1) / kBM;
   const int total = tiles_m * tiles_n;
-  if (epi == 1)
-    mfma_gemm_kernel<1><<<dim3(total), 512, 0, s>>>((const uint16_t*)x, ldx, (const uint16_t*)w, (uint16_t*)y,
-                                                    ldy, M, I, K, tiles_m, total);
+  if (swiglu)
+    (sched ? launch<1, 1> : launch<1, 0>)(x, ldx, w, y, ldy, M, I, K, tiles_m, total, s);
   else
-    mfma_gemm_kernel<0><<<dim3(total), 512, 0, s>>>((const uint16_t*)x, ldx, (const uint16_t*)w, (uint16_t*)y,
-                                                    ldy, M, I, K, tiles_m, total);
+    (sched ? launch<0, 1> : launch<0, 0>)(x, ldx, w, y, ldy, M, I, K, tiles_m, total, s);
   DGI_CHECK_LAUNCH();
   return 0;
 }

@@ -147,6 +147,7 @@ class LLMEngine:
             self.mlp_pad_table = build_for_model(self.model, cfg.max_num_batched_tokens)
             if self.mlp_pad_table is not None:
                 self.model.mlp_pad = self.mlp_pad_table.pad
+                self.model.mlp_impl = self.mlp_pad_table.impl
                 self.mlp_pad_seconds = time.perf_counter() - t1
 
     # ------------------------------------------------------------------ API

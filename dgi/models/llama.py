@@ -73,6 +73,7 @@ class LlamaModel:
         self.reduce = None
         # MLP row padding (dgi.runtime.gemm_pad): T -> rows to run gate_up/down on
         self.mlp_pad = None
+        self.mlp_impl = None     # rows -> (gate_up on the MFMA SwiGLU kernel, down on the MFMA kernel)
         # called with the global layer id once that layer's KV is in the cache
         # (P/D layer-streamed migration sends finished layers while later ones compute)
         self.layer_hook = None
@@ -312,6 +313,8 @@ class LlamaModel:
             if fq or fg:
                 return self._forward_layers_fused(h, meta, residual, fq, fg)
         Mp = self._mlp_rows(T, h) if self.layers else T
+        # hand-written MFMA GEMMs where the start-up table measured them faster (dgi.runtime.gemm_pad)
+        mfma_gu, mfma_dn = self.mlp_impl(Mp) if (self.mlp_impl is not None and self.layers) else (False, False)
         for i, L in enumerate(self.layers):
             if residual is None:
                 residual = h
@@ -328,13 +331,11 @@ class LlamaModel:
             if self.reduce is not None:
                 self.reduce(h)
             ops.fused_add_rmsnorm(h, residual, L.post_norm, eps)
+            x = self._pad_buf[:Mp] if Mp > T else h
+            act = ops.mfma_gemm(x, L.gate_up, 1) if mfma_gu else ops.silu_mul(ops.linear(x, L.gate_up))
+            h = ops.mfma_gemm(act, L.down, 0) if mfma_dn else ops.linear(act, L.down)
             if Mp > T:
-                act = ops.silu_mul(ops.linear(self._pad_buf[:Mp], L.gate_up))
-                h = ops.linear(act, L.down)[:T]
-            else:
-                gu = ops.linear(h, L.gate_up)
-                act = ops.silu_mul(gu)
-                h = ops.linear(act, L.down)
+                h = h[:T]
             if self.reduce is not None:
                 self.reduce(h)
             if self.capture_layers and (self.layer_start + i) in self.capture_layers:

@@ -491,7 +491,11 @@ def mfma_gemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
             and x.shape[1] % 64 == 0 and x.data_ptr() % 16 == 0 and x.shape[0] * x.stride(0) < (1 << 31))
 
 
-def mfma_gemm(x: torch.Tensor, w: torch.Tensor, epi: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+MFMA_SCHED = int(os.environ.get("DGI_MFMA_SCHED", "1"))
+
+
+def mfma_gemm(x: torch.Tensor, w: torch.Tensor, epi: int = 0, out: Optional[torch.Tensor] = None,
+              sched: Optional[int] = None) -> torch.Tensor:
     """Hand-written LDS-tiled MFMA GEMM (256x256 tiles, global_load_lds
     staging, XCD-aware tile order): ``epi`` 0 -> x @ w.T; 1 -> the fused
     SwiGLU of the MLP, silu(x @ gate.T) * (x @ up.T) with w = [gate; up],
@@ -502,7 +506,7 @@ def mfma_gemm(x: torch.Tensor, w: torch.Tensor, epi: int = 0, out: Optional[torc
         load_native(required=True)
         if out is None:
             out = torch.empty(M, N, dtype=x.dtype, device=x.device)
-        _call("mfma_gemm", out, x, w, epi)
+        _call("mfma_gemm", out, x, w, epi | ((MFMA_SCHED if sched is None else sched) << 4))
         return out
     r = mfma_gemm_ref(x, w, epi)
     if out is not None:

@@ -13,6 +13,13 @@ every multiple of ``step`` rows up to the token budget, and ``pad(T)`` returns
 the row count (a multiple of ``step``, at most ``max_grow`` larger than T)
 with the lowest measured time.  ``LlamaModel.forward_layers`` then lets the
 o-projection write into a padded buffer and runs the MLP on the padded rows.
+
+Each half of the MLP is measured with both GEMM implementations — hipBLASLt
+(+ the separate silu_mul pass) and the hand-written LDS-tiled MFMA kernel
+(``ops.mfma_gemm``: gate_up with the SwiGLU epilogue fused, down as a plain
+GEMM) — and ``impl(rows)`` tells the model which one is faster at that row
+count on this GPU (``DGI_MFMA_GEMM=0`` keeps hipBLASLt everywhere, ``=force``
+the MFMA kernel wherever it applies).
 """
 from __future__ import annotations
 
@@ -23,12 +30,17 @@ from typing import Optional
 import torch
 
 
+MFMA_GEMM = os.environ.get("DGI_MFMA_GEMM", "1")
+
+
 class MlpPadTable:
-    def __init__(self, grid: list, times: list, step: int, max_grow: float = 0.15):
+    def __init__(self, grid: list, times: list, step: int, max_grow: float = 0.15, impls: Optional[list] = None):
         self.grid = list(grid)
         self.times = list(times)
         self.step = step
         self.max_grow = max_grow
+        # per grid point: (gate_up via MFMA+SwiGLU?, down via MFMA?)
+        self.impls = list(impls) if impls is not None else [(False, False)] * len(self.grid)
         self._cache: dict = {}
 
     @classmethod
@@ -37,24 +49,47 @@ class MlpPadTable:
         from dgi import ops
         H = gate_up.shape[1]
         x = torch.randn(m_max, H, device=gate_up.device, dtype=gate_up.dtype) * 0.1
+        a = torch.randn(m_max, gate_up.shape[0] // 2, device=gate_up.device, dtype=gate_up.dtype) * 0.1
         grid = list(range(m_min, m_max + 1, step))
-        times = []
+        times, impls = [], []
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        use_mfma = MFMA_GEMM != "0" and ops.mfma_gemm_ok(x, gate_up)
+        mfma_down = use_mfma and ops.mfma_gemm_ok(a, down)
+        force = MFMA_GEMM == "force"
 
-        def mlp(m):
-            ops.linear(ops.silu_mul(ops.linear(x[:m], gate_up)), down)
-
-        for m in grid:
-            mlp(m)
+        def timed(fn):
+            fn()
             best = float("inf")
             for _ in range(reps):
                 e0.record()
-                mlp(m)
+                fn()
                 e1.record()
                 e1.synchronize()
                 best = min(best, e0.elapsed_time(e1))
-            times.append(best)
-        return cls(grid, times, step)
+            return best
+
+        for m in grid:
+            front = timed(lambda: ops.silu_mul(ops.linear(x[:m], gate_up)))
+            back = timed(lambda: ops.linear(a[:m], down))
+            f_mfma = b_mfma = False
+            if use_mfma:
+                t = timed(lambda: ops.mfma_gemm(x[:m], gate_up, 1))
+                if force or t < front:
+                    front, f_mfma = t, True
+            if mfma_down:
+                t = timed(lambda: ops.mfma_gemm(a[:m], down, 0))
+                if force or t < back:
+                    back, b_mfma = t, True
+            times.append(front + back)
+            impls.append((f_mfma, b_mfma))
+        return cls(grid, times, step, impls=impls)
+
+    def impl(self, rows: int) -> tuple:
+        """(gate_up via the fused MFMA SwiGLU kernel, down via the MFMA kernel) at ``rows``."""
+        if not self.grid or not (self.grid[0] <= rows <= self.grid[-1]):
+            return False, False
+        i = bisect.bisect_left(self.grid, rows)
+        return self.impls[i] if self.grid[i] == rows else (False, False)
 
     def pad(self, T: int) -> int:
         """Rows to run the MLP on for a step of ``T`` rows (``T`` when the table has no say)."""

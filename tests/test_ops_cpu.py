@@ -206,3 +206,14 @@ def test_fused_decode_layers_match_unfused_on_cpu():
         assert outs[0] == outs[1], name
         for a, b in zip(*logits):
             torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
+
+
+def test_mlp_pad_table_picks_cheapest_rows_and_reports_impl():
+    from dgi.runtime.gemm_pad import MlpPadTable
+    grid = [512, 544, 576, 608]
+    t = MlpPadTable(grid, [10.0, 12.0, 9.0, 11.0], 32,
+                    impls=[(False, False), (True, False), (True, True), (False, True)])
+    assert t.pad(520) == 576          # within +15 %: the 576-row run is the cheapest
+    assert t.pad(100) == 100          # below the table: no say
+    assert t.impl(576) == (True, True) and t.impl(544) == (True, False)
+    assert t.impl(550) == (False, False) and t.impl(4096) == (False, False)
