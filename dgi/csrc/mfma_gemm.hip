@@ -56,6 +56,41 @@ __device__ __forceinline__ void glds16(const uint16_t* src, char* lds) {
 
 __device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
 
+// Lane holds rows m0 + 128 wm + 16 i + (lane & 15), columns 4 (lane >> 4) + 0..3 of each 16x16 tile.
+template <int EPI>
+__device__ __forceinline__ void epilogue(const f32x4 (&acc)[8][4], uint16_t* __restrict__ Y, int ldy, int M, int m0,
+                                         int tn, int wm, int wn, int lane) {
+  const int r16 = lane & 15;
+  const int c4 = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + r16;
+    if (m >= M) continue;
+    uint16_t* yrow = Y + (size_t)m * ldy;
+    if (EPI == 1) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const f32x4 g = acc[i][j], u = acc[i][j + 2];
+        const int n = tn * 128 + wn * 32 + j * 16 + c4;
+        uint2 v;
+        v.x = pack_bf16x2(silu(g[0]) * u[0], silu(g[1]) * u[1]);
+        v.y = pack_bf16x2(silu(g[2]) * u[2], silu(g[3]) * u[3]);
+        *(uint2*)(yrow + n) = v;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 a = acc[i][j];
+        const int n = tn * 256 + wn * 64 + j * 16 + c4;
+        uint2 v;
+        v.x = pack_bf16x2(a[0], a[1]);
+        v.y = pack_bf16x2(a[2], a[3]);
+        *(uint2*)(yrow + n) = v;
+      }
+    }
+  }
+}
+
 template <int EPI, int SCHED>
 __global__ __launch_bounds__(512) void mfma_gemm_kernel(const uint16_t* __restrict__ X, int ldx,
                                                          const uint16_t* __restrict__ W,
@@ -210,62 +245,185 @@ __global__ __launch_bounds__(512) void mfma_gemm_kernel(const uint16_t* __restri
     body(kt, F_{}, F_{});
   }
 
-  // ---- epilogue: lane holds rows m = .. + (lane & 15), columns 4 (lane >> 4) + 0..3 of each 16x16 tile
-  const int c4 = (lane >> 4) * 4;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + wm * 128 + i * 16 + r16;
-    if (m >= M) continue;
-    uint16_t* yrow = Y + (size_t)m * ldy;
-    if (EPI == 1) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const f32x4 g = acc[i][j], u = acc[i][j + 2];
-        const int n = tn * 128 + wn * 32 + j * 16 + c4;
-        uint2 v;
-        v.x = pack_bf16x2(silu(g[0]) * u[0], silu(g[1]) * u[1]);
-        v.y = pack_bf16x2(silu(g[2]) * u[2], silu(g[3]) * u[3]);
-        *(uint2*)(yrow + n) = v;
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const f32x4 a = acc[i][j];
-        const int n = tn * 256 + wn * 64 + j * 16 + c4;
-        uint2 v;
-        v.x = pack_bf16x2(a[0], a[1]);
-        v.y = pack_bf16x2(a[2], a[3]);
-        *(uint2*)(yrow + n) = v;
-      }
-    }
+  epilogue<EPI>(acc, Y, ldy, M, m0, tn, wm, wn, lane);
+}
+
+
+// ---------------------------------------------------------------------------
+// Ring schedule (sched 2): the K loop advances in 32-deep sub-steps through a
+// ring of four 32 KB LDS slots (X 256 x 32 and W 256 x 32, 64-byte rows).
+// Sub-step u computes on fragments of u already in registers, reads u + 1's
+// fragments, and refills the slot u itself came from with u + 4 — so three
+// sub-steps of loads stay in flight across every barrier (counted
+// s_waitcnt vmcnt(8), never 0 in the steady state, raw s_barrier) and each
+// sub-step's 4 global_load_lds, 12 ds_read_b128 and 32 MFMAs are issued
+// interleaved.  64-byte rows: chunk c of row r holds k-chunk c ^ f((r >> 2) & 3)
+// with f = {0, 2, 3, 1}, conflict-free for the ds_read_b128 lane groups.
+template <int EPI>
+__global__ __launch_bounds__(512) void mfma_gemm_ring_kernel(const uint16_t* __restrict__ X, int ldx,
+                                                              const uint16_t* __restrict__ W,
+                                                              uint16_t* __restrict__ Y, int ldy, int M, int I,
+                                                              int K, int tiles_m, int tiles_total) {
+  constexpr int kSlot = 32768;        // X 16 KB + W 16 KB
+  constexpr int kHalf = 16384;
+  __shared__ __attribute__((aligned(16))) char smem[4 * kSlot];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int wm = w >> 2, wn = w & 3;
+
+  const int b = blockIdx.x;
+  const int xcd = b & 7, li = b >> 3;
+  const int q8 = tiles_total >> 3, r8 = tiles_total & 7;
+  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + li;
+  const int tm = t % tiles_m, tn = t / tiles_m;
+  const int m0 = tm * kBM;
+
+  // staging: instruction i covers tile rows 128 i + (tid >> 2), 16-byte chunk tid & 3
+  const int rq = tid >> 2;
+  const int quad = (tid >> 4) & 3;
+  const int lc = (tid & 3) ^ ((0x1320 >> (quad * 4)) & 3);
+  const int xq = m0 + rq;
+  const uint16_t* const xsrc = X + lc * 8;
+  int wrow0, wstep;
+  if (EPI == 1) {            // tile row r -> wave column r >> 6; 32 gate rows then the 32 matching up rows
+    const int qq = rq & 63;
+    wrow0 = tn * 128 + (rq >> 6) * 32 + (qq < 32 ? qq : I + qq - 32);
+    wstep = 64;              // +128 tile rows = +2 wave columns = +64 weight rows
+  } else {
+    wrow0 = tn * 256 + rq;
+    wstep = 128;
   }
+  const uint16_t* const wsrc = W + (size_t)wrow0 * K + lc * 8;
+  const size_t wslab = (size_t)wstep * K;
+  char* const lds_x = smem + w * 1024;
+  char* const lds_w = smem + kHalf + w * 1024;
+
+  auto issue = [&](int u) {
+    const int k0 = u * 32;
+    const int slot = (u & 3) * kSlot;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      glds16(xsrc + min(xq + i * 128, M - 1) * ldx + k0, lds_x + slot + i * 8192);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) glds16(wsrc + i * wslab + k0, lds_w + slot + i * 8192);
+  };
+
+  const int r16 = lane & 15;
+  const int ph = ((lane >> 4) ^ ((0x1320 >> (((lane >> 2) & 3) * 4)) & 3)) * 16;
+  const int xbase = (wm * 128 + r16) * 64 + ph;
+  const int wbase = kHalf + (wn * 64 + r16) * 64 + ph;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 xa[8], wa[4], xb[8], wb[4];
+  auto read = [&](int u, bf16x8* xf, bf16x8* wf) {
+    const char* s = smem + (u & 3) * kSlot;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wf[j] = *(const bf16x8*)(s + wbase + j * 1024);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) xf[i] = *(const bf16x8*)(s + xbase + i * 1024);
+  };
+  auto mma = [&](const bf16x8* xf, const bf16x8* wf) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+  };
+  // steady-state sub-step (u + 4 < nu): compute on (xc, wc) = fragments of u, read u + 1 into
+  // (xn, wn_), refill slot u with u + 4 — branch-free, so the interleave below is one region
+  auto steady = [&](int u, bf16x8* xc, bf16x8* wc, bf16x8* xn, bf16x8* wn_) {
+    // the refill goes first: each global_load_lds rewrites M0, and hipcc waits for every
+    // outstanding LDS op before an M0 write, so issued behind the fragment reads it would
+    // serialise them
+    issue(u + 4);
+    read(u + 1, xn, wn_);
+    mma(xc, wc);
+    __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // slot u + 2 landed; u + 3, u + 4 in flight
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // the last (up to 4) sub-steps: no refills, the in-flight slots drain
+  auto tail = [&](int u, int nu, bf16x8* xc, bf16x8* wc, bf16x8* xn, bf16x8* wn_) {
+    if (u + 1 < nu) read(u + 1, xn, wn_);
+    mma(xc, wc);
+    __builtin_amdgcn_sched_barrier(0);
+    if (u + 3 < nu)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  const int nu = K / 32;
+  for (int u = 0; u < 4 && u < nu; ++u) issue(u);
+  // slots 0 and 1 landed (2 and 3 may still be in flight)
+  if (nu >= 4)
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  read(0, xa, wa);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();          // every wave holds slot 0 in registers: it may be refilled
+  __builtin_amdgcn_sched_barrier(0);
+  // nu is even (K % 64 == 0): steady pairs while both sub-steps refill, then drain in pairs
+  int u = 0;
+  for (; u + 5 < nu; u += 2) {
+    steady(u, xa, wa, xb, wb);
+    steady(u + 1, xb, wb, xa, wa);
+  }
+  for (; u < nu; u += 2) {
+    tail(u, nu, xa, wa, xb, wb);
+    tail(u + 1, nu, xb, wb, xa, wa);
+  }
+  epilogue<EPI>(acc, Y, ldy, M, m0, tn, wm, wn, lane);
 }
 
 template <int EPI, int SCHED>
 void launch(const void* x, int ldx, const void* w, void* y, int ldy, int M, int I, int K, int tiles_m, int total,
             hipStream_t s) {
-  mfma_gemm_kernel<EPI, SCHED><<<dim3(total), 512, 0, s>>>((const uint16_t*)x, ldx, (const uint16_t*)w,
+  if (SCHED == 2)
+    mfma_gemm_ring_kernel<EPI><<<dim3(total), 512, 0, s>>>((const uint16_t*)x, ldx, (const uint16_t*)w,
                                                           (uint16_t*)y, ldy, M, I, K, tiles_m, total);
+  else
+    mfma_gemm_kernel<EPI, SCHED><<<dim3(total), 512, 0, s>>>((const uint16_t*)x, ldx, (const uint16_t*)w,
+                                                            (uint16_t*)y, ldy, M, I, K, tiles_m, total);
 }
 
 }  // namespace
 
 // epi & 1: 0 = Y[M, N] = X W^T with N = rows of W; 1 = Y[M, I] = SwiGLU with W = [gate; up] (2I rows).
-// epi >> 4: instruction schedule of the K loop (0 = compiler order, 1 = interleaved).
+// epi >> 4: K-loop schedule (0 = compiler order, 1 = interleaved, 2 = 4-slot ring of 32-deep sub-steps).
 extern "C" int dgi_mfma_gemm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K,
                              int epi, hipStream_t s) {
   if (M <= 0) return 0;
   if (K % kBK || ldx % 8 || ldy % 4 || N % 256) return -3;
   const int swiglu = epi & 15, sched = epi >> 4;
-  if (swiglu > 1 || sched > 1) return -4;
+  if (swiglu > 1 || sched > 2) return -4;
   const int I = swiglu ? N / 2 : 0;
   const int tiles_n = swiglu ? I / 128 : N / 256;
   const int tiles_m = (M + kBM - 1) / kBM;
   const int total = tiles_m * tiles_n;
   if (swiglu)
-    (sched ? launch<1, 1> : launch<1, 0>)(x, ldx, w, y, ldy, M, I, K, tiles_m, total, s);
+    (sched == 2 ? launch<1, 2> : sched ? launch<1, 1> : launch<1, 0>)(x, ldx, w, y, ldy, M, I, K, tiles_m, total, s);
   else
-    (sched ? launch<0, 1> : launch<0, 0>)(x, ldx, w, y, ldy, M, I, K, tiles_m, total, s);
+    (sched == 2 ? launch<0, 2> : sched ? launch<0, 1> : launch<0, 0>)(x, ldx, w, y, ldy, M, I, K, tiles_m, total, s);
   DGI_CHECK_LAUNCH();
   return 0;
 }

@@ -54,10 +54,12 @@ def main():
                     "hipblaslt+silu_mul": lambda: ops.silu_mul(F.linear(x, w)),
                     "mfma_swiglu": lambda: ops.mfma_gemm(x, w, 1, sched=1),
                     "mfma_swiglu_s0": lambda: ops.mfma_gemm(x, w, 1, sched=0),
+                    "mfma_swiglu_s2": lambda: ops.mfma_gemm(x, w, 1, sched=2),
                 }
             else:
                 variants = {"hipblaslt": lambda: F.linear(x, w), "mfma": lambda: ops.mfma_gemm(x, w, 0, sched=1),
-                            "mfma_s0": lambda: ops.mfma_gemm(x, w, 0, sched=0)}
+                            "mfma_s0": lambda: ops.mfma_gemm(x, w, 0, sched=0),
+                            "mfma_s2": lambda: ops.mfma_gemm(x, w, 0, sched=2)}
             for f in variants.values():
                 f()
             torch.cuda.synchronize()

@@ -3,14 +3,28 @@
 # per-rank NCCL_HOSTID, RCCL network transport over loopback).  Exercises the
 # 8-GPU code path's RCCL ordering (pair set-up, KV migration, stage hops) at
 # small scale before the driver runs it on a whole node.  Llama-3-8B, short run.
+# A rank still running after DGI_HANG_DUMP_S seconds dumps every thread's
+# Python stack to the .err file and exits.
+# usage: rehearse_rccl_bench.sh [case ...]   (default: all cases)
 set -o pipefail
 mkdir -p gpurun_out
-export DGI_SHARED_GPU=1 NCCL_SOCKET_IFNAME=lo NCCL_IB_DISABLE=1 DGI_HANG_DUMP_S=360
+export DGI_SHARED_GPU=1 NCCL_SOCKET_IFNAME=lo NCCL_IB_DISABLE=1 DGI_HANG_DUMP_S=${DGI_HANG_DUMP_S:-100}
 run() {  # name, nproc, extra args
   local name=$1 n=$2; shift 2
-  timeout -k 10 420 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 \
+  echo "== $name" >&2
+  timeout -k 10 160 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 \
     --master-port $((29600 + n)) bench.py --gpus "$n" --model llama3-8b --steps 8 --warmup 2 --ramp-steps 4 \
     --concurrency 64 --output-len 32 --prompt-len 256 "$@" > "gpurun_out/rehearse_${name}.json" 2> "gpurun_out/rehearse_${name}.err"
+  local rc=$?
+  echo "== $name rc=$rc" >&2
+  return $rc
 }
-run pdpp4_1p_pp3 4 --layout pdpp --prefill-ranks 1 --decode-stages 3 || exit 1
-run pd4_2p_2d 4 --layout pd --prefill-ranks 2 --decode-replicas 2 || exit 1
+cases=${*:-"pdpp4_1p_pp3 pdpp4_2p_pp2 pd4_2p_2d pd3_2p_1d"}
+for c in $cases; do
+  case $c in
+    pdpp4_1p_pp3) run $c 4 --layout pdpp --prefill-ranks 1 --decode-stages 3 || exit 1 ;;
+    pdpp4_2p_pp2) run $c 4 --layout pdpp --prefill-ranks 2 --decode-stages 2 || exit 1 ;;
+    pd4_2p_2d) run $c 4 --layout pd --prefill-ranks 2 --decode-replicas 2 || exit 1 ;;
+    pd3_2p_1d) run $c 3 --layout pd --prefill-ranks 2 --decode-replicas 1 || exit 1 ;;
+  esac
+done

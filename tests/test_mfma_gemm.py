@@ -26,12 +26,13 @@ def test_reference_swiglu_matches_silu_mul_cpu():
 @pytest.mark.parametrize("M,N,K", [(1, 256, 64), (100, 512, 256), (256, 256, 128), (300, 768, 512),
                                    (1000, 1024, 1024), (2048, 2560, 4096), (513, 256, 8192)])
 @pytest.mark.parametrize("epi", [0, 1])
-def test_mfma_gemm_matches_fp32(M, N, K, epi):
+@pytest.mark.parametrize("sched", [0, 1, 2])
+def test_mfma_gemm_matches_fp32(M, N, K, epi, sched):
     ops.load_native(required=True)
     x = _rand(M, K, device="cuda", seed=M + K)
     w = _rand(N, K, device="cuda", scale=0.05, seed=N)
     ref = ops.mfma_gemm_ref(x, w, epi).float()
-    got = ops.mfma_gemm(x, w, epi)
+    got = ops.mfma_gemm(x, w, epi, sched=sched)
     torch.cuda.synchronize()
     assert got.shape == ref.shape
     err = (got.float() - ref).abs()
@@ -40,7 +41,8 @@ def test_mfma_gemm_matches_fp32(M, N, K, epi):
 
 
 @pytest.mark.gpu
-def test_mfma_gemm_strided_rows_and_asymmetric_operands():
+@pytest.mark.parametrize("sched", [0, 1, 2])
+def test_mfma_gemm_strided_rows_and_asymmetric_operands(sched):
     """A = row slice of a wider buffer (ldx > K) and an asymmetric W: catches
     row/column swaps in the C write and ldx handling."""
     ops.load_native(required=True)
@@ -48,6 +50,6 @@ def test_mfma_gemm_strided_rows_and_asymmetric_operands():
     buf = _rand(384, K + 64, device="cuda", seed=5)
     x = buf[:, :K]
     w = (torch.arange(512 * K, device="cuda", dtype=torch.float32).reshape(512, K) % 7 - 3).to(torch.bfloat16)
-    got = ops.mfma_gemm(x, w, 0)
+    got = ops.mfma_gemm(x, w, 0, sched=sched)
     ref = ops.mfma_gemm_ref(x, w, 0).float()
     assert (got.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
