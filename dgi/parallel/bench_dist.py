@@ -201,10 +201,15 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
                 ttfts += srv.ttfts[before:]
             return n, ttfts
 
+        # at each phase boundary: fence first (the drivers post the receives of everything
+        # announced), then synchronise — on RCCL an unmatched KV send never completes
         serve_until_phase()
+        srv.fence()
+        torch.cuda.synchronize() if f.device.type == "cuda" else None
         f.barrier()
         t0 = time.perf_counter()
         n, ttfts = serve_until_phase()
+        srv.fence()
         torch.cuda.synchronize() if f.device.type == "cuda" else None
         f.barrier()
         el = time.perf_counter() - t0
@@ -271,6 +276,7 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
             if is_clock:
                 for ph in phases:
                     ph.send([MSG_PHASE])
+            drv.await_fences()       # receives of every announced migration are posted
             if hasattr(drv.engine, "pause_stages"):
                 drv.engine.pause_stages()
             torch.cuda.synchronize() if f.device.type == "cuda" else None

@@ -63,6 +63,9 @@ from dgi.sched.request import Request, SamplingParams, Status
 from dgi.utils.trace import mark, phase
 
 MSG_MIGRATE, MSG_CREDIT, MSG_DONE, MSG_FINISHED, MSG_TOKENS, MSG_FIRST = 1, 2, 3, 4, 5, 6
+# a prefill rank has stopped stepping: every migration it announced before this message
+# is on this channel, so once the driver has posted their receives the rank's sends can drain
+MSG_FENCE = 7
 REASONS = {0: None, 1: "length", 2: "stop"}
 CTRL = 8
 META_FIELDS = 12
@@ -425,6 +428,15 @@ class PrefillServer:
         st["migration_ms_p50"] = round(float(np.median(lat)), 3) if lat else None
         return st
 
+    def fence(self) -> None:
+        """Tell every replica driver that this rank has stopped stepping (a benchmark
+        phase boundary).  On RCCL a KV send completes only once the receiver has
+        posted the matching receive, so a prefill rank must not synchronise its
+        device (or enter a collective) until the drivers have taken in every
+        migration it announced — ``DecodeDriver.await_fences`` is the other half."""
+        for ch in self.ch.values():
+            ch.send([MSG_FENCE])
+
     def finish(self) -> None:
         """End of stream: every replica driver keeps receiving until it sees DONE."""
         for ch in self.ch.values():
@@ -482,6 +494,7 @@ class DecodeDriver:
         self.refund = collections.Counter()
         self.refund_seqs = collections.Counter()
         self.done = set()
+        self.fenced: set = set()    # prefill ranks at a phase boundary (MSG_FENCE)
         self.inflight: list = []    # migrations whose pages are still on the wire
         self.await_first: dict = {p: collections.deque() for p in self.prefill}
         self.received = 0
@@ -605,6 +618,8 @@ class DecodeDriver:
             self._first(p, m)
         elif m[0] == MSG_DONE:
             self.done.add(p)
+        elif m[0] == MSG_FENCE:
+            self.fenced.add(p)
         elif m[0] == MSG_FINISHED:
             if self.track_arrivals:
                 self.prefill_finished.append((int(m[1]), int(m[2]), REASONS.get(int(m[3]))))
@@ -666,6 +681,19 @@ class DecodeDriver:
         if self.forward_tokens and not self.is_router:
             self._forward(arr, outs)
         return outs
+
+    def await_fences(self, timeout_s: float = 600.0) -> None:
+        """Keep taking in control messages (posting the receives of every announced
+        migration) until each prefill rank has sent its fence, then clear them."""
+        t0 = time.perf_counter()
+        while len(self.fenced) < len(self.prefill):
+            for p in self.chans:
+                self._poll_ctrl(p)
+            if len(self.fenced) < len(self.prefill):
+                if time.perf_counter() - t0 > timeout_s:
+                    raise TimeoutError(f"prefill fences: got {sorted(self.fenced)} of {self.prefill}")
+                time.sleep(0.0005)
+        self.fenced.clear()
 
     def all_prefill_done(self) -> bool:
         if len(self.done) == len(self.prefill) and self.inflight:

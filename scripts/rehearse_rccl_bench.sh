@@ -19,12 +19,13 @@ run() {  # name, nproc, extra args
   echo "== $name rc=$rc" >&2
   return $rc
 }
-cases=${*:-"pdpp4_1p_pp3 pdpp4_2p_pp2 pd4_2p_2d pd3_2p_1d"}
+cases=${*:-"pdpp4_1p_pp3 pdpp4_2p_pp2 pd4_2p_2d pd3_2p_1d pdpp8_5p_pp3"}
 for c in $cases; do
   case $c in
     pdpp4_1p_pp3) run $c 4 --layout pdpp --prefill-ranks 1 --decode-stages 3 || exit 1 ;;
     pdpp4_2p_pp2) run $c 4 --layout pdpp --prefill-ranks 2 --decode-stages 2 || exit 1 ;;
     pd4_2p_2d) run $c 4 --layout pd --prefill-ranks 2 --decode-replicas 2 || exit 1 ;;
     pd3_2p_1d) run $c 3 --layout pd --prefill-ranks 2 --decode-replicas 1 || exit 1 ;;
+    pdpp8_5p_pp3) run $c 8 --layout pdpp --prefill-ranks 5 --decode-stages 3 || exit 1 ;;
   esac
 done
