@@ -176,6 +176,12 @@ ALIASES = {
 
 
 def get_config(name_or_path: str) -> ModelConfig:
+    """Preset, alias, HF config dir/file, or a family guess from the name.
+    ``<model>@L<n>`` keeps the architecture and truncates it to ``n`` layers
+    (multi-rank rehearsals of a big model's shapes on one GPU)."""
+    if "@L" in name_or_path:
+        base, n = name_or_path.rsplit("@L", 1)
+        return dataclasses.replace(get_config(base), name=name_or_path, num_layers=int(n))
     key = ALIASES.get(name_or_path, name_or_path)
     if key in PRESETS:
         return dataclasses.replace(PRESETS[key])

@@ -9,12 +9,15 @@
 set -o pipefail
 mkdir -p gpurun_out
 export DGI_SHARED_GPU=1 NCCL_SOCKET_IFNAME=lo NCCL_IB_DISABLE=1 DGI_HANG_DUMP_S=${DGI_HANG_DUMP_S:-100}
+MODEL=${REHEARSE_MODEL:-llama3-8b}
+CONC=${REHEARSE_CONC:-64}
 run() {  # name, nproc, extra args
   local name=$1 n=$2; shift 2
-  echo "== $name" >&2
+  echo "== $name ($MODEL)" >&2
   timeout -k 10 160 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 \
-    --master-port $((29600 + n)) bench.py --gpus "$n" --model llama3-8b --steps 8 --warmup 2 --ramp-steps 4 \
-    --concurrency 64 --output-len 32 --prompt-len 256 "$@" > "gpurun_out/rehearse_${name}.json" 2> "gpurun_out/rehearse_${name}.err"
+    --master-port $((29600 + n)) bench.py --gpus "$n" --model "$MODEL" --steps 8 --warmup 2 --ramp-steps 4 \
+    --concurrency "$CONC" --output-len 32 --prompt-len 256 "$@" > "gpurun_out/rehearse_${name}${REHEARSE_TAG}.json" \
+    2> "gpurun_out/rehearse_${name}${REHEARSE_TAG}.err"
   local rc=$?
   echo "== $name rc=$rc" >&2
   return $rc

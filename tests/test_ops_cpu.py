@@ -217,3 +217,10 @@ def test_mlp_pad_table_picks_cheapest_rows_and_reports_impl():
     assert t.pad(100) == 100          # below the table: no say
     assert t.impl(576) == (True, True) and t.impl(544) == (True, False)
     assert t.impl(550) == (False, False) and t.impl(4096) == (False, False)
+
+
+def test_layer_truncated_model_name():
+    from dgi.models.config import get_config
+    c = get_config("llama3-70b@L8")
+    full = get_config("llama3-70b")
+    assert c.num_layers == 8 and c.hidden_size == full.hidden_size and c.num_kv_heads == full.num_kv_heads
