@@ -20,6 +20,7 @@ re-normalises it, which is bit-identical to the fused add it replaces.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -29,6 +30,10 @@ from dgi import ops
 from dgi.models.config import ModelConfig
 from dgi.runtime.batch import AttnMeta
 
+
+
+# DGI_TRIM_LAST_LAYER=0 runs the last layer's o-proj and MLP on every row (A/B switch)
+TRIM_LAST_LAYER = os.environ.get("DGI_TRIM_LAST_LAYER", "1") != "0"
 
 class LlamaLayerWeights:
     __slots__ = ("in_norm", "qkv", "o", "post_norm", "gate_up", "down", "qkv_bias")
@@ -304,7 +309,12 @@ class LlamaModel:
                 self.layer_hook(self.layer_start + i)
         return h, residual
 
-    def forward_layers(self, h: torch.Tensor, meta: AttnMeta, residual: Optional[torch.Tensor] = None):
+    def forward_layers(self, h: torch.Tensor, meta: AttnMeta, residual: Optional[torch.Tensor] = None,
+                       trim_last: Optional[torch.Tensor] = None):
+        """Run the local layers.  ``trim_last`` (row indices): the last layer's
+        output is only needed for those rows (the rows that produce logits), so
+        after its attention — which has written every row's K/V — its o-proj and
+        MLP run on those rows alone and the returned (h, residual) hold just them."""
         c = self.cfg
         eps = c.rms_eps
         T = h.shape[0]
@@ -323,6 +333,19 @@ class LlamaModel:
                 ops.fused_add_rmsnorm(h, residual, L.in_norm, eps)
             qkv = ops.linear(h, L.qkv, L.qkv_bias)
             attn = self.attention(i, qkv, meta)
+            if trim_last is not None and i == len(self.layers) - 1:
+                attn = attn.index_select(0, trim_last)
+                residual = residual.index_select(0, trim_last)
+                h = ops.linear(attn, L.o)
+                if self.reduce is not None:
+                    self.reduce(h)
+                ops.fused_add_rmsnorm(h, residual, L.post_norm, eps)
+                h = ops.linear(ops.silu_mul(ops.linear(h, L.gate_up)), L.down)
+                if self.reduce is not None:
+                    self.reduce(h)
+                if self.layer_hook is not None:
+                    self.layer_hook(self.layer_start + i)
+                break
             if Mp > T:
                 # o-proj writes the first T rows of the padded MLP input
                 h = torch.matmul(attn, L.o.t(), out=self._pad_buf[:T])
@@ -356,12 +379,18 @@ class LlamaModel:
         else:
             h = hidden
         residual = None
+        idx = meta.logits_indices
+        # the last layer's o-proj + MLP only for the rows that produce logits (prefill
+        # chunks sample one row each): skipped when layers' hidden states are captured
+        trim = (idx is not None and self.has_head and self.num_local_layers > 0 and TRIM_LAST_LAYER
+                and not self.capture_layers and idx.shape[0] < h.shape[0])
         if self.num_local_layers:
             # a fresh residual tensor: fused_add_rmsnorm updates it in place
-            h, residual = self.forward_layers(h.clone() if not self.has_embed else h, meta)
+            h, residual = self.forward_layers(h.clone() if not self.has_embed else h, meta,
+                                              trim_last=idx if trim else None)
         if not self.has_head:
             return h if residual is None else h + residual
-        return self.compute_logits(h, residual, meta.logits_indices)
+        return self.compute_logits(h, residual, None if trim else idx)
 
     def compute_logits(self, h, residual, idx):
         eps = self.cfg.rms_eps

@@ -224,3 +224,22 @@ def test_layer_truncated_model_name():
     c = get_config("llama3-70b@L8")
     full = get_config("llama3-70b")
     assert c.num_layers == 8 and c.hidden_size == full.hidden_size and c.num_kv_heads == full.num_kv_heads
+
+
+def test_trimmed_last_layer_matches_full(monkeypatch):
+    """Prefill steps run the last layer's o-proj + MLP only on the rows that
+    produce logits; the sampled tokens and logits equal the untrimmed model's."""
+    import dgi.models.llama as llama
+    from dgi.engine import EngineConfig, LLMEngine
+    from dgi.sched.request import SamplingParams
+    cfg = EngineConfig(model="llama-tiny", device="cpu", max_num_seqs=4, max_num_batched_tokens=64,
+                       max_model_len=256, use_graphs=False, num_blocks=64)
+    g = torch.Generator().manual_seed(5)
+    prompts = [torch.randint(5, 500, (n,), generator=g).tolist() for n in (37, 20, 51)]
+    sp = SamplingParams(max_tokens=5, temperature=0.0, ignore_eos=True)
+    outs = {}
+    for flag in (True, False):
+        monkeypatch.setattr(llama, "TRIM_LAST_LAYER", flag)
+        eng = LLMEngine(cfg)
+        outs[flag] = [r.output for r in eng.generate(prompts, sp)]
+    assert outs[True] == outs[False]
