@@ -36,7 +36,7 @@ from dgi.parallel.fabric import Fabric
 from dgi.parallel.plan import plan_layer_split
 from dgi import ops
 from dgi.runtime.batch import AttnMeta
-from dgi.runtime.model_runner import DEFAULT_BUCKETS, ModelRunner
+from dgi.runtime.model_runner import DEFAULT_BUCKETS, ModelRunner, graph_capture
 from dgi.utils.trace import mark, phase
 
 KIND_STOP, KIND_FWD, KIND_KV, KIND_PAUSE = 0, 1, 2, 3
@@ -115,7 +115,7 @@ class StageGraphs:
                 self._body(b)
                 torch.cuda.synchronize()
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=self.pool):
+                with graph_capture(g, pool=self.pool):
                     out = self._body(b)
                 if self.pool is None:
                     self.pool = g.pool()

@@ -11,7 +11,9 @@
 """
 from __future__ import annotations
 
+import contextlib
 import dataclasses
+import gc
 import os
 from typing import Optional
 
@@ -42,6 +44,23 @@ class StepResult:
     tokens: list          # sampled token per logits row (decode rows first, then sampled chunks)
     rows: list            # Request per sampled row
     hidden: Optional[torch.Tensor] = None
+
+
+@contextlib.contextmanager
+def graph_capture(g, pool=None):
+    """``torch.cuda.graph`` with Python's cyclic GC held off while the stream is
+    capturing: a collection that frees an object owning device memory or a graph
+    from an earlier engine during capture aborts the process (seen in the GPU
+    suite when one engine's graphs were collected while the next engine captured)."""
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        with torch.cuda.graph(g, pool=pool):
+            yield
+    finally:
+        if was:
+            gc.enable()
 
 
 class ModelRunner:
@@ -292,7 +311,7 @@ class GraphRunner:
             self._body(b)
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self.pool_handle):
+            with graph_capture(g, pool=self.pool_handle):
                 self._body(b)
             if self.pool_handle is None:
                 self.pool_handle = g.pool()

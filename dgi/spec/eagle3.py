@@ -49,6 +49,8 @@ from typing import Optional
 
 import numpy as np
 import torch
+
+from dgi.runtime.model_runner import graph_capture
 import torch.nn.functional as F
 
 from dgi import ops
@@ -335,7 +337,7 @@ class _VerifyGraph:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize(eng.device)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, pool=eng._graph_pool):
+        with graph_capture(self.graph, pool=eng._graph_pool):
             self.out = self._body()
 
     def run(self, R: int, tok: torch.Tensor, par: torch.Tensor, pos, slots, brows, ctx, samp):
@@ -479,7 +481,7 @@ class _DraftGraph:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize(eng.device)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, pool=eng._graph_pool):
+        with graph_capture(self.graph, pool=eng._graph_pool):
             self.out = self._body()
 
     def run(self, R: int, g_root: torch.Tensor, last: list, n_vec, brows):

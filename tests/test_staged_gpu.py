@@ -95,3 +95,14 @@ def test_rccl_pd_on_shared_gpu(shared_rccl, monkeypatch, replicas, world):
     drivers = [1, 2] if replicas == 2 else [1]
     got = tpc._merged(out, *drivers)
     assert _agree(got, ref) >= 0.75, (got, ref)
+
+
+def test_rccl_pdpp_serves_local_prompts_on_shared_gpu(shared_rccl, monkeypatch):
+    """1 prefill rank + a 2-stage decode pipeline whose driver also admits prompts
+    of its own (the hybrid decode of the 70B N=4 layout), over RCCL."""
+    monkeypatch.setenv("DGI_TEST_PREFILL", "1")
+    monkeypatch.setenv("DGI_TEST_LOCAL", "2")
+    ref = tpc._reference_outputs(model="llama-tiny-hd128")
+    out = tpc._spawn("_pd_body", 3, timeout=150)
+    got = tpc._merged(out, 1)
+    assert _agree(got, ref) >= 0.75, (got, ref)
