@@ -49,8 +49,6 @@ from typing import Optional
 
 import numpy as np
 import torch
-
-from dgi.runtime.model_runner import graph_capture
 import torch.nn.functional as F
 
 from dgi import ops
@@ -60,6 +58,7 @@ from dgi.models.config import ModelConfig
 from dgi.models.llama import LlamaModel, _rand
 from dgi.runtime.batch import AttnMeta
 from dgi.sched.request import Request
+from dgi.runtime.model_runner import graph_capture
 
 
 @dataclasses.dataclass
