@@ -18,7 +18,7 @@ def main(path, title="", top=30):
         n = r["Name"]
         k = ("GEMM (hipBLASLt)" if "Cijk" in n else "dgi HIP kernels" if any(x in n for x in (
             "rmsnorm", "rope_cache", "paged_decode", "prefill_attn", "silu_mul", "sample_kernel", "decode_reduce",
-            "kv_", "tree_", "topk")) else "other (torch)")
+            "kv_", "tree_", "topk", "mfma_gemm", "skinny", "topkp")) else "other (torch)")
         groups[k] = groups.get(k, 0.0) + float(r["TotalDurationNs"])
     print("\n| group | % time |\n|---|---:|")
     for k, v in sorted(groups.items(), key=lambda kv: -kv[1]):
