@@ -34,6 +34,8 @@ from dgi.runtime.batch import AttnMeta
 
 # DGI_TRIM_LAST_LAYER=0 runs the last layer's o-proj and MLP on every row (A/B switch)
 TRIM_LAST_LAYER = os.environ.get("DGI_TRIM_LAST_LAYER", "1") != "0"
+# DGI_QKV_PAD=0: the QKV GEMM runs on the step's T rows even when the MLP ran padded
+QKV_PAD = os.environ.get("DGI_QKV_PAD", "1") != "0"
 
 class LlamaLayerWeights:
     __slots__ = ("in_norm", "qkv", "o", "post_norm", "gate_up", "down", "qkv_bias")
@@ -325,13 +327,19 @@ class LlamaModel:
         Mp = self._mlp_rows(T, h) if self.layers else T
         # hand-written MFMA GEMMs where the start-up table measured them faster (dgi.runtime.gemm_pad)
         mfma_gu, mfma_dn = self.mlp_impl(Mp) if (self.mlp_impl is not None and self.layers) else (False, False)
+        hfull = None
         for i, L in enumerate(self.layers):
             if residual is None:
                 residual = h
                 h = ops.rmsnorm(h, L.in_norm, eps)
             else:
                 ops.fused_add_rmsnorm(h, residual, L.in_norm, eps)
-            qkv = ops.linear(h, L.qkv, L.qkv_bias)
+            if hfull is not None:
+                # the previous MLP ran on Mp padded rows (zeros past T): the QKV GEMM
+                # reuses them, at the row count the start-up table timed for the layer
+                qkv = ops.linear(hfull, L.qkv, L.qkv_bias)[:T]
+            else:
+                qkv = ops.linear(h, L.qkv, L.qkv_bias)
             attn = self.attention(i, qkv, meta)
             if trim_last is not None and i == len(self.layers) - 1:
                 attn = attn.index_select(0, trim_last)
@@ -358,6 +366,7 @@ class LlamaModel:
             act = ops.mfma_gemm(x, L.gate_up, 1) if mfma_gu else ops.silu_mul(ops.linear(x, L.gate_up))
             h = ops.mfma_gemm(act, L.down, 0) if mfma_dn else ops.linear(act, L.down)
             if Mp > T:
+                hfull = h if QKV_PAD else None
                 h = h[:T]
             if self.reduce is not None:
                 self.reduce(h)

@@ -8,7 +8,8 @@ step's row count is whatever the scheduler packed, so it lands on both sides
 of those cliffs.
 
 The MLP is row-independent, so its rows can be padded for free as far as
-correctness goes: ``MlpPadTable.measure`` times gate_up + SiLU·mul + down for
+correctness goes (and so is the next layer's QKV GEMM, which reuses the MLP's
+padded output rows — zeros past T — so the table times it at the same row count): ``MlpPadTable.measure`` times gate_up + SiLU·mul + down for
 every multiple of ``step`` rows up to the token budget, and ``pad(T)`` returns
 the row count (a multiple of ``step``, at most ``max_grow`` larger than T)
 with the lowest measured time.  ``LlamaModel.forward_layers`` then lets the
@@ -45,7 +46,9 @@ class MlpPadTable:
 
     @classmethod
     def measure(cls, gate_up: torch.Tensor, down: torch.Tensor, m_min: int = 512, m_max: int = 4096,
-                step: int = 32, reps: int = 3) -> "MlpPadTable":
+                step: int = 32, reps: int = 3, qkv: Optional[torch.Tensor] = None) -> "MlpPadTable":
+        """``qkv``: the next layer's QKV GEMM runs on the same padded rows
+        (``LlamaModel.forward_layers``), so its time joins the objective."""
         from dgi import ops
         H = gate_up.shape[1]
         x = torch.randn(m_max, H, device=gate_up.device, dtype=gate_up.dtype) * 0.1
@@ -80,7 +83,8 @@ class MlpPadTable:
                 t = timed(lambda: ops.mfma_gemm(a[:m], down, 0))
                 if force or t < back:
                     back, b_mfma = t, True
-            times.append(front + back)
+            q = timed(lambda: ops.linear(x[:m], qkv)) if qkv is not None else 0.0
+            times.append(front + back + q)
             impls.append((f_mfma, b_mfma))
         return cls(grid, times, step, impls=impls)
 
@@ -120,4 +124,6 @@ def build_for_model(model, m_max: int, step: int = 32) -> Optional[MlpPadTable]:
     L = layers[0]
     if L.gate_up.device.type != "cuda" or m_max < 1024:
         return None
-    return MlpPadTable.measure(L.gate_up, L.down, m_max=m_max, step=step)
+    from dgi.models import llama
+    return MlpPadTable.measure(L.gate_up, L.down, m_max=m_max, step=step,
+                               qkv=L.qkv if llama.QKV_PAD else None)
