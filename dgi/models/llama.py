@@ -34,8 +34,12 @@ from dgi.runtime.batch import AttnMeta
 
 # DGI_TRIM_LAST_LAYER=0 runs the last layer's o-proj and MLP on every row (A/B switch)
 TRIM_LAST_LAYER = os.environ.get("DGI_TRIM_LAST_LAYER", "1") != "0"
-# DGI_QKV_PAD=0: the QKV GEMM runs on the step's T rows even when the MLP ran padded
-QKV_PAD = os.environ.get("DGI_QKV_PAD", "1") != "0"
+# DGI_QKV_PAD=1: the QKV GEMM reuses the MLP's padded rows; DGI_OPROJ_PAD=1: the o-proj
+# runs on a zero-padded attention output.  Both off by default: with them the start-up
+# table times qkv / o-proj at every row count too, and the 70B bench measured no gain
+# (1755 / 1743 vs 1761 / 1750 tok/s, profiles/r2_bench70b_qkvpad_ab.md)
+QKV_PAD = os.environ.get("DGI_QKV_PAD", "0") == "1"
+OPROJ_PAD = os.environ.get("DGI_OPROJ_PAD", "0") == "1"
 
 class LlamaLayerWeights:
     __slots__ = ("in_norm", "qkv", "o", "post_norm", "gate_up", "down", "qkv_bias")
@@ -85,6 +89,7 @@ class LlamaModel:
         # (P/D layer-streamed migration sends finished layers while later ones compute)
         self.layer_hook = None
         self._pad_buf: Optional[torch.Tensor] = None
+        self._attn_buf: Optional[torch.Tensor] = None
         self.load_info: Optional[dict] = None
         if checkpoint:
             # real weights: only this rank's layers / TP slices are read (dgi.models.weights)
@@ -212,7 +217,8 @@ class LlamaModel:
         return n
 
     # ------------------------------------------------------------------ forward
-    def attention(self, li: int, qkv: torch.Tensor, meta: AttnMeta, rope: bool = True) -> torch.Tensor:
+    def attention(self, li: int, qkv: torch.Tensor, meta: AttnMeta, rope: bool = True,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
         c = self.cfg
         kc = self.kv_cache[li, 0]
         vc = self.kv_cache[li, 1]
@@ -220,7 +226,8 @@ class LlamaModel:
             ops.rope_cache(qkv, meta.positions, self.cos_sin, c.num_heads, c.num_kv_heads, c.head_dim,
                            meta.slot_mapping, kc, vc, self.rope_mode)
         T = qkv.shape[0]
-        out = torch.empty(T, c.q_size, device=qkv.device, dtype=qkv.dtype)
+        if out is None:
+            out = torch.empty(T, c.q_size, device=qkv.device, dtype=qkv.dtype)
         nd = meta.num_decode
         if nd > 0:
             ops.paged_decode(qkv[:nd], kc, vc, meta.dec_block_tables, meta.dec_context_lens, c.num_heads,
@@ -243,6 +250,12 @@ class LlamaModel:
         if buf is None or buf.shape[0] < Mp or buf.dtype != like.dtype or buf.device != like.device:
             buf = self._pad_buf = torch.empty(max(Mp, 4096), like.shape[1], dtype=like.dtype, device=like.device)
         buf[T:Mp].zero_()       # pad rows: zeros in, ignored out
+        if OPROJ_PAD:           # attention output rows past T stay zero for the padded o-proj
+            ab = self._attn_buf
+            q = self.cfg.q_size
+            if ab is None or ab.shape[0] < Mp or ab.dtype != like.dtype or ab.device != like.device:
+                ab = self._attn_buf = torch.empty(max(Mp, 4096), q, dtype=like.dtype, device=like.device)
+            ab[T:Mp].zero_()
         return Mp
 
     def _fused_decode(self, h: torch.Tensor, meta: AttnMeta) -> tuple:
@@ -340,8 +353,10 @@ class LlamaModel:
                 qkv = ops.linear(hfull, L.qkv, L.qkv_bias)[:T]
             else:
                 qkv = ops.linear(h, L.qkv, L.qkv_bias)
-            attn = self.attention(i, qkv, meta)
-            if trim_last is not None and i == len(self.layers) - 1:
+            last = trim_last is not None and i == len(self.layers) - 1
+            attn_pad = Mp > T and OPROJ_PAD and not last
+            attn = self.attention(i, qkv, meta, out=self._attn_buf[:T] if attn_pad else None)
+            if last:
                 attn = attn.index_select(0, trim_last)
                 residual = residual.index_select(0, trim_last)
                 h = ops.linear(attn, L.o)
@@ -354,7 +369,12 @@ class LlamaModel:
                 if self.layer_hook is not None:
                     self.layer_hook(self.layer_start + i)
                 break
-            if Mp > T:
+            if attn_pad:
+                # attention wrote the first T rows of a zero-padded buffer: the o-proj runs on
+                # all Mp rows (zeros in, zeros out past T) straight into the MLP's input
+                torch.matmul(self._attn_buf[:Mp], L.o.t(), out=self._pad_buf[:Mp])
+                h = self._pad_buf[:T]
+            elif Mp > T:
                 # o-proj writes the first T rows of the padded MLP input
                 h = torch.matmul(attn, L.o.t(), out=self._pad_buf[:T])
             else:

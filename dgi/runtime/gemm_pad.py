@@ -46,13 +46,17 @@ class MlpPadTable:
 
     @classmethod
     def measure(cls, gate_up: torch.Tensor, down: torch.Tensor, m_min: int = 512, m_max: int = 4096,
-                step: int = 32, reps: int = 3, qkv: Optional[torch.Tensor] = None) -> "MlpPadTable":
-        """``qkv``: the next layer's QKV GEMM runs on the same padded rows
-        (``LlamaModel.forward_layers``), so its time joins the objective."""
+                step: int = 32, reps: int = 3, qkv: Optional[torch.Tensor] = None,
+                o_w: Optional[torch.Tensor] = None) -> "MlpPadTable":
+        """``qkv`` / ``o_w``: the next layer's QKV GEMM and this layer's o-proj run on
+        the same padded rows (``LlamaModel.forward_layers``), so their times join
+        the objective."""
         from dgi import ops
         H = gate_up.shape[1]
         x = torch.randn(m_max, H, device=gate_up.device, dtype=gate_up.dtype) * 0.1
         a = torch.randn(m_max, gate_up.shape[0] // 2, device=gate_up.device, dtype=gate_up.dtype) * 0.1
+        ao = torch.randn(m_max, o_w.shape[1], device=gate_up.device, dtype=gate_up.dtype) * 0.1 \
+            if o_w is not None else None
         grid = list(range(m_min, m_max + 1, step))
         times, impls = [], []
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -84,7 +88,8 @@ class MlpPadTable:
                 if force or t < back:
                     back, b_mfma = t, True
             q = timed(lambda: ops.linear(x[:m], qkv)) if qkv is not None else 0.0
-            times.append(front + back + q)
+            o = timed(lambda: ops.linear(ao[:m], o_w)) if o_w is not None else 0.0
+            times.append(front + back + q + o)
             impls.append((f_mfma, b_mfma))
         return cls(grid, times, step, impls=impls)
 
@@ -126,4 +131,4 @@ def build_for_model(model, m_max: int, step: int = 32) -> Optional[MlpPadTable]:
         return None
     from dgi.models import llama
     return MlpPadTable.measure(L.gate_up, L.down, m_max=m_max, step=step,
-                               qkv=L.qkv if llama.QKV_PAD else None)
+                               qkv=L.qkv if llama.QKV_PAD else None, o_w=L.o if llama.OPROJ_PAD else None)
