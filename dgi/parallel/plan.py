@@ -135,12 +135,16 @@ class RoleCapacity:
     mixed_tok_s: float
 
 
-# Llama-3-70B, bf16, measured on one MI355X (profiles/r1_pd_capacity_70b.md;
-# mixed = driver BENCH_r01 1653 tok/s).  A 3-stage replica (~27 layers per
-# stage, 768-row microbatches) is 2/3 of the 40-layer stage time.
+# Measured on one MI355X with scripts/pd_capacity.py (round 2: every timed decode row
+# really decodes — the round-1 table let early sequences finish inside the timed steps),
+# profiles/r2_pd_capacity.md.  decode_tok_s[k] = R / t(L/k layers, R rows) at the row
+# count the layouts use (768-row microbatches for 3-stage 70B replicas); mixed = the
+# 1-GPU bench.py rate (DP / slack filler).
 CAPACITY = {
-    "llama3-70b": RoleCapacity(prefill_tok_s=19.3 * 128, decode_tok_s={1: 4600.0, 2: 11500.0, 3: 15000.0},
-                               mixed_tok_s=1653.0),
+    "llama3-70b": RoleCapacity(prefill_tok_s=19.47 * 128, decode_tok_s={1: 5522.0, 2: 12826.0, 3: 17773.0},
+                               mixed_tok_s=1760.0),
+    "llama3-8b": RoleCapacity(prefill_tok_s=176.2 * 128, decode_tok_s={1: 31566.0, 2: 58028.0, 3: 69373.0},
+                              mixed_tok_s=11842.0),
 }
 
 

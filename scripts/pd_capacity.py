@@ -83,7 +83,9 @@ def decode_step_ms(model, rows, steps, prompt_len, gen_before, layers=None):
                                  graph_buckets=(rows,)), model_cfg=mc)
     eng.warmup()
     rng = random.Random(1)
-    sp = SamplingParams(max_tokens=gen_before + steps + 8, temperature=0.0, ignore_eos=True)
+    # nothing may finish inside the timed steps: the early admissions have already decoded
+    # while the later prompts were prefilling, so size max_tokens to the context budget
+    sp = SamplingParams(max_tokens=2048 - prompt_len - 8, temperature=0.0, ignore_eos=True)
     for _ in range(rows):
         eng.add_request(_prompt(rng, prompt_len, eng.model_cfg.vocab_size), sp)
     # prefill everything, then decode until the mean context reaches prompt_len + gen_before
@@ -98,6 +100,7 @@ def decode_step_ms(model, rows, steps, prompt_len, gen_before, layers=None):
         n += len(eng.step())
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    assert n == rows * steps, f"{n} decode outputs in {steps} steps of {rows} rows (sequences finished or were preempted)"
     del eng
     _release()
     return {"kind": "decode", "model": model, "layers": mc.num_layers, "rows": rows, "ctx": prompt_len + gen_before,
@@ -133,8 +136,9 @@ def main():
         demand = pre["prompts_per_s"] * out_per_prompt
         # S-stage pipeline, S microbatches of R rows: each stage step = t(L/S layers, R rows);
         # the pipeline emits S*R tokens per S stage steps -> R / t tokens/s
-        stage = {r["rows"]: r["rows"] / (r["ms_per_step"] / 1000) for r in dec if r["layers"] * 2 == 80}
-        single = {r["rows"]: r["rows"] / (r["ms_per_step"] / 1000) for r in dec if r["layers"] == 80}
+        L = get_config(a.model).num_layers
+        stage = {r["rows"]: r["rows"] / (r["ms_per_step"] / 1000) for r in dec if r["layers"] * 2 == L}
+        single = {r["rows"]: r["rows"] / (r["ms_per_step"] / 1000) for r in dec if r["layers"] == L}
         est = {"kind": "estimate", "prefill_gpu_output_demand_tok_s": round(demand, 1),
                "decode_gpu_tok_s": {k: round(v, 1) for k, v in single.items()},
                "decode_2stage_pipeline_tok_s": {k: round(v, 1) for k, v in stage.items()}}

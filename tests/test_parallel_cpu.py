@@ -244,8 +244,11 @@ def test_node_layout_defaults():
     assert lay.kind == "pdpp" and len(lay.decode_ranks) == 3 and len(lay.prefill_ranks) == 5
     assert plan_node_layout(1).kind == "single"
     assert plan_node_layout(2).kind == "pd"
-    four = plan_node_layout(4)
-    assert four.kind == "pdpp" and four.decode_groups == [[2, 3]]
+    four = plan_node_layout(4)     # 70B: 3 prefill GPUs feed one decode GPU (decode-bound; prefill overflow)
+    assert four.kind == "pd" and four.prefill_ranks == [0, 1, 2] and four.decode_groups == [[3]]
+    # 8B at 8 GPUs: whole-model decode replicas (prefill is fast, decode replicas are cheap)
+    eight_8b = plan_node_layout(8, model="llama3-8b")
+    assert eight_8b.kind == "pd" and len(eight_8b.decode_groups) == 3 and len(eight_8b.prefill_ranks) == 5
     assert plan_node_layout(8, "pd").decode_groups == [[5], [6], [7]]
     # explicit replica requests and legacy flat decode lists
     lay = plan_node_layout(8, "pdpp", prefill_ranks=4, decode_stages=2)
