@@ -147,6 +147,9 @@ class PrefillServer:
         pcfg = EngineConfig(**{**cfg.__dict__, "device": str(fabric.device),
                                "use_graphs": bool(cfg.use_graphs and local_cap > 0)})
         self.engine = LLMEngine(pcfg)
+        # capture the overflow-decode graphs now: a capture synchronises the device, and
+        # mid-serving that waits on KV sends whose receives the drivers have not posted yet
+        self.engine.warmup()
         self.bs = self.engine.pool.block_size
         self.ch = {d: CtrlChannel(fabric, d, CTRL) for d in self.drivers}
         self.credit, self.seq_credit = {}, {}
@@ -458,6 +461,9 @@ class DecodeDriver:
             self.engine = PipelineEngine(dcfg, fabric, self.group)
         else:
             self.engine = LLMEngine(dcfg)
+            # decode graphs before any migration is in flight (see PrefillServer: a lazy
+            # capture would synchronise the device on receives whose sends are still queued)
+            self.engine.warmup()
         self.L_local = self.engine.model.num_local_layers
         mc = self.engine.model_cfg
         self.mc = mc
