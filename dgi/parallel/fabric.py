@@ -227,7 +227,11 @@ class Fabric:
         return w, t
 
     def barrier(self) -> None:
-        dist.barrier()
+        """Host-side barrier on the gloo control group.  Callers synchronise their
+        own device first; an RCCL barrier would add an all-reduce kernel that spins
+        on every GPU until the last rank arrives (and, with ranks sharing a GPU in the
+        DGI_SHARED_GPU rehearsal, starves the work the late ranks still have queued)."""
+        dist.barrier(group=self.ctrl)
 
     def close(self) -> None:
         if self.watchdog is not None:
