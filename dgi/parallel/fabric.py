@@ -45,7 +45,15 @@ def local_device_index() -> int:
 
 def prepare_rccl_env() -> None:
     """Environment RCCL must see before its first communicator (call before
-    ``init_process_group('nccl')``)."""
+    ``init_process_group('nccl')``).
+
+    ``NCCL_RUNTIME_CONNECT=0``: every channel of a communicator connects when the
+    communicator is created (``Fabric.connect_pairs`` at start-up) instead of at the
+    first transfer that needs it.  A runtime connect is a blocking host handshake
+    with the peer; with one host thread per rank serving several pairs (a prefill
+    rank feeding three replicas, a replica fed by five prefill ranks) those
+    handshakes can wait on each other in a cycle in the middle of serving."""
+    os.environ.setdefault("NCCL_RUNTIME_CONNECT", "0")
     if shared_gpu():
         os.environ["NCCL_HOSTID"] = f"dgi-shared-rank{os.environ.get('RANK', '0')}"
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
@@ -185,8 +193,10 @@ class Fabric:
             if self.rank not in (a, b):
                 continue
             peer = b if self.rank == a else a
-            t = torch.full((1,), self.rank, dtype=torch.int64, device=dev)
-            r = torch.empty(1, dtype=torch.int64, device=dev)
+            # big enough for every protocol / channel a KV page transfer uses
+            n = int(os.environ.get("DGI_PAIR_WARMUP_ELEMS", 1 << 21)) if self.on_gpu else 1
+            t = torch.full((n,), self.rank, dtype=torch.int64, device=dev)
+            r = torch.empty(n, dtype=torch.int64, device=dev)
             if self.staged:
                 t, r = t.cpu(), r.cpu()
             if self.rank == a:
@@ -195,7 +205,7 @@ class Fabric:
             else:
                 dist.recv(r, peer)
                 dist.send(t, peer)
-            if int(r.item()) != peer:
+            if int(r[0].item()) != peer or int(r[-1].item()) != peer:
                 raise RuntimeError(f"rank {self.rank}: pair warm-up with {peer} returned {int(r.item())}")
         if self.on_gpu:
             torch.cuda.synchronize(self.device)
