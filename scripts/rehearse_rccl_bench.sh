@@ -31,6 +31,7 @@ for c in $cases; do
     pd3_2p_1d) run $c 3 --layout pd --prefill-ranks 2 --decode-replicas 1 || exit 1 ;;
     pdpp8_5p_pp3) run $c 8 --layout pdpp --prefill-ranks 5 --decode-stages 3 || exit 1 ;;
     pd8_5p_3d) run $c 8 --layout pd --prefill-ranks 5 --decode-replicas 3 || exit 1 ;;
+    pd8_5p_3d_nooverflow) run $c 8 --layout pd --prefill-ranks 5 --decode-replicas 3 --prefill-local-cap 0 || exit 1 ;;
     pd8_2p_6d) run $c 8 --layout pd --prefill-ranks 2 --decode-replicas 6 || exit 1 ;;
     pd4_3p_1d) run $c 4 --layout pd --prefill-ranks 3 --decode-replicas 1 || exit 1 ;;
     pd2_1p_1d_local) run $c 2 --layout pd --prefill-ranks 1 --decode-replicas 1 --decode-local-frac 0.46 || exit 1 ;;
