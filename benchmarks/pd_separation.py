@@ -1,7 +1,10 @@
 """Prefill/decode disaggregation benchmark (reference benchmarks/pd_separation.py, measured).
 
 ``--mode separated``: ``--prefill-workers`` prefill GPUs + ``--decode-workers``
-decode GPUs (a layer pipeline when > 1) on one node, KV over RCCL.
+decode GPUs on one node, KV over RCCL.  Every decode GPU is its own whole-model
+decode replica (the reference's worker model, pd_scheduler.py:274-323: 2P+6D =
+2 prefill + 6 decode workers); ``--decode-stages k`` groups them into
+``decode_workers / k`` decode layer pipelines of k stages instead.
 ``--mode hybrid``: the same GPUs as independent replicas (no P/D).
 ``--compare`` runs both.  Each run is ``bench.py`` under torch.distributed.run.
 """
@@ -25,8 +28,11 @@ def run(a, mode: str) -> dict:
     if a.concurrent:
         common += ["--concurrency", str(a.concurrent)]
     if mode == "separated":
-        layout = "pdpp" if a.decode_workers > 1 else "pd"
-        args = common + ["--layout", layout, "--prefill-ranks", str(a.prefill_workers)]
+        k = max(1, a.decode_stages)
+        if a.decode_workers % k:
+            raise SystemExit(f"--decode-workers {a.decode_workers} is not a multiple of --decode-stages {k}")
+        args = common + ["--layout", "pdpp" if k > 1 else "pd", "--prefill-ranks", str(a.prefill_workers),
+                         "--decode-stages", str(k), "--decode-replicas", str(a.decode_workers // k)]
         return run_bench(n, args)
     return run_bench(n, common + ["--layout", "dp"])
 
@@ -38,6 +44,8 @@ def main():
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--prefill-workers", type=int, default=2)
     ap.add_argument("--decode-workers", type=int, default=6)
+    ap.add_argument("--decode-stages", type=int, default=1,
+                    help="stages per decode replica (1: every decode GPU is a whole-model replica)")
     ap.add_argument("--num-requests", type=int, default=100, help="kept for CLI compatibility; load is step-bounded")
     ap.add_argument("--concurrent", type=int, default=0)
     ap.add_argument("--prompt-length", type=int, default=512)

@@ -86,6 +86,23 @@ def build(verbose: bool = False, force: bool = False) -> str:
     return OUT
 
 
+SHM_SRC = os.path.join(CSRC, "host", "shm_ring.cc")
+SHM_OUT = os.path.join(HERE, "_shm" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_shm(force: bool = False) -> str:
+    """``dgi/_shm*.so``: the shared-memory control-plane rings (plain C++ /
+    pybind11, no ROCm dependency, so the CPU test-suite uses the same code)."""
+    if not force and not _newer([SHM_SRC], SHM_OUT):
+        return SHM_OUT
+    import pybind11
+    py_inc = sysconfig.get_paths()["include"]
+    _run(["g++", "-O2", "-fPIC", "-shared", "-std=c++17", "-Wall", f"-I{pybind11.get_include()}", f"-I{py_inc}",
+          SHM_SRC, "-o", SHM_OUT, "-lrt"])
+    return SHM_OUT
+
+
 if __name__ == "__main__":
+    print(build_shm(force="--force" in sys.argv))
     p = build(verbose=True, force="--force" in sys.argv)
     print(p)

@@ -336,7 +336,10 @@ class LlamaModel:
         if self.layers:
             fq, fg = self._fused_decode(h, meta)
             if fq or fg:
-                return self._forward_layers_fused(h, meta, residual, fq, fg)
+                h, residual = self._forward_layers_fused(h, meta, residual, fq, fg)
+                if trim_last is not None:     # same contract as the unfused path: only the logits rows
+                    h, residual = h.index_select(0, trim_last), residual.index_select(0, trim_last)
+                return h, residual
         Mp = self._mlp_rows(T, h) if self.layers else T
         # hand-written MFMA GEMMs where the start-up table measured them faster (dgi.runtime.gemm_pad)
         mfma_gu, mfma_dn = self.mlp_impl(Mp) if (self.mlp_impl is not None and self.layers) else (False, False)

@@ -39,9 +39,9 @@ def run_distributed(args, layout_kind: str, dist):
     layout = plan_node_layout(world, layout_kind, getattr(args, "prefill_ranks", None) or None,
                               decode_stages=getattr(args, "decode_stages", None) or None,
                               decode_replicas=getattr(args, "decode_replicas", None) or None, model=args.model)
-    # every RCCL pair communicator up front (one tiny send/recv per pair, deadlock-free order)
-    t_pairs = f.connect_pairs(layout.p2p_pairs()) if layout.kind != "pp" else \
-        f.connect_pairs([(a, b) for a, b in zip(range(world), range(1, world))])
+    # every communicator of the layout up front (world KV pairs + pipeline sub-communicators),
+    # each warmed with one transfer per pair in a deadlock-free order
+    t_pairs = f.setup_layout(layout)
     # decode-side concurrency: one microbatch of 768 rows per decode stage keeps the
     # decode GEMMs out of the small-M regime (70B down-proj: 0.76 PF/s at M=512,
     # 1.28 at 1024); a single decode GPU is capped by its KV pool (credits) instead
@@ -146,9 +146,11 @@ def _run_pp(args, f, cfg, layout, role, sp, rng, conc):
         f.barrier()
         el = time.perf_counter() - t0
         eng.stop_stages()
-        return toks, el, ttfts, {"steps": eng.stats["steps"]}
+        return toks, el, ttfts, {"tokens": toks, "steps": eng.stats["steps"],
+                                 "token_wait_s": round(eng.wait_s, 3)}
     w = StageWorker(cfg, f, ranks)
     w.run()
+    torch.cuda.synchronize() if f.device.type == "cuda" else None
     f.barrier()
     t0 = time.perf_counter()
     w.run()
@@ -201,8 +203,9 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
                 ttfts += srv.ttfts[before:]
             return n, ttfts
 
-        # at each phase boundary: fence first (the drivers post the receives of everything
-        # announced), then synchronise — on RCCL an unmatched KV send never completes
+        # at each phase boundary: fence = drain every KV transfer this rank started (the
+        # decode ranks keep servicing their handshakes) and report the migration count;
+        # afterwards nothing is in flight and the device can be synchronised
         serve_until_phase()
         srv.fence()
         torch.cuda.synchronize() if f.device.type == "cuda" else None
@@ -303,12 +306,14 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
         return n, el, list(local_ttfts), {"tokens": n, "received": drv.received, "running_at_end": running,
                                           "recv_GB": round(drv.recv_bytes / 1e9, 3), "local_fraction": local_frac,
                                           "steps": drv.engine.stats["steps"], "tpots": _tpots(finished),
+                                          "kv_transport": drv.kvr.stats(),
                                           "e2es": [r.finish_time - r.arrival for r in finished
                                                    if r.finish_time is not None]}
 
-    # later stages of a decode pipeline replica
-    w = StageWorker(cfg, f, layout.group_of(f.rank))
+    # later stages of a decode pipeline replica (receive their KV slices from the prefill ranks)
+    w = StageWorker(cfg, f, layout.group_of(f.rank), kv_sources=layout.prefill_ranks)
     w.run()
+    torch.cuda.synchronize() if f.device.type == "cuda" else None
     f.barrier()
     t0 = time.perf_counter()
     w.run()
@@ -316,4 +321,5 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
     f.barrier()
     el = time.perf_counter() - t0
     w.run()
-    return 0, el, [], {"tokens": 0, "stage_steps": w.steps}
+    return 0, el, [], {"tokens": 0, "stage_steps": w.steps, "installed": w.installed,
+                       "kv_transport": w.kvr.stats() if w.kvr is not None else None}

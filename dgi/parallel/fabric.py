@@ -1,26 +1,53 @@
-"""RCCL fabric: process groups and point-to-point channels between ranks.
+"""RCCL fabric: process groups, data channels and the node-local control plane.
 
-One process per GPU.  On MI355X the default group is ``nccl`` (= RCCL on
-ROCm) and every tensor moved between GPUs of the node goes over xGMI as an
-RCCL send/recv — pipeline activations and prefill->decode KV pages alike
-(SURVEY §2.9.2 C1-C4).  A second ``gloo`` group carries small control
-messages that must be polled without blocking a GPU stream (P/D admission
-headers, credits).  On a CPU-only box both roles fall back to gloo, which is
-how the multi-process tests run.
+One process per GPU.  On MI355X the data plane is RCCL (``nccl`` backend) over
+xGMI; on a CPU box (tests) everything falls back to gloo.
 
-Sends run on a dedicated comm stream so a send waiting for its peer never
-stalls the compute stream; buffers stay referenced until their work
-completes.
+Data plane (device tensors)
+  * ``kv`` — the world communicator, created EAGERLY (``init_process_group``
+    with ``device_id``) so every point-to-point op runs on the one world
+    communicator instead of a lazily created 2-rank communicator per pair
+    (round 2: one extra RCCL stream per peer).  Carries prefill -> decode KV
+    pages only.
+  * ``pp`` — one sub-communicator per decode layer pipeline (``setup_layout``),
+    carrying stage activations only.  Keeping KV and activations on separate
+    communicators (= separate RCCL streams) is what makes the P/D protocol
+    deadlock-free: a KV receive never queues behind an activation transfer
+    and vice versa (``dgi.parallel.pd`` docstring has the argument).
+
+Hardware queues.  HIP maps a process's streams lazily onto
+``GPU_MAX_HW_QUEUES`` (4) hardware queues PER PRIORITY, round-robin; two
+streams on one queue are ordered (a spinning RCCL kernel blocks the other
+stream's work) — measured with ``scripts/probe_hwq.py``
+(``profiles/r3_hw_queue_probe.md``).  So communication lives on HIGH-priority
+streams (both RCCL communicators and the stream receives are posted from) and
+compute on the default stream: at most 3 high-priority streams per rank,
+never sharing a queue with each other or with compute.  ``stream_budget``
+counts them and the tests assert the bound for every role.
+
+Control plane (host, pollable): ``CtrlChannel`` — one shared-memory SPSC ring
+per directed rank pair and tag (``dgi/csrc/host/shm_ring.cc``), a memcpy and a
+release store per message, instead of the round-2 TCPStore round trip to rank
+0 per poll.  ``DGI_CTRL=store`` selects the store transport (multi-host
+debugging only).
 """
 from __future__ import annotations
 
+import atexit
 import datetime
 import os
+import time
+import uuid
 from typing import Optional
 
 import numpy as np
 import torch
 import torch.distributed as dist
+
+GPU_HW_QUEUES = 4          # HIP default hardware queues per priority class per process
+# DGI_BATCH_P2P=1: CTS'd sends to several peers leave as one RCCL group (concurrent links);
+# default 0: one ordered send each on the world communicator's stream
+BATCH_P2P = os.environ.get("DGI_BATCH_P2P", "0") == "1"
 
 
 def shared_gpu() -> bool:
@@ -44,42 +71,71 @@ def local_device_index() -> int:
 
 
 def prepare_rccl_env() -> None:
-    """Environment RCCL must see before its first communicator (call before
-    ``init_process_group('nccl')``).
+    """Environment RCCL must see before its first communicator.
 
-    ``NCCL_RUNTIME_CONNECT=0``: every channel of a communicator connects when the
-    communicator is created (``Fabric.connect_pairs`` at start-up) instead of at the
-    first transfer that needs it.  A runtime connect is a blocking host handshake
-    with the peer; with one host thread per rank serving several pairs (a prefill
-    rank feeding three replicas, a replica fed by five prefill ranks) those
-    handshakes can wait on each other in a cycle in the middle of serving."""
+    ``NCCL_RUNTIME_CONNECT=0``: every channel connects when the communicator
+    is created instead of at the first transfer that needs it (a runtime
+    connect is a blocking host handshake with the peer in the middle of
+    serving)."""
     os.environ.setdefault("NCCL_RUNTIME_CONNECT", "0")
+    # eager init already serialises unbatched p2p on the world communicator: that
+    # is the point, so the one-time warning is noise
+    os.environ.setdefault("TORCH_NCCL_SHOW_EAGER_INIT_P2P_SERIALIZATION_WARNING", "0")
     if shared_gpu():
         os.environ["NCCL_HOSTID"] = f"dgi-shared-rank{os.environ.get('RANK', '0')}"
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         os.environ.setdefault("NCCL_IB_DISABLE", "1")
 
 
+def _nccl_options():
+    """RCCL communicators on high-priority streams (their own hardware queues)."""
+    try:
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        return opts
+    except Exception:  # pragma: no cover - CPU-only torch builds
+        return None
+
+
+def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0) -> str:
+    """Initialise the default process group for this process (idempotent).
+
+    RCCL: eager init bound to this rank's GPU (``device_id``) with
+    high-priority communicator streams.  Returns the backend in use."""
+    if dist.is_initialized():
+        return dist.get_backend()
+    be = backend or ("nccl" if torch.cuda.is_available() and os.environ.get("DGI_STAGED_GPU", "0") != "1"
+                     else "gloo")
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29511")
+    to = datetime.timedelta(seconds=timeout_s)
+    if be == "nccl":
+        prepare_rccl_env()
+        dev = torch.device("cuda", local_device_index())
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", timeout=to, device_id=dev, pg_options=_nccl_options())
+    else:
+        dist.init_process_group(be, timeout=to)
+    return be
+
+
+_FABRICS = [0]
+
+
 class Fabric:
+    """Per-rank view of the node: communicators, streams and control rings."""
+
     def __init__(self, backend: Optional[str] = None, device: Optional[torch.device] = None,
                  timeout_s: float = 1800.0):
-        self.owns_pg = False
-        if not dist.is_initialized():
-            be = backend or ("nccl" if torch.cuda.is_available() else "gloo")
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            os.environ.setdefault("MASTER_PORT", "29511")
-            if be == "nccl":
-                prepare_rccl_env()
-                torch.cuda.set_device(local_device_index())
-            dist.init_process_group(be, timeout=datetime.timedelta(seconds=timeout_s))
-            self.owns_pg = True
+        self.owns_pg = not dist.is_initialized()
+        init_distributed(backend, timeout_s)
         self.rank = dist.get_rank()
         self.world = dist.get_world_size()
         self.backend = dist.get_backend()
         self.on_gpu = self.backend == "nccl"
         # "staged" mode: GPU compute with a gloo data plane (tensors bounce
         # through host memory).  Lets the multi-rank GPU code paths run when
-        # the ranks share one device (rehearsals on a single-GPU box).
+        # the ranks share one device without RCCL.
         self.staged = False
         if device is None:
             if self.on_gpu:
@@ -91,66 +147,169 @@ class Fabric:
             else:
                 device = torch.device("cpu")
         self.device = device
-        # control traffic gets its own gloo group so it never queues behind (or
-        # forms a dependency cycle with) data transfers on the RCCL pair channel
+        self.kv_group = None                 # world communicator
+        self.pp_groups: dict = {}           # tuple(stage ranks) -> sub-communicator
+        # host barriers / object gathers: gloo, never a spinning RCCL collective
         self.ctrl = dist.new_group(backend="gloo")
-        self.comm_stream = torch.cuda.Stream(device=device) if self.on_gpu else None
-        # KV-migration receives land on their own stream so decode compute never
-        # queues behind a multi-hundred-MB transfer (see ``irecv_async``)
-        self.recv_stream = torch.cuda.Stream(device=device) if self.on_gpu else None
+        # receives are POSTED from this (empty, high-priority) stream so the RCCL
+        # stream waits on nothing the compute stream has queued (a KV receive must
+        # never depend on this rank's own compute: pd.py deadlock argument)
+        self.recv_stream = torch.cuda.Stream(device=device, priority=-1) if self.on_gpu else None
         self._pending: list = []
         # DGI_DEBUG_STREAMS=1: send buffers must not be rewritten while in flight (dgi.utils.debug)
         from dgi.utils.debug import stream_checker
         self.checker = stream_checker()
+        # control plane
+        self.job = self._job_id()
+        self._rings_out: dict = {}
+        self._rings_in: dict = {}
+        self.ctrl_kind = os.environ.get("DGI_CTRL", "shm")
+        self.sent_msgs = 0
+        self.pairs_connected = 0
+        atexit.register(self._unlink_rings)
         # liveness watchdog over the rendezvous store (dgi.parallel.fault)
         self.watchdog = None
         if self.world > 1 and os.environ.get("DGI_WATCHDOG", "1") != "0":
             from dgi.parallel.fault import Watchdog
             self.watchdog = Watchdog(self.rank, self.world).start()
 
-    # ------------------------------------------------------------------ data (device tensors)
-    def send(self, t: torch.Tensor, dst: int) -> None:
-        """Ordered send on the data group; the compute stream is not blocked."""
+    # ------------------------------------------------------------------ set-up
+    def _job_id(self) -> str:
+        """Name space of this fabric's shared-memory rings (same on every rank)."""
+        from torch.distributed import distributed_c10d as c10d
+        _FABRICS[0] += 1
+        key = f"dgi/job/{_FABRICS[0]}"
+        store = c10d._get_default_store()
+        if self.rank == 0:
+            store.set(key, uuid.uuid4().hex[:12])
+        return store.get(key).decode()
+
+    def setup_layout(self, layout, warmup: bool = True) -> float:
+        """Create every communicator this node layout uses, on every rank in the
+        same order (collective), and move one tensor over each pair so that RCCL
+        connection set-up (and any failure of it) happens now.  Returns seconds."""
+        t0 = time.perf_counter()
+        groups = [tuple(g) for g in layout.pipeline_groups()]
+        for g in groups:                       # every rank, same order: new_group is collective
+            pg = dist.new_group(ranks=list(g), pg_options=_nccl_options() if self.on_gpu else None)
+            if self.rank in g:
+                self.pp_groups[g] = pg
+        if warmup:
+            self._warm(layout.kv_pairs(), None)
+            for g in groups:
+                if self.rank in g:
+                    self._warm(list(zip(g, g[1:])), self.pp_groups[g])
+        if self.on_gpu:
+            torch.cuda.synchronize(self.device)
+        return time.perf_counter() - t0
+
+    def connect_pairs(self, pairs: list) -> float:
+        """Warm up the world communicator over ``pairs`` (sorted, same list on every
+        rank: each rank walks its own pairs in that global order, so the walk cannot
+        deadlock on one FIFO stream)."""
+        t0 = time.perf_counter()
+        self._warm(pairs, None)
+        if self.on_gpu:
+            torch.cuda.synchronize(self.device)
+        return time.perf_counter() - t0
+
+    def _warm(self, pairs, group) -> None:
+        dev = self.device if (self.on_gpu or self.staged) else torch.device("cpu")
+        n = int(os.environ.get("DGI_PAIR_WARMUP_ELEMS", 1 << 21)) if self.on_gpu else 1
+        for a, b in sorted(pairs):
+            if self.rank not in (a, b):
+                continue
+            peer = b if self.rank == a else a
+            t = torch.full((n,), self.rank, dtype=torch.int64, device=dev)
+            r = torch.empty(n, dtype=torch.int64, device=dev)
+            if self.staged:
+                t, r = t.cpu(), r.cpu()
+            if self.rank == a:
+                dist.send(t, peer, group=group)
+                dist.recv(r, peer, group=group)
+            else:
+                dist.recv(r, peer, group=group)
+                dist.send(t, peer, group=group)
+            if int(r[0]) != peer or int(r[-1]) != peer:
+                raise RuntimeError(f"rank {self.rank}: pair warm-up with {peer} returned "
+                                   f"{int(r[0])}..{int(r[-1])}")
+            self.pairs_connected += 1
+
+    def pp_group(self, ranks) -> Optional[object]:
+        return self.pp_groups.get(tuple(ranks))
+
+    def stream_budget(self, roles: Optional[set] = None) -> dict:
+        """Streams this rank issues GPU work on, per priority class.
+
+        normal: the compute (default) stream, plus the host KV tier's copy stream
+        when one exists; high: the world (KV) communicator's RCCL stream, each
+        pipeline sub-communicator's, and the stream receives are posted from.
+        Each class must fit in ``GPU_HW_QUEUES`` so no two streams share a
+        hardware queue."""
+        high = ["rccl:kv", "recv"] + [f"rccl:pp{list(g)}" for g in self.pp_groups]
+        return {"normal": ["compute"], "high": high}
+
+    # ------------------------------------------------------------------ data plane (device tensors)
+    def send(self, t: torch.Tensor, dst: int, group=None) -> None:
+        """Ordered send; ordered after the compute stream's queued work (the
+        buffer's producer), never blocking it."""
         if self.staged:
             h = t.detach().cpu()
-            self._pending.append((dist.isend(h, dst), h, None))
+            self._pending.append((dist.isend(h, dst, group=group), h, None))
             self._reap()
             return
-        if self.on_gpu:
-            ev = torch.cuda.current_stream().record_event()
-            with torch.cuda.stream(self.comm_stream):
-                self.comm_stream.wait_event(ev)
-                w = dist.isend(t, dst)
-            self._track(w, t)
-        else:
-            self._track(dist.isend(t, dst), t)
+        self._track(dist.isend(t, dst, group=group), t)
 
-    def recv(self, t: torch.Tensor, src: int) -> torch.Tensor:
-        """Blocking (stream-ordered on GPU) receive into ``t``."""
+    def send_many(self, items: list, group=None) -> None:
+        """Several sends (``[(tensor, dst), ...]``) as ONE RCCL group: transfers to
+        different peers progress concurrently over their own xGMI links."""
+        if not items:
+            return
+        if self.staged or len(items) == 1 or not BATCH_P2P:
+            for t, d in items:
+                self.send(t, d, group=group)
+            return
+        ops_ = [dist.P2POp(dist.isend, t, d, group=group) for t, d in items]
+        works = dist.batch_isend_irecv(ops_)
+        for w, (t, _d) in zip(works, items):
+            self._track(w, t)
+
+    def recv(self, t: torch.Tensor, src: int, group=None) -> torch.Tensor:
+        """Receive into ``t``, stream-ordered after this rank's compute and before
+        anything the compute stream enqueues next (pipeline activations)."""
         if self.staged:
             h = torch.empty(t.shape, dtype=t.dtype)
-            dist.recv(h, src)
+            dist.recv(h, src, group=group)
             t.copy_(h)
             return t
-        w = dist.irecv(t, src)
+        w = dist.irecv(t, src, group=group)
         w.wait()
         return t
 
-    def irecv_async(self, t: torch.Tensor, src: int) -> "AsyncRecv":
-        """Post a receive into ``t`` without ordering it before later compute.
+    def irecv_async(self, t: torch.Tensor, src: int, group=None) -> "AsyncRecv":
+        """Post a receive into ``t`` that waits on NOTHING this rank has queued.
 
-        On RCCL the receive is enqueued with ``recv_stream`` as the issuing
-        stream, so nothing on the compute stream waits for it; poll
-        ``ready()`` from the host and call ``complete()`` to order follow-up
-        work (e.g. a page scatter) on ``recv_stream``."""
+        On RCCL it is posted from ``recv_stream`` (empty, high priority), so its
+        kernel starts at once on the communicator's own hardware queue; poll
+        ``ready()`` from the host and call ``complete()`` to order follow-up work
+        on the current stream.  ``t`` must have been allocated on
+        ``recv_stream`` (``alloc_recv``)."""
         if self.staged:
             h = torch.empty(t.shape, dtype=t.dtype)
-            return AsyncRecv(self, dist.irecv(h, src), t, host=h)
+            return AsyncRecv(self, dist.irecv(h, src, group=group), t, host=h)
         if self.on_gpu:
             with torch.cuda.stream(self.recv_stream):
-                w = dist.irecv(t, src)
+                w = dist.irecv(t, src, group=group)
             return AsyncRecv(self, w, t)
-        return AsyncRecv(self, dist.irecv(t, src), t)
+        return AsyncRecv(self, dist.irecv(t, src, group=group), t)
+
+    def alloc_recv(self, shape, dtype) -> torch.Tensor:
+        """A receive buffer owned by ``recv_stream`` (caching-allocator safe for
+        ``irecv_async``)."""
+        if self.on_gpu:
+            with torch.cuda.stream(self.recv_stream):
+                return torch.empty(shape, dtype=dtype, device=self.device)
+        return torch.empty(shape, dtype=dtype, device=self.device if self.staged else "cpu")
 
     def _track(self, w, t: torch.Tensor) -> None:
         rec = self.checker.on_send(t) if self.checker is not None else None
@@ -170,83 +329,60 @@ class Fabric:
                 keep.append((w, t, rec))
         self._pending = keep
 
+    def sends_in_flight(self) -> int:
+        self._reap()
+        return len(self._pending)
+
     def flush(self) -> None:
+        """Host-wait for every tracked send.  Only call when each of them is known
+        to have its receive posted (P/D: every send is clear-to-send gated)."""
         for w, _t, rec in self._pending:
             w.wait()
             self._done(rec)
         self._pending = []
-        if self.on_gpu:
-            torch.cuda.current_stream().wait_stream(self.comm_stream)
 
-    def connect_pairs(self, pairs: list) -> float:
-        """Create every point-to-point communicator this rank will use NOW, with
-        one tiny send/recv per pair, so that RCCL set-up (and any failure of
-        it) happens at start-up instead of inside the first KV migration or
-        pipeline hop.  ``pairs`` must be the same sorted list on every rank
-        (``NodeLayout.p2p_pairs``): each rank walks its own pairs in that
-        global order and the first unfinished pair always has both ends ready,
-        so the walk cannot deadlock.  Returns the seconds it took."""
-        import time as _time
-        t0 = _time.perf_counter()
-        dev = self.device if (self.on_gpu or self.staged) else torch.device("cpu")
-        for a, b in pairs:
-            if self.rank not in (a, b):
-                continue
-            peer = b if self.rank == a else a
-            # big enough for every protocol / channel a KV page transfer uses
-            n = int(os.environ.get("DGI_PAIR_WARMUP_ELEMS", 1 << 21)) if self.on_gpu else 1
-            t = torch.full((n,), self.rank, dtype=torch.int64, device=dev)
-            r = torch.empty(n, dtype=torch.int64, device=dev)
-            if self.staged:
-                t, r = t.cpu(), r.cpu()
-            if self.rank == a:
-                dist.send(t, peer)
-                dist.recv(r, peer)
-            else:
-                dist.recv(r, peer)
-                dist.send(t, peer)
-            if int(r[0].item()) != peer or int(r[-1].item()) != peer:
-                raise RuntimeError(f"rank {self.rank}: pair warm-up with {peer} returned {int(r.item())}")
-        if self.on_gpu:
-            torch.cuda.synchronize(self.device)
-        self.pairs_connected = len([1 for a, b in pairs if self.rank in (a, b)])
-        return _time.perf_counter() - t0
+    # ------------------------------------------------------------------ control plane
+    def _ring_name(self, src: int, dst: int, tag: str) -> str:
+        return f"/dgi.{self.job}.{src}.{dst}.{tag}"
 
-    # ------------------------------------------------------------------ control (host, pollable)
+    def ring_out(self, peer: int, tag: str, capacity: int):
+        key = (peer, tag)
+        r = self._rings_out.get(key)
+        if r is None:
+            from dgi.parallel.shm import create_ring
+            r = create_ring(self._ring_name(self.rank, peer, tag), capacity)
+            self._rings_out[key] = r
+        return r
+
+    def ring_in(self, peer: int, tag: str, wait_s: float = 0.0):
+        key = (peer, tag)
+        r = self._rings_in.get(key)
+        if r is None:
+            from dgi.parallel.shm import open_ring
+            r = open_ring(self._ring_name(peer, self.rank, tag), wait_s)
+            if r is not None:
+                self._rings_in[key] = r
+        return r
+
+    def _unlink_rings(self) -> None:
+        from dgi.parallel.shm import unlink
+        for r in list(self._rings_out.values()):
+            unlink(r.name)
+
     def ctrl_group(self):
         return self.ctrl
-
-    def ctrl_isend(self, arr: np.ndarray, dst: int):
-        t = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.int64))
-        w = dist.isend(t, dst, group=self.ctrl)
-        self._pending.append((w, t, None))
-        return w
-
-    def ctrl_send_tensor(self, t: torch.Tensor, dst: int) -> None:
-        """Non-blocking host tensor send on the control group."""
-        t = t.detach().cpu().contiguous()
-        self._pending.append((dist.isend(t, dst, group=self.ctrl), t, None))
-
-    def ctrl_recv_tensor(self, t: torch.Tensor, src: int) -> torch.Tensor:
-        dist.recv(t, src, group=self.ctrl)
-        return t
-
-    def ctrl_irecv(self, size: int, src: int):
-        t = torch.zeros(size, dtype=torch.int64)
-        w = dist.irecv(t, src, group=self.ctrl)
-        return w, t
 
     def barrier(self) -> None:
         """Host-side barrier on the gloo control group.  Callers synchronise their
         own device first; an RCCL barrier would add an all-reduce kernel that spins
-        on every GPU until the last rank arrives (and, with ranks sharing a GPU in the
-        DGI_SHARED_GPU rehearsal, starves the work the late ranks still have queued)."""
+        on every GPU until the last rank arrives."""
         dist.barrier(group=self.ctrl)
 
     def close(self) -> None:
         if self.watchdog is not None:
             self.watchdog.stop()
         self.flush()
+        self._unlink_rings()
         if self.owns_pg and dist.is_initialized():
             dist.destroy_process_group()
 
@@ -254,82 +390,116 @@ class Fabric:
 class AsyncRecv:
     """Handle of one ``Fabric.irecv_async``."""
 
-    __slots__ = ("f", "work", "t", "host", "done")
+    __slots__ = ("f", "work", "t", "host", "done", "t_post")
 
     def __init__(self, fabric: Fabric, work, t: torch.Tensor, host: Optional[torch.Tensor] = None):
         self.f, self.work, self.t, self.host, self.done = fabric, work, t, host, False
+        self.t_post = time.perf_counter()
 
     def ready(self) -> bool:
         # gloo completes a p2p receive only inside wait(): on CPU / staged runs
-        # report ready and let complete() block (rehearsals, not a hot path)
+        # report ready and let complete() block (the sender is clear-to-send
+        # gated, so the data is on its way)
         if self.done or not self.f.on_gpu:
             return True
         return self.work.is_completed()
 
     def complete(self) -> None:
-        """Make the data visible: afterwards work issued on ``fabric.recv_stream``
-        (GPU) or the host (CPU / staged) sees the received bytes."""
+        """Make the data visible to work issued next on the CURRENT stream (GPU) or
+        to the host (CPU / staged)."""
         if self.done:
             return
+        self.work.wait()       # GPU: current stream waits on the RCCL stream's event
+        if self.host is not None:
+            self.t.copy_(self.host)
         if self.f.on_gpu:
-            with torch.cuda.stream(self.f.recv_stream):
-                self.work.wait()
-        else:
-            self.work.wait()
-            if self.host is not None:
-                self.t.copy_(self.host)
+            self.t.record_stream(torch.cuda.current_stream())
         self.done = True
 
 
 class CtrlChannel:
-    """Pollable fixed-size int64 control messages to/from one peer.
+    """Pollable int64 control messages to/from one peer (one direction each way).
 
-    Carried by the c10d rendezvous store (TCPStore): a gloo ``irecv`` cannot
-    be polled (its completion is only observed by ``wait``), while a store
-    key can be checked without blocking.  Messages are sequence-numbered per
-    direction and deleted once read.  Used for P/D admission headers,
-    credits and end-of-stream markers — a few small messages per step.
-    """
+    Shared-memory rings by default (``dgi.parallel.shm``); ``DGI_CTRL=store``
+    uses the c10d store.  ``send`` pads to ``size`` words, ``send_var`` sends
+    any length; ``poll`` returns the next message or None, ``wait`` blocks.
+    Both ends must construct the channel (each creates its outgoing ring)."""
 
-    def __init__(self, fabric: Fabric, peer: int, size: int = 32, tag: str = "ctrl"):
-        from torch.distributed import distributed_c10d as c10d
+    RING_BYTES = 1 << 21
+
+    def __init__(self, fabric: Fabric, peer: int, size: int = 32, tag: str = "ctrl", capacity: int = 0):
         self.f = fabric
         self.peer = peer
         self.size = size
-        self.store = c10d._get_default_store()
-        self.me = fabric.rank
         self.tag = tag
+        self.me = fabric.rank
         self.sseq = 0
         self.rseq = 0
+        self.shm = fabric.ctrl_kind == "shm"
+        if self.shm:
+            cap = capacity or int(os.environ.get("DGI_SHM_RING_BYTES", self.RING_BYTES))
+            self._out = fabric.ring_out(peer, tag, cap)
+            self._in = None
+        else:
+            from torch.distributed import distributed_c10d as c10d
+            self.store = c10d._get_default_store()
 
-    def _key(self, src: int, dst: int, seq: int) -> str:
-        return f"dgi/{self.tag}/{src}->{dst}/{seq}"
+    # ---------------------------------------------------------------- shm
+    def _inbox(self, wait_s: float = 0.0):
+        if self._in is None:
+            self._in = self.f.ring_in(self.peer, self.tag, wait_s)
+        return self._in
 
+    def send_bytes(self, b: bytes) -> None:
+        self.f.sent_msgs += 1
+        if self.shm:
+            self._out.send(b, 600.0)
+        else:
+            self.store.set(f"dgi/{self.tag}/{self.me}->{self.peer}/{self.sseq}", b)
+        self.sseq += 1
+
+    def poll_bytes(self) -> Optional[bytes]:
+        if self.shm:
+            r = self._inbox()
+            return None if r is None else r.poll()
+        k = f"dgi/{self.tag}/{self.peer}->{self.me}/{self.rseq}"
+        if not self.store.check([k]):
+            return None
+        v = self.store.get(k)
+        self.store.delete_key(k)
+        self.rseq += 1
+        return v
+
+    def wait_bytes(self, timeout_s: float = 1800.0) -> bytes:
+        if self.shm:
+            r = self._inbox(timeout_s)
+            if r is None:
+                raise TimeoutError(f"rank {self.me}: ring {self.tag} from {self.peer} never created")
+            v = r.wait(timeout_s)
+            if v is None:
+                raise TimeoutError(f"rank {self.me}: no {self.tag} message from {self.peer} in {timeout_s}s")
+            return v
+        k = f"dgi/{self.tag}/{self.peer}->{self.me}/{self.rseq}"
+        self.store.wait([k], datetime.timedelta(seconds=timeout_s))
+        v = self.store.get(k)
+        self.store.delete_key(k)
+        self.rseq += 1
+        return v
+
+    # ---------------------------------------------------------------- int64 messages
     def send(self, arr) -> None:
         a = np.zeros(self.size, np.int64)
         v = np.asarray(arr, np.int64).ravel()
         a[: v.size] = v
-        self.store.set(self._key(self.me, self.peer, self.sseq), a.tobytes())
-        self.sseq += 1
+        self.send_bytes(a.tobytes())
 
     def send_var(self, arr) -> None:
         """Variable-length message (e.g. a prompt's token ids)."""
-        self.store.set(self._key(self.me, self.peer, self.sseq), np.asarray(arr, np.int64).ravel().tobytes())
-        self.sseq += 1
+        self.send_bytes(np.ascontiguousarray(np.asarray(arr, np.int64).ravel()).tobytes())
 
     def poll(self) -> Optional[np.ndarray]:
-        k = self._key(self.peer, self.me, self.rseq)
-        if not self.store.check([k]):
-            return None
-        return self._take(k)
+        v = self.poll_bytes()
+        return None if v is None else np.frombuffer(v, dtype=np.int64).copy()
 
-    def wait(self) -> np.ndarray:
-        k = self._key(self.peer, self.me, self.rseq)
-        self.store.wait([k])
-        return self._take(k)
-
-    def _take(self, k: str) -> np.ndarray:
-        v = self.store.get(k)
-        self.store.delete_key(k)
-        self.rseq += 1
-        return np.frombuffer(v, dtype=np.int64).copy()
+    def wait(self, timeout_s: float = 1800.0) -> np.ndarray:
+        return np.frombuffer(self.wait_bytes(timeout_s), dtype=np.int64).copy()

@@ -8,39 +8,40 @@ SURVEY §3.5).  Here:
   model per GPU (Llama-3-70B bf16 fits in 288 GB), batched/chunked prefill.
   When a prompt completes, its first token is sampled locally and its KV
   pages are packed per decode stage with the ``kv_gather`` HIP kernel (that
-  stage's layer slice, one contiguous buffer); each slice goes straight to
-  its stage with an RCCL send over that pair's own xGMI link.  Request
-  metadata rides the control store.
+  stage's layer slice, one contiguous buffer per layer group); each group goes
+  straight to its stage over RCCL — after a ready-to-send / clear-to-send
+  handshake (``dgi.parallel.kv_transfer``) that makes the data plane
+  deadlock-free by construction.  Request metadata rides the control plane.
 * **Decode replicas**: the node runs R decode replicas (``NodeLayout.
   decode_groups``), each a whole-model decode GPU or a decode layer pipeline.
-  A replica's **driver** (``DecodeDriver``) allocates pages, posts its slice
-  receive on a side stream (decode compute never waits on a migration in
-  flight), tells its later stages the page ids (they post their own receives
-  from the prefill rank) and admits the requests once their slice landed.
+  A replica's **driver** (``DecodeDriver``) allocates pages when a migration
+  is announced, tells its later stages the page ids (each stage receives its
+  own slice straight from the prefill rank) and admits the requests once the
+  driver's slice has landed; a stage installs every announced migration before
+  the first micro-step that can read it.
 * **Placement**: each prefill rank runs a node-local instance of the
   reference's ``PrefillDecodeScheduler`` (server/app/services/pd_scheduler.py
   API, reference :274-323): every replica is a registered DECODE worker whose
   KV headroom is the credit it granted this rank, and ``assign_job`` picks the
   replica by bandwidth x headroom / (1 + active) at admission.  Migrations
-  are accounted through ``KVCacheMigrator.record``.
+  are accounted through ``KVCacheMigrator.record`` (the reference's stub
+  transfer, pd_scheduler.py:452-479, is the RCCL path here).
 * **Flow control**: every driver grants block *credits* to every prefill
   rank; a prefill rank admits a prompt only when some replica holds credit
-  for the whole sequence (prompt + max_tokens), and credits flow back when
-  sequences finish, so no decode pool can run out and nothing is ever
-  preempted on the decode side.
+  for the whole sequence (prompt + max_tokens), and credits flow back — with
+  the ids of the finished requests — when sequences finish, so no decode pool
+  can run out and nothing is ever preempted on the decode side.
 
-Control messages (int64[CTRL]) on the rendezvous store:
-  MIGRATE n_reqs total_blocks meta_len tok_len chunk_layers | CREDIT blocks seqs | DONE |
-  FINISHED rid tok code | TOKENS (rid tok code)* | FIRST n (tok code)*
+Control messages (int64, "ctrl" tag, prefill <-> driver):
+  MIGRATE n_reqs total_blocks meta_len tok_len chunk_layers key | CREDIT blocks seqs rid* | DONE |
+  FENCE n_migrations | FINISHED rid tok code | TOKENS (rid tok code)* | FIRST n (tok code)*
 
 Layer-streamed migration (``stream_layers`` = C > 0): the
 prefill rank announces the prompts that finish in a step BEFORE it runs
-(MIGRATE, first tokens unknown), and a model layer hook sends each C-layer
-group of their pages (kv_gather on the compute stream -> RCCL send on the comm
-stream) as soon as the step's forward has written those layers, so the
-transfer overlaps the remaining layers' compute; the first tokens follow in a
-FIRST message once sampled.  The receiving stages post one receive per group
-into the matching layer slice of their buffer.
+(MIGRATE, first tokens unknown), and a model layer hook gathers each C-layer
+group of their pages as soon as the step's forward has written those layers;
+each group is its own handshake transfer, so the data overlaps the remaining
+layers' compute.  The first tokens follow in a FIRST message once sampled.
 """
 from __future__ import annotations
 
@@ -57,14 +58,15 @@ from dgi import ops
 from dgi.engine import EngineConfig, LLMEngine, StepOutput
 from dgi.models.config import get_config
 from dgi.parallel.fabric import CtrlChannel, Fabric
+from dgi.parallel.kv_transfer import KVReceiver, KVSender, scatter_groups
 from dgi.parallel.pipeline import PipelineEngine
 from dgi.parallel.plan import NodeLayout
 from dgi.sched.request import Request, SamplingParams, Status
 from dgi.utils.trace import mark, phase
 
 MSG_MIGRATE, MSG_CREDIT, MSG_DONE, MSG_FINISHED, MSG_TOKENS, MSG_FIRST = 1, 2, 3, 4, 5, 6
-# a prefill rank has stopped stepping: every migration it announced before this message
-# is on this channel, so once the driver has posted their receives the rank's sends can drain
+# a prefill rank has stopped stepping and drained every transfer it started: the
+# message carries how many migrations it announced to this driver in total
 MSG_FENCE = 7
 REASONS = {0: None, 1: "length", 2: "stop"}
 CTRL = 8
@@ -112,6 +114,10 @@ def _blocks_for(n_tokens: int, bs: int) -> int:
     return (n_tokens + bs - 1) // bs
 
 
+def _code(o) -> int:
+    return {"length": 1, "stop": 2}.get(o.finish_reason, 2) if o.finished else -1
+
+
 def _req_meta(r: Request, nblocks: int, first: Optional[int] = None) -> list:
     p = r.params
     age_us = int((time.perf_counter() - r.arrival) * 1e6)    # time since arrival on the prefill rank
@@ -147,11 +153,13 @@ class PrefillServer:
         pcfg = EngineConfig(**{**cfg.__dict__, "device": str(fabric.device),
                                "use_graphs": bool(cfg.use_graphs and local_cap > 0)})
         self.engine = LLMEngine(pcfg)
-        # capture the overflow-decode graphs now: a capture synchronises the device, and
-        # mid-serving that waits on KV sends whose receives the drivers have not posted yet
         self.engine.warmup()
         self.bs = self.engine.pool.block_size
         self.ch = {d: CtrlChannel(fabric, d, CTRL) for d in self.drivers}
+        # KV data plane: ready-to-send / clear-to-send with every decode rank
+        self.sender = KVSender(fabric, layout.decode_ranks)
+        # while the host waits for a step's sampled tokens it keeps the handshakes moving
+        self.engine.runner.wait_hook = self.sender.service
         self.credit, self.seq_credit = {}, {}
         for d in self.drivers:   # initial credit grant of every replica
             msg = self.ch[d].wait()
@@ -163,6 +171,8 @@ class PrefillServer:
         self.migrated = 0
         self.migrate_time = 0.0
         self.sent_bytes = 0
+        self.announced = collections.Counter()     # migrations announced per driver (FENCE count)
+        self.next_key = 1
         # each replica's stages are sent their own layer slice of every page
         from dgi.parallel.pipeline import stage_split
         self.splits = {d: stage_split(self.engine.model_cfg, len(g)) for d, g in self.groups.items()}
@@ -180,21 +190,24 @@ class PrefillServer:
                 str(d), m.WorkerRole.DECODE, memory_bandwidth_gbps=MI355X_HBM_GBPS * len(g),
                 kv_cache_tokens_total=self.credit_total[d] * self.bs))
         self.migrator = m.KVCacheMigrator(self.pd)
-        self.placed: dict = {d: collections.deque() for d in self.drivers}
+        self.placed: dict = {d: set() for d in self.drivers}
         # layer-streamed migration: C-layer groups leave while later layers compute
         self.stream_layers = int(stream_layers)
-        self._streams: list = []       # this step's (driver, reqs, ids_t, {end layer: [(stage, c0, c1)]})
+        self._streams: list = []       # this step's (driver, reqs, ids_t, {end layer: [...]}, t0)
         self.streamed_bytes = 0
+        self._plans = {d: self.chunk_plan(self.splits[d], self.stream_layers) for d in self.drivers}
         if self.stream_layers > 0:
             self.engine.pre_execute = self._plan_stream
 
     @staticmethod
     def chunk_plan(split: list, C: int) -> list:
-        """(stage, c0, c1) layer groups of at most C layers inside each stage slice, in layer order."""
+        """(stage, c0, c1, group, ngroups) layer groups of at most C layers inside
+        each stage slice, in layer order (C <= 0: one group per stage)."""
         out = []
         for si, (a, b) in enumerate(split):
-            for c0 in range(a, b, C):
-                out.append((si, c0, min(b, c0 + C)))
+            gs = [(a, b)] if C <= 0 else [(c0, min(b, c0 + C)) for c0 in range(a, b, C)]
+            for gi, (c0, c1) in enumerate(gs):
+                out.append((si, c0, c1, gi, len(gs)))
         return out
 
     # ------------------------------------------------------------------ API
@@ -204,7 +217,12 @@ class PrefillServer:
         return r
 
     def busy(self) -> bool:
-        return bool(self.pending) or self.engine.has_unfinished()
+        """Work left: prompts, engine steps, or KV transfers not yet delivered."""
+        return bool(self.pending) or self.engine.has_unfinished() or self.sender.pending() > 0
+
+    def service(self) -> None:
+        """Move the KV handshakes forward (also called from inside engine waits)."""
+        self.sender.service()
 
     def _poll_credit(self) -> None:
         for d, ch in self.ch.items():
@@ -215,8 +233,11 @@ class PrefillServer:
                 if m[0] == MSG_CREDIT:
                     self.credit[d] += int(m[1])
                     self.seq_credit[d] += int(m[2])
-                    for _ in range(min(int(m[2]), len(self.placed[d]))):
-                        run_sync(self.pd.complete_job(self.placed[d].popleft(), self._pdm.JobPhase.DECODE))
+                    for rid in m[3:3 + int(m[2])]:      # exactly the sequences that finished
+                        key = str(int(rid))
+                        if key in self.placed[d]:
+                            self.placed[d].discard(key)
+                            run_sync(self.pd.complete_job(key, self._pdm.JobPhase.DECODE))
 
     def _pick(self, r: Request, need: int) -> Optional[int]:
         """Replica for a prompt needing ``need`` blocks: the P/D scheduler's
@@ -230,15 +251,21 @@ class PrefillServer:
             self.pd.update_worker_stats(str(d), {"kv_cache_tokens_used": used * self.bs,
                                                  "kv_cache_tokens_total": tot * self.bs})
         m = self._pdm
-        job = m.PendingJob(0.0, time.time(), str(r.rid), m.JobPhase.DECODE, len(r.prompt), r.params.max_tokens,
-                           kv_cache_key=f"kv:{r.rid}", kv_cache_worker=self.me)
+        job = m.PendingJob(0.0, time.time(), str(int(r.rid) & 0x7FFFFFFF), m.JobPhase.DECODE, len(r.prompt),
+                           r.params.max_tokens, kv_cache_key=f"kv:{r.rid}", kv_cache_worker=self.me)
         a = run_sync(self.pd.assign_job(job))
         d = int(a.worker_id)
         if not ok.get(d):
-            run_sync(self.pd.complete_job(str(r.rid), m.JobPhase.DECODE))
+            run_sync(self.pd.complete_job(job.job_id, m.JobPhase.DECODE))
             return None
-        self.placed[d].append(str(r.rid))
+        self.placed[d].add(job.job_id)
         return d
+
+    def _unplace(self, d: int, rid) -> None:
+        key = str(int(rid) & 0x7FFFFFFF)
+        if key in self.placed[d]:
+            self.placed[d].discard(key)
+            run_sync(self.pd.complete_job(key, self._pdm.JobPhase.DECODE))
 
     def _admit(self) -> None:
         while self.pending:
@@ -257,6 +284,24 @@ class PrefillServer:
             self.engine.scheduler.add(r)
             self.engine.requests[r.rid] = r
 
+    def _announce(self, d: int, rs: list, streamed: bool) -> tuple:
+        """MIGRATE message for requests ``rs`` to replica ``d``; returns (key, ids_t, nblk).
+        A streamed migration is announced before its step (first tokens follow in FIRST)."""
+        ids, meta, toks = [], [], []
+        for r in rs:
+            nb = _blocks_for(len(r.prompt) if streamed else r.num_computed, self.bs)
+            ids += r.blocks[:nb]
+            meta += _req_meta(r, nb, first=-1 if streamed else None) + [int(self.target[r.rid][1])]
+            toks += r.prompt
+        key = self.next_key
+        self.next_key += 1
+        self.announced[d] += 1
+        ids_t = torch.tensor(ids, dtype=torch.int32, device=self.f.device)
+        chunk = self.stream_layers if streamed else 0
+        self.ch[d].send([MSG_MIGRATE, len(rs), len(ids), len(meta), len(toks), chunk, key])
+        self.ch[d].send_var(np.asarray(meta + toks, dtype=np.int64))
+        return key, ids_t, len(ids)
+
     # ------------------------------------------------------------------ layer-streamed migration
     def _plan_stream(self, sb) -> None:
         """Before a step runs: announce the prompts whose prefill completes in it
@@ -265,36 +310,26 @@ class PrefillServer:
         fin = [c.req for c in sb.prefill if c.sample and c.req.rid not in self.local and c.req.rid in self.target]
         if not fin:
             return
-        dev = self.f.device
         by_d: dict = collections.defaultdict(list)
         for r in fin:
             by_d[self.target[r.rid][0]].append(r)
-        hooks_any = False
         for d, rs in by_d.items():
-            ids, meta, toks = [], [], []
-            for r in rs:
-                nb = _blocks_for(len(r.prompt), self.bs)
-                ids += r.blocks[:nb]
-                meta += _req_meta(r, nb, first=-1) + [int(self.target[r.rid][1])]
-                toks += r.prompt
-            ids_t = torch.tensor(ids, dtype=torch.int32, device=dev)
-            self.ch[d].send([MSG_MIGRATE, len(rs), len(ids), len(meta), len(toks), self.stream_layers])
-            self.ch[d].send_var(np.asarray(meta + toks, dtype=np.int64))
+            key, ids_t, nblk = self._announce(d, rs, streamed=True)
             by_end: dict = collections.defaultdict(list)
-            for si, c0, c1 in self.chunk_plan(self.splits[d], self.stream_layers):
-                by_end[c1 - 1].append((si, c0, c1))
-            self._streams.append((d, rs, ids_t, by_end, time.perf_counter()))
-            hooks_any = True
-        if hooks_any:
-            self.engine.model.layer_hook = self._layer_done
+            for item in self._plans[d]:
+                by_end[item[2] - 1].append(item)
+            self._streams.append((d, rs, ids_t, by_end, time.perf_counter(), key, nblk))
+        self.engine.model.layer_hook = self._layer_done
 
     def _layer_done(self, li: int) -> None:
         kv = self.engine.pool.kv
-        for d, _rs, ids_t, by_end, _t0 in self._streams:
-            for si, c0, c1 in by_end.get(li, ()):
+        for d, _rs, ids_t, by_end, _t0, key, nblk in self._streams:
+            for si, c0, c1, gi, ng in by_end.get(li, ()):
                 buf = ops.kv_gather(kv[c0:c1], ids_t)
-                self.f.send(buf, self.groups[d][si])
+                a = self.splits[d][si][0]
+                self.sender.submit(self.groups[d][si], buf, key, gi, ng, c0 - a, c1 - a, nblk)
                 self.streamed_bytes += buf.numel() * buf.element_size()
+        self.sender.service()
 
     def _finish_streams(self, outs) -> set:
         """After the step: first tokens (and finish codes) of the streamed prompts."""
@@ -304,21 +339,17 @@ class PrefillServer:
             return done
         by_rid = {o.rid: o for o in outs}
         eng = self.engine
-        for d, rs, ids_t, by_end, t0 in self._streams:
+        for d, rs, ids_t, by_end, t0, key, nblk in self._streams:
             msg = [MSG_FIRST, len(rs)]
-            nbytes = 0
             for r in rs:
                 o = by_rid[r.rid]
-                code = {"length": 1, "stop": 2}.get(o.finish_reason, 2) if o.finished else -1
+                code = _code(o)
                 msg += [int(o.token), code]
                 _d, need = self.target.pop(r.rid)
-                nbytes += _blocks_for(len(r.prompt), self.bs)
                 if o.finished:        # done at the first token: the decode side frees its pages
                     self.credit[d] += need
                     self.seq_credit[d] += 1
-                    if str(r.rid) in self.placed[d]:
-                        self.placed[d].remove(str(r.rid))
-                        run_sync(self.pd.complete_job(str(r.rid), self._pdm.JobPhase.DECODE))
+                    self._unplace(d, r.rid)
                     self.ch[self.router].send([MSG_FINISHED, int(o.rid), int(o.token), max(0, code)])
                 else:
                     eng.scheduler.finish(r, "migrated")
@@ -326,7 +357,7 @@ class PrefillServer:
                 done.add(r.rid)
             self.ch[d].send_var(msg)
             dt = time.perf_counter() - t0
-            pb = nbytes * self.engine.pool.page_bytes()
+            pb = nblk * self.engine.pool.page_bytes()
             self.migrator.record(f"kv:{rs[0].rid}", self.me, str(d), pb, dt * 1000.0)
             self.migrated += sum(1 for r in rs if not by_rid[r.rid].finished)
             self.sent_bytes += pb
@@ -336,12 +367,13 @@ class PrefillServer:
 
     def step(self) -> list[StepOutput]:
         from dgi.parallel.fault import plan
-        if plan():
-            plan().check(self.f.rank, self.engine.stats["steps"])
+        self.service()
         self._poll_credit()
         self._admit()
         if not self.engine.has_unfinished():
             return []
+        if plan():      # fault sites count engine steps (a call that only services transfers is not one)
+            plan().check(self.f.rank, self.engine.stats["steps"])
         outs = self.engine.step()
         streamed = self._finish_streams(outs)
         ready = []
@@ -360,8 +392,7 @@ class PrefillServer:
                 if o.finished:
                     self.local.discard(o.rid)
                 if self.report_tokens:
-                    report += [int(o.rid), int(o.token),
-                               {"length": 1, "stop": 2}.get(o.finish_reason, 2) if o.finished else -1]
+                    report += [int(o.rid), int(o.token), _code(o)]
                 continue
             self.first_tokens += 1
             if o.request.ttft is not None:
@@ -370,9 +401,7 @@ class PrefillServer:
                 d, need = self.target.pop(o.rid)
                 self.credit[d] += need
                 self.seq_credit[d] += 1
-                if self.placed[d] and str(o.rid) in self.placed[d]:
-                    self.placed[d].remove(str(o.rid))
-                    run_sync(self.pd.complete_job(str(o.rid), self._pdm.JobPhase.DECODE))
+                self._unplace(d, o.rid)
                 code = {"length": 1, "stop": 2}.get(o.finish_reason, 0)
                 self.ch[self.router].send([MSG_FINISHED, int(o.rid), int(o.token), code])
             else:
@@ -382,39 +411,31 @@ class PrefillServer:
                 self._migrate(ready)
         if report:
             self.ch[self.router].send_var([MSG_TOKENS] + report)
+        self.service()
         return outs
 
     def _migrate(self, reqs: list) -> None:
-        """Hand finished prefills to their decode replicas.
-
-        Request metadata (ids, sampling params, prompt tokens) travels on the
-        control store; each stage of the target replica receives ONLY its own
-        layer slice of the pages, straight from this rank over its own xGMI
-        link (no relay through the replica's driver)."""
+        """Hand finished prefills to their decode replicas (bulk: one transfer per
+        stage slice).  Each stage of the target replica receives ONLY its own layer
+        slice, straight from this rank over its own xGMI link."""
         eng = self.engine
-        dev = self.f.device
         by_d: dict = collections.defaultdict(list)
         for r in reqs:
             by_d[self.target[r.rid][0]].append(r)
         for d, rs in by_d.items():
             t0 = time.perf_counter()
-            ids, meta, toks = [], [], []
+            key, ids_t, nblk = self._announce(d, rs, streamed=False)
             for r in rs:
-                nb = _blocks_for(r.num_computed, self.bs)
-                ids += r.blocks[:nb]
-                meta += _req_meta(r, nb) + [int(self.target.pop(r.rid)[1])]
-                toks += r.prompt
-            ids_t = torch.tensor(ids, dtype=torch.int32, device=dev)
+                self.target.pop(r.rid)
             bufs = [ops.kv_gather(eng.pool.kv[a:b], ids_t) for a, b in self.splits[d]]
             from dgi.parallel.fault import plan
             if plan():
                 def corrupt():
                     bufs[0].view(-1)[: max(1, bufs[0].numel() // 64)] = float("nan")
                 plan().check(self.f.rank, self.migrated + 100000, corrupt=corrupt)
-            self.ch[d].send([MSG_MIGRATE, len(rs), len(ids), len(meta), len(toks)])
-            self.ch[d].send_var(np.asarray(meta + toks, dtype=np.int64))
-            for rank, buf in zip(self.groups[d], bufs):
-                self.f.send(buf, rank)
+            for si, (rank, buf) in enumerate(zip(self.groups[d], bufs)):
+                a, b = self.splits[d][si]
+                self.sender.submit(rank, buf, key, 0, 1, 0, b - a, nblk)
             for r in rs:
                 eng.scheduler.finish(r, "migrated")
                 eng.requests.pop(r.rid, None)
@@ -429,22 +450,32 @@ class PrefillServer:
         st = self.pd.get_stats()
         lat = self.migrator.latencies_ms
         st["migration_ms_p50"] = round(float(np.median(lat)), 3) if lat else None
+        st["kv_transport"] = self.sender.stats()
         return st
 
-    def fence(self) -> None:
-        """Tell every replica driver that this rank has stopped stepping (a benchmark
-        phase boundary).  On RCCL a KV send completes only once the receiver has
-        posted the matching receive, so a prefill rank must not synchronise its
-        device (or enter a collective) until the drivers have taken in every
-        migration it announced — ``DecodeDriver.await_fences`` is the other half."""
-        for ch in self.ch.values():
-            ch.send([MSG_FENCE])
+    def fence(self, timeout_s: float = 600.0) -> None:
+        """Phase boundary: finish every transfer this rank started (the decode ranks
+        keep servicing their handshakes meanwhile), then tell every replica driver
+        how many migrations it was announced in total.  Afterwards this rank has
+        nothing in flight and may synchronise its device."""
+        self.sender.drain(timeout_s)
+        for d, ch in self.ch.items():
+            ch.send([MSG_FENCE, self.announced[d]])
 
     def finish(self) -> None:
-        """End of stream: every replica driver keeps receiving until it sees DONE."""
+        """End of stream: drain, then every replica driver keeps serving until DONE."""
+        self.sender.drain()
         for ch in self.ch.values():
             ch.send([MSG_DONE])
         self.f.flush()
+
+
+class _Migration:
+    __slots__ = ("p", "key", "ids", "ids_t", "meta", "toks", "first_known")
+
+    def __init__(self, p, key, ids, ids_t, meta, toks, first_known):
+        self.p, self.key, self.ids, self.ids_t = p, key, ids, ids_t
+        self.meta, self.toks, self.first_known = meta, toks, first_known
 
 
 class DecodeDriver:
@@ -457,19 +488,25 @@ class DecodeDriver:
         self.group = layout.group_of(fabric.rank)
         assert self.group[0] == fabric.rank, "DecodeDriver runs on a replica's first rank"
         dcfg = EngineConfig(**{**cfg.__dict__, "device": str(fabric.device), "enable_prefix_caching": False})
+        self.prefill = list(layout.prefill_ranks)
         if len(self.group) > 1:
-            self.engine = PipelineEngine(dcfg, fabric, self.group)
+            self.engine = PipelineEngine(dcfg, fabric, self.group, kv_sources=self.prefill)
         else:
             self.engine = LLMEngine(dcfg)
-            # decode graphs before any migration is in flight (see PrefillServer: a lazy
-            # capture would synchronise the device on receives whose sends are still queued)
+            # decode graphs before any migration is in flight
             self.engine.warmup()
         self.L_local = self.engine.model.num_local_layers
         mc = self.engine.model_cfg
         self.mc = mc
         self.bs = self.engine.pool.block_size
-        self.prefill = list(layout.prefill_ranks)
         self.chans = {p: CtrlChannel(fabric, p, CTRL) for p in self.prefill}
+        self.kvr = KVReceiver(fabric, self.prefill, (2, mc.num_kv_heads, self.bs, mc.head_dim),
+                              self.engine.pool.dtype)
+        # waits inside the engine (sampled tokens, pipeline token returns) keep the
+        # receive queue moving
+        self.engine.runner.wait_hook = self.kvr.service
+        if isinstance(self.engine, PipelineEngine):
+            self.engine.idle_hook = self.kvr.service
         # node router (serving): the other replicas' drivers forward their tokens to it
         self.router = layout.drivers[0] if router is None else router
         self.is_router = fabric.rank == self.router
@@ -498,73 +535,63 @@ class DecodeDriver:
         self.prefill_finished: list = []   # (rid, token, reason) of sequences done at their first token
         self.remote_tokens: list = []      # (rid, token, reason|None) from prefill ranks / other replicas
         self.refund = collections.Counter()
-        self.refund_seqs = collections.Counter()
+        self.refund_rids: dict = collections.defaultdict(list)
         self.done = set()
-        self.fenced: set = set()    # prefill ranks at a phase boundary (MSG_FENCE)
-        self.inflight: list = []    # migrations whose pages are still on the wire
+        self.fenced: dict = {}      # prefill rank -> migrations it announced (MSG_FENCE)
+        self.announced = collections.Counter()
+        self.inflight: list = []    # announced migrations not admitted yet
         self.await_first: dict = {p: collections.deque() for p in self.prefill}
         self.received = 0
         self.recv_bytes = 0
 
-    def _post_migration(self, p: int, msg) -> None:
-        """Start receiving a migration from prefill rank ``p``: allocate pages,
-        post this stage's slice receive(s) off the compute stream, tell the
-        later pipeline stages (which post their own receives from ``p``).  A
-        layer-streamed migration (chunk_layers > 0) arrives as one message per
-        layer group and waits for its FIRST message (the sampled first tokens)."""
-        n_reqs, nblk, meta_len, tok_len, chunk = (int(x) for x in msg[1:6])
+    # ------------------------------------------------------------------ migrations
+    def _announced(self, p: int, msg) -> None:
+        """MIGRATE from ``p``: allocate pages and tell the later pipeline stages
+        (each receives its own layer slice straight from ``p``)."""
+        n_reqs, nblk, meta_len, tok_len, chunk, key = (int(x) for x in msg[1:7])
         payload = self.chans[p].wait()
         meta = payload[:meta_len].reshape(n_reqs, META_FIELDS + 1).tolist()
         toks = payload[meta_len:meta_len + tok_len].tolist()
-        dev = self.f.device
         ids = self.engine.pool.allocate(nblk)
-        ids_t = torch.tensor(ids, dtype=torch.int32, device=dev)
-        mc = self.mc
-        buf = torch.empty(self.L_local, 2, nblk, mc.num_kv_heads, self.bs, mc.head_dim, dtype=self.engine.pool.dtype,
-                          device=dev)
-        recs = [self.f.irecv_async(buf[a:b], p) for a, b in layer_groups(self.L_local, chunk)]
+        ids_t = torch.tensor(ids, dtype=torch.int32, device=self.f.device)
         if isinstance(self.engine, PipelineEngine):
-            self.engine.send_kv_notice(ids_t, p, chunk)
-        item = [p, recs, buf, ids, ids_t, meta, toks, chunk == 0]
+            self.engine.send_kv_notice(p, key, ids)
+        item = _Migration(p, key, ids, ids_t, meta, toks, chunk == 0)
         self.inflight.append(item)
+        self.announced[p] += 1
         if chunk:
             self.await_first[p].append(item)
-        self.recv_bytes += buf.numel() * buf.element_size()     # this stage's slice
 
     def _first(self, p: int, m) -> None:
         """FIRST message of the oldest streamed migration from ``p``."""
         item = self.await_first[p].popleft()
         n = int(m[1])
         for i in range(n):
-            item[5][i][3] = int(m[2 + 2 * i])           # first token
-            item[5][i][1] = int(m[3 + 2 * i])           # finish code (-1: keeps decoding)
-        item[7] = True
+            item.meta[i][3] = int(m[2 + 2 * i])           # first token
+            item.meta[i][1] = int(m[3 + 2 * i])           # finish code (-1: keeps decoding)
+        item.first_known = True
+
     def _admit_arrived(self, block: bool = False) -> None:
-        """Scatter every completed migration into the pool and admit its requests."""
+        """Install every migration whose slice has landed (and whose first tokens
+        are known) into the pool and admit its requests."""
         keep = []
+        self.kvr.service()
         for item in self.inflight:
-            p, recs, buf, ids, ids_t, meta, toks, first_known = item
-            if block and not first_known:
-                while not item[7]:       # the FIRST message follows its MIGRATE on the same channel
-                    self._poll_ctrl(p)
-                    time.sleep(0.0005)
-                first_known = True
-            if not (first_known and (block or all(r.ready() for r in recs))):
+            if block:
+                while not item.first_known:      # FIRST follows its MIGRATE on the same channel
+                    self._poll_ctrl(item.p)
+                    self.kvr.service()
+                    time.sleep(0.0002)
+                groups = self.kvr.wait_landed(item.p, item.key) if self.L_local else []
+            elif item.first_known and (self.L_local == 0 or self.kvr.is_landed(item.p, item.key)):
+                groups = self.kvr.take(item.p, item.key)
+            else:
                 keep.append(item)
                 continue
-            for r in recs:
-                r.complete()
-            mark("kv_migration_landed", len(meta))
-            if self.f.on_gpu:
-                rs = self.f.recv_stream
-                rs.wait_stream(torch.cuda.current_stream())     # ids_t was made on the compute stream
-                with torch.cuda.stream(rs):
-                    ops.kv_scatter(self.engine.pool.kv, ids_t, buf)
-                torch.cuda.current_stream().wait_stream(rs)
-                buf.record_stream(rs)
-            else:
-                ops.kv_scatter(self.engine.pool.kv, ids_t, buf)
-            self._admit(p, ids, meta, toks)
+            mark("kv_migration_landed", len(item.meta))
+            scatter_groups(self.engine.pool.kv, item.ids_t, groups)
+            self.recv_bytes += sum(b.numel() * b.element_size() for _a, _b, b in groups)
+            self._admit(item.p, item.ids, item.meta, item.toks)
         self.inflight = keep
 
     def _admit(self, p: int, ids: list, meta: list, toks: list) -> None:
@@ -592,7 +619,7 @@ class DecodeDriver:
             o += plen
             sch.add_prefilled(r, ids[k:k + nb])
             self.engine.requests[r.rid] = r
-            self.origin[r.rid] = (p, credit)
+            self.origin[r.rid] = (p, credit, rid)
             if self.track_arrivals:
                 self.arrivals.append(r)
             k += nb
@@ -609,6 +636,7 @@ class DecodeDriver:
         self.local_used[r.rid] = need
         return r
 
+    # ------------------------------------------------------------------ control
     def _poll_ctrl(self, p: int) -> None:
         ch = self.chans[p]
         while True:
@@ -619,13 +647,13 @@ class DecodeDriver:
 
     def _handle(self, p: int, m) -> None:
         if m[0] == MSG_MIGRATE:
-            self._post_migration(p, m)
+            self._announced(p, m)
         elif m[0] == MSG_FIRST:
             self._first(p, m)
         elif m[0] == MSG_DONE:
             self.done.add(p)
         elif m[0] == MSG_FENCE:
-            self.fenced.add(p)
+            self.fenced[p] = int(m[1])
         elif m[0] == MSG_FINISHED:
             if self.track_arrivals:
                 self.prefill_finished.append((int(m[1]), int(m[2]), REASONS.get(int(m[3]))))
@@ -658,8 +686,7 @@ class DecodeDriver:
         for o in outs:
             if o.request.user is None:
                 continue
-            msg += [int(o.request.user), int(o.token),
-                    {"length": 1, "stop": 2}.get(o.finish_reason, 2) if o.finished else -1]
+            msg += [int(o.request.user), int(o.token), _code(o)]
         if msg:
             self.fwd.send_var([MSG_TOKENS] + msg)
 
@@ -676,29 +703,44 @@ class DecodeDriver:
         for o in outs:
             if o.finished:
                 self.local_used.pop(o.rid, None)
-                p, credit = self.origin.pop(o.rid, (None, 0))
+                p, credit, prid = self.origin.pop(o.rid, (None, 0, 0))
                 if p is not None:
                     self.refund[p] += credit
-                    self.refund_seqs[p] += 1
-        for p in list(self.refund_seqs):
-            self.chans[p].send([MSG_CREDIT, self.refund[p], self.refund_seqs[p]])
+                    self.refund_rids[p].append(prid)
+        for p, rids in list(self.refund_rids.items()):
+            self.chans[p].send_var([MSG_CREDIT, self.refund[p], len(rids)] + rids)
         self.refund.clear()
-        self.refund_seqs.clear()
+        self.refund_rids.clear()
         if self.forward_tokens and not self.is_router:
             self._forward(arr, outs)
         return outs
 
+    def quiesced(self) -> bool:
+        """Every prefill rank has fenced and every migration it announced is admitted."""
+        return (len(self.fenced) == len(self.prefill) and not self.inflight
+                and all(self.announced[p] >= n for p, n in self.fenced.items()))
+
     def await_fences(self, timeout_s: float = 600.0) -> None:
-        """Keep taking in control messages (posting the receives of every announced
-        migration) until each prefill rank has sent its fence, then clear them."""
+        """Keep servicing control messages and KV handshakes until each prefill rank
+        has fenced and everything it announced has been admitted, then clear."""
+        from dgi.parallel.kv_transfer import DIAG_S, _diag
         t0 = time.perf_counter()
-        while len(self.fenced) < len(self.prefill):
+        nxt = t0 + DIAG_S
+        while True:
             for p in self.chans:
                 self._poll_ctrl(p)
-            if len(self.fenced) < len(self.prefill):
-                if time.perf_counter() - t0 > timeout_s:
-                    raise TimeoutError(f"prefill fences: got {sorted(self.fenced)} of {self.prefill}")
-                time.sleep(0.0005)
+            self._admit_arrived()
+            if self.quiesced():
+                break
+            if time.perf_counter() > nxt:
+                nxt += DIAG_S
+                _diag(f"driver {self.f.rank} awaiting fences: fenced {self.fenced}, announced "
+                      f"{dict(self.announced)}, not admitted {[(m.p, m.key) for m in self.inflight][:8]}; "
+                      + self.kvr.describe())
+            if time.perf_counter() - t0 > timeout_s:
+                raise TimeoutError(f"prefill fences: got {sorted(self.fenced)} of {self.prefill}, "
+                                   f"{len(self.inflight)} migrations not landed")
+            time.sleep(0.0002)
         self.fenced.clear()
 
     def all_prefill_done(self) -> bool:
@@ -711,6 +753,9 @@ class DecodeDriver:
         if isinstance(self.engine, PipelineEngine):
             self.engine.stop_stages()
         self.f.flush()
+
+    def stats(self) -> dict:
+        return {"kv_transport": self.kvr.stats()}
 
 
 def build_engine_config(model: str, **kw) -> EngineConfig:

@@ -2,22 +2,31 @@
 
 The reference chains stages with sequential HTTP/JSON hops, keeps no KV on
 the shards and has one stage busy at a time (worker/distributed/session.py:
-271-337, grpc_server.py:351-388).  Here S stages on S GPUs form an ordered
-RCCL channel ring:
+271-337, grpc_server.py:351-388).  Here S stages on S GPUs form a chain:
 
     driver (stage 0, scheduler + block tables + layers [0, l1))
-      --[header | step metadata | hidden]--> stage 1 --> ... --> stage S-1
-      <--------------------- sampled token ids ------------------------'
+      --[header + step metadata: shm ring | hidden: RCCL pp communicator]--> stage 1 --> ... --> stage S-1
+      <------------------- sampled token ids (shm ring, async D2H) -----------------------------'
 
 * every stage keeps the paged KV of its own layers; block ids are chosen by
   the driver's scheduler and are valid in every stage's pool (all pools have
   the same block count, agreed at start-up);
 * up to S microbatches (disjoint request sets) are in flight, so all GPUs
   work concurrently (``busy`` requests are skipped by the scheduler);
-* activations travel as ONE bf16 residual-stream tensor [T, H] per hop
-  (8192 * 2 B = 16 KiB per token on 70B);
-* the same channel carries KV-install messages (P/D migration into a decode
-  pipeline) and PAUSE/STOP control, so ordering is never ambiguous.
+* only the bf16 residual stream [T, H] moves over RCCL (8192 * 2 B = 16 KiB
+  per token on 70B), on the replica's own sub-communicator (``Fabric.
+  setup_layout``): activations never share an RCCL stream with KV migrations;
+* the step header + packed int32 metadata travel on the node-local
+  shared-memory control plane and every stage does its own pinned H2D copy,
+  so a stage reads the next hop's shape without touching its GPU;
+* the last stage copies sampled tokens to pinned memory asynchronously and
+  publishes them when the copy's event completes — no host sync in the stage
+  loop; the driver's wait for them keeps servicing its KV handshakes
+  (``idle_hook``);
+* P/D migrations into a decode pipeline: the driver sends each later stage the
+  page ids of an announced migration directly (``send_kv_notice``); the stage
+  receives its own layer slice from the prefill rank (``KVReceiver``) and
+  installs it before the first micro-step that follows the notice.
 """
 from __future__ import annotations
 
@@ -174,36 +183,35 @@ def stage_split(mc: ModelConfig, stages: int) -> list[tuple[int, int]]:
     return plan_layer_split(mc.num_layers, stages, 1.0, 0.0, head)
 
 
-def _hdr_tensor(hdr: np.ndarray, kind: int) -> torch.Tensor:
-    """Step header as a HOST tensor: headers travel on the gloo control group,
-    so a stage reads the shape of the next hop without synchronising its GPU
-    (its host runs ahead and enqueues the next receive + forward while the
-    current one still computes)."""
+def _pack(hdr, kind: int, flat: Optional[np.ndarray] = None) -> bytes:
+    """Control-plane message of one hop: int64 header (kind in word 0) + int32 metadata."""
     h = np.array(hdr, dtype=np.int64, copy=True)
     h[0] = kind
-    return torch.from_numpy(h)
+    return h.tobytes() + (b"" if flat is None else np.ascontiguousarray(flat, np.int32).tobytes())
+
+
+def _unpack(b: bytes):
+    hdr = np.frombuffer(b, dtype=np.int64, count=HDR)
+    flat = np.frombuffer(b, dtype=np.int32, offset=HDR * 8) if len(b) > HDR * 8 else None
+    return hdr, flat
 
 
 def agree_num_blocks(fabric: Fabric, ranks: list, mine: int) -> int:
-    """All stages of a pipeline use the minimum of their block budgets."""
+    """All stages of a pipeline use the minimum of their block budgets (host
+    control plane: no RCCL traffic before the communicators are warm)."""
     if len(ranks) == 1:
         return mine
+    from dgi.parallel.fabric import CtrlChannel
     me = ranks.index(fabric.rank)
-    t = torch.tensor([mine], dtype=torch.int64, device=fabric.device)
     if me == 0:
-        best = mine
-        for r in ranks[1:]:
-            fabric.recv(t, r)
-            best = min(best, int(t.item()))
-        out = torch.tensor([best], dtype=torch.int64, device=fabric.device)
-        for r in ranks[1:]:
-            fabric.send(out.clone(), r)
-        fabric.flush()
+        chans = [CtrlChannel(fabric, r, 1, tag="agree") for r in ranks[1:]]
+        best = min([mine] + [int(c.wait()[0]) for c in chans])
+        for c in chans:
+            c.send([best])
         return best
-    fabric.send(t, ranks[0])
-    fabric.flush()
-    fabric.recv(t, ranks[0])
-    return int(t.item())
+    c = CtrlChannel(fabric, ranks[0], 1, tag="agree")
+    c.send([mine])
+    return int(c.wait()[0])
 
 
 def stage_block_budget(mc: ModelConfig, device: torch.device, n_layers: int, cfg: EngineConfig) -> int:
@@ -223,7 +231,9 @@ class PipelineEngine(LLMEngine):
     """Stage 0 of an S-stage pipeline; same API as ``LLMEngine``."""
 
     def __init__(self, cfg: EngineConfig, fabric: Fabric, stage_ranks: list, microbatches: Optional[int] = None,
-                 model_cfg: Optional[ModelConfig] = None, split: Optional[list] = None):
+                 model_cfg: Optional[ModelConfig] = None, split: Optional[list] = None,
+                 kv_sources: Optional[list] = None):
+        from dgi.parallel.fabric import CtrlChannel
         self.f = fabric
         self.ranks = list(stage_ranks)
         assert self.ranks[0] == fabric.rank
@@ -246,6 +256,15 @@ class PipelineEngine(LLMEngine):
         self.inflight: collections.deque = collections.deque()
         self.next_rank = self.ranks[1] if len(self.ranks) > 1 else None
         self.last_rank = self.ranks[-1]
+        self.pp = fabric.pp_group(self.ranks)
+        # control plane: hop headers to stage 1, tokens back from the last stage,
+        # KV-migration notices straight to every later stage
+        self.hop = CtrlChannel(fabric, self.next_rank, HDR, tag="pp", capacity=1 << 23) if self.next_rank is not None \
+            else None
+        self.tok = CtrlChannel(fabric, self.last_rank, 1, tag="tok") if self.next_rank is not None else None
+        self.notice = {r: CtrlChannel(fabric, r, 1, tag="kvn") for r in self.ranks[1:]} if kv_sources else {}
+        self.idle_hook = None       # called while waiting for a microbatch's tokens (P/D: KV handshakes)
+        self.wait_s = 0.0
         # decode micro-steps of this stage replay hipGraphs (same buckets on every stage)
         self.sgraphs = None
         if cfg.use_graphs and device.type == "cuda" and len(self.ranks) > 1:
@@ -276,6 +295,8 @@ class PipelineEngine(LLMEngine):
         if g is not None and not sb.prefill and len(sb.decode) <= g.max_bucket:
             pad = next(b for b in g.buckets if b >= len(sb.decode))
         flat, hdr, sampled = self.runner.build_host(sb, pad_decode_to=pad)
+        # the next stage reads the hop from shared memory and copies it to its own GPU
+        self.hop.send_bytes(_pack(hdr, KIND_FWD, flat))
         dev = self.runner.to_device(flat)
         with torch.inference_mode():
             if pad:
@@ -284,19 +305,22 @@ class PipelineEngine(LLMEngine):
             else:
                 ids, meta, _samp = self.runner.meta_from_device(dev, hdr)
                 hidden = self.model.forward(meta, input_ids=ids)
-        self.f.ctrl_send_tensor(_hdr_tensor(hdr, KIND_FWD), self.next_rank)
-        self.f.send(dev, self.next_rank)
-        self.f.send(hidden.contiguous(), self.next_rank)
+        self.f.send(hidden.contiguous(), self.next_rank, group=self.pp)
         self.inflight.append((sb, sampled, int(hdr[ModelRunner.H_NLOG])))
         return True
 
     def _retire(self) -> list[StepOutput]:
         sb, sampled, nlog = self.inflight.popleft()
-        # tokens come back on the gloo control group: an RCCL recv here would
-        # queue behind the next microbatch's sends on the (0,1) pair channel
-        toks = torch.empty(self.mb_cap + 1, dtype=torch.long)
-        self.f.ctrl_recv_tensor(toks, self.last_rank)
-        tl = toks[1: 1 + int(toks[0])].tolist()
+        t0 = time.perf_counter()
+        while True:
+            m = self.tok.poll()
+            if m is not None:
+                break
+            if self.idle_hook is not None:
+                self.idle_hook()
+            time.sleep(0.00005)
+        self.wait_s += time.perf_counter() - t0
+        tl = m[1: 1 + int(m[0])].tolist()
         assert len(tl) == nlog, (len(tl), nlog)
         for r in sb.decode:
             r.busy = False
@@ -327,65 +351,34 @@ class PipelineEngine(LLMEngine):
         return outs
 
     # ------------------------------------------------------------------ control
-    def send_kv_notice(self, ids: torch.Tensor, src: int, chunk: int = 0) -> None:
-        """Tell later stages that pages ``ids`` of a P/D migration are on their
-        way from prefill rank ``src`` (each stage receives its own layer slice,
-        in ``chunk``-layer groups when the migration is layer-streamed)."""
-        if self.next_rank is None:
-            return
-        hdr = np.zeros(HDR, np.int64)
-        hdr[1] = ids.numel()
-        hdr[2] = src
-        hdr[3] = chunk
-        self.f.ctrl_send_tensor(_hdr_tensor(hdr, KIND_KV), self.next_rank)
-        self.f.send(ids.to(self.f.device, torch.int32).contiguous(), self.next_rank)
+    def send_kv_notice(self, src: int, key: int, ids: list) -> None:
+        """Tell every later stage that migration ``key`` from prefill rank ``src``
+        lands in pages ``ids`` (each stage receives its own layer slice from
+        ``src``).  Sent before any micro-step that reads those pages."""
+        msg = [src, key] + [int(x) for x in ids]
+        for ch in self.notice.values():
+            ch.send_var(msg)
+
+    def _ctl(self, kind: int) -> None:
+        self.drain()
+        if self.hop is not None:
+            self.hop.send_bytes(_pack(np.zeros(HDR, np.int64), kind))
 
     def pause_stages(self) -> None:
-        """Stage workers return from ``run()`` (e.g. to join a barrier)."""
-        self.drain()
-        if self.next_rank is not None:
-            self.f.ctrl_send_tensor(_hdr_tensor(np.zeros(HDR, np.int64), KIND_PAUSE), self.next_rank)
-        self.f.flush()
+        """Stage workers install every announced migration and return from ``run()``."""
+        self._ctl(KIND_PAUSE)
 
     def stop_stages(self) -> None:
-        self.drain()
-        if self.next_rank is not None:
-            self.f.ctrl_send_tensor(_hdr_tensor(np.zeros(HDR, np.int64), KIND_STOP), self.next_rank)
-        self.f.flush()
+        self._ctl(KIND_STOP)
 
 
 class StageWorker:
     """Stages 1..S-1: receive -> local layers -> forward (or sample on the last stage)."""
 
-    def _install_kv(self) -> None:
-        """Scatter migrated page slices posted so far into the pool.  The driver
-        announced them before any step that reads them, so ordering the
-        compute stream after the scatter here is all the sync needed; the
-        transfers themselves ran off the compute stream."""
-        if not self.kv_pending:
-            return
-        from dgi import ops
-        f = self.f
-        if f.on_gpu:
-            rs = f.recv_stream
-            rs.wait_stream(torch.cuda.current_stream())
-            for recs, buf, ids in self.kv_pending:
-                for rec in recs:
-                    rec.complete()
-                with torch.cuda.stream(rs):
-                    ops.kv_scatter(self.pool.kv, ids, buf)
-                buf.record_stream(rs)
-                ids.record_stream(rs)
-            torch.cuda.current_stream().wait_stream(rs)
-        else:
-            for recs, buf, ids in self.kv_pending:
-                for rec in recs:
-                    rec.complete()
-                ops.kv_scatter(self.pool.kv, ids, buf)
-        self.kv_pending = []
-
     def __init__(self, cfg: EngineConfig, fabric: Fabric, stage_ranks: list, model_cfg: Optional[ModelConfig] = None,
-                 split: Optional[list] = None, microbatches: Optional[int] = None):
+                 split: Optional[list] = None, microbatches: Optional[int] = None,
+                 kv_sources: Optional[list] = None):
+        from dgi.parallel.fabric import CtrlChannel
         self.f = fabric
         self.mb_cap = max(1, cfg.max_num_seqs // (microbatches or len(stage_ranks)))
         self.ranks = list(stage_ranks)
@@ -413,74 +406,140 @@ class StageWorker:
         self.model.kv_cache = self.pool.kv
         self.n_layers = b - a
         self.steps = 0
-        self.kv_pending: list = []   # (AsyncRecv, buf, ids) of P/D page slices in flight
+        self.pp = fabric.pp_group(self.ranks)
+        self.hop_in = CtrlChannel(fabric, self.prev, HDR, tag="pp", capacity=1 << 23)
+        self.hop_out = CtrlChannel(fabric, self.next, HDR, tag="pp", capacity=1 << 23) if self.next is not None \
+            else None
+        self.tok = CtrlChannel(fabric, self.driver, 1, tag="tok") if self.is_last else None
+        self.tok_pending: collections.deque = collections.deque()   # (event, pinned tokens, n) in order
+        # P/D: page-id notices from the driver, slices from the prefill ranks
+        self.kvr = None
+        self.notice = None
+        self.kv_pending: collections.deque = collections.deque()    # (src, key, ids_t) not installed yet
+        if kv_sources:
+            from dgi.parallel.kv_transfer import KVReceiver
+            self.notice = CtrlChannel(fabric, self.driver, 1, tag="kvn")
+            self.kvr = KVReceiver(fabric, kv_sources, (2, mc.num_kv_heads, cfg.block_size, mc.head_dim), cfg.dtype)
+        self.installed = 0
         self.sgraphs = None
         if cfg.use_graphs and dev.type == "cuda":
             self.sgraphs = StageGraphs(self.model, self.runner, pipeline_buckets(self.mb_cap), first=False,
                                        last=self.is_last)
             self.capture_seconds = self.sgraphs.capture()
 
+    # ------------------------------------------------------------------ P/D installs
+    def _take_notices(self) -> None:
+        if self.notice is None:
+            return
+        while True:
+            m = self.notice.poll()
+            if m is None:
+                return
+            ids_t = torch.tensor(m[2:], dtype=torch.int32, device=self.f.device)
+            self.kv_pending.append((int(m[0]), int(m[1]), ids_t))
+
+    def _service(self) -> None:
+        """Everything a stage does while it waits: KV handshakes, notices, token
+        publication, and installing migrations whose slices have landed."""
+        self._take_notices()
+        if self.kvr is not None:
+            self.kvr.service()
+            while self.kv_pending and (self.n_layers == 0 or
+                                       self.kvr.is_landed(self.kv_pending[0][0], self.kv_pending[0][1])):
+                self._install_one()
+        self._publish_tokens()
+
+    def _install_one(self, block: bool = False) -> None:
+        from dgi.parallel.kv_transfer import scatter_groups
+        src, key, ids_t = self.kv_pending.popleft()
+        if self.n_layers == 0:          # a layer-less stage (more stages than layers): nothing is sent to it
+            return
+        groups = self.kvr.wait_landed(src, key, idle=self._publish_tokens) if block else self.kvr.take(src, key)
+        scatter_groups(self.pool.kv, ids_t, groups)
+        self.installed += 1
+
+    def _install_all(self) -> None:
+        """Every migration the driver announced before this point is in the pool
+        (its notice was written before the hop that follows it)."""
+        self._take_notices()
+        while self.kv_pending:
+            self._install_one(block=True)
+
+    # ------------------------------------------------------------------ tokens (last stage)
+    def _publish_tokens(self, block: bool = False) -> None:
+        while self.tok_pending:
+            ev, host, n = self.tok_pending[0]
+            if ev is not None and not ev.query():
+                if not block:
+                    return
+                ev.synchronize()
+            self.tok_pending.popleft()
+            self.tok.send_var(np.concatenate([[n], host[:n].numpy()]) if n else [0])
+
+    def _emit_tokens(self, out: torch.Tensor, nlog: int) -> None:
+        if not nlog:
+            self.tok_pending.append((None, None, 0))
+            return
+        if out.is_cuda:
+            host = torch.empty(nlog, dtype=torch.long, pin_memory=True)
+            host.copy_(out[:nlog], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            host, ev = out[:nlog].clone(), None
+        self.tok_pending.append((ev, host, nlog))
+
+    # ------------------------------------------------------------------ serve
+    def _next_hop(self) -> bytes:
+        while True:
+            b = self.hop_in.poll_bytes()
+            if b is not None:
+                return b
+            self._service()
+            time.sleep(0.00005)
+
     @torch.inference_mode()
     def run(self) -> str:
         """Serve until PAUSE (returns "pause") or STOP (returns "stop")."""
         f, dev = self.f, self.f.device
         H = self.mc.hidden_size
-        from dgi import ops
         while True:
-            hb = torch.empty(HDR, dtype=torch.int64)
-            f.ctrl_recv_tensor(hb, self.prev)      # host tensor: no GPU sync to read the next hop's shape
-            hdr = hb.tolist()
-            kind = hdr[0]
+            b = self._next_hop()
+            hdr, flat_np = _unpack(b)
+            kind = int(hdr[0])
             if kind in (KIND_STOP, KIND_PAUSE):
-                self._install_kv()
-                if self.next is not None:
-                    f.ctrl_send_tensor(hb, self.next)
-                f.flush()
+                self._install_all()
+                self._publish_tokens(block=True)
+                if self.hop_out is not None:
+                    self.hop_out.send_bytes(b)
                 return "stop" if kind == KIND_STOP else "pause"
-            if kind == KIND_KV:
-                n, src, chunk = hdr[1], hdr[2], hdr[3]
-                ids = torch.empty(n, dtype=torch.int32, device=dev)
-                f.recv(ids, self.prev)
-                if self.next is not None:
-                    f.ctrl_send_tensor(hb, self.next)
-                    f.send(ids, self.next)
-                buf = torch.empty(self.n_layers, 2, n, self.mc.num_kv_heads, self.pool.block_size, self.mc.head_dim,
-                                  dtype=self.pool.dtype, device=dev)
-                from dgi.parallel.pd import layer_groups
-                self.kv_pending.append(([f.irecv_async(buf[a:b], src) for a, b in layer_groups(self.n_layers, chunk)],
-                                        buf, ids))
-                continue
             # KIND_FWD
             from dgi.parallel.fault import plan
             if plan():
                 plan().check(f.rank, self.steps)
-            self._install_kv()
-            flat = torch.empty(hdr[ModelRunner.H_LEN], dtype=torch.int32, device=dev)
-            f.recv(flat, self.prev)
-            T = hdr[ModelRunner.H_T]
+            self._install_all()
+            h = [int(x) for x in hdr]
+            if self.hop_out is not None:           # the next stage can post its receive now
+                self.hop_out.send_bytes(b)
+            flat = self.runner.to_device(flat_np.copy())
+            T = h[ModelRunner.H_T]
             g = self.sgraphs
-            use_graph = g is not None and g.eligible(hdr)
+            use_graph = g is not None and g.eligible(h)
             hidden = g.input_hidden(T) if use_graph else torch.empty(T, H, dtype=self.pool.dtype, device=dev)
-            f.recv(hidden, self.prev)
+            f.recv(hidden, self.prev, group=self.pp)
             with phase("stage_forward", rows=T, graph=int(use_graph)):
                 if use_graph:
-                    out = g.run(flat, hdr)
+                    out = g.run(flat, h)
                     if not self.is_last:
                         out = out.clone()      # the next replay rewrites the graph's output buffer
                 else:
-                    _ids, meta, samp = self.runner.meta_from_device(flat, hdr)
+                    _ids, meta, samp = self.runner.meta_from_device(flat, h)
                     out = self.model.forward(meta, hidden=hidden)
-                    if self.is_last and hdr[ModelRunner.H_NLOG]:
+                    if self.is_last and h[ModelRunner.H_NLOG]:
                         out = samp.sample(out)
             self.steps += 1
             if self.is_last:
-                nlog = hdr[ModelRunner.H_NLOG]
-                toks = torch.zeros(self.mb_cap + 1, dtype=torch.long)
-                toks[0] = nlog
-                if nlog:
-                    toks[1: 1 + nlog] = out[:nlog].cpu()
-                f.ctrl_send_tensor(toks, self.driver)
+                self._emit_tokens(out, h[ModelRunner.H_NLOG])
+                self._publish_tokens()
             else:
-                f.ctrl_send_tensor(hb, self.next)
-                f.send(flat, self.next)
-                f.send(out.contiguous(), self.next)
+                f.send(out.contiguous(), self.next, group=self.pp)

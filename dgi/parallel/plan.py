@@ -112,6 +112,30 @@ class NodeLayout:
                 pairs.add((min(a, b), max(a, b)))
         return sorted(pairs)
 
+    def kv_pairs(self) -> list:
+        """(prefill, decode rank) pairs that move KV pages on the world communicator."""
+        return sorted((min(p, d), max(p, d)) for p in self.prefill_ranks for d in self.decode_ranks)
+
+    def pipeline_groups(self) -> list:
+        """Rank lists that get their own activation sub-communicator (every
+        multi-stage decode replica; the whole node for a pure pipeline)."""
+        return [list(g) for g in self.decode_groups if len(g) > 1]
+
+    def streams_per_rank(self) -> dict:
+        """High-priority (communication) streams each rank uses: the world
+        communicator, the receive-posting stream (decode ranks) and its
+        pipeline's sub-communicator.  Must stay within the hardware queues of
+        one priority class (``fabric.GPU_HW_QUEUES``)."""
+        out = {}
+        for r in range(self.world):
+            n = 1                                     # world communicator (KV / collectives)
+            if r in self.decode_ranks and self.prefill_ranks:
+                n += 1                                # receive-posting stream
+            if any(r in g for g in self.pipeline_groups()):
+                n += 1                                # activation sub-communicator
+            out[r] = n
+        return out
+
     def describe(self) -> str:
         if self.kind in ("single", "dp", "pp"):
             return f"{self.kind}{self.world if self.kind != 'dp' else self.replicas}"

@@ -15,6 +15,7 @@ import contextlib
 import dataclasses
 import gc
 import os
+import time
 from typing import Optional
 
 import numpy as np
@@ -94,6 +95,9 @@ class ModelRunner:
                            torch.empty(maxb * nh * self.ws_splits, dtype=torch.float32, device=self.device))
             if os.environ.get("DGI_DECODE_FUSED_REDUCE", "0") == "1":
                 self.dec_ws += (torch.zeros(maxb * model.cfg.num_kv_heads, dtype=torch.int32, device=self.device),)
+        # called while the host waits for a step's sampled tokens (P/D ranks keep
+        # their KV handshakes moving instead of blocking in a stream synchronize)
+        self.wait_hook = None
         self.graphs = None
         if use_graphs and self.is_cuda and model.has_head:
             self.graphs = GraphRunner(self, [b for b in graph_buckets if b <= max_num_seqs])
@@ -224,7 +228,25 @@ class ModelRunner:
         logits = self.model.forward(meta, input_ids=ids)
         if not sampled:
             return StepResult([], [])
-        return StepResult(samp.sample(logits).tolist(), sampled)
+        return StepResult(self.fetch(samp.sample(logits)), sampled)
+
+    def fetch(self, t: torch.Tensor, host: Optional[torch.Tensor] = None) -> list:
+        """Device tokens -> host list.  With a ``wait_hook`` the copy is async and
+        the hook runs until its event completes (no blocking synchronize)."""
+        if not t.is_cuda:
+            return t.tolist()
+        if host is None:
+            host = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        host.copy_(t, non_blocking=True)
+        if self.wait_hook is None:
+            torch.cuda.current_stream().synchronize()
+        else:
+            ev = torch.cuda.Event()
+            ev.record()
+            while not ev.query():
+                self.wait_hook()
+                time.sleep(0.00002)
+        return host.tolist()
 
 
 class GraphRunner:
@@ -363,9 +385,7 @@ class GraphRunner:
         self.bt[:b].copy_(dev[S * b:].view(b, maxw))
         self.graphs[b].replay()
         self.last_bucket = b
-        self.host_out[:b].copy_(self.out[:b], non_blocking=True)
-        torch.cuda.current_stream().synchronize()
-        return self.host_out[:n].tolist()
+        return self.r.fetch(self.out[:n], self.host_out[:n])
 
     def last_features(self, n: int) -> torch.Tensor:
         """Fused EAGLE-3 features of the last replay's first ``n`` rows (feature tap on)."""

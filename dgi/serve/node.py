@@ -404,7 +404,7 @@ def main(argv=None) -> int:
         layout = plan_node_layout(world, "pdpp" if args.layout == "auto" else args.layout,
                                   args.prefill_ranks or None, decode_stages=args.decode_stages or None,
                                   decode_replicas=args.decode_replicas or None, model=args.model)
-        fabric.connect_pairs(layout.p2p_pairs())
+        fabric.setup_layout(layout)
         role = layout.role(fabric.rank)
         if role == "prefill":
             _prefill_loop(args, fabric, layout)
@@ -420,7 +420,7 @@ def main(argv=None) -> int:
             cfg = EngineConfig(model=args.model, device=str(fabric.device), max_num_seqs=args.max_num_seqs,
                                max_num_batched_tokens=args.max_batched_tokens, max_model_len=args.max_model_len,
                                use_graphs=False, seed=args.seed, enable_prefix_caching=False)
-            w = StageWorker(cfg, fabric, layout.group_of(fabric.rank))
+            w = StageWorker(cfg, fabric, layout.group_of(fabric.rank), kv_sources=layout.prefill_ranks)
             while w.run() != "stop":
                 pass
             fabric.close()

@@ -14,7 +14,7 @@ CONC=${REHEARSE_CONC:-64}
 run() {  # name, nproc, extra args
   local name=$1 n=$2; shift 2
   echo "== $name ($MODEL)" >&2
-  timeout -k 10 160 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 \
+  timeout -k 10 ${REHEARSE_TIMEOUT:-200} python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 \
     --master-port $((29600 + n)) bench.py --gpus "$n" --model "$MODEL" --steps 8 --warmup 2 --ramp-steps 4 \
     --concurrency "$CONC" --output-len 32 --prompt-len 256 "$@" > "gpurun_out/rehearse_${name}${REHEARSE_TAG}.json" \
     2> "gpurun_out/rehearse_${name}${REHEARSE_TAG}.err"
@@ -33,6 +33,10 @@ for c in $cases; do
     pd8_5p_3d) run $c 8 --layout pd --prefill-ranks 5 --decode-replicas 3 || exit 1 ;;
     pd8_5p_3d_nooverflow) run $c 8 --layout pd --prefill-ranks 5 --decode-replicas 3 --prefill-local-cap 0 || exit 1 ;;
     pd8_2p_6d) run $c 8 --layout pd --prefill-ranks 2 --decode-replicas 6 || exit 1 ;;
+    pp8) run $c 8 --layout pp || exit 1 ;;
+    pp4) run $c 4 --layout pp || exit 1 ;;
+    pdpp8_6p_pp2) run $c 8 --layout pdpp --prefill-ranks 6 --decode-stages 2 || exit 1 ;;
+    pdpp8_2p_2xpp3) run $c 8 --layout pdpp --prefill-ranks 2 --decode-stages 3 --decode-replicas 2 || exit 1 ;;
     pd4_3p_1d) run $c 4 --layout pd --prefill-ranks 3 --decode-replicas 1 || exit 1 ;;
     pd2_1p_1d_local) run $c 2 --layout pd --prefill-ranks 1 --decode-replicas 1 --decode-local-frac 0.46 || exit 1 ;;
     pdpp4_2p_pp2_local) run $c 4 --layout pdpp --prefill-ranks 2 --decode-stages 2 --decode-local-frac 0.5 || exit 1 ;;

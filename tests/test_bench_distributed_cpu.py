@@ -40,3 +40,20 @@ def test_bench_pd_layouts_on_gloo(n, args):
     d = json.loads(line)
     assert d["n_gpus"] == n and d["value"] > 0
     assert d["extra"]["layout"]["kind"] in ("pd", "pdpp")
+
+
+def test_pd_separation_cli_runs_config4_as_2p_6d(tmp_path):
+    """BASELINE config #4: ``benchmarks/pd_separation.py --prefill-workers 2
+    --decode-workers 6`` is 2 prefill GPUs + 6 single-GPU decode replicas (8 gloo
+    ranks here), reported in the reference's PDSeparationResult schema."""
+    env = {**os.environ, "OMP_NUM_THREADS": "1", "DGI_WATCHDOG": "0"}
+    env.pop("DGI_STAGED_GPU", None)
+    out = tmp_path / "pd.json"
+    cmd = [sys.executable, "benchmarks/pd_separation.py", "--model", "llama-tiny", "--prefill-workers", "2",
+           "--decode-workers", "6", "--steps", "3", "--warmup", "1", "--max-tokens", "8", "--prompt-length", "32",
+           "--concurrent", "8", "--output", str(out)]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(out.read_text())["separated"]
+    assert d["prefill_workers"] == 2 and d["decode_workers"] == 6 and d["tokens_per_second"] > 0
+    assert "2P+6D[1+1+1+1+1+1]" in r.stdout + r.stderr or d["mode"] == "separated"

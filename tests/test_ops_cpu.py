@@ -243,3 +243,31 @@ def test_trimmed_last_layer_matches_full(monkeypatch):
         eng = LLMEngine(cfg)
         outs[flag] = [r.output for r in eng.generate(prompts, sp)]
     assert outs[True] == outs[False]
+
+
+def test_fused_decode_honours_trim_last_on_padded_batch():
+    """A padded pure-decode batch (pipeline stage without graphs: T = bucket > nlog
+    rows) through the fused decode layers returns exactly nlog logits rows — the
+    sampler's per-row views are nlog long (llama.py fused early return)."""
+    from dgi.engine import EngineConfig, LLMEngine
+    from dgi.sched.request import SamplingParams
+    e = LLMEngine(EngineConfig(model="llama-tiny-hd128", device="cpu", dtype=torch.float32, num_blocks=64,
+                               max_num_seqs=4, max_model_len=256, max_num_batched_tokens=64, use_graphs=False,
+                               enable_prefix_caching=False))
+    for p in ([1, 5, 9, 300, 17], [1, 2, 3]):
+        e.add_request(p, SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True))
+    e.step()                                   # both prompts prefilled: the next batch is pure decode
+    sb = e.scheduler.schedule()
+    assert len(sb.decode) == 2 and not sb.prefill
+    r = e.runner
+    flat, hdr, sampled = r.build_host(sb, pad_decode_to=4)
+    ids, meta, samp = r.meta_from_device(r.to_device(flat), hdr)
+    ref = e.model.forward(meta, input_ids=ids)
+    e.model.force_fused = True
+    calls = []
+    real = e.model._forward_layers_fused
+    e.model._forward_layers_fused = lambda *a: calls.append(1) or real(*a)
+    got = e.model.forward(meta, input_ids=ids)
+    assert calls and got.shape[0] == len(sampled) == 2
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)
+    assert samp.sample(got).shape[0] == 2

@@ -65,12 +65,9 @@ def _worker(rank, world, port, fn_name, q):
     torch.set_num_threads(1)
     try:
         import torch.distributed as dist
-        backend = os.environ.get("DGI_TEST_BACKEND", "gloo")
-        if backend == "nccl":       # DGI_SHARED_GPU=1: every rank on device 0, RCCL data plane
-            from dgi.parallel.fabric import local_device_index, prepare_rccl_env
-            prepare_rccl_env()
-            torch.cuda.set_device(local_device_index())
-        dist.init_process_group(backend, rank=rank, world_size=world)
+        from dgi.parallel.fabric import init_distributed
+        # nccl (DGI_SHARED_GPU=1: every rank on device 0): eager RCCL world communicator
+        init_distributed(os.environ.get("DGI_TEST_BACKEND", "gloo"))
         res = globals()[fn_name](rank, world)
         q.put((rank, "ok", res))
         dist.barrier()
@@ -108,9 +105,11 @@ def _pp_body(rank, world):
     from dgi.parallel.fabric import Fabric
     from dgi.parallel.pipeline import PipelineEngine, StageWorker
     from dgi.sched.request import SamplingParams
+    from dgi.parallel.plan import NodeLayout
     f = Fabric()
     cfg = _engine_cfg()
     ranks = list(range(world))
+    f.setup_layout(NodeLayout("pp", [], ranks))
     if rank == 0:
         eng = PipelineEngine(cfg, f, ranks)
         reqs = [eng.add_request(p, _sp(i)) for i, p in enumerate(PROMPTS)]
@@ -140,7 +139,7 @@ def _pd_body(rank, world):
     k = (world - npre) // reps
     groups = [list(range(npre + i * k, npre + (i + 1) * k)) for i in range(reps)]
     layout = NodeLayout("pd" if k == 1 else "pdpp", list(range(npre)), groups)
-    f.connect_pairs(layout.p2p_pairs())
+    f.setup_layout(layout)
     if rank in layout.prefill_ranks:
         srv = PrefillServer(cfg, f, layout, stream_layers=int(os.environ.get("DGI_TEST_STREAM", "8")))
         nlocal = int(os.environ.get("DGI_TEST_LOCAL", "0"))
@@ -167,7 +166,7 @@ def _pd_body(rank, world):
         drv.finish()
         return done
     from dgi.parallel.pipeline import StageWorker
-    w = StageWorker(cfg, f, layout.group_of(rank))
+    w = StageWorker(cfg, f, layout.group_of(rank), kv_sources=layout.prefill_ranks)
     w.run()
     f.flush()
     return None
@@ -530,3 +529,80 @@ def test_stream_order_checker_flags_send_buffer_reuse(monkeypatch):
     monkeypatch.setenv("DGI_WATCHDOG", "0")
     out = _spawn("_reuse_body", 2)
     assert out[0]["caught"] and out[0]["violations"] == 1 and out[0]["sends"] == 1
+
+
+# ---------------------------------------------------------------------------- KV handshake protocol order
+def _pd_trace_body(rank, world):
+    """2 prefill ranks + 2 decode pipelines of 2 stages (world 6) with the KV
+    protocol trace on: returns every rank's sender / receiver event log."""
+    from dgi.parallel.fabric import Fabric
+    from dgi.parallel.pd import DecodeDriver, PrefillServer
+    from dgi.parallel.pipeline import StageWorker
+    from dgi.parallel.plan import NodeLayout
+    f = Fabric()
+    cfg = _engine_cfg()
+    layout = NodeLayout("pdpp", [0, 1], [[2, 3], [4, 5]])
+    f.setup_layout(layout)
+    budget = f.stream_budget()
+    if rank in layout.prefill_ranks:
+        srv = PrefillServer(cfg, f, layout, stream_layers=1)
+        for i, p in enumerate(PROMPTS * 2):
+            if i % 2 == rank:
+                srv.submit(p, _sp(i))
+        while srv.busy():
+            srv.step()
+        srv.finish()
+        return {"role": "prefill", "trace": srv.sender.trace, "budget": budget}
+    if rank in layout.drivers:
+        drv = DecodeDriver(cfg, f, layout)
+        n = 0
+        while not drv.all_prefill_done() or drv.engine.has_unfinished():
+            n += sum(1 for o in drv.step() if o.finished)
+        drv.finish()
+        return {"role": "driver", "trace": drv.kvr.trace, "finished": n, "budget": budget}
+    w = StageWorker(cfg, f, layout.group_of(rank), kv_sources=layout.prefill_ranks)
+    w.run()
+    return {"role": "stage", "trace": w.kvr.trace, "installed": w.installed, "budget": budget}
+
+
+def test_kv_handshake_order_and_one_receive_in_flight(monkeypatch):
+    """Clear-to-send protocol (dgi.parallel.kv_transfer): every send is enqueued
+    only after its RTS went out and its CTS came back, and no decode rank ever
+    has two receives posted at once."""
+    monkeypatch.setenv("DGI_KV_TRACE", "1")
+    monkeypatch.setenv("DGI_TEST_MODEL", "llama-tiny-hd128")
+    out = _spawn("_pd_trace_body", 6)
+    sends = 0
+    for r, o in out.items():
+        tr = o["trace"]
+        if o["role"] == "prefill":
+            seen = {}
+            for ev, tid, _dst, _t in tr:
+                seen.setdefault(tid, []).append(ev)
+            assert seen and all(v == ["rts", "cts", "send"] for v in seen.values()), seen
+            sends += len(seen)
+        else:
+            evs = [e for e, *_ in tr]
+            assert evs[0::2] == ["post"] * len(evs[0::2]) and evs[1::2] == ["land"] * len(evs[1::2]), evs
+            assert len(evs) % 2 == 0
+        # communication streams of every role fit the hardware queues of one priority class
+        from dgi.parallel.fabric import GPU_HW_QUEUES
+        assert len(o["budget"]["high"]) <= GPU_HW_QUEUES - 1 and len(o["budget"]["normal"]) <= GPU_HW_QUEUES
+    received = sum(len(o["trace"]) // 2 for o in out.values() if o["role"] != "prefill")
+    assert received == sends > 0
+    assert out[2]["finished"] + out[4]["finished"] == 2 * len(PROMPTS)
+    assert out[3]["installed"] >= 1 and out[5]["installed"] >= 1
+
+
+def test_streams_per_rank_fit_hardware_queues():
+    """Every 8-GPU layout the planner or the benchmarks can produce keeps each
+    rank's communication streams within one priority class's hardware queues."""
+    from dgi.parallel.fabric import GPU_HW_QUEUES
+    from dgi.parallel.plan import NodeLayout
+    lays = [plan_node_layout(8), plan_node_layout(8, model="llama3-8b"), plan_node_layout(8, "pd", 2, decode_replicas=6),
+            plan_node_layout(8, "pp"), plan_node_layout(8, "pdpp", 6, decode_stages=2),
+            plan_node_layout(4), plan_node_layout(2), NodeLayout("pdpp", [0, 1], [[2, 3, 4], [5, 6, 7]])]
+    for lay in lays:
+        per = lay.streams_per_rank()
+        assert len(per) == lay.world
+        assert max(per.values()) <= GPU_HW_QUEUES - 1, (lay.describe(), per)

@@ -171,8 +171,15 @@ class DistributedInferenceSession:
     def position(self, value: int) -> None:
         self._position = value
 
+    def _new_worker_session(self, info: WorkerInfo) -> WorkerSession:
+        ws = WorkerSession(worker_info=info)
+        ws.session_id = self.session_id
+        return ws
+
     async def setup(self) -> None:
-        sessions = [WorkerSession(w, self.session_id) for w in self.route]
+        # one-argument construction (the reference builds ``WorkerSession(worker_info=...)``,
+        # reference worker/distributed/session.py:252, and tests substitute that signature)
+        sessions = [self._new_worker_session(w) for w in self.route]
         try:
             await asyncio.gather(*[s.connect(self.config.connect_timeout) for s in sessions])
         except Exception:
@@ -220,7 +227,7 @@ class DistributedInferenceSession:
         if spare is None:
             self.state = SessionState.ERROR
             raise RuntimeError(f"worker {failed.worker_info.worker_id} failed and no replacement is available: {error}")
-        ws = WorkerSession(spare, self.session_id)
+        ws = self._new_worker_session(spare)
         await ws.connect(self.config.connect_timeout)
         await ws.replay(failed.history)
         ws.next_session = failed.next_session

@@ -14,6 +14,14 @@ from ._chat import format_messages
 from .llm_base import GenerationConfig, GenerationResult, LLMBackend, LLMBaseEngine
 
 
+async def _request(req):
+    """aiohttp's ``session.post()`` is both awaitable and an async context manager;
+    accept either form (test doubles and wrapped sessions return a coroutine)."""
+    if not hasattr(req, "__aenter__") and hasattr(req, "__await__"):
+        return await req
+    return req
+
+
 class SGLangEngine(LLMBaseEngine):
     def __init__(self, config: Dict[str, Any]):
         super().__init__(config)
@@ -77,7 +85,7 @@ class SGLangEngine(LLMBaseEngine):
         if cfg.stop_sequences:
             payload["stop"] = cfg.stop_sequences
         async with aiohttp.ClientSession() as session:
-            async with session.post(f"{self._url()}/v1/chat/completions", json=payload) as resp:
+            async with await _request(session.post(f"{self._url()}/v1/chat/completions", json=payload)) as resp:
                 if resp.status != 200:
                     raise RuntimeError(f"SGLang API error {resp.status}: {await resp.text()}")
                 d = await resp.json()
