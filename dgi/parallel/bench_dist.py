@@ -17,6 +17,7 @@ from __future__ import annotations
 import os
 import random
 import time
+from typing import Optional
 
 import torch
 
@@ -33,6 +34,29 @@ def _prompt(rng, n, vocab):
     return [rng.randrange(lo, vocab - lo) for _ in range(n)]
 
 
+def ctrl_ping(f, a: int, b: int, n: int = 400) -> Optional[dict]:
+    """Round trip of one control message between ranks ``a`` and ``b`` over the
+    node-local control plane (shared-memory rings), microseconds."""
+    from dgi.parallel.fabric import CtrlChannel
+    if f.rank not in (a, b) or a == b:
+        return None
+    ch = CtrlChannel(f, b if f.rank == a else a, 4, tag="ping")
+    ts = []
+    for _ in range(n):
+        if f.rank == a:
+            t0 = time.perf_counter()
+            ch.send([1])
+            ch.wait()
+            ts.append((time.perf_counter() - t0) * 1e6)
+        else:
+            ch.wait()
+            ch.send([2])
+    if not ts:
+        return None
+    ts.sort()
+    return {"p50": round(ts[len(ts) // 2], 2), "p99": round(ts[int(0.99 * (len(ts) - 1))], 2), "n": n}
+
+
 def run_distributed(args, layout_kind: str, dist):
     f = Fabric()
     rank, world = f.rank, f.world
@@ -42,6 +66,7 @@ def run_distributed(args, layout_kind: str, dist):
     # every communicator of the layout up front (world KV pairs + pipeline sub-communicators),
     # each warmed with one transfer per pair in a deadlock-free order
     t_pairs = f.setup_layout(layout)
+    ctrl_rtt = ctrl_ping(f, 0, world - 1)
     # decode-side concurrency: one microbatch of 768 rows per decode stage keeps the
     # decode GEMMs out of the small-M regime (70B down-proj: 0.76 PF/s at M=512,
     # 1.28 at 1024); a single decode GPU is capped by its KV pool (credits) instead
@@ -90,9 +115,18 @@ def run_distributed(args, layout_kind: str, dist):
     for r in roles.values():
         r["tok_s"] = round(r["tokens"] / el, 1) if el > 0 else 0.0
     mig = [o["migration_ms_p50"] for o in per_rank if o.get("migration_ms_p50") is not None]
-    return total, el, all_ttfts, {"layout": {"kind": layout.kind, "describe": layout.describe(),
+    from dgi.parallel.plan import CAPACITY, layout_estimate
+    cap = CAPACITY.get(args.model)
+    est = None
+    if cap is not None and layout.kind in ("pd", "pdpp"):
+        k = len(layout.decode_groups[0])
+        if k in cap.decode_tok_s:
+            est = layout_estimate(len(layout.prefill_ranks), k, len(layout.decode_groups), cap)
+    return total, el, all_ttfts, {"planner_estimate": est,
+                                  "layout": {"kind": layout.kind, "describe": layout.describe(),
                                              "prefill": layout.prefill_ranks, "decode_groups": layout.decode_groups},
                                   "concurrency": conc, "pair_setup_s": round(t_pairs, 3), "roles": roles,
+                                  "ctrl_rtt_us": ctrl_rtt,
                                   "migration_ms_p50": round(float(sorted(mig)[len(mig) // 2]), 3) if mig else None,
                                   "tpots": all_tpots, "e2es": all_e2es, "ranks": per_rank}
 

@@ -145,30 +145,40 @@ class NodeLayout:
 
 @dataclasses.dataclass
 class RoleCapacity:
-    """Per-role throughput of one model on one MI355X (output tok/s of a
-    512-in / 128-out load; ``scripts/pd_capacity.py`` measures it).
+    """Per-role throughput and step latency of one model on one MI355X
+    (512-in / 128-out load; ``scripts/pd_capacity.py`` measures it).
 
     * ``prefill_tok_s``: decode demand one prefill-only GPU creates
-      (prompts/s x output_len);
-    * ``decode_tok_s[k]``: what one decode replica of k pipeline stages
-      emits (k GPUs, k microbatches);
-    * ``mixed_tok_s``: one GPU running mixed prefill+decode steps (DP / the
-      hybrid slack filler)."""
+      (prompts/s x output_len) at ``prefill_mbt`` tokens per step, whose step
+      takes ``prefill_step_ms`` (the TTFT floor of a prompt admitted just in time);
+    * ``decode_tok_s[k]``: what one decode replica of k pipeline stages emits
+      (k GPUs, k microbatches of ``decode_rows[k]`` rows, one stage step taking
+      ``decode_step_ms[k]``: a replica's TPOT is k x that);
+    * ``mixed_tok_s`` / ``mixed_step_ms``: one GPU running mixed
+      prefill+decode steps (DP, the overflow / local-prompt filler); in DP every
+      token of a sequence waits one mixed step, so TTFT ~ TPOT ~ the step."""
     prefill_tok_s: float
     decode_tok_s: dict
     mixed_tok_s: float
+    prefill_step_ms: float = 0.0
+    prefill_mbt: int = 4096
+    decode_step_ms: dict = dataclasses.field(default_factory=dict)
+    decode_rows: dict = dataclasses.field(default_factory=dict)
+    mixed_step_ms: float = 0.0
 
 
-# Measured on one MI355X with scripts/pd_capacity.py (round 2: every timed decode row
-# really decodes — the round-1 table let early sequences finish inside the timed steps),
-# profiles/r2_pd_capacity.md.  decode_tok_s[k] = R / t(L/k layers, R rows) at the row
-# count the layouts use (768-row microbatches for 3-stage 70B replicas); mixed = the
-# 1-GPU bench.py rate (DP / slack filler).
+# Measured on one MI355X with scripts/pd_capacity.py (profiles/r2_pd_capacity.md,
+# profiles/r3_pd_capacity.md).  decode_tok_s[k] = R / t(L/k layers, R rows) at the row
+# count the layouts use; mixed = the 1-GPU bench.py rate and step (DP / slack filler).
 CAPACITY = {
     "llama3-70b": RoleCapacity(prefill_tok_s=19.47 * 128, decode_tok_s={1: 5522.0, 2: 12826.0, 3: 17773.0},
-                               mixed_tok_s=1760.0),
+                               mixed_tok_s=1760.0, prefill_step_ms=410.9, prefill_mbt=4096,
+                               decode_step_ms={1: 92.7, 2: 79.8, 3: 43.2}, decode_rows={1: 512, 2: 1024, 3: 768},
+                               mixed_step_ms=213.0),
     "llama3-8b": RoleCapacity(prefill_tok_s=176.2 * 128, decode_tok_s={1: 31566.0, 2: 58028.0, 3: 69373.0},
-                              mixed_tok_s=11842.0),
+                              mixed_tok_s=11842.0, prefill_step_ms=45.4, prefill_mbt=4096,
+                              decode_step_ms={1: 32.4, 2: 18.2, 3: 11.2}, decode_rows={1: 1024, 2: 1024, 3: 768},
+                              mixed_step_ms=30.6),
 }
 
 
@@ -189,13 +199,38 @@ def estimate_layout(n_prefill: int, stages: int, replicas: int, cap: RoleCapacit
     return base + (1.0 - dec / pre) * n_prefill * cap.mixed_tok_s
 
 
+def layout_estimate(n_prefill: int, stages: int, replicas: int, cap: RoleCapacity) -> dict:
+    """Throughput AND latency of a P/D layout under ``cap`` (what ``bench.py --gpus N``
+    reports next to its measurement).
+
+    tok_s: with the slack filler; disagg_tok_s: without it; tpot_ms: a sequence
+    decoded on a replica (k stage steps per token); ttft_ms: one prefill step
+    (prompts admitted just in time); filler_share: fraction of the output the
+    filler (mixed steps, DP-like TPOT) produces."""
+    pre = n_prefill * cap.prefill_tok_s
+    dec = replicas * cap.decode_tok_s.get(stages, 0.0)
+    base = min(pre, dec)
+    tot = estimate_layout(n_prefill, stages, replicas, cap, fill=True)
+    return {"layout": f"{n_prefill}P+{replicas}D[" + "+".join([f"pp{stages}" if stages > 1 else "1"] * replicas) + "]",
+            "tok_s": round(tot, 1), "disagg_tok_s": round(base, 1),
+            "bound": "prefill" if pre < dec else "decode",
+            "tpot_ms": round(stages * cap.decode_step_ms.get(stages, 0.0), 1) or None,
+            "ttft_ms": round(cap.prefill_step_ms, 1) or None,
+            "filler_share": round((tot - base) / tot, 3) if tot > 0 else 0.0,
+            "dp_tok_s": round((n_prefill + stages * replicas) * cap.mixed_tok_s, 1),
+            "dp_tpot_ms": cap.mixed_step_ms or None}
+
+
 def choose_pd_layout(n_gpus: int, cap: RoleCapacity, max_stages: int = 3, prefer_pipeline: bool = True,
-                     tol: float = 0.03) -> tuple:
-    """(n_prefill, stages, replicas, est tok/s) with the highest disaggregated
-    rate (``estimate_layout`` without the filler); candidates within ``tol``
-    of the best are ranked by pipeline depth (deeper first when
-    ``prefer_pipeline``: more KV per GPU, bigger decode microbatches), then by
-    how little slack they leave."""
+                     tol: float = 0.03, objective: str = "node") -> tuple:
+    """(n_prefill, stages, replicas, est tok/s).
+
+    ``objective="node"`` (default): among layouts whose replica TPOT beats a
+    mixed-step (DP) GPU's, the highest disaggregated rate (the filler only tops
+    a layout up towards DP and would otherwise make "1 prefill GPU + a DP node"
+    look as good as any P/D split); candidates within ``tol`` of the best are
+    ranked by the node rate with the filler, then by TPOT.
+    ``objective="disagg"``: the round-2 rule (deeper pipelines first within ``tol``)."""
     cands = []
     for npre in range(1, n_gpus):
         left = n_gpus - npre
@@ -203,13 +238,24 @@ def choose_pd_layout(n_gpus: int, cap: RoleCapacity, max_stages: int = 3, prefer
             if left % k or k not in cap.decode_tok_s:
                 continue
             reps = left // k
-            est = estimate_layout(npre, k, reps, cap)
             pre, dec = npre * cap.prefill_tok_s, reps * cap.decode_tok_s[k]
-            cands.append((est, k, npre, reps, abs(pre - dec) / max(pre, dec)))
+            tpot = k * cap.decode_step_ms.get(k, 0.0)
+            est = estimate_layout(npre, k, reps, cap)
+            if objective == "node":
+                beats_dp = not (cap.mixed_step_ms and tpot and tpot >= cap.mixed_step_ms)
+                cands.append((est, k, npre, reps, (-estimate_layout(npre, k, reps, cap, fill=True), tpot),
+                              beats_dp))
+            else:
+                cands.append((est, k, npre, reps, abs(pre - dec) / max(pre, dec), True))
+    if any(c[5] for c in cands):
+        cands = [c for c in cands if c[5]]
     top = max(c[0] for c in cands)
     near = [c for c in cands if c[0] >= (1.0 - tol) * top]
-    near.sort(key=lambda c: ((-c[1] if prefer_pipeline else c[1]), c[4], -c[0]))
-    est, k, npre, reps, _ = near[0]
+    if objective == "node":
+        near.sort(key=lambda c: (c[4], -c[0]))
+    else:
+        near.sort(key=lambda c: ((-c[1] if prefer_pipeline else c[1]), c[4], -c[0]))
+    est, k, npre, reps = near[0][:4]
     return npre, k, reps, est
 
 

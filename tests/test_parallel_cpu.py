@@ -239,8 +239,10 @@ def test_plan_layer_split_gives_head_stage_fewer_layers():
 
 
 def test_node_layout_defaults():
+    # 70B at 8 GPUs: 6 prefill GPUs feed a 2-stage decode pipeline (highest disaggregated rate among
+    # layouts whose decode TPOT beats a mixed-step DP GPU; the prefill ranks' slack decodes overflow)
     lay = plan_node_layout(8)
-    assert lay.kind == "pdpp" and len(lay.decode_ranks) == 3 and len(lay.prefill_ranks) == 5
+    assert lay.kind == "pdpp" and lay.decode_groups == [[6, 7]] and len(lay.prefill_ranks) == 6
     assert plan_node_layout(1).kind == "single"
     assert plan_node_layout(2).kind == "pd"
     four = plan_node_layout(4)     # 70B: 3 prefill GPUs feed one decode GPU (decode-bound; prefill overflow)
@@ -606,3 +608,14 @@ def test_streams_per_rank_fit_hardware_queues():
         per = lay.streams_per_rank()
         assert len(per) == lay.world
         assert max(per.values()) <= GPU_HW_QUEUES - 1, (lay.describe(), per)
+
+
+def test_layout_estimate_reports_rate_and_latency():
+    """The 70B 8-GPU pick is estimated at or above 8 DP GPUs (with the prefill ranks'
+    overflow filler) while its replica TPOT beats the DP mixed step."""
+    from dgi.parallel.plan import CAPACITY, choose_pd_layout, layout_estimate
+    cap = CAPACITY["llama3-70b"]
+    npre, k, reps, _ = choose_pd_layout(8, cap)
+    est = layout_estimate(npre, k, reps, cap)
+    assert est["tok_s"] >= 0.995 * est["dp_tok_s"] and est["tpot_ms"] < est["dp_tpot_ms"]
+    assert est["filler_share"] < 0.2 and est["ttft_ms"] is not None
