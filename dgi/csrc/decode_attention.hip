@@ -6,7 +6,8 @@
 // the paged pool written by rope_cache.hip.
 //
 // Work decomposition (CDNA4, wave64):
-//   grid = (max_splits, n_kv_heads, batch), 256 threads = 4 waves.
+//   grid = (max_splits, n_kv_heads, batch), 4 waves (8 when a short-context,
+//   small-batch step runs one split per sequence: no partials, no reduce kernel).
 //   A workgroup owns one (sequence, kv-head, KV split) and all G = nh/nkv
 //   query heads of that kv head, so each K/V byte is read from HBM once per
 //   decode step regardless of the GQA ratio.
@@ -34,8 +35,16 @@ __device__ __forceinline__ int v_lds_off(int row, int col) {
   return row * HD + (ch << 3) + (col & 7);
 }
 
+// per-wave LDS: the V tile (32 x HD bf16), reused after the loop for the wave's
+// partial O (16 queries x HD fp32, rows padded by 4 floats so the 16 query rows
+// of one store land in different banks) plus m / l
 template <int HD>
-__global__ __launch_bounds__(256) void paged_decode_kernel(
+constexpr int decode_wave_lds() {
+  return (32 * HD * 2 > 16 * (HD + 4) * 4 ? 32 * HD * 2 : 16 * (HD + 4) * 4) + 128;
+}
+
+template <int HD, int NW>
+__global__ __launch_bounds__(64 * NW) void paged_decode_kernel(
     const uint16_t* __restrict__ q, int q_stride, const uint16_t* __restrict__ k_cache,
     const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ context_lens, uint16_t* __restrict__ out, int out_stride,
@@ -44,7 +53,9 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
   constexpr int KS = HD / 32;   // k-steps of the QK^T product
   constexpr int NC = HD / 16;   // 16-wide dim blocks of the PV product
   constexpr int VCH = HD / 8;   // 16-byte chunks per V row
-  constexpr int WREG = 32 * HD * 2 + 128;  // per-wave LDS bytes (V tile, then O/m/l)
+  constexpr int WREG = decode_wave_lds<HD>();  // per-wave LDS bytes (V tile, then O/m/l)
+  constexpr int OROW = HD + 4;                 // padded fp32 row of the merged partial O
+  constexpr int NT = 64 * NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int split = blockIdx.x;
@@ -97,7 +108,7 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
   for (int c = 0; c < NC; ++c) o[c] = f32x4{0, 0, 0, 0};
 
   const int ntiles = (end - start + 31) >> 5;
-  for (int t = w; t < ntiles; t += 4) {
+  for (int t = w; t < ntiles; t += NW) {
     const int tb = start + (t << 5);
     // ---- K fragments straight to VGPRs (A operand: row = token, k = dims)
     u32x4 kf[2][KS];
@@ -197,34 +208,35 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
     }
   }
 
-  // ---- merge the 4 waves through LDS
+  // ---- merge the NW waves through LDS
   __syncthreads();
-  float* ow = reinterpret_cast<float*>(smem + w * WREG);  // [16 q][HD] fp32 fits in 32*HD*2 bytes
-  float* ml = reinterpret_cast<float*>(smem + w * WREG + 32 * HD * 2);  // m[16], l[16]
+  constexpr int MLOFF = WREG - 128;
+  float* ow = reinterpret_cast<float*>(smem + w * WREG);            // [16 q][OROW] fp32
+  float* ml = reinterpret_cast<float*>(smem + w * WREG + MLOFF);    // m[16], l[16]
   if (qi < G) {
 #pragma unroll
     for (int c = 0; c < NC; ++c)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) ow[qi * HD + 16 * c + 4 * g + i] = o[c][i];
+      for (int i = 0; i < 4; ++i) ow[qi * OROW + 16 * c + 4 * g + i] = o[c][i];
     if (g == 0) {
       ml[qi] = m_run;
       ml[16 + qi] = l_run;
     }
   }
   __syncthreads();
-  for (int idx = tid; idx < G * HD; idx += 256) {
+  for (int idx = tid; idx < G * HD; idx += NT) {
     const int qq = idx / HD;
     const int d = idx - qq * HD;
     float M = -1e30f;
 #pragma unroll
-    for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, reinterpret_cast<float*>(smem + ww * WREG + 32 * HD * 2)[qq]);
+    for (int ww = 0; ww < NW; ++ww) M = fmaxf(M, reinterpret_cast<float*>(smem + ww * WREG + MLOFF)[qq]);
     float L = 0.f, acc = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < 4; ++ww) {
-      const float* mlw = reinterpret_cast<float*>(smem + ww * WREG + 32 * HD * 2);
+    for (int ww = 0; ww < NW; ++ww) {
+      const float* mlw = reinterpret_cast<float*>(smem + ww * WREG + MLOFF);
       const float sc = exp2f(mlw[qq] - M);
       L += mlw[16 + qq] * sc;
-      acc += reinterpret_cast<float*>(smem + ww * WREG)[qq * HD + d] * sc;
+      acc += reinterpret_cast<float*>(smem + ww * WREG)[qq * OROW + d] * sc;
     }
     const int head = h * G + qq;
     const float r = acc / L;
@@ -250,7 +262,7 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
   __syncthreads();
   if (!s_last) return;
   __threadfence();
-  for (int idx = tid; idx < G * HD; idx += 256) {
+  for (int idx = tid; idx < G * HD; idx += NT) {
     const int qq = idx / HD;
     const int d = idx - qq * HD;
     const int head = h * G + qq;
@@ -313,12 +325,21 @@ extern "C" int dgi_paged_decode(const void* q, int q_stride, const void* k_cache
   if ((1 << bs_log2) != block_size) return -4;
   const float scale_log2 = scale * 1.4426950408889634f;
   dim3 grid(max_splits, nkv, B);
+  // few workgroups (small batch, one split: every (sequence, kv head) walks its whole
+  // context): 8 waves per workgroup halve the serial tile chain of each wave
+  const bool wide = max_splits == 1 && B * nkv <= 128;
   if (hd == 128) {
-    const size_t lds = 4 * (32 * 128 * 2 + 128);
-    paged_decode_kernel<128><<<grid, 256, lds, s>>>(
-        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,
-        block_tables, bt_stride, context_lens, (uint16_t*)out, out_stride, part_o, part_lse,
-        counters, max_splits, nh, nkv, bs_log2, part_size, scale_log2);
+    if (wide) {
+      paged_decode_kernel<128, 8><<<grid, 512, 8 * decode_wave_lds<128>(), s>>>(
+          (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,
+          block_tables, bt_stride, context_lens, (uint16_t*)out, out_stride, part_o, part_lse,
+          counters, max_splits, nh, nkv, bs_log2, part_size, scale_log2);
+    } else {
+      paged_decode_kernel<128, 4><<<grid, 256, 4 * decode_wave_lds<128>(), s>>>(
+          (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,
+          block_tables, bt_stride, context_lens, (uint16_t*)out, out_stride, part_o, part_lse,
+          counters, max_splits, nh, nkv, bs_log2, part_size, scale_log2);
+    }
     DGI_CHECK_LAUNCH();
     if (max_splits > 1 && counters == nullptr) {
       decode_reduce_kernel<128><<<dim3(B, nh), 128, 0, s>>>(part_o, part_lse, context_lens,
@@ -327,11 +348,17 @@ extern "C" int dgi_paged_decode(const void* q, int q_stride, const void* k_cache
       DGI_CHECK_LAUNCH();
     }
   } else if (hd == 64) {
-    const size_t lds = 4 * (32 * 64 * 2 + 128);
-    paged_decode_kernel<64><<<grid, 256, lds, s>>>(
-        (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,
-        block_tables, bt_stride, context_lens, (uint16_t*)out, out_stride, part_o, part_lse,
-        counters, max_splits, nh, nkv, bs_log2, part_size, scale_log2);
+    if (wide) {
+      paged_decode_kernel<64, 8><<<grid, 512, 8 * decode_wave_lds<64>(), s>>>(
+          (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,
+          block_tables, bt_stride, context_lens, (uint16_t*)out, out_stride, part_o, part_lse,
+          counters, max_splits, nh, nkv, bs_log2, part_size, scale_log2);
+    } else {
+      paged_decode_kernel<64, 4><<<grid, 256, 4 * decode_wave_lds<64>(), s>>>(
+          (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,
+          block_tables, bt_stride, context_lens, (uint16_t*)out, out_stride, part_o, part_lse,
+          counters, max_splits, nh, nkv, bs_log2, part_size, scale_log2);
+    }
     DGI_CHECK_LAUNCH();
     if (max_splits > 1 && counters == nullptr) {
       decode_reduce_kernel<64><<<dim3(B, nh), 64, 0, s>>>(part_o, part_lse, context_lens,

@@ -71,7 +71,10 @@ def run_distributed(args, layout_kind: str, dist):
     # decode GEMMs out of the small-M regime (70B down-proj: 0.76 PF/s at M=512,
     # 1.28 at 1024); a single decode GPU is capped by its KV pool (credits) instead
     k = len(layout.decode_groups[0]) if layout.decode_groups else 1
-    conc = args.concurrency or (768 * k if k > 1 else 1024)
+    from dgi.parallel.plan import capacity_for
+    cap = capacity_for(args.model)
+    rows = (cap.decode_rows.get(k) if cap is not None else None) or 768
+    conc = args.concurrency or (rows * k if k > 1 else 1024)
     # staged rehearsal: every rank shares one GPU, so each takes a slice of its memory
     from dgi.parallel.fabric import shared_gpu
     kv_frac = float(os.environ.get("DGI_KV_FRACTION", 0.5 / world if (f.staged or shared_gpu()) else 0.9))
@@ -115,8 +118,8 @@ def run_distributed(args, layout_kind: str, dist):
     for r in roles.values():
         r["tok_s"] = round(r["tokens"] / el, 1) if el > 0 else 0.0
     mig = [o["migration_ms_p50"] for o in per_rank if o.get("migration_ms_p50") is not None]
-    from dgi.parallel.plan import CAPACITY, layout_estimate
-    cap = CAPACITY.get(args.model)
+    from dgi.parallel.plan import capacity_for, layout_estimate
+    cap = capacity_for(args.model)
     est = None
     if cap is not None and layout.kind in ("pd", "pdpp"):
         k = len(layout.decode_groups[0])
@@ -221,17 +224,37 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
     if role == "prefill":
         lc = getattr(args, "prefill_local_cap", -1)
         lc = prefill_overflow_cap(layout, model=args.model) if lc < 0 else lc
-        pcfg = EngineConfig(**{**cfg.__dict__, "max_num_seqs": 64 + lc})
+        # prefill step size: the capacity table's (TTFT: a prompt admitted just in time waits ~1 step)
+        from dgi.parallel.plan import capacity_for
+        cap = capacity_for(args.model)
+        pmbt = getattr(args, "prefill_mbt", 0) or (cap.prefill_mbt if cap is not None else args.max_batched_tokens)
+        pcfg = EngineConfig(**{**cfg.__dict__, "max_num_seqs": 64 + lc, "max_num_batched_tokens": pmbt})
         srv = PrefillServer(pcfg, f, layout, local_cap=lc)
         ph = CtrlChannel(f, clock, 4, tag="phase")
         vocab = srv.engine.model_cfg.vocab_size
-        depth = max(2, args.max_batched_tokens // max(1, args.prompt_len))
+        # one step's worth of prompts, topped up right before each step
+        depth = max(1, pmbt // max(1, args.prompt_len))
+
+        # open loop (--arrival-rate, node-wide req/s): this rank's Poisson share; the prompt's
+        # arrival is its scheduled time, so TTFT includes every wait (queue, credit, prefill)
+        rate = float(getattr(args, "arrival_rate", 0.0) or 0.0) / max(1, len(layout.prefill_ranks))
+        nxt = {"t": time.perf_counter()}
+
+        def top_up():
+            if rate > 0:
+                now = time.perf_counter()
+                while nxt["t"] <= now:
+                    r = srv.submit(_prompt(rng, args.prompt_len, vocab), sp)
+                    r.arrival = nxt["t"]
+                    nxt["t"] += rng.expovariate(rate)
+                return
+            while len(srv.pending) + len(srv.engine.scheduler.waiting) < depth:
+                srv.submit(_prompt(rng, args.prompt_len, vocab), sp)
 
         def serve_until_phase():
             n, ttfts = 0, []
             while ph.poll() is None:
-                while len(srv.pending) + len(srv.engine.scheduler.waiting) < depth:
-                    srv.submit(_prompt(rng, args.prompt_len, vocab), sp)
+                top_up()
                 before = len(srv.ttfts)
                 n += len(srv.step())
                 ttfts += srv.ttfts[before:]
@@ -251,7 +274,7 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
         f.barrier()
         el = time.perf_counter() - t0
         srv.finish()
-        return n, el, ttfts, {"tokens": n, "migrated": srv.migrated, "migrate_s": round(srv.migrate_time, 3),
+        return n, el, ttfts, {"tokens": n, "prefill_mbt": pmbt, "migrated": srv.migrated, "migrate_s": round(srv.migrate_time, 3),
                               "sent_GB": round(srv.sent_bytes / 1e9, 3), "local_cap": lc,
                               "local_tokens": srv.local_tokens, "pd_scheduler": srv.pd_stats(),
                               "migration_ms_p50": srv.pd_stats()["migration_ms_p50"]}

@@ -171,15 +171,24 @@ class RoleCapacity:
 # profiles/r3_pd_capacity.md).  decode_tok_s[k] = R / t(L/k layers, R rows) at the row
 # count the layouts use; mixed = the 1-GPU bench.py rate and step (DP / slack filler).
 CAPACITY = {
-    "llama3-70b": RoleCapacity(prefill_tok_s=19.47 * 128, decode_tok_s={1: 5522.0, 2: 12826.0, 3: 17773.0},
-                               mixed_tok_s=1760.0, prefill_step_ms=410.9, prefill_mbt=4096,
-                               decode_step_ms={1: 92.7, 2: 79.8, 3: 43.2}, decode_rows={1: 512, 2: 1024, 3: 768},
-                               mixed_step_ms=213.0),
+    # r3: prefill at 2048 tokens / step is as fast as 4096 (19.62 vs 19.47 prompts/s) in half the
+    # step (TTFT); 2-stage replicas at 768-row microbatches (the KV pool of a 40-layer stage holds
+    # ~1800 full sequences), whole-model decode GPUs at 576 rows (their pool holds ~610)
+    "llama3-70b": RoleCapacity(prefill_tok_s=19.62 * 128, decode_tok_s={1: 5692.0, 2: 12209.0, 3: 17773.0},
+                               mixed_tok_s=1760.0, prefill_step_ms=203.9, prefill_mbt=2048,
+                               decode_step_ms={1: 101.2, 2: 62.9, 3: 43.2}, decode_rows={1: 576, 2: 768, 3: 768},
+                               mixed_step_ms=207.0),
     "llama3-8b": RoleCapacity(prefill_tok_s=176.2 * 128, decode_tok_s={1: 31566.0, 2: 58028.0, 3: 69373.0},
                               mixed_tok_s=11842.0, prefill_step_ms=45.4, prefill_mbt=4096,
                               decode_step_ms={1: 32.4, 2: 18.2, 3: 11.2}, decode_rows={1: 1024, 2: 1024, 3: 768},
                               mixed_step_ms=30.6),
 }
+
+
+def capacity_for(model: str) -> Optional[RoleCapacity]:
+    """Capacity table entry of ``model``; a layer-truncated rehearsal name
+    (``llama3-70b@L8``) plans like the full model it stands in for."""
+    return CAPACITY.get(model.split("@")[0] if model else model)
 
 
 def estimate_layout(n_prefill: int, stages: int, replicas: int, cap: RoleCapacity, fill: bool = False) -> float:
@@ -280,7 +289,7 @@ def plan_node_layout(n_gpus: int, kind: str = "pdpp", prefill_ranks: Optional[in
         return NodeLayout("pp", [], list(range(n_gpus)))
     if kind == "dp":
         return NodeLayout("dp", [], [0], replicas=n_gpus)
-    cap = CAPACITY.get(model)
+    cap = capacity_for(model)
     if decode_stages is None and kind == "pd":
         decode_stages = 1
     if prefill_ranks is None and decode_replicas is None and cap is not None and \
@@ -309,7 +318,7 @@ def prefill_overflow_cap(layout: NodeLayout, cap: int = 256, model: str = "llama
     bottleneck of the capacity estimate (e.g. 70B with 3 prefill GPUs per
     decode GPU: each prefill GPU supplies ~2.5k tok/s, a decode GPU absorbs
     ~4.6k — profiles/r1_pd_capacity_70b.md)."""
-    c = CAPACITY.get(model)
+    c = capacity_for(model)
     if c is None:
         return cap if layout.kind == "pd" and len(layout.prefill_ranks) >= 2 else 0
     k = len(layout.decode_groups[0])
@@ -321,7 +330,7 @@ def prefill_overflow_cap(layout: NodeLayout, cap: int = 256, model: str = "llama
 def decode_local_fraction(layout: NodeLayout, model: str = "llama3-70b") -> float:
     """Share of a decode replica's KV pool for prompts it admits itself (hybrid
     decode) when the prefill side cannot saturate it."""
-    c = CAPACITY.get(model)
+    c = capacity_for(model)
     if c is None:
         return {1: 0.35, 2: 0.15}.get(len(layout.prefill_ranks), 0.0) if layout.kind == "pd" else 0.0
     k = len(layout.decode_groups[0])

@@ -257,6 +257,14 @@ class GraphRunner:
         self.buckets = sorted(set(buckets))
         self.max_bucket = self.buckets[-1] if self.buckets else 0
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
+        # small buckets also get a one-split variant (8-wave workgroups walk each
+        # sequence's whole context: no partials, no reduce kernel) replayed when
+        # every context is short (DGI_DECODE_SHORT_CTX tokens, 0 = off; at ~900 tokens the split
+        # plan is faster again: profiles/r3_decode8b_short_ctx.md)
+        self.short_ctx = int(os.environ.get("DGI_DECODE_SHORT_CTX", "512"))
+        self.short_max_b = int(os.environ.get("DGI_DECODE_SHORT_B", "8"))
+        self.short_graphs: dict[int, torch.cuda.CUDAGraph] = {}
+        self._short = False
         self.pool_handle = None
         dev = runner.device
         maxb = self.max_bucket
@@ -302,7 +310,7 @@ class GraphRunner:
 
     def _meta(self, b):
         r = self.r
-        splits, part = self.split_plan(b)
+        splits, part = (1, 1 << 20) if self._short else self.split_plan(b)
         return AttnMeta(positions=self.pos[:b], slot_mapping=self.slots[:b], num_decode=b,
                         dec_block_tables=self.bt[:b], dec_context_lens=self.ctx[:b],
                         dec_max_splits=splits, dec_part_size=part, dec_workspace=r.dec_ws,
@@ -315,7 +323,7 @@ class GraphRunner:
             m.capture_layers, m.captured = tuple(layers), {}
             try:
                 logits = m.forward(self._meta(b), input_ids=self.ids[:b])
-                self.feats_out[b] = fuse(torch.cat([m.captured[li] for li in layers], dim=-1))
+                self.feats_out[(b, self._short)] = fuse(torch.cat([m.captured[li] for li in layers], dim=-1))
             finally:
                 m.capture_layers, m.captured = (), {}
         else:
@@ -338,6 +346,17 @@ class GraphRunner:
             if self.pool_handle is None:
                 self.pool_handle = g.pool()
             self.graphs[b] = g
+            if self.short_ctx > 0 and b <= self.short_max_b and self.r.model.cfg.head_dim in (64, 128):
+                self._short = True
+                try:
+                    self._body(b)
+                    torch.cuda.synchronize()
+                    gs = torch.cuda.CUDAGraph()
+                    with graph_capture(gs, pool=self.pool_handle):
+                        self._body(b)
+                    self.short_graphs[b] = gs
+                finally:
+                    self._short = False
         torch.cuda.synchronize()
         self.captured = True
 
@@ -356,6 +375,7 @@ class GraphRunner:
         temps, seeds, topk = seg[4].view(np.float32), seg[5], seg[6]
         topp = seg[7].view(np.float32)
         bt = h[S * b: S * b + b * maxw].reshape(b, maxw)
+        max_ctx = 0
         seg[:] = 0
         ctx[:] = 1
         topp[:] = 1.0
@@ -369,6 +389,7 @@ class GraphRunner:
             pos[i] = p
             slots[i] = rq.blocks[p // bs] * bs + p % bs
             ctx[i] = p + 1
+            max_ctx = max(max_ctx, p + 1)
             bt[i, : len(rq.blocks)] = rq.blocks
             temps[i] = rq.params.temperature
             seeds[i] = rq.sample_seed()
@@ -383,10 +404,13 @@ class GraphRunner:
         self.topk[:b].copy_(dseg[6])
         self.topp[:b].copy_(dseg[7].view(torch.float32))
         self.bt[:b].copy_(dev[S * b:].view(b, maxw))
-        self.graphs[b].replay()
+        gs = self.short_graphs.get(b)
+        short = gs is not None and max_ctx <= self.short_ctx
+        (gs if short else self.graphs[b]).replay()
         self.last_bucket = b
+        self.last_key = (b, short)
         return self.r.fetch(self.out[:n], self.host_out[:n])
 
     def last_features(self, n: int) -> torch.Tensor:
         """Fused EAGLE-3 features of the last replay's first ``n`` rows (feature tap on)."""
-        return self.feats_out[self.last_bucket][:n]
+        return self.feats_out[self.last_key][:n]
