@@ -137,6 +137,9 @@ class LLMEngine:
         self.requests: dict = {}
         # optional callback(ScheduledBatch) between scheduling and execution (P/D streaming)
         self.pre_execute = None
+        # optional callback(Request) when a request's first token is sampled, BEFORE any
+        # stop check may free its pages (cross-worker KV export)
+        self.first_token_hook = None
         self.stats = {"steps": 0, "prefill_tokens": 0, "decode_tokens": 0, "generated": 0,
                       "finished": 0, "step_time": 0.0}
         # MLP row padding measured on this GPU (hipBLASLt kernel-selection cliffs, dgi.runtime.gemm_pad)
@@ -203,6 +206,8 @@ class LLMEngine:
             req.token_times.append(now)
             if req.first_token_time is None:
                 req.first_token_time = now
+                if self.first_token_hook is not None:
+                    self.first_token_hook(req)
             st["generated"] += 1
             reason = self._check_stop(req, int(tok))
             if reason is not None:
@@ -221,6 +226,39 @@ class LLMEngine:
         if req.total_len >= self.cfg.max_model_len - 1:
             return "length"
         return None
+
+    # ------------------------------------------------------------------ cross-worker KV (dgi.kv.transfer)
+    def export_request_kv(self, req: Request) -> torch.Tensor:
+        """The pages holding ``req``'s computed tokens, all local layers, on the host:
+        [L, 2, n_pages, n_kv, page, head_dim]."""
+        from dgi import ops
+        nb = (req.num_computed + self.pool.block_size - 1) // self.pool.block_size
+        ids = torch.tensor(req.blocks[:nb], dtype=torch.int32, device=self.device)
+        return ops.kv_gather(self.pool.kv, ids).cpu()
+
+    def import_prefilled(self, prompt: list[int], first_token: int, kv: torch.Tensor,
+                         params: Optional[SamplingParams] = None, rid=None) -> Request:
+        """Adopt a sequence another worker prefilled: its pages ``kv`` (``export_request_kv``
+        layout) go into fresh pages of this pool and decoding continues from
+        ``first_token`` — no prompt recompute."""
+        from dgi import ops
+        L, two, n, nkv, bs, hd = kv.shape
+        pool = self.pool
+        if (L, nkv, bs, hd) != (pool.kv.shape[0], pool.kv.shape[3], pool.kv.shape[4], pool.kv.shape[5]):
+            raise ValueError(f"KV geometry {tuple(kv.shape)} does not match this engine's pool "
+                             f"{tuple(pool.kv.shape)}")
+        if n != (len(prompt) + bs - 1) // bs:
+            raise ValueError(f"{n} pages for a {len(prompt)}-token prompt")
+        ids = pool.allocate(n)
+        ops.kv_scatter(pool.kv, torch.tensor(ids, dtype=torch.int32, device=self.device),
+                       kv.to(self.device, pool.dtype))
+        req = Request(prompt, params or SamplingParams(), rid=rid)
+        req.output = [int(first_token)]
+        req.first_token_time = time.perf_counter()
+        req.token_times.append(req.first_token_time)
+        self.scheduler.add_prefilled(req, ids)
+        self.requests[req.rid] = req
+        return req
 
     def generate(self, prompts: Iterable[list[int]], params: Optional[SamplingParams] = None) -> list[Request]:
         reqs = [self.add_request(p, params) for p in prompts]

@@ -18,8 +18,10 @@ drives them from the pull-based job API:
   decode, else the best decode worker by bandwidth x headroom / load), and
   requeues the job as ``phase = "decode"`` pinned to that worker
   (``target_worker_id``), with ``params.kv_source`` naming the holder when the
-  KV has to move (``KVCacheMigrator`` accounts it; inside one MI355X node the
-  move is dgi's RCCL migration, across nodes the decode worker re-prefills);
+  KV has to move and ``params.kv_url`` where to pull it from (``KVCacheMigrator``
+  accounts it; inside one MI355X node the move is dgi's RCCL migration, across
+  workers the decode worker pulls the exported pages over HTTP —
+  dgi/kv/transfer.py — and re-prefills only when they are gone);
 * the decode completion releases the scheduler's load accounting.
 
 ``/api/v1/admin/pd/stats`` reports ``get_stats()``; the observability
@@ -154,6 +156,10 @@ class PDCoordinator:
         params["kv_cache_key"] = kv_key
         if a is not None and a.kv_migration_needed:
             params["kv_source"] = a.migration_source
+            # the decode worker pulls the pages from the prefill worker (dgi.kv.transfer)
+            # instead of re-running the prompt, when the prefill worker exported them
+            if res.get("kv_url"):
+                params["kv_url"] = res["kv_url"]
         return {"phase": "decode", "target_worker_id": a.worker_id if a is not None else None, "params": params,
                 "estimated_latency_ms": a.estimated_latency_ms if a is not None else None}
 

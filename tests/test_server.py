@@ -327,7 +327,8 @@ def test_api_pd_job_path_places_decode_by_scheduler(client):
     a = c.get(f"/api/v1/workers/{pre}/next-job", headers=hp).json()
     assert a["job_id"] == job_id
     r = c.post(f"/api/v1/workers/{pre}/jobs/{job_id}/complete",
-               json={"success": True, "result": {"response": "W", "first_token": "W", "kv_cache_key": "kv-1"},
+               json={"success": True, "result": {"response": "W", "first_token": "W", "kv_cache_key": "kv-1",
+                                                 "kv_url": "http://10.0.0.9:8080/kv/kv-1"},
                      "processing_time_ms": 12}, headers=hp).json()
     assert r["next_phase"] == "decode" and r["decode_worker"] == dec1
     assert c.get(f"/api/v1/jobs/{job_id}").json()["status"] == "queued"
@@ -335,6 +336,7 @@ def test_api_pd_job_path_places_decode_by_scheduler(client):
     assert c.get(f"/api/v1/workers/{dec2}/next-job", headers=hd2).json() is None
     b = c.get(f"/api/v1/workers/{dec1}/next-job", headers=hd1).json()
     assert b["job_id"] == job_id and b["params"]["pd_phase"] == "decode" and b["params"]["kv_source"] == pre
+    assert b["params"]["kv_url"] == "http://10.0.0.9:8080/kv/kv-1"      # where the decode worker pulls the KV
     c.post(f"/api/v1/workers/{dec1}/jobs/{job_id}/complete",
            json={"success": True, "result": {"response": "World", "usage": {"completion_tokens": 8}},
                  "processing_time_ms": 30}, headers=hd1)

@@ -79,6 +79,18 @@ class DirectServer:
                     "gpu_info": w._get_gpu_info(), "accepting_jobs": w.accepting_jobs,
                     "engines": {k: e.get_status() for k, e in w.engines.items()}}
 
+        @app.get("/kv/{key}")
+        async def kv_pull(key: str):
+            """Cluster P/D: the pages of a sequence this worker prefilled (dgi.kv.transfer
+            blob), pulled once by the decode worker the scheduler placed it on."""
+            from fastapi.responses import Response
+            eng = self.worker.engines.get("llm")
+            store = getattr(eng, "kv_exports", None)
+            blob = store.take(key) if store is not None else None
+            if blob is None:
+                raise HTTPException(404, f"no exported KV under {key}")
+            return Response(content=blob, media_type="application/octet-stream")
+
         @app.post("/inference", response_model=DirectInferenceResponse)
         async def direct_inference(req: DirectInferenceRequest):
             self._admit(req.type)

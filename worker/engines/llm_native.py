@@ -44,10 +44,11 @@ def _merged(config: Dict[str, Any]) -> Dict[str, Any]:
 
 
 class _Pending:
-    __slots__ = ("req", "loop", "future", "stream_q", "sent", "cfg", "prompt_len")
+    __slots__ = ("req", "loop", "future", "stream_q", "sent", "cfg", "prompt_len", "export_key")
 
-    def __init__(self, loop, future, stream_q, cfg, prompt_len):
+    def __init__(self, loop, future, stream_q, cfg, prompt_len, export_key=None):
         self.req = None
+        self.export_key = export_key    # cluster P/D prefill phase: export the KV at the first token
         self.loop = loop
         self.future = future
         self.stream_q = stream_q
@@ -66,7 +67,10 @@ class NativeLLMEngine(LLMBaseEngine):
         self._thread: Optional[threading.Thread] = None
         self._stop = threading.Event()
         self._wake = threading.Event()
-        self.stats = {"requests": 0, "completed": 0, "errors": 0}
+        self.stats = {"requests": 0, "completed": 0, "errors": 0, "kv_exported": 0, "kv_imported": 0}
+        # cluster P/D: sequences this worker prefilled, waiting for their decode worker's pull
+        from dgi.kv.transfer import KVExportStore
+        self.kv_exports = KVExportStore(int(float(_merged(config).get("kv_export_gb", 8)) * (1 << 30)))
 
     # ------------------------------------------------------------------ lifecycle
     def load_model(self) -> None:
@@ -126,6 +130,7 @@ class NativeLLMEngine(LLMBaseEngine):
                 # speculation graphs for the batch buckets this worker serves, at every depth
                 sb = (spec if isinstance(spec, dict) else {}).get("graph_batches", (1, 2, 4, 8))
                 self.engine.warmup_spec(tuple(sb))
+        self.engine.first_token_hook = self._on_first_token
         self._stop.clear()
         self._thread = threading.Thread(target=self._loop, name="dgi-engine", daemon=True)
         self._thread.start()
@@ -149,13 +154,24 @@ class NativeLLMEngine(LLMBaseEngine):
         while not self._stop.is_set():
             while True:
                 try:
-                    prompt, p, cfg = self._inbox.get_nowait()
+                    prompt, p, cfg, imported = self._inbox.get_nowait()
                 except queue.Empty:
                     break
                 try:
                     sp = SamplingParams(max_tokens=cfg.max_tokens, temperature=cfg.temperature, top_p=cfg.top_p,
                                         top_k=cfg.top_k)
-                    p.req = eng.add_request(prompt, sp)
+                    if imported is not None:       # decode phase of a cluster P/D job: KV pulled from its prefill worker
+                        first, kv = imported
+                        p.req = eng.import_prefilled(prompt, first, kv, sp)
+                        self.stats["kv_imported"] += 1
+                        if p.stream_q is not None:
+                            p.loop.call_soon_threadsafe(p.stream_q.put_nowait, first)
+                        if sp.max_tokens <= 1:
+                            eng.abort(p.req.rid)
+                            self._resolve(p, p.req)
+                            continue
+                    else:
+                        p.req = eng.add_request(prompt, sp)
                     self._pending[p.req.rid] = p
                 except Exception as e:  # prompt too long etc.
                     self._resolve_error(p, e)
@@ -180,6 +196,20 @@ class NativeLLMEngine(LLMBaseEngine):
                 if o.finished:
                     self._pending.pop(o.rid, None)
                     self._resolve(p, o.request)
+
+    def _on_first_token(self, req) -> None:
+        """Engine thread, first token of ``req`` sampled and its pages still held:
+        a P/D prefill-phase request exports them for its decode worker."""
+        p = self._pending.get(req.rid)
+        if p is None or p.export_key is None:
+            return
+        from dgi.kv.transfer import pack_kv
+        mc = self.engine.model_cfg
+        blob = pack_kv(self.engine.export_request_kv(req),
+                       {"prompt": list(req.prompt), "first_token": int(req.output[0]), "model": mc.name,
+                        "num_layers": mc.num_layers, "seed": int(req.seed)})
+        self.kv_exports.put(p.export_key, blob)
+        self.stats["kv_exported"] += 1
 
     def _resolve(self, p: _Pending, req) -> None:
         text = self.tokenizer.decode(req.output, skip_special_tokens=True)
@@ -206,16 +236,53 @@ class NativeLLMEngine(LLMBaseEngine):
                 p.stream_q.put_nowait(None)
         p.loop.call_soon_threadsafe(_set)
 
-    def _submit(self, messages, cfg: GenerationConfig, stream: bool = False) -> _Pending:
+    def _submit(self, messages, cfg: GenerationConfig, stream: bool = False, export_key: Optional[str] = None,
+                prompt: Optional[List[int]] = None, imported=None) -> _Pending:
         if not self.loaded:
             raise RuntimeError("model not loaded")
         loop = asyncio.get_running_loop()
-        prompt = chat_prompt_ids(self.tokenizer, messages)
-        p = _Pending(loop, loop.create_future(), asyncio.Queue() if stream else None, cfg, len(prompt))
+        if prompt is None:
+            prompt = chat_prompt_ids(self.tokenizer, messages)
+        p = _Pending(loop, loop.create_future(), asyncio.Queue() if stream else None, cfg, len(prompt), export_key)
         self.stats["requests"] += 1
-        self._inbox.put((prompt, p, cfg))
+        self._inbox.put((prompt, p, cfg, imported))
         self._wake.set()
         return p
+
+    # ------------------------------------------------------------------ cluster P/D (server services/pd_runtime.py)
+    def prefill_export(self, params: Dict[str, Any], key: str) -> Dict[str, Any]:
+        """Prefill phase: sample the first token and keep the sequence's KV pages under
+        ``key`` (``kv_exports``) for the decode worker to pull (``GET /kv/{key}``)."""
+        from .llm_base import generation_config_from_params, result_to_response
+        cfg = generation_config_from_params({**params, "max_tokens": 1})
+
+        async def run():
+            return await self._submit(self._messages_of(params), cfg, export_key=key).future
+        res = self._run_sync(run())
+        out = result_to_response(res)
+        out["kv_cache_key"] = key
+        return out
+
+    def decode_import(self, params: Dict[str, Any], blob: bytes) -> Dict[str, Any]:
+        """Decode phase with the prefill worker's pages: no prompt recompute."""
+        from dgi.kv.transfer import unpack_kv
+        from .llm_base import generation_config_from_params, result_to_response
+        kv, meta = unpack_kv(blob)
+        if meta.get("model") not in (None, self.engine.model_cfg.name):
+            raise ValueError(f"KV of model {meta.get('model')} offered to a {self.engine.model_cfg.name} engine")
+        cfg = generation_config_from_params(params)
+
+        async def run():
+            return await self._submit(None, cfg, prompt=list(meta["prompt"]),
+                                      imported=(int(meta["first_token"]), kv)).future
+        return result_to_response(self._run_sync(run()))
+
+    def _run_sync(self, coro):
+        try:
+            asyncio.get_running_loop()
+        except RuntimeError:
+            return asyncio.run(coro)
+        return self._run_coroutine_in_new_thread(coro)
 
     # ------------------------------------------------------------------ LLMBaseEngine
     async def generate_async(self, messages: List[Dict[str, str]],

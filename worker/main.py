@@ -265,18 +265,42 @@ class Worker:
         return self._execute(job_type, params, job_id)
 
     def _execute_pd(self, params: Dict[str, Any], job_id: str) -> Dict[str, Any]:
-        """Cluster P/D job (server services/pd_runtime.py).  Prefill phase: one
-        token, reported with the KV key the decode placement uses.  Decode phase:
-        the full completion on the worker the P/D scheduler chose; the KV cannot
-        cross nodes through this HTTP path, so the decode worker rebuilds it by
-        re-prefill (inside one MI355X node dgi migrates it over RCCL instead)."""
+        """Cluster P/D job (server services/pd_runtime.py).
+
+        Prefill phase: one token, reported with the KV key the decode placement
+        uses; a native engine keeps the sequence's pages under that key and the
+        result names the URL they can be pulled from (``GET /kv/{key}`` on this
+        worker's direct server).  Decode phase: the full completion on the worker
+        the P/D scheduler chose — from the pulled pages when ``kv_url`` is given
+        (no prompt recompute: the reference's ``TransferKVCache`` made real,
+        dgi/kv/transfer.py), else by re-prefilling.  Inside one MI355X node dgi
+        migrates KV over RCCL instead (dgi/parallel/pd.py)."""
         phase = params.get("pd_phase", "prefill")
+        key = f"{getattr(self, 'worker_id', None)}:{job_id}"
+        engine = getattr(self, "engines", {}).get("llm")
         if phase == "prefill":
+            if engine is not None and hasattr(engine, "prefill_export"):
+                out = engine.prefill_export({**params, "max_tokens": 1}, key)
+                base = getattr(self, "direct_url", None)
+                return {**out, "phase": "prefill", "first_token": out.get("response", ""), "kv_cache_key": key,
+                        "kv_url": f"{base.rstrip('/')}/kv/{key}" if base else None}
             out = self._execute("llm", {**params, "max_tokens": 1}, job_id)
-            return {**out, "phase": "prefill", "first_token": out.get("response", ""),
-                    "kv_cache_key": f"{self.worker_id}:{job_id}"}
-        out = self._execute("llm", {k: v for k, v in params.items() if k not in ("pd_phase", "first_token")},
-                            job_id)
+            return {**out, "phase": "prefill", "first_token": out.get("response", ""), "kv_cache_key": key}
+        clean = {k: v for k, v in params.items() if k not in ("pd_phase", "first_token", "kv_url")}
+        url = params.get("kv_url")
+        if url and engine is not None and hasattr(engine, "decode_import"):
+            try:
+                import httpx
+                t0 = time.perf_counter()
+                r = httpx.get(url, timeout=60.0)
+                r.raise_for_status()
+                pull_ms = (time.perf_counter() - t0) * 1000.0
+                out = engine.decode_import(clean, r.content)
+                return {**out, "phase": "decode", "kv_source": params.get("kv_source"), "reprefilled": False,
+                        "kv_bytes": len(r.content), "kv_pull_ms": round(pull_ms, 2)}
+            except Exception as e:     # source gone / evicted: fall back to recomputing the prompt
+                logger.warning("KV pull from %s failed (%s): re-prefilling", url, e)
+        out = self._execute("llm", clean, job_id)
         return {**out, "phase": "decode", "kv_source": params.get("kv_source"), "reprefilled": True}
 
     def _execute(self, job_type: str, params: Dict[str, Any], job_id: str = "direct") -> Dict[str, Any]:
@@ -385,6 +409,9 @@ class Worker:
         from direct_server import DirectServer
         self.direct_server = DirectServer(self, self.config.direct.host, self.config.direct.port)
         self.direct_server.start_background()
+        d = self.config.direct
+        # where decode workers pull this worker's exported KV (cluster P/D, GET /kv/{key})
+        self.direct_url = d.public_url or f"http://{'127.0.0.1' if d.host in ('0.0.0.0', '') else d.host}:{d.port}"
 
     def start(self, install_signals: bool = True) -> None:
         self._load_engines()
