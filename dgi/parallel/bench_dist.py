@@ -57,6 +57,22 @@ def ctrl_ping(f, a: int, b: int, n: int = 400) -> Optional[dict]:
     return {"p50": round(ts[len(ts) // 2], 2), "p99": round(ts[int(0.99 * (len(ts) - 1))], 2), "n": n}
 
 
+def capacity_check(cap, layout, per_rank: list, el: float) -> Optional[dict]:
+    """The start-up layout pick against what the run measured, per role (the capacity
+    table is one box's numbers: profiles/r3_pd_capacity_70b.jsonl)."""
+    if cap is None or layout.kind not in ("pd", "pdpp") or el <= 0:
+        return None
+    k = len(layout.decode_groups[0])
+    pre = [o for o in per_rank if o.get("role") == "prefill"]
+    drv = [o for o in per_rank if o.get("role") == "decode_driver"]
+    ppg = sum(o.get("prompts", 0) for o in pre) / el / max(1, len(pre))
+    dpr = sum(o.get("tokens", 0) for o in drv) / el / max(1, len(drv))
+    tab = cap.decode_tok_s.get(k)
+    return {"prefill_prompts_s_per_gpu": round(ppg, 2), "table_prompts_s": round(cap.prefill_tok_s / 128, 2),
+            "decode_tok_s_per_replica": round(dpr, 1), "table_decode_tok_s": tab,
+            "decode_utilization": round(dpr / tab, 3) if tab else None}
+
+
 def run_distributed(args, layout_kind: str, dist):
     f = Fabric()
     rank, world = f.rank, f.world
@@ -125,7 +141,8 @@ def run_distributed(args, layout_kind: str, dist):
         k = len(layout.decode_groups[0])
         if k in cap.decode_tok_s:
             est = layout_estimate(len(layout.prefill_ranks), k, len(layout.decode_groups), cap)
-    return total, el, all_ttfts, {"planner_estimate": est,
+    check = capacity_check(cap, layout, per_rank, el)
+    return total, el, all_ttfts, {"planner_estimate": est, "capacity_check": check,
                                   "layout": {"kind": layout.kind, "describe": layout.describe(),
                                              "prefill": layout.prefill_ranks, "decode_groups": layout.decode_groups},
                                   "concurrency": conc, "pair_setup_s": round(t_pairs, 3), "roles": roles,
@@ -274,7 +291,7 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
         f.barrier()
         el = time.perf_counter() - t0
         srv.finish()
-        return n, el, ttfts, {"tokens": n, "prefill_mbt": pmbt, "migrated": srv.migrated, "migrate_s": round(srv.migrate_time, 3),
+        return n, el, ttfts, {"tokens": n, "prompts": len(ttfts), "prefill_mbt": pmbt, "migrated": srv.migrated, "migrate_s": round(srv.migrate_time, 3),
                               "sent_GB": round(srv.sent_bytes / 1e9, 3), "local_cap": lc,
                               "local_tokens": srv.local_tokens, "pd_scheduler": srv.pd_stats(),
                               "migration_ms_p50": srv.pd_stats()["migration_ms_p50"]}

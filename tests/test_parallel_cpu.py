@@ -619,3 +619,33 @@ def test_layout_estimate_reports_rate_and_latency():
     est = layout_estimate(npre, k, reps, cap)
     assert est["tok_s"] >= 0.995 * est["dp_tok_s"] and est["tpot_ms"] < est["dp_tpot_ms"]
     assert est["filler_share"] < 0.2 and est["ttft_ms"] is not None
+
+
+def _tp_gpu_body(rank, world):
+    """TP over the real device data plane (RCCL all-reduce twice per layer): outputs
+    of the 2-way TP engine vs a single-GPU engine with the same weights."""
+    from dgi.engine import LLMEngine
+    from dgi.parallel.fabric import Fabric
+    from dgi.parallel.tensor import TPEngine
+    from dgi.sched.request import SamplingParams
+    Fabric()                      # eager world communicator (device-bound) for the all-reduces
+    cfg = _engine_cfg("llama-tiny-tp", num_blocks=None, max_num_seqs=4, max_num_batched_tokens=128,
+                      use_graphs=False, enable_prefix_caching=True)
+    g = torch.Generator().manual_seed(0)
+    prompts = [torch.randint(5, 500, (n,), generator=g).tolist() for n in (9, 17, 30)]
+    sp = SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True)
+    out = [r.output for r in TPEngine(cfg, rank, world).generate(prompts, sp)]
+    ref = [r.output for r in LLMEngine(cfg).generate(prompts, sp)] if rank == 0 else None
+    return {"out": out, "ref": ref}
+
+
+def test_bench_capacity_check_against_table():
+    from dgi.parallel.bench_dist import capacity_check
+    from dgi.parallel.plan import capacity_for
+    lay = plan_node_layout(8)
+    ranks = [{"role": "prefill", "prompts": 196, "tokens": 40}] * 6 + [{"role": "decode_driver", "tokens": 12000},
+                                                                        {"role": "decode_stage"}]
+    c = capacity_check(capacity_for("llama3-70b"), lay, ranks, 10.0)
+    assert c["prefill_prompts_s_per_gpu"] == 19.6 and c["decode_tok_s_per_replica"] == 1200.0
+    assert 0 < c["decode_utilization"] < 1 and c["table_prompts_s"] > 19
+    assert capacity_check(None, lay, ranks, 10.0) is None

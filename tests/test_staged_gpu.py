@@ -106,3 +106,11 @@ def test_rccl_pdpp_serves_local_prompts_on_shared_gpu(shared_rccl, monkeypatch):
     out = tpc._spawn("_pd_body", 3, timeout=150)
     got = tpc._merged(out, 1)
     assert _agree(got, ref) >= 0.75, (got, ref)
+
+
+def test_rccl_tensor_parallel_on_shared_gpu(shared_rccl):
+    """2-way tensor parallelism with its two all-reduces per layer on RCCL (eager
+    world communicator), against a single-GPU engine with the same seeded weights."""
+    out = tpc._spawn("_tp_gpu_body", 2, timeout=150)
+    assert out[0]["out"] == out[1]["out"]                  # SPMD: both ranks emit the same tokens
+    assert _agree(out[0]["out"], out[0]["ref"]) >= 0.75, (out[0]["out"], out[0]["ref"])
