@@ -142,7 +142,9 @@ def run_distributed(args, layout_kind: str, dist):
         if k in cap.decode_tok_s:
             est = layout_estimate(len(layout.prefill_ranks), k, len(layout.decode_groups), cap)
     check = capacity_check(cap, layout, per_rank, el)
+    from dgi.parallel.topology import read_topology, summary
     return total, el, all_ttfts, {"planner_estimate": est, "capacity_check": check,
+                                  "topology": summary(read_topology()),
                                   "layout": {"kind": layout.kind, "describe": layout.describe(),
                                              "prefill": layout.prefill_ranks, "decode_groups": layout.decode_groups},
                                   "concurrency": conc, "pair_setup_s": round(t_pairs, 3), "roles": roles,

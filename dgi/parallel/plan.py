@@ -13,6 +13,7 @@
 from __future__ import annotations
 
 import dataclasses
+import os
 from typing import Optional
 
 
@@ -309,6 +310,10 @@ def plan_node_layout(n_gpus: int, kind: str = "pdpp", prefill_ranks: Optional[in
     reps = max(1, min(reps, (n_gpus - npre) // k))
     npre = n_gpus - k * reps
     groups = _groups(npre, k, reps)
+    if k > 2:      # consecutive stages on the cheapest links (identity on a full xGMI mesh)
+        from dgi.parallel.topology import order_stages, read_topology
+        topo = read_topology() if os.environ.get("DGI_SHARED_GPU", "0") != "1" else None
+        groups = [order_stages(topo, g) for g in groups]
     return NodeLayout("pdpp" if k > 1 else "pd", list(range(npre)), groups)
 
 

@@ -649,3 +649,35 @@ def test_bench_capacity_check_against_table():
     assert c["prefill_prompts_s_per_gpu"] == 19.6 and c["decode_tok_s_per_replica"] == 1200.0
     assert 0 < c["decode_utilization"] < 1 and c["table_prompts_s"] > 19
     assert capacity_check(None, lay, ranks, 10.0) is None
+
+
+def _fake_kfd(root, n_gpus, missing=()):
+    import os as _os
+    for node in range(n_gpus + 1):                     # node 0: the CPU
+        d = root / str(node)
+        (d / "io_links").mkdir(parents=True)
+        (d / "properties").write_text(f"cpu_cores_count 0\ngpu_id {0 if node == 0 else 1000 + node}\n")
+        if node == 0:
+            continue
+        for j, peer in enumerate(p for p in range(1, n_gpus + 1) if p != node):
+            if (node - 1, peer - 1) in missing:
+                continue
+            ld = d / "io_links" / str(j)
+            ld.mkdir()
+            ld.joinpath("properties").write_text(f"type 11\nnode_from {node}\nnode_to {peer}\nweight 15\n"
+                                                 f"max_bandwidth 153600\n")
+
+
+def test_topology_full_mesh_and_stage_order(tmp_path):
+    from dgi.parallel.topology import order_stages, read_topology, summary
+    _fake_kfd(tmp_path, 8)
+    t = read_topology(str(tmp_path))
+    s = summary(t)
+    assert s["gpus"] == 8 and s["xgmi_links"] == 56 and s["full_xgmi_mesh"]
+    assert order_stages(t, [5, 6, 7]) == [5, 6, 7]               # full mesh: identity
+    part = tmp_path / "p"
+    _fake_kfd(part, 4, missing={(1, 2), (2, 1)})              # no direct 1 <-> 2 link
+    t2 = read_topology(str(part))
+    assert not summary(t2)["full_xgmi_mesh"]
+    assert order_stages(t2, [1, 2, 3]) == [1, 3, 2]           # hop 1 -> 3 -> 2 stays on xGMI
+    assert read_topology(str(tmp_path / "absent")) is None
