@@ -133,6 +133,11 @@ class Fabric:
         self.world = dist.get_world_size()
         self.backend = dist.get_backend()
         self.on_gpu = self.backend == "nccl"
+        if self.on_gpu and getattr(dist.distributed_c10d._get_default_group(), "bound_device_id", None) is None:
+            # lazily initialised RCCL: every point-to-point pair would get its own 2-rank
+            # communicator and stream, and a first batched op hangs unless every rank joins it
+            raise RuntimeError("dgi needs the RCCL process group initialised eagerly: call "
+                               "dgi.parallel.fabric.init_distributed() (init_process_group(device_id=...))")
         # "staged" mode: GPU compute with a gloo data plane (tensors bounce
         # through host memory).  Lets the multi-rank GPU code paths run when
         # the ranks share one device without RCCL.
