@@ -7,8 +7,8 @@ and layouts need no placement search.  The runtime still checks it at start-up
 pipeline stages on direct xGMI links when a node is not a full mesh (partial
 partitions, PCIe-attached boards).
 
-KFD layout: ``/sys/class/kfd/kfd/topology/nodes/<n>/properties`` (``gpu_id`` 0 on
-CPU nodes) and ``nodes/<n>/io_links/<m>/properties`` (``type``: 11 = xGMI,
+KFD layout: ``/sys/class/kfd/kfd/topology/nodes/<n>/gpu_id`` (0 on CPU nodes),
+``nodes/<n>/properties`` (``simd_count``) and ``nodes/<n>/io_links/<m>/properties`` (``type``: 11 = xGMI,
 2 = PCIe; ``node_to``; ``weight``: lower is closer; ``max_bandwidth``).
 GPU nodes in node-id order are the HIP device ordinals.
 """
@@ -36,13 +36,23 @@ def _props(path: str) -> dict:
     return out
 
 
+def _is_gpu(node_dir: str) -> bool:
+    """KFD exposes the GPU id in its own ``gpu_id`` file (0 on CPU nodes); the
+    ``properties`` file has ``simd_count`` > 0 for GPUs."""
+    try:
+        with open(os.path.join(node_dir, "gpu_id")) as f:
+            return int(f.read().strip() or 0) != 0
+    except (OSError, ValueError):
+        return _props(os.path.join(node_dir, "properties")).get("simd_count", 0) > 0
+
+
 def read_topology(root: str = KFD_NODES) -> Optional[dict]:
     """{"gpus": n, "links": {(i, j): {"type", "weight", "max_bw"}}} over HIP ordinals,
     or None when the KFD tree is absent (CPU boxes)."""
     if not os.path.isdir(root):
         return None
     nodes = sorted(int(n) for n in os.listdir(root) if n.isdigit())
-    gpu_nodes = [n for n in nodes if _props(os.path.join(root, str(n), "properties")).get("gpu_id", 0) != 0]
+    gpu_nodes = [n for n in nodes if _is_gpu(os.path.join(root, str(n)))]
     ordinal = {n: i for i, n in enumerate(gpu_nodes)}
     links = {}
     for n in gpu_nodes:

@@ -656,7 +656,8 @@ def _fake_kfd(root, n_gpus, missing=()):
     for node in range(n_gpus + 1):                     # node 0: the CPU
         d = root / str(node)
         (d / "io_links").mkdir(parents=True)
-        (d / "properties").write_text(f"cpu_cores_count 0\ngpu_id {0 if node == 0 else 1000 + node}\n")
+        (d / "properties").write_text(f"cpu_cores_count {64 if node == 0 else 0}\nsimd_count {0 if node == 0 else 1024}\n")
+        (d / "gpu_id").write_text(f"{0 if node == 0 else 1000 + node}\n")
         if node == 0:
             continue
         for j, peer in enumerate(p for p in range(1, n_gpus + 1) if p != node):
