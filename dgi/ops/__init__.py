@@ -371,7 +371,12 @@ def _use_skinny(M: int, N: int, K: int) -> bool:
     return M <= 8 or (N <= 4096 and M <= 16) or (N >= 16384 and M <= 16)
 
 
+SKINNY_CFG = int(os.environ.get("DGI_SKINNY_CFG", "0"))    # > 0 forces a skinny_gemm launch config (sweeps)
+
+
 def _skinny_cfg(M: int, N: int) -> int:
+    if SKINNY_CFG > 0:
+        return SKINNY_CFG
     return 5 if (M > 8 and N >= 16384) else 0
 
 

@@ -34,6 +34,8 @@ for c in $cases; do
     pd8_5p_3d_nooverflow) run $c 8 --layout pd --prefill-ranks 5 --decode-replicas 3 --prefill-local-cap 0 || exit 1 ;;
     pd8_2p_6d) run $c 8 --layout pd --prefill-ranks 2 --decode-replicas 6 || exit 1 ;;
     auto2) run $c 2 || exit 1 ;;         # what the driver's scaling run launches: the planner's layout
+    dp2) run $c 2 --layout dp || exit 1 ;;
+    dp4) run $c 4 --layout dp || exit 1 ;;
     auto4) run $c 4 || exit 1 ;;
     auto8) run $c 8 || exit 1 ;;
     pp8) run $c 8 --layout pp || exit 1 ;;

@@ -24,7 +24,8 @@ def row(path: str) -> str:
             if r.get("role") == "prefill" and r.get("pd_scheduler", {}).get("kv_transport", {}).get("cts_rtt_us_p50")]
     migrated = sum(r.get("migrated", 0) for r in ranks if r.get("role") == "prefill")
     rtt = f"{sorted(rtts)[len(rtts) // 2]:.0f}" if rtts else "—"
-    return (f"| `{name}` | {d['config']['model']} | {e['layout']['describe']} | completes | "
+    lay = e["layout"]["describe"] if isinstance(e.get("layout"), dict) else d["config"].get("parallelism")
+    return (f"| `{name}` | {d['config']['model']} | {lay} | completes | "
             f"{e.get('pair_setup_s', 0):.2f} | {migrated} | {kv_tx} | {rtt} |")
 
 
