@@ -201,20 +201,35 @@ class LLMEngine:
         for r in sb.decode:
             r.num_computed += 1
         outs = []
+        eos = self.model_cfg.eos_token_id
+        len_cap = self.cfg.max_model_len - 1
+        hook = self.first_token_hook
+        finish = self.scheduler.finish
         for req, tok in zip(rows, tokens):
-            req.output.append(int(tok))
+            tok = int(tok)
+            out = req.output
+            out.append(tok)
             req.token_times.append(now)
             if req.first_token_time is None:
                 req.first_token_time = now
-                if self.first_token_hook is not None:
-                    self.first_token_hook(req)
-            st["generated"] += 1
-            reason = self._check_stop(req, int(tok))
+                if hook is not None:
+                    hook(req)
+            p = req.params
+            # stop checks (``_check_stop``) inlined: this loop runs once per sampled row
+            if len(out) >= p.max_tokens:
+                reason = "length"
+            elif not p.ignore_eos and (tok == eos or tok in p.stop_token_ids):
+                reason = "stop"
+            elif len(req.prompt) + len(out) >= len_cap:
+                reason = "length"
+            else:
+                reason = None
             if reason is not None:
-                self.scheduler.finish(req, reason)
+                finish(req, reason)
                 st["finished"] += 1
                 self.requests.pop(req.rid, None)
-            outs.append(StepOutput(req.rid, int(tok), reason is not None, reason, req))
+            outs.append(StepOutput(req.rid, tok, reason is not None, reason, req))
+        st["generated"] += len(outs)
         return outs
 
     def _check_stop(self, req: Request, tok: int) -> Optional[str]:

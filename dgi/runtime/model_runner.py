@@ -14,6 +14,7 @@ from __future__ import annotations
 import contextlib
 import dataclasses
 import gc
+import itertools
 import os
 import time
 from typing import Optional
@@ -62,6 +63,36 @@ def graph_capture(g, pool=None):
     finally:
         if was:
             gc.enable()
+
+
+def decode_rows(reqs: list, bs: int, bt_out: np.ndarray):
+    """Per-row decode metadata of ``reqs``, vectorised (the per-request Python work is
+    one attribute read per field): returns (input token, position, KV slot, context
+    length) int32 arrays and fills ``bt_out[:n]`` (zeroed by the caller) with the
+    block tables."""
+    n = len(reqs)
+    pos = np.fromiter((r.num_computed for r in reqs), np.int32, n)
+    ids = np.fromiter((r.output[-1] if r.output else r.prompt[-1] for r in reqs), np.int32, n)
+    lens = np.fromiter((len(r.blocks) for r in reqs), np.int64, n)
+    tot = int(lens.sum())
+    flatb = np.fromiter(itertools.chain.from_iterable(r.blocks for r in reqs), np.int32, tot)
+    starts = np.cumsum(lens) - lens
+    rows = np.repeat(np.arange(n), lens)
+    cols = np.arange(tot) - np.repeat(starts, lens)
+    bt_out[rows, cols] = flatb
+    slots = bt_out[np.arange(n), pos // bs] * bs + pos % bs
+    return ids, pos, slots.astype(np.int32), pos + 1
+
+
+def sampling_rows(sampled: list):
+    """(temperature bits, seed, top-k, top-p bits, any filtered) of the sampled rows."""
+    n = len(sampled)
+    nf = [r.params.needs_filter for r in sampled]
+    temps = np.fromiter((r.params.temperature for r in sampled), np.float32, n).view(np.int32)
+    seeds = np.fromiter((r.sample_seed() for r in sampled), np.int64, n).astype(np.int32)
+    topk = np.fromiter((max(0, r.params.top_k) if f else 0 for r, f in zip(sampled, nf)), np.int32, n)
+    topp = np.fromiter((r.params.top_p if f else 1.0 for r, f in zip(sampled, nf)), np.float32, n).view(np.int32)
+    return temps, seeds, topk, topp, any(nf)
 
 
 class ModelRunner:
@@ -122,13 +153,8 @@ class ModelRunner:
         maxw = self.max_blocks
         dec_bt = np.zeros((ndp, maxw), np.int32)
         dec_ctx = np.ones(ndp, np.int32)
-        for i, r in enumerate(sb.decode):
-            p = r.num_computed
-            ids[i] = r.output[-1] if r.output else r.prompt[-1]
-            pos[i] = p
-            slots[i] = r.blocks[p // bs] * bs + p % bs
-            dec_bt[i, : len(r.blocks)] = r.blocks
-            dec_ctx[i] = p + 1
+        if nd:
+            ids[:nd], pos[:nd], slots[:nd], dec_ctx[:nd] = decode_rows(sb.decode, bs, dec_bt)
         # padded decode rows write into reserved block 0 and read it back
         nb = len(chunks)
         pre_bt = np.zeros((nb, maxw), np.int32)
@@ -159,13 +185,8 @@ class ModelRunner:
         tiles_np = np.asarray(tiles, np.int32).reshape(-1, 2)
         nlog = len(logit_rows)
         lidx = np.asarray(logit_rows, np.int32)
-        temps = np.asarray([r.params.temperature for r in sampled], np.float32).view(np.int32)
-        seeds = np.asarray([r.sample_seed() for r in sampled], np.int32)
         # top-k / top-p ride in the same flat buffer (one H2D copy; pipeline stages get them too)
-        filt = any(r.params.needs_filter for r in sampled)
-        topk = np.asarray([max(0, r.params.top_k) if r.params.needs_filter else 0 for r in sampled], np.int32)
-        topp = np.asarray([r.params.top_p if r.params.needs_filter else 1.0 for r in sampled],
-                          np.float32).view(np.int32)
+        temps, seeds, topk, topp, filt = sampling_rows(sampled)
         parts = [ids, pos, slots, dec_bt.ravel(), dec_ctx, pre_bt.ravel(), cu, pctx, tiles_np.ravel(), lidx,
                  temps, seeds, topk, topp]
         flat = np.concatenate(parts)
@@ -375,24 +396,16 @@ class GraphRunner:
         temps, seeds, topk = seg[4].view(np.float32), seg[5], seg[6]
         topp = seg[7].view(np.float32)
         bt = h[S * b: S * b + b * maxw].reshape(b, maxw)
-        max_ctx = 0
         seg[:] = 0
         ctx[:] = 1
         topp[:] = 1.0
         bt[:] = 0
-        for i, rq in enumerate(sb.decode):
-            if rq.params.needs_filter:
-                topk[i] = max(0, rq.params.top_k)
-                topp[i] = rq.params.top_p
-            p = rq.num_computed
-            ids[i] = rq.output[-1]
-            pos[i] = p
-            slots[i] = rq.blocks[p // bs] * bs + p % bs
-            ctx[i] = p + 1
-            max_ctx = max(max_ctx, p + 1)
-            bt[i, : len(rq.blocks)] = rq.blocks
-            temps[i] = rq.params.temperature
-            seeds[i] = rq.sample_seed()
+        dec = sb.decode
+        ids[:n], pos[:n], slots[:n], ctx[:n] = decode_rows(dec, bs, bt)
+        tb, seeds[:n], topk[:n], pb, _f = sampling_rows(dec)
+        temps[:n] = tb.view(np.float32)
+        topp[:n] = pb.view(np.float32)
+        max_ctx = int(ctx[:n].max()) if n else 0
         dev = self.host_in[: S * b + b * maxw].to(r.device, non_blocking=True)
         dseg = dev[: S * b].view(S, b)
         self.ids[:b].copy_(dseg[0])

@@ -217,12 +217,21 @@ class Scheduler:
         decode: list[Request] = []
         preempted: list[Request] = []
         # 1) decode rows
+        bs = self.bs
         for req in self.running:            # a snapshot: preemption may remove entries
             if len(decode) >= seq_cap or budget <= 0:
                 break
-            if req.busy or req.in_prefill or req not in self.running:
+            if req.busy:
                 continue
             pos = req.num_computed  # position of the token being fed (== total_len - 1)
+            if pos < req.prefill_target:     # still prefilling
+                continue
+            if len(req.blocks) * bs > pos:   # fast path: the page for this token exists (a preempted
+                decode.append(req)           # request has no pages and takes the slow path)
+                budget -= 1
+                continue
+            if req not in self.running:
+                continue
             while True:
                 try:
                     self._grow(req, pos + 1)
