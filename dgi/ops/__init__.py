@@ -410,7 +410,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
 FUSED_DECODE = os.environ.get("DGI_FUSED_DECODE", "1")
 FUSED_MAX_M = {"qkv": 8, "gate_up": 2}
 # launch config per projection (fused_decode.hip cfg: 4 = 8 waves x 1 K-step, 5 = 4 waves x 2)
-FUSED_KIND_CFG = {"qkv": 4, "gate_up": 5}
+FUSED_KIND_CFG = {"qkv": int(os.environ.get("DGI_FUSED_QKV_CFG", "4")),
+                  "gate_up": int(os.environ.get("DGI_FUSED_GU_CFG", "5"))}
 
 
 def fused_decode_ok(M: int, K: int, kind: str = "qkv") -> bool:
