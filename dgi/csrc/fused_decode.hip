@@ -61,17 +61,23 @@ struct FusedArgs {
   int nh, nkv, bs_log2;
 };
 
-template <int U>
+template <int U, int TW>
 struct Frag {
-  u32x4 w[U][2][2];
+  u32x4 w[U][TW][2];
 };
 
-template <int NW, int U, int PRO, int EPI>
+// TW: 16-row weight tiles per workgroup.  TW = 2 is the pair (c0 + r, c1 + r);
+// TW = 1 packs both halves of a pair into one tile — lanes r < 8 read rows c0 + r,
+// lanes r >= 8 rows c1 + r - 8 — and swaps the halves with a lane shuffle in the
+// epilogue: half the rows per workgroup, twice the workgroups (qkv on 8B: 384
+// instead of 192 on 256 CUs).  D: load groups in flight (register ring); the
+// first D are issued before the X staging.
+template <int NW, int U, int TW, int D, int PRO, int EPI>
 __global__ __launch_bounds__(NW * 64) void fused_skinny_kernel(FusedArgs a) {
   // normalised X rows live in LDS for the whole kernel: [M][K + 8] bf16 (16-byte
   // row pad keeps the 16-row fragment reads off one bank)
   extern __shared__ __attribute__((aligned(16))) uint16_t xs[];
-  __shared__ f32x4 red[NW][2][64];
+  __shared__ f32x4 red[NW][TW][64];
   __shared__ float s_part[NW][16];
   __shared__ float s_inv[16];
   const int tid = threadIdx.x;
@@ -83,29 +89,35 @@ __global__ __launch_bounds__(NW * 64) void fused_skinny_kernel(FusedArgs a) {
   const int M = a.M;
   const int ldx = K + 8;
   const int bid = blockIdx.x;
-  const int c0 = (bid / a.tpg) * a.gstride + (bid % a.tpg) * 16;
+  const int c0 = (bid / a.tpg) * a.gstride + (bid % a.tpg) * (TW == 2 ? 16 : 8);
   const int c1 = c0 + a.pair_off;
   const int ngroups = (K >> 6) / (NW * U);
   const size_t lane_k = (size_t)g * 16 + (size_t)w * 64;
-  const uint16_t* w0 = a.w + (size_t)(c0 + r) * K + lane_k;
+  const bool lo = r < 8;
+  const uint16_t* w0 = a.w + (size_t)(TW == 2 ? c0 + r : (lo ? c0 + r : c1 + r - 8)) * K + lane_k;
   const uint16_t* w1 = a.w + (size_t)(c1 + r) * K + lane_k;
   const bool xval = r < M;
 
-  auto load = [&](Frag<U>& f, int grp) {
+  auto load = [&](Frag<U, TW>& f, int grp) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const size_t off = ((size_t)grp * NW * U + (size_t)u * NW) * 64;
       const u32x4* p0 = reinterpret_cast<const u32x4*>(w0 + off);
-      const u32x4* p1 = reinterpret_cast<const u32x4*>(w1 + off);
       f.w[u][0][0] = __builtin_nontemporal_load(p0);
       f.w[u][0][1] = __builtin_nontemporal_load(p0 + 1);
-      f.w[u][1][0] = __builtin_nontemporal_load(p1);
-      f.w[u][1][1] = __builtin_nontemporal_load(p1 + 1);
+      if (TW == 2) {
+        const u32x4* p1 = reinterpret_cast<const u32x4*>(w1 + off);
+        f.w[u][TW - 1][0] = __builtin_nontemporal_load(p1);
+        f.w[u][TW - 1][1] = __builtin_nontemporal_load(p1 + 1);
+      }
     }
   };
 
-  Frag<U> cur, nxt;
-  load(cur, 0);  // first weight group in flight while X is staged
+  // the first D groups stream while X is staged
+  Frag<U, TW> ring[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (d < ngroups) load(ring[d], d);
 
   // ---- stage X (residual add, norm) into LDS once per workgroup: only the
   // M useful rows, spread over all threads (not 16 MFMA rows per lane)
@@ -161,8 +173,10 @@ __global__ __launch_bounds__(NW * 64) void fused_skinny_kernel(FusedArgs a) {
   __syncthreads();
 
   const uint16_t* xl = xs + (xval ? r : 0) * ldx + lane_k;
-  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-  auto compute = [&](const Frag<U>& f, int grp) {
+  f32x4 acc[TW];
+#pragma unroll
+  for (int nt = 0; nt < TW; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](const Frag<U, TW>& f, int grp) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int off = (grp * NW * U + u * NW) * 64;
@@ -172,46 +186,65 @@ __global__ __launch_bounds__(NW * 64) void fused_skinny_kernel(FusedArgs a) {
         xb = *reinterpret_cast<const u32x4*>(xl + off + 8);
       }
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
+      for (int nt = 0; nt < TW; ++nt) {
         acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xa), as_bf16x8(f.w[u][nt][0]), acc[nt], 0, 0, 0);
         acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xb), as_bf16x8(f.w[u][nt][1]), acc[nt], 0, 0, 0);
       }
     }
   };
-  for (int grp = 0; grp + 1 < ngroups; ++grp) {
-    load(nxt, grp + 1);
-    compute(cur, grp);
-    cur = nxt;
+  for (int base = 0; base < ngroups; base += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      if (base + d < ngroups) {  // uniform; only the last round of a ragged ring is partial
+        compute(ring[d], base + d);
+        if (base + D + d < ngroups) load(ring[d], base + D + d);
+      }
+    }
   }
-  compute(cur, ngroups - 1);
 
-  red[w][0][lane] = acc[0];
-  red[w][1][lane] = acc[1];
+#pragma unroll
+  for (int nt = 0; nt < TW; ++nt) red[w][nt][lane] = acc[nt];
   __syncthreads();
   if (w != 0) return;
-  f32x4 v0 = red[0][0][lane], v1 = red[0][1][lane];
+  f32x4 v0 = red[0][0][lane], v1 = red[0][TW - 1][lane];
 #pragma unroll
   for (int j = 1; j < NW; ++j) {
     v0 += red[j][0][lane];
-    v1 += red[j][1][lane];
+    if (TW == 2) v1 += red[j][1][lane];
   }
-  const float b0 = a.bias ? bf16_to_f32(a.bias[c0 + r]) : 0.f;
-  const float b1 = a.bias ? bf16_to_f32(a.bias[c1 + r]) : 0.f;
+  if (TW == 1) {
+    // this lane holds row c0 + r (r < 8) or c1 + r - 8; bring the other half of
+    // the pair over from lane ^ 8 (same row group g) so the epilogue below sees
+    // (v0, v1) = (row c0 + (r & 7), row c1 + (r & 7)) on every lane
+    const float bo = a.bias ? bf16_to_f32(a.bias[lo ? c0 + r : c1 + r - 8]) : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float own = v0[i] + bo;
+      const float oth = __shfl_xor(own, 8);
+      v0[i] = lo ? own : oth;
+      v1[i] = lo ? oth : own;
+    }
+  }
+  const int rr = TW == 2 ? r : (r & 7);
+  const float b0 = (TW == 2 && a.bias) ? bf16_to_f32(a.bias[c0 + r]) : 0.f;
+  const float b1 = (TW == 2 && a.bias) ? bf16_to_f32(a.bias[c1 + r]) : 0.f;
+  // TW 1: lanes r < 8 store the pair's first half, r >= 8 the second
+  const bool st0 = TW == 2 || lo, st1 = TW == 2 || !lo;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = g * 4 + i;
     if (m >= a.M) break;
     uint16_t* yrow = a.y + (size_t)m * a.ldy;
     if (EPI == 0) {
-      yrow[c0 + r] = f32_to_bf16(v0[i] + b0);
-      yrow[c1 + r] = f32_to_bf16(v1[i] + b1);
+      if (st0) yrow[c0 + rr] = f32_to_bf16(v0[i] + b0);
+      if (st1) yrow[c1 + rr] = f32_to_bf16(v1[i] + b1);
     } else if (EPI == 1) {
       const float gt = bf16_to_f32(f32_to_bf16(v0[i] + b0));
       const float up = bf16_to_f32(f32_to_bf16(v1[i] + b1));
-      yrow[c0 + r] = f32_to_bf16(gt * __builtin_amdgcn_rcpf(1.f + __expf(-gt)) * up);
+      if (st0) yrow[c0 + rr] = f32_to_bf16(gt * __builtin_amdgcn_rcpf(1.f + __expf(-gt)) * up);
     } else {
       const int head = c0 >> 7;
-      const int d = (c0 & 127) + r;  // 0..63
+      const int d = (c0 & 127) + rr;  // 0..63
       const uint16_t x1 = f32_to_bf16(v0[i] + b0), x2 = f32_to_bf16(v1[i] + b1);
       if (head < a.nh + a.nkv) {
         const float* cs = a.cos_sin + (size_t)a.positions[m] * 128;
@@ -220,56 +253,75 @@ __global__ __launch_bounds__(NW * 64) void fused_skinny_kernel(FusedArgs a) {
         const uint16_t o1 = f32_to_bf16(f1 * cv - f2 * sv);
         const uint16_t o2 = f32_to_bf16(f2 * cv + f1 * sv);
         if (head < a.nh) {
-          yrow[c0 + r] = o1;
-          yrow[c1 + r] = o2;
+          if (st0) yrow[c0 + rr] = o1;
+          if (st1) yrow[c1 + rr] = o2;
         } else {
-          yrow[c0 + r] = x1;
-          yrow[c1 + r] = x2;
+          if (st0) yrow[c0 + rr] = x1;
+          if (st1) yrow[c1 + rr] = x2;
           const int slot = a.slots[m];
           if (slot >= 0) {
             const int bs = 1 << a.bs_log2;
             const size_t base = (((size_t)(slot >> a.bs_log2) * a.nkv + (head - a.nh)) * bs + (slot & (bs - 1))) * 128;
-            a.k_cache[base + d] = o1;
-            a.k_cache[base + d + 64] = o2;
+            if (st0) a.k_cache[base + d] = o1;
+            if (st1) a.k_cache[base + d + 64] = o2;
           }
         }
       } else {
-        yrow[c0 + r] = x1;
-        yrow[c1 + r] = x2;
+        if (st0) yrow[c0 + rr] = x1;
+        if (st1) yrow[c1 + rr] = x2;
         const int slot = a.slots[m];
         if (slot >= 0) {
           const int bs = 1 << a.bs_log2;
           const size_t base =
               (((size_t)(slot >> a.bs_log2) * a.nkv + (head - a.nh - a.nkv)) * bs + (slot & (bs - 1))) * 128;
-          a.v_cache[base + d] = x1;
-          a.v_cache[base + d + 64] = x2;
+          if (st0) a.v_cache[base + d] = x1;
+          if (st1) a.v_cache[base + d + 64] = x2;
         }
       }
     }
   }
 }
 
-template <int NW, int U, int PRO, int EPI>
-int launch_cfg(const FusedArgs& a, int nblocks, hipStream_t s) {
+template <int NW, int U, int TW, int D, int PRO, int EPI>
+int launch_cfg(FusedArgs a, int N, int ntiles, hipStream_t s) {
   if ((a.K / 64) % (NW * U)) return -7;
   const size_t lds = (size_t)a.M * (a.K + 8) * 2;
   // static (reduce tiles + norm partials) + staged X must fit the 160 KB of LDS
-  const size_t lds_static = (size_t)NW * 2 * 64 * 16 + (size_t)NW * 16 * 4 + 16 * 4;
+  const size_t lds_static = (size_t)NW * TW * 64 * 16 + (size_t)NW * 16 * 4 + 16 * 4;
   if (lds + lds_static > 160 * 1024) return -6;
-  fused_skinny_kernel<NW, U, PRO, EPI><<<dim3(nblocks), NW * 64, lds, s>>>(a);
+  if (TW == 1) {
+    // pairs of 8 rows: epi 0 16 consecutive columns, epi 1 8 gate + 8 up, epi 2 8 (d, d + 64) pairs
+    if (EPI == 0) {
+      a.gstride = 16;
+      a.pair_off = 8;
+    } else if (EPI == 1) {
+      a.gstride = 8;
+    } else {
+      a.tpg = 8;
+    }
+  }
+  const int nblocks = TW == 2 ? ntiles / 2 : ntiles;
+  fused_skinny_kernel<NW, U, TW, D, PRO, EPI><<<dim3(nblocks), NW * 64, lds, s>>>(a);
   DGI_CHECK_LAUNCH();
+  (void)N;
   return 0;
 }
 
-// cfg: (waves per workgroup, K-steps per load group)
+// cfg: (waves per workgroup, K-steps per load group, tiles per workgroup, groups in flight)
 template <int PRO, int EPI>
-int launch(const FusedArgs& a, int nblocks, int cfg, hipStream_t s) {
+int launch(const FusedArgs& a, int N, int ntiles, int cfg, hipStream_t s) {
   switch (cfg) {
-    case 0: case 1: return launch_cfg<8, 2, PRO, EPI>(a, nblocks, s);
-    case 2: return launch_cfg<4, 4, PRO, EPI>(a, nblocks, s);
-    case 3: return launch_cfg<16, 1, PRO, EPI>(a, nblocks, s);
-    case 4: return launch_cfg<8, 1, PRO, EPI>(a, nblocks, s);
-    case 5: return launch_cfg<4, 2, PRO, EPI>(a, nblocks, s);
+    case 0: case 1: return launch_cfg<8, 2, 2, 2, PRO, EPI>(a, N, ntiles, s);
+    case 2: return launch_cfg<4, 4, 2, 2, PRO, EPI>(a, N, ntiles, s);
+    case 3: return launch_cfg<16, 1, 2, 2, PRO, EPI>(a, N, ntiles, s);
+    case 4: return launch_cfg<8, 1, 2, 2, PRO, EPI>(a, N, ntiles, s);
+    case 5: return launch_cfg<4, 2, 2, 2, PRO, EPI>(a, N, ntiles, s);
+    case 6: return launch_cfg<8, 1, 1, 4, PRO, EPI>(a, N, ntiles, s);
+    case 7: return launch_cfg<8, 1, 2, 4, PRO, EPI>(a, N, ntiles, s);
+    case 8: return launch_cfg<4, 2, 1, 4, PRO, EPI>(a, N, ntiles, s);
+    case 9: return launch_cfg<4, 2, 2, 4, PRO, EPI>(a, N, ntiles, s);
+    case 10: return launch_cfg<8, 2, 1, 2, PRO, EPI>(a, N, ntiles, s);
+    case 11: return launch_cfg<4, 1, 1, 8, PRO, EPI>(a, N, ntiles, s);
     default: return -5;
   }
 }
@@ -291,15 +343,15 @@ extern "C" int dgi_fused_skinny(const void* x, int ldx, const void* res, int ldr
   FusedArgs a{(const uint16_t*)x, ldx, (const uint16_t*)res, ldr, (uint16_t*)res_out, (const uint16_t*)gamma,
               eps, (const uint16_t*)w, (const uint16_t*)bias, (uint16_t*)y, ldy, M, K, 1, 32, 16,
               positions, cos_sin, slots, (uint16_t*)k_cache, (uint16_t*)v_cache, nh, nkv, 0};
-  int nblocks;
+  int ntiles;  // 16-row weight tiles of the launch (two per workgroup at TW = 2)
   if (epi == 0) {
     if (N % 32) return -4;
-    nblocks = N / 32;
+    ntiles = N / 16;
   } else if (epi == 1) {
     if (N % 16) return -4;
     a.gstride = 16;
     a.pair_off = N;
-    nblocks = N / 16;
+    ntiles = N / 8;
   } else if (epi == 2) {
     if (N != (nh + 2 * nkv) * 128) return -4;
     int bl = 0;
@@ -309,12 +361,12 @@ extern "C" int dgi_fused_skinny(const void* x, int ldx, const void* res, int ldr
     a.tpg = 4;
     a.gstride = 128;
     a.pair_off = 64;
-    nblocks = N / 32;
+    ntiles = N / 16;
   } else {
     return -5;
   }
   if (pro < 0 || pro > 2) return -5;
-#define DGI_FS(P, E) if (pro == P && epi == E) return launch<P, E>(a, nblocks, cfg, s);
+#define DGI_FS(P, E) if (pro == P && epi == E) return launch<P, E>(a, N, ntiles, cfg, s);
   DGI_FS(0, 0) DGI_FS(1, 0) DGI_FS(2, 0)
   DGI_FS(0, 1) DGI_FS(1, 1) DGI_FS(2, 1)
   DGI_FS(0, 2) DGI_FS(1, 2) DGI_FS(2, 2)

@@ -21,7 +21,8 @@
 //    the bias and rounds to bf16.
 // MT = 2 handles 17..32 rows with the same weight registers (two A tiles);
 // NT > 1 column tiles per wave reuse each X fragment NT times.  Loads run
-// one group of U K-steps ahead of the MFMAs (register double buffer).
+// D - 1 groups of U K-steps ahead of the MFMAs (register ring, D = 2 is the
+// double buffer).
 #include "common.h"
 
 using namespace dgi;
@@ -35,7 +36,7 @@ struct Frag {
   u32x4 x[U][MT][2];
 };
 
-template <int NW, int MT, int NT, int U>
+template <int NW, int MT, int NT, int U, int D>
 __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
     const uint16_t* __restrict__ X, int ldx, const uint16_t* __restrict__ W,
     const uint16_t* __restrict__ bias, uint16_t* __restrict__ Y, int ldy, int M, int K) {
@@ -99,15 +100,20 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
                                                                 as_bf16x8(f.w[u][nt][1]), acc[mt][nt], 0, 0, 0);
         }
   };
-  // one group in flight ahead of the one being multiplied
-  Frag<MT, NT, U> cur, nxt;
-  load(cur, 0);
-  for (int grp = 0; grp + 1 < ngroups; ++grp) {
-    load(nxt, grp + 1);
-    compute(cur);
-    cur = nxt;
+  // register ring of D groups: D - 1 in flight ahead of the one being multiplied
+  Frag<MT, NT, U> ring[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (d < ngroups) load(ring[d], d);
+  for (int base = 0; base < ngroups; base += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      if (base + d < ngroups) {  // uniform
+        compute(ring[d]);
+        if (base + D + d < ngroups) load(ring[d], base + D + d);
+      }
+    }
   }
-  compute(cur);
 
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
@@ -129,11 +135,11 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
   }
 }
 
-template <int NW, int MT, int NT, int U>
+template <int NW, int MT, int NT, int U, int D = 2>
 int launch(const void* x, int ldx, const void* w, const void* bias, void* y, int ldy, int M, int N, int K,
            hipStream_t s) {
   if (N % (16 * NT) || (K / 64) % (NW * U)) return -5;
-  skinny_gemm_kernel<NW, MT, NT, U><<<dim3(N / (16 * NT)), NW * 64, 0, s>>>(
+  skinny_gemm_kernel<NW, MT, NT, U, D><<<dim3(N / (16 * NT)), NW * 64, 0, s>>>(
       (const uint16_t*)x, ldx, (const uint16_t*)w, (const uint16_t*)bias, (uint16_t*)y, ldy, M, K);
   DGI_CHECK_LAUNCH();
   return 0;
@@ -150,6 +156,12 @@ int dispatch(int cfg, const void* x, int ldx, const void* w, const void* bias, v
     case 5: return MT == 1 ? launch<16, 1, 4, 1>(x, ldx, w, bias, y, ldy, M, N, K, s)   // MT 2 would spill
                            : launch<16, MT, 2, 1>(x, ldx, w, bias, y, ldy, M, N, K, s);
     case 6: return launch<4, MT, 2, 4>(x, ldx, w, bias, y, ldy, M, N, K, s);
+    // deeper rings: more bytes in flight per wave for short kernels (o-proj) and long K (down)
+    case 7: return launch<8, MT, 1, 1, 4>(x, ldx, w, bias, y, ldy, M, N, K, s);
+    case 8: return launch<8, MT, 1, 2, 4>(x, ldx, w, bias, y, ldy, M, N, K, s);
+    case 9: return launch<4, MT, 1, 2, 4>(x, ldx, w, bias, y, ldy, M, N, K, s);
+    case 10: return launch<4, MT, 1, 1, 8>(x, ldx, w, bias, y, ldy, M, N, K, s);
+    case 11: return launch<8, MT, 1, 1, 8>(x, ldx, w, bias, y, ldy, M, N, K, s);
     default: return -4;
   }
 }

@@ -109,7 +109,7 @@ def bench_plain(shapes, Ms):
             y = torch.empty(M, N, device=dev, dtype=bf)
             row = {"gemm": name, "M": M, "N": N, "K": K,
                    "hipblaslt": round(graph_time(lambda i: torch.matmul(x, ws[i % nbuf].t(), out=y)), 2)}
-            for cfg in (1, 2, 3, 4, 5, 6):
+            for cfg in range(1, 12):
                 try:
                     row[f"skinny_c{cfg}"] = round(graph_time(
                         lambda i: torch.ops.dgi.skinny_gemm(y, x, ws[i % nbuf], None, cfg)), 2)

@@ -174,7 +174,9 @@ def test_silu_mul(T, I):
 
 @pytest.mark.parametrize("M", [1, 3, 16, 17, 32])
 @pytest.mark.parametrize("N,K,cfg", [(6144, 4096, 0), (4096, 14336, 0), (1152, 1024, 1), (256, 1024, 4),
-                                     (512, 2048, 2), (1024, 2048, 5), (512, 4096, 6), (96, 1024, 3)])
+                                     (512, 2048, 2), (1024, 2048, 5), (512, 4096, 6), (96, 1024, 3),
+                                     (512, 4096, 7), (256, 14336, 8), (512, 2048, 9), (256, 3072, 10),
+                                     (512, 4096, 11), (128, 1024, 11)])
 def test_skinny_gemm(M, N, K, cfg):
     if N % (16 * {2: 2, 3: 2, 5: 4, 6: 2}.get(cfg, 1)):
         pytest.skip("column tiles do not divide N")
@@ -442,6 +444,19 @@ def test_graph_decode_with_top_k_one_matches_greedy():
 def test_fused_skinny_matches_reference(pro, epi, M):
     """Fused decode GEMM (RMSNorm prologue, SwiGLU / RoPE+KV epilogue) vs the
     unfused reference ops in fp32 on the same bf16 inputs."""
+    _fused_skinny_case(pro, epi, M, None)
+
+
+@pytest.mark.parametrize("pro,epi", [(0, 0), (2, 0), (2, 1), (1, 2), (2, 2)])
+def test_fused_skinny_every_launch_config(pro, epi):
+    """Every fused_decode.hip launch config (waves, K-steps per group, one- or
+    two-tile workgroups, load ring depth) against the reference, at M = 1 and 3."""
+    for cfg in range(12):
+        for M in (1, 3):
+            _fused_skinny_case(pro, epi, M, cfg)
+
+
+def _fused_skinny_case(pro, epi, M, cfg):
     torch.manual_seed(M * 10 + pro * 3 + epi)
     K = 4096
     nh, nkv, bs, nb = 32, 8, 16, 64
@@ -471,14 +486,14 @@ def test_fused_skinny_matches_reference(pro, epi, M):
     y_r = torch.empty_like(y)
     ro = torch.empty_like(x) if pro == 2 else None
     ro_r = torch.empty_like(x) if pro == 2 else None
-    ops.fused_skinny(y, x, res, ro, gamma, 1e-5, w, bias, pro, epi, pos, cos_sin, slots, kc, vc, nh, nkv)
+    ops.fused_skinny(y, x, res, ro, gamma, 1e-5, w, bias, pro, epi, pos, cos_sin, slots, kc, vc, nh, nkv, cfg=cfg)
     ops.fused_skinny_ref(y_r, x, res, ro_r, gamma, 1e-5, w, bias, pro, epi, pos, cos_sin, slots, kc_r, vc_r,
                          nh, nkv)
     torch.cuda.synchronize()
     if pro == 2:
         assert torch.equal(ro, ro_r)
     scale = float(y_r.float().abs().max()) + 1e-3
-    assert float((y.float() - y_r.float()).abs().max()) <= 0.02 * scale, float((y.float() - y_r.float()).abs().max())
+    assert float((y.float() - y_r.float()).abs().max()) <= 0.02 * scale, (cfg, float((y.float() - y_r.float()).abs().max()))
     if epi == 2:
         for a_, b_ in ((kc, kc_r), (vc, vc_r)):
             s2 = float(b_.float().abs().max()) + 1e-3
