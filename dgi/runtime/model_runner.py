@@ -129,6 +129,8 @@ class ModelRunner:
         # called while the host waits for a step's sampled tokens (P/D ranks keep
         # their KV handshakes moving instead of blocking in a stream synchronize)
         self.wait_hook = None
+        self._spans = []
+        self.span_total_ms = 0.0
         self.graphs = None
         if use_graphs and self.is_cuda and model.has_head:
             self.graphs = GraphRunner(self, [b for b in graph_buckets if b <= max_num_seqs])
@@ -246,10 +248,41 @@ class ModelRunner:
             return StepResult(toks, list(sb.decode))
         flat, hdr, sampled = self.build_host(sb)
         ids, meta, samp = self.meta_from_device(self.to_device(flat), hdr)
+        span = self._span_begin()
         logits = self.model.forward(meta, input_ids=ids)
         if not sampled:
             return StepResult([], [])
-        return StepResult(self.fetch(samp.sample(logits)), sampled)
+        toks = samp.sample(logits)
+        self._span_end(span)
+        return StepResult(self.fetch(toks), sampled)
+
+    # DGI_GPU_SPAN=1: events around each eager step's device work (forward + sampling);
+    # wall time minus the summed spans is the time the GPU waited for the host
+    GPU_SPAN = os.environ.get("DGI_GPU_SPAN", "0") == "1"
+
+    def _span_begin(self):
+        if not (self.GPU_SPAN and self.is_cuda):
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def _span_end(self, e0) -> None:
+        if e0 is None:
+            return
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        self._spans.append((e0, e1))
+        if len(self._spans) > 64:
+            self.gpu_span_ms()
+
+    def gpu_span_ms(self) -> float:
+        """Summed device time of the recorded eager steps so far (resolves pending events)."""
+        for e0, e1 in self._spans:
+            e1.synchronize()
+            self.span_total_ms += e0.elapsed_time(e1)
+        self._spans.clear()
+        return self.span_total_ms
 
     def fetch(self, t: torch.Tensor, host: Optional[torch.Tensor] = None) -> list:
         """Device tokens -> host list.  With a ``wait_hook`` the copy is async and

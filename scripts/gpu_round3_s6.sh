@@ -2,8 +2,10 @@
 # workgroups, deeper load rings), their kernel timings, the MALL prefetch probe,
 # then 8B batch-1/4 TPOT with the promising configs.
 set -o pipefail
-timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread \
-  -k "fused_skinny or skinny_gemm" > gpurun_out/r3_s6_tests.log 2>&1 || { tail -30 gpurun_out/r3_s6_tests.log; exit 1; }
+if [ -n "$RUN_TESTS" ]; then
+  timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread \
+    -k "fused_skinny or skinny_gemm" > gpurun_out/r3_s6_tests.log 2>&1 || { tail -30 gpurun_out/r3_s6_tests.log; exit 1; }
+fi
 tail -2 gpurun_out/r3_s6_tests.log
 timeout -k 10 300 python -u scripts/fused_decode_bench.py --cfgs 0 2 3 4 5 6 7 8 9 10 11 --skip-attn \
   --out gpurun_out/fdb_s6.json > gpurun_out/fdb_s6.log 2>&1 || { tail -20 gpurun_out/fdb_s6.log; exit 1; }
@@ -18,6 +20,10 @@ run() {  # tag, env...
   python -c "import json; d=json.load(open('gpurun_out/s6_${tag}.json')); print('${tag}', [(r['batch'], r['tpot_ms']) for r in d])"
 }
 run base DGI_X=0 || exit 1
-for c in 6 7 10; do run q$c DGI_FUSED_QKV_CFG=$c || exit 1; done
-for c in 8 9 6; do run g$c DGI_FUSED_GU_CFG=$c || exit 1; done
+for c in 3 6 10; do run q$c DGI_FUSED_QKV_CFG=$c || exit 1; done
+for c in 6 11 8; do run g$c DGI_FUSED_GU_CFG=$c || exit 1; done
+run q6g6 DGI_FUSED_QKV_CFG=6 DGI_FUSED_GU_CFG=6 || exit 1
+run q3g6 DGI_FUSED_QKV_CFG=3 DGI_FUSED_GU_CFG=6 || exit 1
 for c in 7 8 11; do run s$c DGI_SKINNY_CFG=$c || exit 1; done
+DGI_GPU_SPAN=1 timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/bench70_s6_span.json 2> gpurun_out/bench70_s6_span.err || exit 1
+python -c "import json; d=json.load(open('gpurun_out/bench70_s6_span.json')); print(d['value'], d['ms_per_step'], d['extra']['phases'])"
