@@ -408,10 +408,26 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
 # unfused chain wins.  K <= 4096 (8B-class) like _use_skinny.
 # DGI_FUSED_DECODE=0 disables, =force uses it for every M <= 16 and K.
 FUSED_DECODE = os.environ.get("DGI_FUSED_DECODE", "1")
-FUSED_MAX_M = {"qkv": 8, "gate_up": 2}
-# launch config per projection (fused_decode.hip cfg: 4 = 8 waves x 1 K-step, 5 = 4 waves x 2)
-FUSED_KIND_CFG = {"qkv": int(os.environ.get("DGI_FUSED_QKV_CFG", "4")),
-                  "gate_up": int(os.environ.get("DGI_FUSED_GU_CFG", "5"))}
+FUSED_MAX_M = {"qkv": 8, "gate_up": 4}
+# launch config per projection and row count (fused_decode.hip cfg = waves, K-steps per load
+# group, tiles per workgroup, load ring depth: 6 = 8x1 one-tile ring 4, 7 = 8x1 two-tile ring 4,
+# 8 = 4x2 one-tile ring 4, 10 = 8x2 one-tile, 11 = 4x1 one-tile ring 8).  Fastest per M on the
+# 8B shapes, weights cold, hipGraph-timed (profiles/r3_decode_gemm/README.md): qkv 16.6 -> 15.0 us
+# and gate_up + SwiGLU 48.6 -> 43.8 us at M = 1 against round 2's fixed configs 4 / 5.
+FUSED_M_CFG = {"qkv": ((2, 10), (16, 7)), "gate_up": ((1, 6), (2, 8), (16, 11))}
+FUSED_KIND_CFG = {"qkv": int(os.environ.get("DGI_FUSED_QKV_CFG", "-1")),
+                  "gate_up": int(os.environ.get("DGI_FUSED_GU_CFG", "-1"))}
+
+
+def fused_cfg(kind: str, M: int) -> int:
+    if FUSED_CFG >= 0:
+        return FUSED_CFG
+    if FUSED_KIND_CFG[kind] >= 0:
+        return FUSED_KIND_CFG[kind]
+    for m, c in FUSED_M_CFG[kind]:
+        if M <= m:
+            return c
+    return FUSED_M_CFG[kind][-1][1]
 
 
 def fused_decode_ok(M: int, K: int, kind: str = "qkv") -> bool:
@@ -454,7 +470,7 @@ def fused_skinny(y, x, res, res_out, gamma, eps, w, bias, pro: int, epi: int, po
     into the paged cache at ``slots`` (head_dim 128, full rotary)."""
     if _native(x):
         if cfg is None:
-            cfg = FUSED_CFG if FUSED_CFG >= 0 else FUSED_KIND_CFG["gate_up" if epi == 1 else "qkv"]
+            cfg = fused_cfg("gate_up" if epi == 1 else "qkv", x.shape[0])
         _call("fused_skinny", y, x, res, res_out, gamma, eps, w, bias, pro, epi, positions, cos_sin, slots,
               k_cache, v_cache, nh, nkv, cfg)
         return y

@@ -27,3 +27,7 @@ run q3g6 DGI_FUSED_QKV_CFG=3 DGI_FUSED_GU_CFG=6 || exit 1
 for c in 7 8 11; do run s$c DGI_SKINNY_CFG=$c || exit 1; done
 DGI_GPU_SPAN=1 timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/bench70_s6_span.json 2> gpurun_out/bench70_s6_span.err || exit 1
 python -c "import json; d=json.load(open('gpurun_out/bench70_s6_span.json')); print(d['value'], d['ms_per_step'], d['extra']['phases'])"
+# open-loop P/D rehearsal (70B layer shapes, the N=8 auto layout) at ~90 % of its closed-loop request rate
+REHEARSE_MODEL=llama3-70b@L8 REHEARSE_TAG=_open280 REHEARSE_STEPS=40 REHEARSE_WARMUP=20 REHEARSE_TIMEOUT=300 \
+  REHEARSE_EXTRA="--arrival-rate 280 --decode-local-frac 0" bash scripts/rehearse_rccl_bench.sh auto8 || exit 1
+python scripts/summarize_rehearsal.py gpurun_out/rehearse_auto8_open280.json 2>&1 | tail -5 || true

@@ -6,6 +6,8 @@
 # A rank still running after DGI_HANG_DUMP_S seconds dumps every thread's
 # Python stack to the .err file and exits.
 # usage: rehearse_rccl_bench.sh [case ...]   (default: all cases)
+# env: REHEARSE_MODEL, REHEARSE_CONC, REHEARSE_STEPS / _WARMUP, REHEARSE_TIMEOUT, REHEARSE_TAG,
+#      REHEARSE_EXTRA (appended bench.py flags, e.g. "--arrival-rate 280" for an open-loop run)
 set -o pipefail
 mkdir -p gpurun_out
 export DGI_SHARED_GPU=1 NCCL_SOCKET_IFNAME=lo NCCL_IB_DISABLE=1 DGI_HANG_DUMP_S=${DGI_HANG_DUMP_S:-100}
@@ -15,8 +17,8 @@ run() {  # name, nproc, extra args
   local name=$1 n=$2; shift 2
   echo "== $name ($MODEL)" >&2
   timeout -k 10 ${REHEARSE_TIMEOUT:-200} python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 \
-    --master-port $((29600 + n)) bench.py --gpus "$n" --model "$MODEL" --steps 8 --warmup 2 --ramp-steps 4 \
-    --concurrency "$CONC" --output-len 32 --prompt-len 256 "$@" > "gpurun_out/rehearse_${name}${REHEARSE_TAG}.json" \
+    --master-port $((29600 + n)) bench.py --gpus "$n" --model "$MODEL" --steps ${REHEARSE_STEPS:-8} --warmup ${REHEARSE_WARMUP:-2} --ramp-steps 4 \
+    --concurrency "$CONC" --output-len 32 --prompt-len 256 "$@" $REHEARSE_EXTRA > "gpurun_out/rehearse_${name}${REHEARSE_TAG}.json" \
     2> "gpurun_out/rehearse_${name}${REHEARSE_TAG}.err"
   local rc=$?
   echo "== $name rc=$rc" >&2
