@@ -395,10 +395,334 @@ __global__ __launch_bounds__(512) void mfma_gemm_ring_kernel(const uint16_t* __r
   epilogue<EPI>(acc, Y, ldy, M, m0, tn, wm, wn, lane);
 }
 
+// ---------------------------------------------------------------------------
+// Ping-pong schedule (sched 3).  Same tile, LDS image and fragment map as the
+// kernel above, but each K tile runs as 4 phases of 16 MFMAs per wave and the two
+// wave groups of a SIMD (waves 0-3: rows 0-127, waves 4-7: rows 128-255) are
+// staggered by one barrier: while one wave of a SIMD issues its fragment reads
+// and staging loads ("R" section), its partner runs its MFMAs ("M" section),
+// and every section ends at a raw s_barrier.  The phases of tile t, per wave
+// (Xa / Xb = first / second 64 of the wave's 128 X rows, Wa / Wb = first /
+// second 32 of its 64 W rows):
+//
+//   phase  reads        MFMAs      staging (slab = 64 rows x 64 k, one glds)   wait before the barrier
+//   0      Xa, Wa (12)  Xa x Wa    W2, W3 of t+1
+//   1      Wb (4)       Xa x Wb    X3 of t+1, X0 of t+2                      vmcnt(7): X1, X3 of t landed
+//   2      Xb (8)       Xb x Wb    X1 of t+1, X2 of t+2
+//   3      -            Xb x Wa    W0, W1 of t+2                             vmcnt(6): all but X1, X3 of t+1
+//
+// Every slab is refilled at least two sections after the last read of the
+// slab it replaces (WAR; each wave retires its reads with lgkmcnt(0) at the
+// top of the following M section) and waited for by every wave before the
+// barrier that precedes its first read (RAW): staging loads stay 3-6 phases in
+// flight and vmcnt never drains to 0 in the steady state.  The last two tiles
+// issue less and wait with smaller counts (MODE 1, 2).  A work item is any even
+// number (>= 2) of K tiles of one output tile.
+//
+// Work decomposition.  When the output tiles are a multiple of the CU count
+// (or many waves of it) every block owns whole tiles (grid = tiles).  Otherwise
+// the launch is persistent (grid = P blocks, P = CUs) and hybrid split-K: the
+// first `rem` = tiles % P tiles are cut along K into `splits` (2-4) pieces of
+// 128-deep units, piece j of tile t going to block g = j * rem + t, so the
+// blocks of one XCD (consecutive g) work on neighbouring tiles over the SAME K
+// range and share their X / W slabs in L2 (a stream-K split, whose pieces start
+// at staggered K offsets, measured slower for that reason); every block then
+// owns `full` whole tiles.  Each piece stores its fp32 partial tile to its
+// block's workspace slab, publishes it (agent-scope release, then a relaxed
+// counter increment), and the last piece to arrive for a tile acquires, sums
+// every slab in piece order (deterministic) and writes the bf16 tile (and
+// resets the counter for the next launch).  No block waits for another, so
+// the protocol holds for any block placement or dispatch order.
+struct PPArgs {
+  const uint16_t* X;
+  const uint16_t* W;
+  uint16_t* Y;
+  float* ws;     // one 256 x 256 fp32 slab per block (hybrid launches)
+  int* cnt;      // one arrival counter per split tile, zero between launches
+  int ldx, ldy, M, I, K, tiles_m, tiles_total;
+  int rem, splits, full, P;
+};
+
+template <int EPI>
+__global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * kStageBytes];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int wm = w >> 2, wn = w & 3;
+  const int M = a.M, K = a.K, ldx = a.ldx;
+
+  const int q = tid >> 3;
+  const int lc = (tid & 7) ^ ((tid >> 4) & 7);
+  char* const lds_x = smem + w * 1024;
+  char* const lds_w = smem + kTileBytes + w * 1024;
+  const int r16 = lane & 15;
+  const int sw = (lane >> 1) & 7;
+  const int ph0 = ((lane >> 4) ^ sw) * 16;
+  const int ph1 = ((4 + (lane >> 4)) ^ sw) * 16;
+  const int xbase = (wm * 128 + r16) * 128;
+  const int wbase = kTileBytes + (wn * 64 + r16) * 128;
+
+  f32x4 acc[8][4];
+  bf16x8 xa[4][2], xb[4][2], wa[2][2], wb[2][2];
+  // x fragments of row tiles i0 .. i0 + 3, w fragments of row tiles j0, j0 + 1; both k halves
+  auto rx = [&](int st, int i0, bf16x8 (&f)[4][2]) {
+    const char* s = smem + st * kStageBytes + xbase + i0 * 2048;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f[i][0] = *(const bf16x8*)(s + i * 2048 + ph0);
+      f[i][1] = *(const bf16x8*)(s + i * 2048 + ph1);
+    }
+  };
+  auto rw = [&](int st, int j0, bf16x8 (&f)[2][2]) {
+    const char* s = smem + st * kStageBytes + wbase + j0 * 2048;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      f[j][0] = *(const bf16x8*)(s + j * 2048 + ph0);
+      f[j][1] = *(const bf16x8*)(s + j * 2048 + ph1);
+    }
+  };
+  auto mma = [&](int i0, int j0, const bf16x8 (&xf)[4][2], const bf16x8 (&wf)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][h], xf[i][h], acc[i0 + i][j0 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // acc = X[tile rows] . W[tile cols]^T over K tiles kb .. kb + L - 1 (L even, >= 2)
+  auto run = [&](int tm, int tn, int kb, int L) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int m0 = tm * kBM;
+    const uint16_t* xs[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xs[i] = a.X + (size_t)min(m0 + q + i * 64, M - 1) * ldx + lc * 8 + kb * kBK;
+    int wrow0, wstep;
+    if (EPI == 1) {
+      wrow0 = tn * 128 + (q < 32 ? q : a.I + q - 32);
+      wstep = 32;
+    } else {
+      wrow0 = tn * 256 + q;
+      wstep = 64;
+    }
+    const uint16_t* const wsrc = a.W + (size_t)wrow0 * K + lc * 8 + kb * kBK;
+    const size_t wslab = (size_t)wstep * K;
+    // slab i (rows 64 i .. 64 i + 63) of local K tile kt into LDS stage st
+    auto gx = [&](int kt, int i, int st) { glds16(xs[i] + kt * kBK, lds_x + st * kStageBytes + i * 8192); };
+    auto gw = [&](int kt, int i, int st) { glds16(wsrc + i * wslab + kt * kBK, lds_w + st * kStageBytes + i * 8192); };
+
+    // one K tile; ST = its LDS stage, MODE 0: t + 2 < L, 1: t + 2 == L, 2: t + 1 == L
+    auto tile = [&](int t, auto ST_, auto MODE_) {
+      constexpr int ST = decltype(ST_)::value, MODE = decltype(MODE_)::value;
+      // phase 0
+      if constexpr (MODE < 2) { gw(t + 1, 2, ST ^ 1); gw(t + 1, 3, ST ^ 1); }
+      rw(ST, 0, wa);
+      rx(ST, 0, xa);
+      barrier();
+      mma(0, 0, xa, wa);
+      barrier();
+      // phase 1
+      if constexpr (MODE < 2) gx(t + 1, 3, ST ^ 1);
+      if constexpr (MODE == 0) gx(t + 2, 0, ST);
+      rw(ST, 2, wb);
+      if constexpr (MODE == 0) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+      else if constexpr (MODE == 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      barrier();
+      mma(0, 2, xa, wb);
+      barrier();
+      // phase 2
+      if constexpr (MODE < 2) gx(t + 1, 1, ST ^ 1);
+      if constexpr (MODE == 0) gx(t + 2, 2, ST);
+      rx(ST, 4, xb);
+      barrier();
+      mma(4, 2, xb, wb);
+      barrier();
+      // phase 3
+      if constexpr (MODE == 0) { gw(t + 2, 0, ST); gw(t + 2, 1, ST); }
+      if constexpr (MODE == 0) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if constexpr (MODE == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      barrier();
+      mma(4, 0, xb, wa);
+      barrier();
+    };
+
+    using Z = std::integral_constant<int, 0>;
+    using O = std::integral_constant<int, 1>;
+    using T2 = std::integral_constant<int, 2>;
+    // prologue: everything the steady state would have issued before tile 0
+    gx(0, 0, 0); gx(0, 2, 0); gw(0, 0, 0); gw(0, 1, 0); gw(0, 2, 0); gw(0, 3, 0);
+    gx(0, 3, 0); gx(1, 0, 1); gx(0, 1, 0); gx(1, 2, 1); gw(1, 0, 1); gw(1, 1, 1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    barrier();
+    if (wm == 1) barrier();     // stagger: waves 4-7 run one section behind
+    int t = 0;
+    for (; t + 4 <= L; t += 2) {
+      tile(t, Z{}, Z{});
+      tile(t + 1, O{}, Z{});
+    }
+    tile(t, Z{}, O{});
+    tile(t + 1, O{}, T2{});
+    if (wm == 0) barrier();     // pairs with the last barrier of waves 4-7: every LDS read retired
+  };
+
+  const int nt = K / kBK;
+  const int nt2 = nt >> 1;                    // 128-deep units per tile
+  // persistent hybrid: block g (blocks that share an XCD take consecutive g)
+  const int g = (blockIdx.x & 7) * (a.P >> 3) + (blockIdx.x >> 3);
+  bool split = a.rem && g < a.rem * a.splits;
+  int k = 0;
+  for (;;) {
+    // next work item: the block's one tile (rem == 0), its split-K piece, then its whole tiles
+    int t, kb = 0, L = nt;
+    bool piece = false;
+    if (a.rem == 0) {
+      if (k++) break;
+      const int b = blockIdx.x, T = a.tiles_total;
+      const int xcd = b & 7, li = b >> 3;
+      const int q8 = T >> 3, r8 = T & 7;
+      t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + li;
+    } else if (split) {
+      split = false;
+      const int j = g / a.rem;
+      t = g - j * a.rem;
+      const int u0 = j * nt2 / a.splits, u1 = (j + 1) * nt2 / a.splits;
+      kb = 2 * u0;
+      L = 2 * (u1 - u0);
+      piece = true;
+    } else if (k < a.full) {
+      t = a.rem + k * a.P + g;
+      ++k;
+    } else {
+      break;
+    }
+    const int tm = t % a.tiles_m, tn = t / a.tiles_m;
+    run(tm, tn, kb, L);
+    bool store = true;
+    if (piece) {
+      // slab offsets from a laundered thread id: otherwise hipcc hoists all 32 per-lane
+      // addresses out of the work-item loop and spills them
+      int lt = tid;
+      asm volatile("" : "+v"(lt));
+      float* slab = a.ws + (size_t)g * 65536 + lt * 4;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) *(f32x4*)(slab + (i * 4 + j) * 2048) = acc[i][j];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int old = __hip_atomic_fetch_add(a.cnt + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == a.splits - 1;
+        if (last) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_store(a.cnt + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        *(volatile int*)smem = last;
+      }
+      __syncthreads();
+      store = *(volatile int*)smem;
+      __syncthreads();          // flag read by every wave before the next item's staging overwrites it
+      if (store) {
+        // every slab, own included, in piece order: the sum does not depend on which piece arrived last
+        for (int jj = 0; jj < a.splits; ++jj) {
+          const float* o = a.ws + (size_t)(jj * a.rem + t) * 65536 + lt * 4;
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const f32x4 v = *(const f32x4*)(o + (i * 4 + j) * 2048);
+              acc[i][j] = jj == 0 ? v : acc[i][j] + v;
+            }
+        }
+      }
+    }
+    if (store) epilogue<EPI>(acc, a.Y, a.ldy, M, tm * kBM, tn, wm, wn, lane);
+  }
+}
+
+// Per-device split-K workspace (one fp32 slab per block + one counter per tile),
+// allocated on first use outside stream capture.  Shared by every stream of
+// the process: the engine issues its projection GEMMs on one stream at a time.
+struct SkWorkspace {
+  float* ws = nullptr;
+  int* cnt = nullptr;
+  int P = 0;
+};
+
+SkWorkspace* sk_workspace(hipStream_t s) {
+  static SkWorkspace per_dev[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  SkWorkspace& w = per_dev[dev];
+  if (w.ws) return &w;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 8) return nullptr;
+  const int P = cus & ~7;
+  float* ws = nullptr;
+  int* cnt = nullptr;
+  if (hipMalloc(&ws, (size_t)P * 65536 * sizeof(float)) != hipSuccess) return nullptr;
+  if (hipMalloc(&cnt, (size_t)P * sizeof(int)) != hipSuccess || hipMemset(cnt, 0, (size_t)P * sizeof(int)) != hipSuccess) {
+    hipFree(ws);
+    return nullptr;
+  }
+  w.ws = ws;
+  w.cnt = cnt;
+  w.P = P;
+  return &w;
+}
+
+// skmode 0: whole tiles only; 1: hybrid split-K when the tiles leave the last wave at most half
+// full (and fewer than 8 full waves); 2: hybrid whenever tiles % CUs leaves room for 2 splits
+template <int EPI>
+void launch_pp(const void* x, int ldx, const void* w, void* y, int ldy, int M, int I, int K, int tiles_m, int total,
+               int skmode, hipStream_t s) {
+  PPArgs a{(const uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, nullptr, nullptr, ldx, ldy, M, I, K, tiles_m, total,
+           0, 0, 0, 0};
+  const int nt = K / kBK;
+  SkWorkspace* sk = (skmode && nt >= 8) ? sk_workspace(s) : nullptr;
+  if (sk) {
+    const int full = total / sk->P, rem = total % sk->P;
+    const int splits = rem ? min(4, sk->P / rem) : 0;
+    if (splits >= 2 && (full < 8 || skmode == 2)) {
+      a.ws = sk->ws;
+      a.cnt = sk->cnt;
+      a.rem = rem;
+      a.splits = splits;
+      a.full = full;
+      a.P = sk->P;
+      mfma_gemm_pp_kernel<EPI><<<dim3(sk->P), 512, 0, s>>>(a);
+      return;
+    }
+  }
+  mfma_gemm_pp_kernel<EPI><<<dim3(total), 512, 0, s>>>(a);
+}
+
 template <int EPI, int SCHED>
 void launch(const void* x, int ldx, const void* w, void* y, int ldy, int M, int I, int K, int tiles_m, int total,
-            hipStream_t s) {
-  if (SCHED == 2)
+            int skmode, hipStream_t s) {
+  if (SCHED == 3)
+    launch_pp<EPI>(x, ldx, w, y, ldy, M, I, K, tiles_m, total, skmode, s);
+  else if (SCHED == 2)
     mfma_gemm_ring_kernel<EPI><<<dim3(total), 512, 0, s>>>((const uint16_t*)x, ldx, (const uint16_t*)w,
                                                           (uint16_t*)y, ldy, M, I, K, tiles_m, total);
   else
@@ -409,21 +733,28 @@ void launch(const void* x, int ldx, const void* w, void* y, int ldy, int M, int 
 }  // namespace
 
 // epi & 1: 0 = Y[M, N] = X W^T with N = rows of W; 1 = Y[M, I] = SwiGLU with W = [gate; up] (2I rows).
-// epi >> 4: K-loop schedule (0 = compiler order, 1 = interleaved, 2 = 4-slot ring of 32-deep sub-steps).
+// epi >> 4: K-loop schedule (0 = compiler order, 1 = interleaved, 2 = 4-slot ring of 32-deep sub-steps,
+// 3 = ping-pong wave groups, 4 phases per K tile).  (epi >> 8) & 3: stream-K policy of schedule 3
+// (0 = auto, 1 = off, 2 = whenever the tiles leave the last wave part-empty).
 extern "C" int dgi_mfma_gemm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K,
                              int epi, hipStream_t s) {
   if (M <= 0) return 0;
   if (K % kBK || ldx % 8 || ldy % 4 || N % 256) return -3;
-  const int swiglu = epi & 15, sched = epi >> 4;
-  if (swiglu > 1 || sched > 2) return -4;
+  const int swiglu = epi & 15;
+  int sched = (epi >> 4) & 15;
+  const int skmode = ((epi >> 8) & 3) == 0 ? 1 : ((epi >> 8) & 3) == 1 ? 0 : 2;
+  if (swiglu > 1 || sched > 3) return -4;
+  if (sched == 3 && (K % (2 * kBK) || K < 4 * kBK)) sched = 1;   // ping-pong needs an even count of >= 4 K tiles
   const int I = swiglu ? N / 2 : 0;
   const int tiles_n = swiglu ? I / 128 : N / 256;
   const int tiles_m = (M + kBM - 1) / kBM;
   const int total = tiles_m * tiles_n;
   if (swiglu)
-    (sched == 2 ? launch<1, 2> : sched ? launch<1, 1> : launch<1, 0>)(x, ldx, w, y, ldy, M, I, K, tiles_m, total, s);
+    (sched == 3 ? launch<1, 3> : sched == 2 ? launch<1, 2> : sched ? launch<1, 1> : launch<1, 0>)(
+        x, ldx, w, y, ldy, M, I, K, tiles_m, total, skmode, s);
   else
-    (sched == 2 ? launch<0, 2> : sched ? launch<0, 1> : launch<0, 0>)(x, ldx, w, y, ldy, M, I, K, tiles_m, total, s);
+    (sched == 3 ? launch<0, 3> : sched == 2 ? launch<0, 2> : sched ? launch<0, 1> : launch<0, 0>)(
+        x, ldx, w, y, ldy, M, I, K, tiles_m, total, skmode, s);
   DGI_CHECK_LAUNCH();
   return 0;
 }

@@ -151,6 +151,7 @@ class LLMEngine:
             if self.mlp_pad_table is not None:
                 self.model.mlp_pad = self.mlp_pad_table.pad
                 self.model.mlp_impl = self.mlp_pad_table.impl
+                self.model.proj_impl = self.mlp_pad_table.proj_impl
                 self.mlp_pad_seconds = time.perf_counter() - t1
 
     # ------------------------------------------------------------------ API

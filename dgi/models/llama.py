@@ -85,6 +85,7 @@ class LlamaModel:
         # MLP row padding (dgi.runtime.gemm_pad): T -> rows to run gate_up/down on
         self.mlp_pad = None
         self.mlp_impl = None     # rows -> (gate_up on the MFMA SwiGLU kernel, down on the MFMA kernel)
+        self.proj_impl = None    # rows -> (QKV on the MFMA kernel, o-proj on the MFMA kernel)
         # called with the global layer id once that layer's KV is in the cache
         # (P/D layer-streamed migration sends finished layers while later ones compute)
         self.layer_hook = None
@@ -343,6 +344,8 @@ class LlamaModel:
         Mp = self._mlp_rows(T, h) if self.layers else T
         # hand-written MFMA GEMMs where the start-up table measured them faster (dgi.runtime.gemm_pad)
         mfma_gu, mfma_dn = self.mlp_impl(Mp) if (self.mlp_impl is not None and self.layers) else (False, False)
+        mfma_q, mfma_o = self.proj_impl(T) if (self.proj_impl is not None and self.layers and h.is_cuda
+                                               and not torch.cuda.is_current_stream_capturing()) else (False, False)
         hfull = None
         for i, L in enumerate(self.layers):
             if residual is None:
@@ -354,6 +357,8 @@ class LlamaModel:
                 # the previous MLP ran on Mp padded rows (zeros past T): the QKV GEMM
                 # reuses them, at the row count the start-up table timed for the layer
                 qkv = ops.linear(hfull, L.qkv, L.qkv_bias)[:T]
+            elif mfma_q and L.qkv_bias is None:
+                qkv = ops.mfma_gemm(h, L.qkv, 0)
             else:
                 qkv = ops.linear(h, L.qkv, L.qkv_bias)
             last = trim_last is not None and i == len(self.layers) - 1
@@ -379,9 +384,10 @@ class LlamaModel:
                 h = self._pad_buf[:T]
             elif Mp > T:
                 # o-proj writes the first T rows of the padded MLP input
-                h = torch.matmul(attn, L.o.t(), out=self._pad_buf[:T])
+                h = ops.mfma_gemm(attn, L.o, 0, out=self._pad_buf[:T]) if mfma_o else \
+                    torch.matmul(attn, L.o.t(), out=self._pad_buf[:T])
             else:
-                h = ops.linear(attn, L.o)
+                h = ops.mfma_gemm(attn, L.o, 0) if mfma_o else ops.linear(attn, L.o)
             if self.reduce is not None:
                 self.reduce(h)
             ops.fused_add_rmsnorm(h, residual, L.post_norm, eps)

@@ -20,7 +20,10 @@ Each half of the MLP is measured with both GEMM implementations — hipBLASLt
 (``ops.mfma_gemm``: gate_up with the SwiGLU epilogue fused, down as a plain
 GEMM) — and ``impl(rows)`` tells the model which one is faster at that row
 count on this GPU (``DGI_MFMA_GEMM=0`` keeps hipBLASLt everywhere, ``=force``
-the MFMA kernel wherever it applies).
+the MFMA kernel wherever it applies).  The QKV and o projections get the same
+per-row-count choice (``proj_impl(rows)``, at the first grid point >= rows): with
+the ping-pong schedule and its split-K remainder (``ops.mfma_gemm`` sched 3) the
+hand-written kernel beats hipBLASLt on several of their row counts.
 """
 from __future__ import annotations
 
@@ -38,30 +41,37 @@ MFMA_MARGIN = 0.98
 
 
 class MlpPadTable:
-    def __init__(self, grid: list, times: list, step: int, max_grow: float = 0.15, impls: Optional[list] = None):
+    def __init__(self, grid: list, times: list, step: int, max_grow: float = 0.15, impls: Optional[list] = None,
+                 proj_impls: Optional[list] = None):
         self.grid = list(grid)
         self.times = list(times)
         self.step = step
         self.max_grow = max_grow
         # per grid point: (gate_up via MFMA+SwiGLU?, down via MFMA?)
         self.impls = list(impls) if impls is not None else [(False, False)] * len(self.grid)
+        # per grid point: (QKV via MFMA?, o-proj via MFMA?)
+        self.proj_impls = list(proj_impls) if proj_impls is not None else [(False, False)] * len(self.grid)
         self._cache: dict = {}
 
     @classmethod
     def measure(cls, gate_up: torch.Tensor, down: torch.Tensor, m_min: int = 512, m_max: int = 4096,
                 step: int = 32, reps: int = 3, qkv: Optional[torch.Tensor] = None,
-                o_w: Optional[torch.Tensor] = None) -> "MlpPadTable":
+                o_w: Optional[torch.Tensor] = None, proj_qkv: Optional[torch.Tensor] = None,
+                proj_o: Optional[torch.Tensor] = None) -> "MlpPadTable":
         """``qkv`` / ``o_w``: the next layer's QKV GEMM and this layer's o-proj run on
         the same padded rows (``LlamaModel.forward_layers``), so their times join
-        the objective."""
+        the objective.  ``proj_qkv`` / ``proj_o``: the (bias-free) QKV and o-proj
+        weights whose implementation is chosen per row count (``proj_impl``)."""
         from dgi import ops
         H = gate_up.shape[1]
         x = torch.randn(m_max, H, device=gate_up.device, dtype=gate_up.dtype) * 0.1
         a = torch.randn(m_max, gate_up.shape[0] // 2, device=gate_up.device, dtype=gate_up.dtype) * 0.1
         ao = torch.randn(m_max, o_w.shape[1], device=gate_up.device, dtype=gate_up.dtype) * 0.1 \
             if o_w is not None else None
+        pa = torch.randn(m_max, proj_o.shape[1], device=gate_up.device, dtype=gate_up.dtype) * 0.1 \
+            if proj_o is not None else None
         grid = list(range(m_min, m_max + 1, step))
-        times, impls = [], []
+        times, impls, proj_impls = [], [], []
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         use_mfma = MFMA_GEMM != "0" and ops.mfma_gemm_ok(x, gate_up)
         mfma_down = use_mfma and ops.mfma_gemm_ok(a, down)
@@ -94,7 +104,15 @@ class MlpPadTable:
             o = timed(lambda: ops.linear(ao[:m], o_w)) if o_w is not None else 0.0
             times.append(front + back + q + o)
             impls.append((f_mfma, b_mfma))
-        return cls(grid, times, step, impls=impls)
+            pq = po = False
+            if use_mfma and proj_qkv is not None and ops.mfma_gemm_ok(x, proj_qkv):
+                t = timed(lambda: ops.mfma_gemm(x[:m], proj_qkv, 0))
+                pq = force or t < timed(lambda: ops.linear(x[:m], proj_qkv)) * MFMA_MARGIN
+            if use_mfma and proj_o is not None and ops.mfma_gemm_ok(pa, proj_o):
+                t = timed(lambda: ops.mfma_gemm(pa[:m], proj_o, 0))
+                po = force or t < timed(lambda: ops.linear(pa[:m], proj_o)) * MFMA_MARGIN
+            proj_impls.append((pq, po))
+        return cls(grid, times, step, impls=impls, proj_impls=proj_impls)
 
     def impl(self, rows: int) -> tuple:
         """(gate_up via the fused MFMA SwiGLU kernel, down via the MFMA kernel) at ``rows``."""
@@ -102,6 +120,12 @@ class MlpPadTable:
             return False, False
         i = bisect.bisect_left(self.grid, rows)
         return self.impls[i] if self.grid[i] == rows else (False, False)
+
+    def proj_impl(self, rows: int) -> tuple:
+        """(QKV via the MFMA kernel, o-proj via the MFMA kernel) at ``rows`` (first grid point >= rows)."""
+        if not self.grid or not (self.grid[0] <= rows <= self.grid[-1]):
+            return False, False
+        return self.proj_impls[bisect.bisect_left(self.grid, rows)]
 
     def pad(self, T: int) -> int:
         """Rows to run the MLP on for a step of ``T`` rows (``T`` when the table has no say)."""
@@ -134,4 +158,5 @@ def build_for_model(model, m_max: int, step: int = 32) -> Optional[MlpPadTable]:
         return None
     from dgi.models import llama
     return MlpPadTable.measure(L.gate_up, L.down, m_max=m_max, step=step,
-                               qkv=L.qkv if llama.QKV_PAD else None, o_w=L.o if llama.OPROJ_PAD else None)
+                               qkv=L.qkv if llama.QKV_PAD else None, o_w=L.o if llama.OPROJ_PAD else None,
+                               proj_qkv=L.qkv if L.qkv_bias is None else None, proj_o=L.o)

@@ -28,6 +28,8 @@ SHAPES = {  # name: (N, K)
 MS = [int(x) for x in os.environ.get("GEMM_MS", "512,1024,1536,1792,2048,4096").split(",")]
 ROUNDS = int(os.environ.get("GEMM_ROUNDS", "7"))
 ITERS = int(os.environ.get("GEMM_ITERS", "10"))
+# schedule ids; "3k" = schedule 3 with stream-K off
+SCHEDS = os.environ.get("GEMM_SCHEDS", "1,0,2,3").split(",")
 
 
 def timed(fn):
@@ -49,17 +51,12 @@ def main():
         for M in MS:
             x = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
             fused = name.endswith("gate_up")
-            if fused:
-                variants = {
-                    "hipblaslt+silu_mul": lambda: ops.silu_mul(F.linear(x, w)),
-                    "mfma_swiglu": lambda: ops.mfma_gemm(x, w, 1, sched=1),
-                    "mfma_swiglu_s0": lambda: ops.mfma_gemm(x, w, 1, sched=0),
-                    "mfma_swiglu_s2": lambda: ops.mfma_gemm(x, w, 1, sched=2),
-                }
-            else:
-                variants = {"hipblaslt": lambda: F.linear(x, w), "mfma": lambda: ops.mfma_gemm(x, w, 0, sched=1),
-                            "mfma_s0": lambda: ops.mfma_gemm(x, w, 0, sched=0),
-                            "mfma_s2": lambda: ops.mfma_gemm(x, w, 0, sched=2)}
+            epi = 1 if fused else 0
+            variants = {"hipblaslt+silu_mul": lambda: ops.silu_mul(F.linear(x, w))} if fused else \
+                {"hipblaslt": lambda: F.linear(x, w)}
+            for sc in SCHEDS:
+                variants[("mfma_swiglu" if fused else "mfma") + ("" if sc == SCHEDS[0] else f"_s{sc}")] = \
+                    (lambda sc=sc: ops.mfma_gemm(x, w, epi, sched=int(sc.rstrip("k")), streamk=int(sc.endswith("k"))))
             for f in variants.values():
                 f()
             torch.cuda.synchronize()

@@ -60,9 +60,9 @@ def load(path):
 def main(path, title=""):
     per, dur = load(path)
     print(f"# {title or path}\n")
-    print("| kernel | dispatches | time ms | MFMA busy % | bf16 MFMA TF/s | LDS bank-conflict % | MFMA inst/wave |"
-          " LDS inst/wave |")
-    print("|---|---:|---:|---:|---:|---:|---:|---:|")
+    print("| kernel | dispatches | time ms | eff. clock GHz | MFMA busy % | bf16 MFMA TF/s | LDS bank-conflict % |"
+          " MFMA inst/wave | LDS inst/wave | wait % | issue-stall % |")
+    print("|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
     for k, c in sorted(per.items(), key=lambda kv: -dur.get(kv[0], 0)):
         t = dur.get(k, 0.0)
         gui = c.get("GRBM_GUI_ACTIVE", 0.0)
@@ -73,8 +73,12 @@ def main(path, title=""):
         waves = c.get("SQ_WAVES", 0.0)
         mi = c.get("SQ_INSTS_MFMA", c.get("SQ_INSTS_VALU_MFMA_BF16", 0.0)) / waves if waves else float("nan")
         li = c.get("SQ_INSTS_LDS", 0.0) / waves if waves else float("nan")
-        print(f"| `{k}` | {int(c['_dispatches'])} | {t * 1e3:.2f} | {busy:.1f} | {tf:.1f} | {conf:.2f} | {mi:.1f} |"
-              f" {li:.1f} |")
+        clk = gui / 8 / t / 1e9 if t else float("nan")
+        wc = c.get("SQ_WAVE_CYCLES", 0.0)
+        wait = 100.0 * c.get("SQ_WAIT_ANY", 0.0) / wc if wc else float("nan")
+        stall = 100.0 * c.get("SQ_WAIT_INST_ANY", 0.0) / wc if wc else float("nan")
+        print(f"| `{k}` | {int(c['_dispatches'])} | {t * 1e3:.2f} | {clk:.2f} | {busy:.1f} | {tf:.1f} | {conf:.2f} |"
+              f" {mi:.1f} | {li:.1f} | {wait:.1f} | {stall:.1f} |")
     print("\nRaw counter totals:\n")
     for k, c in per.items():
         vals = ", ".join(f"{n}={v:.4g}" for n, v in sorted(c.items()) if not n.startswith("_"))

@@ -26,7 +26,7 @@ def test_reference_swiglu_matches_silu_mul_cpu():
 @pytest.mark.parametrize("M,N,K", [(1, 256, 64), (100, 512, 256), (256, 256, 128), (300, 768, 512),
                                    (1000, 1024, 1024), (2048, 2560, 4096), (513, 256, 8192)])
 @pytest.mark.parametrize("epi", [0, 1])
-@pytest.mark.parametrize("sched", [0, 1, 2])
+@pytest.mark.parametrize("sched", [0, 1, 2, 3])
 def test_mfma_gemm_matches_fp32(M, N, K, epi, sched):
     ops.load_native(required=True)
     x = _rand(M, K, device="cuda", seed=M + K)
@@ -41,7 +41,7 @@ def test_mfma_gemm_matches_fp32(M, N, K, epi, sched):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("sched", [0, 1, 2])
+@pytest.mark.parametrize("sched", [0, 1, 2, 3])
 def test_mfma_gemm_strided_rows_and_asymmetric_operands(sched):
     """A = row slice of a wider buffer (ldx > K) and an asymmetric W: catches
     row/column swaps in the C write and ldx handling."""
@@ -53,3 +53,43 @@ def test_mfma_gemm_strided_rows_and_asymmetric_operands(sched):
     got = ops.mfma_gemm(x, w, 0, sched=sched)
     ref = ops.mfma_gemm_ref(x, w, 0).float()
     assert (got.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(2048, 1024, 256), (1920, 2560, 1024), (4096, 512, 8192)])
+@pytest.mark.parametrize("epi", [0, 1])
+def test_mfma_gemm_pingpong_bitwise_stable(M, N, K, epi):
+    """Race screen for the ping-pong schedule (sched 3): it accumulates in the same
+    order as sched 1, so every one of repeated launches must match sched 1 bit for
+    bit -- a slab read before its load landed (or overwritten before every wave
+    read it) shows up as a mismatch on some launch."""
+    ops.load_native(required=True)
+    x = _rand(M, K, device="cuda", seed=M)
+    w = _rand(N, K, device="cuda", scale=0.05, seed=K)
+    ref = ops.mfma_gemm(x, w, epi, sched=1)
+    for _ in range(12):
+        got = ops.mfma_gemm(x, w, epi, sched=3, streamk=1)
+        assert torch.equal(got, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(2048, 2560, 512), (1920, 10240, 8192), (1000, 768, 2048), (2432, 8192, 1024),
+                                   (300, 57344 // 8, 4096)])
+@pytest.mark.parametrize("epi", [0, 1])
+@pytest.mark.parametrize("streamk", [0, 2])
+def test_mfma_gemm_splitk_matches_fp32_and_is_deterministic(M, N, K, epi, streamk):
+    """Hybrid split-K of the last partial wave (persistent launch, 2-4 K pieces per
+    remainder tile reduced by the last arriving block through fp32 slabs; uneven
+    piece lengths at K = 512): matches the fp32 reference, and repeated launches
+    agree bit for bit (slabs are summed in piece order)."""
+    ops.load_native(required=True)
+    x = _rand(M, K, device="cuda", seed=M + 1)
+    w = _rand(N, K, device="cuda", scale=0.05, seed=N + 1)
+    ref = ops.mfma_gemm_ref(x, w, epi).float()
+    got = ops.mfma_gemm(x, w, epi, sched=3, streamk=streamk)
+    torch.cuda.synchronize()
+    err = (got.float() - ref).abs()
+    tol = 2e-2 * ref.abs().max().item() + 1e-3
+    assert err.max().item() <= tol, (err.max().item(), tol)
+    for _ in range(6):
+        assert torch.equal(ops.mfma_gemm(x, w, epi, sched=3, streamk=streamk), got)
