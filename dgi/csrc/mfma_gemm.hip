@@ -443,7 +443,90 @@ struct PPArgs {
   int rem, splits, full, P;
 };
 
-template <int EPI>
+// The work items of one block (see "Work decomposition" above): its one tile
+// (rem == 0), its split-K piece, then its whole tiles.  run(tm, tn, kb, L)
+// accumulates K tiles kb .. kb + L - 1 of output tile (tm, tn) into the
+// caller's registers; slab_store / slab_add move them to / from a 256 x 256 fp32
+// slab (per-thread base pointer, NT threads interleaved by 16 bytes); epi stores
+// the bf16 tile.
+template <int NT, class Run, class Store, class Add, class Epi>
+__device__ __forceinline__ void drive(const PPArgs& a, char* smem, Run&& run, Store&& slab_store, Add&& slab_add,
+                                      Epi&& epi) {
+  const int tid = threadIdx.x;
+  const int nt = a.K / kBK;
+  const int nt2 = nt >> 1;                    // 128-deep units per tile
+  // persistent hybrid: block g (blocks that share an XCD take consecutive g)
+  const int g = (blockIdx.x & 7) * (a.P >> 3) + (blockIdx.x >> 3);
+  bool split = a.rem && g < a.rem * a.splits;
+  int k = 0;
+  for (;;) {
+    int t, kb = 0, L = nt;
+    bool piece = false;
+    if (a.rem == 0) {
+      if (k++) break;
+      const int b = blockIdx.x, T = a.tiles_total;
+      const int xcd = b & 7, li = b >> 3;
+      const int q8 = T >> 3, r8 = T & 7;
+      t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + li;
+    } else if (split) {
+      split = false;
+      const int j = g / a.rem;
+      t = g - j * a.rem;
+      const int u0 = j * nt2 / a.splits, u1 = (j + 1) * nt2 / a.splits;
+      kb = 2 * u0;
+      L = 2 * (u1 - u0);
+      piece = true;
+    } else if (k < a.full) {
+      t = a.rem + k * a.P + g;
+      ++k;
+    } else {
+      break;
+    }
+    const int tm = t % a.tiles_m, tn = t / a.tiles_m;
+    run(tm, tn, kb, L);
+    bool store = true;
+    if (piece) {
+      // slab offsets from a laundered thread id: otherwise hipcc hoists every per-lane
+      // address out of the work-item loop and spills them
+      int lt = tid;
+      asm volatile("" : "+v"(lt));
+      slab_store(a.ws + (size_t)g * 65536 + lt * 4);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int old = __hip_atomic_fetch_add(a.cnt + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == a.splits - 1;
+        if (last) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_store(a.cnt + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        *(volatile int*)smem = last;
+      }
+      __syncthreads();
+      store = *(volatile int*)smem;
+      __syncthreads();          // flag read by every wave before the next item's staging overwrites it
+      if (store) {
+        // every slab, own included, in piece order: the sum does not depend on which piece arrived last
+        for (int jj = 0; jj < a.splits; ++jj) slab_add(a.ws + (size_t)(jj * a.rem + t) * 65536 + lt * 4, jj == 0);
+      }
+    }
+    if (store) epi(tm, tn);
+  }
+}
+
+// PRIO: 0 = s_setprio 1 around each MFMA cluster (keeps hipcc from moving MFMAs across the
+// barriers; the instructions themselves are near free); 1 = static s_setprio 1 for waves 4-7
+// (the second-dispatched half) and no per-cluster flips; 2 = no s_setprio.
+// PH: phases per K tile, 4 (16 MFMAs per section, the table above) or 2 (32 MFMAs per
+// section, half the barrier hand-offs):
+//
+//   phase  reads             MFMAs          staging                       wait before the barrier
+//   0      Xa, Wa, Wb (16)   Xa x (Wa, Wb)  W0-3, X2 of t+1               vmcnt(6): X1, X3 of t landed
+//   1      Xb (8)            Xb x (Wa, Wb)  X3, X1 of t+1, X0 of t+2      vmcnt(3): all but X3, X1 of t+1
+template <int EPI, int PRIO, int PH>
 __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kStageBytes];
   const int tid = threadIdx.x;
@@ -483,7 +566,7 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
     }
   };
   auto mma = [&](int i0, int j0, const bf16x8 (&xf)[4][2], const bf16x8 (&wf)[2][2]) {
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -491,8 +574,11 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][h], xf[i][h], acc[i0 + i][j0 + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(0);
   };
+  if constexpr (PRIO == 1) {
+    if (wm == 1) __builtin_amdgcn_s_setprio(1);
+  }
   auto barrier = [&]() {
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
@@ -561,101 +647,87 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
       barrier();
     };
 
+    // the same K tile in two phases of 32 MFMAs (PH == 2)
+    auto tile2 = [&](int t, auto ST_, auto MODE_) {
+      constexpr int ST = decltype(ST_)::value, MODE = decltype(MODE_)::value;
+      // phase 0
+      if constexpr (MODE < 2) {
+        gw(t + 1, 0, ST ^ 1); gw(t + 1, 1, ST ^ 1); gw(t + 1, 2, ST ^ 1); gw(t + 1, 3, ST ^ 1);
+        gx(t + 1, 2, ST ^ 1);
+      }
+      rw(ST, 0, wa);
+      rw(ST, 2, wb);
+      rx(ST, 0, xa);
+      if constexpr (MODE < 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      barrier();
+      mma(0, 0, xa, wa);
+      mma(0, 2, xa, wb);
+      barrier();
+      // phase 1
+      if constexpr (MODE < 2) { gx(t + 1, 3, ST ^ 1); gx(t + 1, 1, ST ^ 1); }
+      if constexpr (MODE == 0) gx(t + 2, 0, ST);
+      rx(ST, 4, xb);
+      if constexpr (MODE == 0) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else if constexpr (MODE == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      barrier();
+      mma(4, 0, xb, wa);
+      mma(4, 2, xb, wb);
+      barrier();
+    };
+
     using Z = std::integral_constant<int, 0>;
     using O = std::integral_constant<int, 1>;
     using T2 = std::integral_constant<int, 2>;
-    // prologue: everything the steady state would have issued before tile 0
-    gx(0, 0, 0); gx(0, 2, 0); gw(0, 0, 0); gw(0, 1, 0); gw(0, 2, 0); gw(0, 3, 0);
-    gx(0, 3, 0); gx(1, 0, 1); gx(0, 1, 0); gx(1, 2, 1); gw(1, 0, 1); gw(1, 1, 1);
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    barrier();
-    if (wm == 1) barrier();     // stagger: waves 4-7 run one section behind
-    int t = 0;
-    for (; t + 4 <= L; t += 2) {
-      tile(t, Z{}, Z{});
-      tile(t + 1, O{}, Z{});
+    if constexpr (PH == 2) {
+      // prologue: everything the steady state would have issued before tile 0
+      gx(0, 0, 0); gw(0, 0, 0); gw(0, 1, 0); gw(0, 2, 0); gw(0, 3, 0); gx(0, 2, 0);
+      gx(0, 3, 0); gx(0, 1, 0); gx(1, 0, 1);
+      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      barrier();
+      if (wm == 1) barrier();     // stagger: waves 4-7 run one section behind
+      int t = 0;
+      for (; t + 4 <= L; t += 2) {
+        tile2(t, Z{}, Z{});
+        tile2(t + 1, O{}, Z{});
+      }
+      tile2(t, Z{}, O{});
+      tile2(t + 1, O{}, T2{});
+    } else {
+      // prologue: everything the steady state would have issued before tile 0
+      gx(0, 0, 0); gx(0, 2, 0); gw(0, 0, 0); gw(0, 1, 0); gw(0, 2, 0); gw(0, 3, 0);
+      gx(0, 3, 0); gx(1, 0, 1); gx(0, 1, 0); gx(1, 2, 1); gw(1, 0, 1); gw(1, 1, 1);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      barrier();
+      if (wm == 1) barrier();     // stagger: waves 4-7 run one section behind
+      int t = 0;
+      for (; t + 4 <= L; t += 2) {
+        tile(t, Z{}, Z{});
+        tile(t + 1, O{}, Z{});
+      }
+      tile(t, Z{}, O{});
+      tile(t + 1, O{}, T2{});
     }
-    tile(t, Z{}, O{});
-    tile(t + 1, O{}, T2{});
     if (wm == 0) barrier();     // pairs with the last barrier of waves 4-7: every LDS read retired
   };
 
-  const int nt = K / kBK;
-  const int nt2 = nt >> 1;                    // 128-deep units per tile
-  // persistent hybrid: block g (blocks that share an XCD take consecutive g)
-  const int g = (blockIdx.x & 7) * (a.P >> 3) + (blockIdx.x >> 3);
-  bool split = a.rem && g < a.rem * a.splits;
-  int k = 0;
-  for (;;) {
-    // next work item: the block's one tile (rem == 0), its split-K piece, then its whole tiles
-    int t, kb = 0, L = nt;
-    bool piece = false;
-    if (a.rem == 0) {
-      if (k++) break;
-      const int b = blockIdx.x, T = a.tiles_total;
-      const int xcd = b & 7, li = b >> 3;
-      const int q8 = T >> 3, r8 = T & 7;
-      t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + li;
-    } else if (split) {
-      split = false;
-      const int j = g / a.rem;
-      t = g - j * a.rem;
-      const int u0 = j * nt2 / a.splits, u1 = (j + 1) * nt2 / a.splits;
-      kb = 2 * u0;
-      L = 2 * (u1 - u0);
-      piece = true;
-    } else if (k < a.full) {
-      t = a.rem + k * a.P + g;
-      ++k;
-    } else {
-      break;
-    }
-    const int tm = t % a.tiles_m, tn = t / a.tiles_m;
-    run(tm, tn, kb, L);
-    bool store = true;
-    if (piece) {
-      // slab offsets from a laundered thread id: otherwise hipcc hoists all 32 per-lane
-      // addresses out of the work-item loop and spills them
-      int lt = tid;
-      asm volatile("" : "+v"(lt));
-      float* slab = a.ws + (size_t)g * 65536 + lt * 4;
+  drive<512>(a, smem, run,
+             [&](float* slab) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+               for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) *(f32x4*)(slab + (i * 4 + j) * 2048) = acc[i][j];
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int old = __hip_atomic_fetch_add(a.cnt + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = old == a.splits - 1;
-        if (last) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __hip_atomic_store(a.cnt + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        *(volatile int*)smem = last;
-      }
-      __syncthreads();
-      store = *(volatile int*)smem;
-      __syncthreads();          // flag read by every wave before the next item's staging overwrites it
-      if (store) {
-        // every slab, own included, in piece order: the sum does not depend on which piece arrived last
-        for (int jj = 0; jj < a.splits; ++jj) {
-          const float* o = a.ws + (size_t)(jj * a.rem + t) * 65536 + lt * 4;
+                 for (int j = 0; j < 4; ++j) *(f32x4*)(slab + (i * 4 + j) * 2048) = acc[i][j];
+             },
+             [&](const float* o, bool first) {
 #pragma unroll
-          for (int i = 0; i < 8; ++i)
+               for (int i = 0; i < 8; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const f32x4 v = *(const f32x4*)(o + (i * 4 + j) * 2048);
-              acc[i][j] = jj == 0 ? v : acc[i][j] + v;
-            }
-        }
-      }
-    }
-    if (store) epilogue<EPI>(acc, a.Y, a.ldy, M, tm * kBM, tn, wm, wn, lane);
-  }
+                 for (int j = 0; j < 4; ++j) {
+                   const f32x4 v = *(const f32x4*)(o + (i * 4 + j) * 2048);
+                   acc[i][j] = first ? v : acc[i][j] + v;
+                 }
+             },
+             [&](int tm, int tn) { epilogue<EPI>(acc, a.Y, a.ldy, M, tm * kBM, tn, wm, wn, lane); });
 }
 
 // Per-device split-K workspace (one fp32 slab per block + one counter per tile),
@@ -695,7 +767,13 @@ SkWorkspace* sk_workspace(hipStream_t s) {
 // full (and fewer than 8 full waves); 2: hybrid whenever tiles % CUs leaves room for 2 splits
 template <int EPI>
 void launch_pp(const void* x, int ldx, const void* w, void* y, int ldy, int M, int I, int K, int tiles_m, int total,
-               int skmode, hipStream_t s) {
+               int skmode, int prio, hipStream_t s) {
+  auto kern = (prio & 4) ? (prio & 3) == 1   ? mfma_gemm_pp_kernel<EPI, 1, 2>
+                            : (prio & 3) == 2 ? mfma_gemm_pp_kernel<EPI, 2, 2>
+                                              : mfma_gemm_pp_kernel<EPI, 0, 2>
+                          : (prio & 3) == 1   ? mfma_gemm_pp_kernel<EPI, 1, 4>
+                          : (prio & 3) == 2   ? mfma_gemm_pp_kernel<EPI, 2, 4>
+                                              : mfma_gemm_pp_kernel<EPI, 0, 4>;
   PPArgs a{(const uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, nullptr, nullptr, ldx, ldy, M, I, K, tiles_m, total,
            0, 0, 0, 0};
   const int nt = K / kBK;
@@ -710,18 +788,18 @@ void launch_pp(const void* x, int ldx, const void* w, void* y, int ldy, int M, i
       a.splits = splits;
       a.full = full;
       a.P = sk->P;
-      mfma_gemm_pp_kernel<EPI><<<dim3(sk->P), 512, 0, s>>>(a);
+      kern<<<dim3(sk->P), 512, 0, s>>>(a);
       return;
     }
   }
-  mfma_gemm_pp_kernel<EPI><<<dim3(total), 512, 0, s>>>(a);
+  kern<<<dim3(total), 512, 0, s>>>(a);
 }
 
 template <int EPI, int SCHED>
 void launch(const void* x, int ldx, const void* w, void* y, int ldy, int M, int I, int K, int tiles_m, int total,
-            int skmode, hipStream_t s) {
+            int skmode, int prio, hipStream_t s) {
   if (SCHED == 3)
-    launch_pp<EPI>(x, ldx, w, y, ldy, M, I, K, tiles_m, total, skmode, s);
+    launch_pp<EPI>(x, ldx, w, y, ldy, M, I, K, tiles_m, total, skmode, prio, s);
   else if (SCHED == 2)
     mfma_gemm_ring_kernel<EPI><<<dim3(total), 512, 0, s>>>((const uint16_t*)x, ldx, (const uint16_t*)w,
                                                           (uint16_t*)y, ldy, M, I, K, tiles_m, total);
@@ -735,7 +813,9 @@ void launch(const void* x, int ldx, const void* w, void* y, int ldy, int M, int 
 // epi & 1: 0 = Y[M, N] = X W^T with N = rows of W; 1 = Y[M, I] = SwiGLU with W = [gate; up] (2I rows).
 // epi >> 4: K-loop schedule (0 = compiler order, 1 = interleaved, 2 = 4-slot ring of 32-deep sub-steps,
 // 3 = ping-pong wave groups, 4 phases per K tile).  (epi >> 8) & 3: stream-K policy of schedule 3
-// (0 = auto, 1 = off, 2 = whenever the tiles leave the last wave part-empty).
+// (0 = auto, 1 = off, 2 = whenever the tiles leave the last wave part-empty).  (epi >> 10) & 3:
+// s_setprio variant of schedule 3, (epi >> 12) & 1: two 32-MFMA phases per K tile, (epi >> 13) & 1:
+// four 16-MFMA phases (default: two up to M = 2560, see mfma_gemm_pp_kernel).
 extern "C" int dgi_mfma_gemm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K,
                              int epi, hipStream_t s) {
   if (M <= 0) return 0;
@@ -743,6 +823,10 @@ extern "C" int dgi_mfma_gemm(const void* x, int ldx, const void* w, void* y, int
   const int swiglu = epi & 15;
   int sched = (epi >> 4) & 15;
   const int skmode = ((epi >> 8) & 3) == 0 ? 1 : ((epi >> 8) & 3) == 1 ? 0 : 2;
+  int prio = (epi >> 10) & 7;
+  // phases per K tile: (epi >> 13) & 1 forces 4; otherwise 2 up to 10 row tiles (M <= 2560: the
+  // 2-phase body measured 2-4 % faster there) and 4 above (its deeper prefetch wins at M = 4096)
+  if (!((epi >> 13) & 1) && !(prio & 4) && M <= 2560) prio |= 4;
   if (swiglu > 1 || sched > 3) return -4;
   if (sched == 3 && (K % (2 * kBK) || K < 4 * kBK)) sched = 1;   // ping-pong needs an even count of >= 4 K tiles
   const int I = swiglu ? N / 2 : 0;
@@ -751,10 +835,10 @@ extern "C" int dgi_mfma_gemm(const void* x, int ldx, const void* w, void* y, int
   const int total = tiles_m * tiles_n;
   if (swiglu)
     (sched == 3 ? launch<1, 3> : sched == 2 ? launch<1, 2> : sched ? launch<1, 1> : launch<1, 0>)(
-        x, ldx, w, y, ldy, M, I, K, tiles_m, total, skmode, s);
+        x, ldx, w, y, ldy, M, I, K, tiles_m, total, skmode, prio, s);
   else
     (sched == 3 ? launch<0, 3> : sched == 2 ? launch<0, 2> : sched ? launch<0, 1> : launch<0, 0>)(
-        x, ldx, w, y, ldy, M, I, K, tiles_m, total, skmode, s);
+        x, ldx, w, y, ldy, M, I, K, tiles_m, total, skmode, prio, s);
   DGI_CHECK_LAUNCH();
   return 0;
 }

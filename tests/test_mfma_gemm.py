@@ -58,7 +58,8 @@ def test_mfma_gemm_strided_rows_and_asymmetric_operands(sched):
 @pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K", [(2048, 1024, 256), (1920, 2560, 1024), (4096, 512, 8192)])
 @pytest.mark.parametrize("epi", [0, 1])
-def test_mfma_gemm_pingpong_bitwise_stable(M, N, K, epi):
+@pytest.mark.parametrize("phases", [4, 2])
+def test_mfma_gemm_pingpong_bitwise_stable(M, N, K, epi, phases):
     """Race screen for the ping-pong schedule (sched 3): it accumulates in the same
     order as sched 1, so every one of repeated launches must match sched 1 bit for
     bit -- a slab read before its load landed (or overwritten before every wave
@@ -68,7 +69,7 @@ def test_mfma_gemm_pingpong_bitwise_stable(M, N, K, epi):
     w = _rand(N, K, device="cuda", scale=0.05, seed=K)
     ref = ops.mfma_gemm(x, w, epi, sched=1)
     for _ in range(12):
-        got = ops.mfma_gemm(x, w, epi, sched=3, streamk=1)
+        got = ops.mfma_gemm(x, w, epi, sched=3, streamk=1, phases=phases)
         assert torch.equal(got, ref)
 
 
@@ -77,7 +78,8 @@ def test_mfma_gemm_pingpong_bitwise_stable(M, N, K, epi):
                                    (300, 57344 // 8, 4096)])
 @pytest.mark.parametrize("epi", [0, 1])
 @pytest.mark.parametrize("streamk", [0, 2])
-def test_mfma_gemm_splitk_matches_fp32_and_is_deterministic(M, N, K, epi, streamk):
+@pytest.mark.parametrize("phases", [4, 2])
+def test_mfma_gemm_splitk_matches_fp32_and_is_deterministic(M, N, K, epi, streamk, phases):
     """Hybrid split-K of the last partial wave (persistent launch, 2-4 K pieces per
     remainder tile reduced by the last arriving block through fp32 slabs; uneven
     piece lengths at K = 512): matches the fp32 reference, and repeated launches
@@ -86,10 +88,10 @@ def test_mfma_gemm_splitk_matches_fp32_and_is_deterministic(M, N, K, epi, stream
     x = _rand(M, K, device="cuda", seed=M + 1)
     w = _rand(N, K, device="cuda", scale=0.05, seed=N + 1)
     ref = ops.mfma_gemm_ref(x, w, epi).float()
-    got = ops.mfma_gemm(x, w, epi, sched=3, streamk=streamk)
+    got = ops.mfma_gemm(x, w, epi, sched=3, streamk=streamk, phases=phases)
     torch.cuda.synchronize()
     err = (got.float() - ref).abs()
     tol = 2e-2 * ref.abs().max().item() + 1e-3
     assert err.max().item() <= tol, (err.max().item(), tol)
     for _ in range(6):
-        assert torch.equal(ops.mfma_gemm(x, w, epi, sched=3, streamk=streamk), got)
+        assert torch.equal(ops.mfma_gemm(x, w, epi, sched=3, streamk=streamk, phases=phases), got)
