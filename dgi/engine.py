@@ -43,6 +43,8 @@ class EngineConfig:
                                        # preempted sequences (0 = off, < 0 = auto-size: ``auto_host_kv_gb``)
     graph_buckets: Optional[tuple] = None   # decode batch sizes captured as hipGraphs (None = defaults)
     model_path: Optional[str] = None   # HF safetensors checkpoint dir (None: ``model`` if it is one, else random init)
+    token_align: int = -1              # round mixed-step row counts down to a multiple of this (the GEMM
+                                       # row tile; -1 = 256 on GPU engines, 0 = off): SchedulerConfig
 
 
 @dataclasses.dataclass
@@ -117,8 +119,10 @@ class LLMEngine:
         nblocks = engine_block_budget(cfg, mc, n_local, self.device)
         self.pool = BlockPool(nblocks, cfg.block_size, max(1, n_local), mc.num_kv_heads, mc.head_dim,
                               cfg.dtype, self.device)
+        align = cfg.token_align if cfg.token_align >= 0 else (256 if self.device.type == "cuda" else 0)
         self.scheduler = Scheduler(self.pool, SchedulerConfig(cfg.max_num_seqs, cfg.max_num_batched_tokens,
-                                                              cfg.max_model_len, cfg.enable_prefix_caching))
+                                                              cfg.max_model_len, cfg.enable_prefix_caching,
+                                                              token_align=align))
         self.host_tier = None
         host_gb = cfg.host_kv_gb
         if host_gb < 0:      # auto: GPU engines only (CPU rehearsals have no HBM to relieve)

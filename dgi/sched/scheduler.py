@@ -40,6 +40,14 @@ class SchedulerConfig:
     max_model_len: int = 8192
     enable_prefix_caching: bool = True
     decode_first: bool = True
+    # Tile-aligned steps: when a step mixes prefill with more than ``token_align`` rows,
+    # its row count is rounded DOWN to a multiple of ``token_align`` and the rest of
+    # the prefill waits for the next step.  The projection GEMMs cost whole 256-row
+    # tiles (an M = 1917 step pays for 2048 rows), so a closed-loop load that packs
+    # 1536 prefill + ~380 decode rows runs 7- and 8-tile steps instead of
+    # 8-tile steps with a half-empty last tile; the prefill tokens are the same,
+    # some prompts just finish their prefill one step later.
+    token_align: int = 0
 
 
 @dataclasses.dataclass
@@ -253,6 +261,9 @@ class Scheduler:
         n_seqs = len(decode)
         if not allow_prefill:
             return ScheduledBatch(decode, prefill, preempted)
+        align = self.cfg.token_align
+        if align > 0 and budget > 0:
+            budget = self._aligned_budget(len(decode), budget, align, seq_cap)
         for req in self.running:
             if budget <= 0 or n_seqs >= seq_cap:
                 break
@@ -307,6 +318,29 @@ class Scheduler:
             budget -= n
             n_seqs += 1
         return ScheduledBatch(decode, prefill, preempted)
+
+    def _aligned_budget(self, nd: int, budget: int, align: int, seq_cap: int) -> int:
+        """Prefill budget that ends the step on a multiple of ``align`` rows (see
+        SchedulerConfig.token_align); unchanged when the step would not exceed
+        one tile or the alignment would leave no prefill at all."""
+        avail, n = 0, nd
+        for req in self.running:
+            if avail >= budget:
+                break
+            if req.in_prefill and not req.busy and n < seq_cap:
+                avail += req.prefill_target - req.num_computed
+                n += 1
+        room = min(self.cfg.max_num_seqs - len(self.running), seq_cap - n)
+        for req in self.waiting:
+            if avail >= budget or room <= 0:
+                break
+            avail += req.prefill_target - req.num_computed
+            room -= 1
+        rows = nd + min(avail, budget)
+        if avail <= 0 or rows <= align:
+            return budget
+        aligned = rows // align * align
+        return aligned - nd if aligned > nd else budget
 
     # ------------------------------------------------------------------ update
     def finish(self, req: Request, reason: str) -> None:

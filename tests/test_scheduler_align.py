@@ -1,0 +1,76 @@
+"""Tile-aligned mixed steps (SchedulerConfig.token_align): with decode rows plus
+waiting prompts worth more than one tile, the step's row count is rounded down
+to a multiple of the tile and the rest of the prefill runs in a later step; no
+prefill token is dropped or duplicated, and every prompt still completes."""
+import torch
+
+from dgi.kv.block_pool import BlockPool
+from dgi.sched.request import Request, SamplingParams
+from dgi.sched.scheduler import Scheduler, SchedulerConfig
+
+
+def _sched(align):
+    pool = BlockPool(6000, 16, num_layers=1, num_kv_heads=1, head_dim=8, dtype=torch.float32, device="cpu")
+    return Scheduler(pool, SchedulerConfig(max_num_seqs=512, max_num_batched_tokens=4096, max_model_len=2048,
+                                           enable_prefix_caching=False, token_align=align))
+
+
+def _decoding(s, n, plen=16):
+    """n running sequences already past their prefill (one decode row each)."""
+    for _ in range(n):
+        r = Request(list(range(1, plen + 1)), SamplingParams(max_tokens=64))
+        r.output.append(7)
+        s.add_prefilled(r, s.pool.allocate(2))
+
+
+def _apply(s, batch):
+    for c in batch.prefill:
+        c.req.num_computed += c.length
+        if c.sample:
+            c.req.output.append(7)
+    for r in batch.decode:
+        r.num_computed += 1
+        r.output.append(7)
+
+
+def test_mixed_step_rounds_down_to_the_tile():
+    s = _sched(256)
+    _decoding(s, 381)
+    for _ in range(3):
+        s.add(Request(list(range(1, 513)), SamplingParams(max_tokens=8)))
+    b = s.schedule()
+    assert len(b.decode) == 381
+    assert b.num_tokens == 1792                     # 381 + 1536 = 1917 -> 7 tiles
+    assert sum(c.length for c in b.prefill) == 1792 - 381
+
+
+def test_deferred_prefill_completes_and_steps_stay_aligned():
+    s = _sched(256)
+    _decoding(s, 381)
+    prompts = [Request(list(range(1, 513)), SamplingParams(max_tokens=8)) for _ in range(9)]
+    for r in prompts:
+        s.add(r)
+    done = 0
+    for _ in range(12):
+        b = s.schedule()
+        if b.empty:
+            break
+        if b.prefill and b.num_tokens > 256:
+            # aligned, unless rounding down would leave no room for any prefill row
+            assert b.num_tokens % 256 == 0 or len(b.decode) >= b.num_tokens // 256 * 256
+        done += sum(c.length for c in b.prefill)
+        _apply(s, b)
+    assert done == 9 * 512
+    assert all(not r.in_prefill and r.output for r in prompts)
+
+
+def test_small_steps_and_align_off_unchanged():
+    s = _sched(256)
+    _decoding(s, 10)
+    s.add(Request(list(range(1, 101)), SamplingParams(max_tokens=8)))
+    assert s.schedule().num_tokens == 110          # one tile or less: no rounding
+    s0 = _sched(0)
+    _decoding(s0, 381)
+    for _ in range(3):
+        s0.add(Request(list(range(1, 513)), SamplingParams(max_tokens=8)))
+    assert s0.schedule().num_tokens == 1917
