@@ -174,11 +174,14 @@ class RoleCapacity:
 CAPACITY = {
     # r3: prefill at 2048 tokens / step is as fast as 4096 (19.62 vs 19.47 prompts/s) in half the
     # step (TTFT); 2-stage replicas at 768-row microbatches (the KV pool of a 40-layer stage holds
-    # ~1800 full sequences), whole-model decode GPUs at 576 rows (their pool holds ~610)
-    "llama3-70b": RoleCapacity(prefill_tok_s=19.62 * 128, decode_tok_s={1: 5692.0, 2: 12209.0, 3: 17773.0},
-                               mixed_tok_s=1760.0, prefill_step_ms=203.9, prefill_mbt=2048,
-                               decode_step_ms={1: 101.2, 2: 62.9, 3: 43.2}, decode_rows={1: 576, 2: 768, 3: 768},
-                               mixed_step_ms=207.0),
+    # ~1800 full sequences), whole-model decode GPUs at 576 rows (their pool holds ~610).
+    # Re-measured after the ping-pong MFMA GEMM + tile-aligned mixed steps
+    # (profiles/r3_gemm/pd_capacity_70b.jsonl, bench70b_token_align256.json): the mixed (DP) GPU
+    # gained 5.5 % (1760 -> 1857 tok/s), the prefill and decode roles ~1 %.
+    "llama3-70b": RoleCapacity(prefill_tok_s=19.79 * 128, decode_tok_s={1: 5723.0, 2: 12189.0, 3: 18088.0},
+                               mixed_tok_s=1857.0, prefill_step_ms=202.1, prefill_mbt=2048,
+                               decode_step_ms={1: 100.6, 2: 63.0, 3: 42.5}, decode_rows={1: 576, 2: 768, 3: 768},
+                               mixed_step_ms=189.7),
     "llama3-8b": RoleCapacity(prefill_tok_s=176.2 * 128, decode_tok_s={1: 31566.0, 2: 58028.0, 3: 69373.0},
                               mixed_tok_s=11842.0, prefill_step_ms=45.4, prefill_mbt=4096,
                               decode_step_ms={1: 32.4, 2: 18.2, 3: 11.2}, decode_rows={1: 1024, 2: 1024, 3: 768},
