@@ -40,7 +40,7 @@ class SchedulerConfig:
     max_model_len: int = 8192
     enable_prefix_caching: bool = True
     decode_first: bool = True
-    # Tile-aligned steps: when a step mixes prefill with more than ``token_align`` rows,
+    # Tile-aligned steps: when a step mixes decode rows and prefill into more than ``token_align`` rows,
     # its row count is rounded DOWN to a multiple of ``token_align`` and the rest of
     # the prefill waits for the next step.  The projection GEMMs cost whole 256-row
     # tiles (an M = 1917 step pays for 2048 rows), so a closed-loop load that packs
@@ -262,8 +262,8 @@ class Scheduler:
         if not allow_prefill:
             return ScheduledBatch(decode, prefill, preempted)
         align = self.cfg.token_align
-        if align > 0 and budget > 0:
-            budget = self._aligned_budget(len(decode), budget, align, seq_cap)
+        if align > 0 and budget > 0 and decode:     # mixed steps only: a pure prefill step
+            budget = self._aligned_budget(len(decode), budget, align, seq_cap)   # keeps its TTFT
         for req in self.running:
             if budget <= 0 or n_seqs >= seq_cap:
                 break

@@ -74,3 +74,12 @@ def test_small_steps_and_align_off_unchanged():
     for _ in range(3):
         s0.add(Request(list(range(1, 513)), SamplingParams(max_tokens=8)))
     assert s0.schedule().num_tokens == 1917
+
+
+def test_pure_prefill_steps_are_not_rounded():
+    """A prefill-only step (P/D prefill rank, idle engine) keeps every waiting token:
+    deferring part of a prompt would cost it a whole step of TTFT."""
+    s = _sched(256)
+    for _ in range(3):
+        s.add(Request(list(range(1, 301)), SamplingParams(max_tokens=8)))
+    assert s.schedule().num_tokens == 900
