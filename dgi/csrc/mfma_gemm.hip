@@ -428,8 +428,9 @@ __global__ __launch_bounds__(512) void mfma_gemm_ring_kernel(const uint16_t* __r
 // range and share their X / W slabs in L2 (a stream-K split, whose pieces start
 // at staggered K offsets, measured slower for that reason); every block then
 // owns `full` whole tiles.  Each piece stores its fp32 partial tile to its
-// block's workspace slab, publishes it (agent-scope release, then a relaxed
-// counter increment), and the last piece to arrive for a tile acquires, sums
+// block's workspace slab with write-through (sc1) stores, publishes it (every wave
+// drains its stores, then one relaxed counter increment; no release fence, which
+// would write back the whole L2), and the last piece to arrive for a tile acquires, sums
 // every slab in piece order (deterministic) and writes the bf16 tile (and
 // resets the counter for the next launch).  No block waits for another, so
 // the protocol holds for any block placement or dispatch order.
@@ -443,12 +444,17 @@ struct PPArgs {
   int rem, splits, full, P;
 };
 
+// buffer resource word 3 of a raw (stride 0, byte-addressed) buffer on gfx9, and the cache
+// policy bit of a write-through (sc1) access
+constexpr int kRsrcWord3 = 0x00020000;
+constexpr int kSc1 = 16;
+
 // The work items of one block (see "Work decomposition" above): its one tile
 // (rem == 0), its split-K piece, then its whole tiles.  run(tm, tn, kb, L)
 // accumulates K tiles kb .. kb + L - 1 of output tile (tm, tn) into the
-// caller's registers; slab_store / slab_add move them to / from a 256 x 256 fp32
-// slab (per-thread base pointer, NT threads interleaved by 16 bytes); epi stores
-// the bf16 tile.
+// caller's registers; slab_store(store16) / slab_add(load16, first) move them to /
+// from a 256 x 256 fp32 slab through store16(e, v) / load16(e) (16-byte element e of
+// this thread; NT threads interleaved by 16 bytes); epi stores the bf16 tile.
 template <int NT, class Run, class Store, class Add, class Epi>
 __device__ __forceinline__ void drive(const PPArgs& a, char* smem, Run&& run, Store&& slab_store, Add&& slab_add,
                                       Epi&& epi) {
@@ -490,12 +496,17 @@ __device__ __forceinline__ void drive(const PPArgs& a, char* smem, Run&& run, St
       // address out of the work-item loop and spills them
       int lt = tid;
       asm volatile("" : "+v"(lt));
-      slab_store(a.ws + (size_t)g * 65536 + lt * 4);
+      const int lo = lt * 16;
+      // publish: write-through (sc1) 16-byte stores drained by every wave, then one relaxed
+      // counter add — no release fence (an agent release writes back the whole L2)
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(a.ws + (size_t)g * 65536), 0, 65536 * 4, kRsrcWord3);
+      slab_store([&](int e, const f32x4& v) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, e * NT * 16 + lo, 0, kSc1);
+      });
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int old = __hip_atomic_fetch_add(a.cnt + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int last = old == a.splits - 1;
         if (last) {
@@ -510,7 +521,13 @@ __device__ __forceinline__ void drive(const PPArgs& a, char* smem, Run&& run, St
       __syncthreads();          // flag read by every wave before the next item's staging overwrites it
       if (store) {
         // every slab, own included, in piece order: the sum does not depend on which piece arrived last
-        for (int jj = 0; jj < a.splits; ++jj) slab_add(a.ws + (size_t)(jj * a.rem + t) * 65536 + lt * 4, jj == 0);
+        for (int jj = 0; jj < a.splits; ++jj) {
+          const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+              (void*)(a.ws + (size_t)(jj * a.rem + t) * 65536), 0, 65536 * 4, kRsrcWord3);
+          slab_add([&](int e) {
+            return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rl, e * NT * 16 + lo, 0, 0));
+          }, jj == 0);
+        }
       }
     }
     if (store) epi(tm, tn);
@@ -712,18 +729,18 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
   };
 
   drive<512>(a, smem, run,
-             [&](float* slab) {
+             [&](auto&& store16) {
 #pragma unroll
                for (int i = 0; i < 8; ++i)
 #pragma unroll
-                 for (int j = 0; j < 4; ++j) *(f32x4*)(slab + (i * 4 + j) * 2048) = acc[i][j];
+                 for (int j = 0; j < 4; ++j) store16(i * 4 + j, acc[i][j]);
              },
-             [&](const float* o, bool first) {
+             [&](auto&& load16, bool first) {
 #pragma unroll
                for (int i = 0; i < 8; ++i)
 #pragma unroll
                  for (int j = 0; j < 4; ++j) {
-                   const f32x4 v = *(const f32x4*)(o + (i * 4 + j) * 2048);
+                   const f32x4 v = load16(i * 4 + j);
                    acc[i][j] = first ? v : acc[i][j] + v;
                  }
              },
