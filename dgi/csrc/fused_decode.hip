@@ -66,61 +66,18 @@ struct Frag {
   u32x4 w[U][TW][2];
 };
 
-// TW: 16-row weight tiles per workgroup.  TW = 2 is the pair (c0 + r, c1 + r);
-// TW = 1 packs both halves of a pair into one tile — lanes r < 8 read rows c0 + r,
-// lanes r >= 8 rows c1 + r - 8 — and swaps the halves with a lane shuffle in the
-// epilogue: half the rows per workgroup, twice the workgroups (qkv on 8B: 384
-// instead of 192 on 256 CUs).  D: load groups in flight (register ring); the
-// first D are issued before the X staging.
-template <int NW, int U, int TW, int D, int PRO, int EPI>
-__global__ __launch_bounds__(NW * 64) void fused_skinny_kernel(FusedArgs a) {
-  // normalised X rows live in LDS for the whole kernel: [M][K + 8] bf16 (16-byte
-  // row pad keeps the 16-row fragment reads off one bank)
-  extern __shared__ __attribute__((aligned(16))) uint16_t xs[];
-  __shared__ f32x4 red[NW][TW][64];
-  __shared__ float s_part[NW][16];
-  __shared__ float s_inv[16];
+// Stage the M normalised X rows into LDS (residual add + RMSNorm per PRO): only the
+// M useful rows, spread over all threads (not 16 MFMA rows per lane).  Workgroup 0
+// writes res_out.
+template <int NW, int PRO>
+__device__ __forceinline__ void stage_x(const FusedArgs& a, uint16_t* xs, float (*s_part)[16], float* s_inv,
+                                        int bid) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int w = tid >> 6;
-  const int r = lane & 15;
-  const int g = lane >> 4;
   const int K = a.K;
   const int M = a.M;
   const int ldx = K + 8;
-  const int bid = blockIdx.x;
-  const int c0 = (bid / a.tpg) * a.gstride + (bid % a.tpg) * (TW == 2 ? 16 : 8);
-  const int c1 = c0 + a.pair_off;
-  const int ngroups = (K >> 6) / (NW * U);
-  const size_t lane_k = (size_t)g * 16 + (size_t)w * 64;
-  const bool lo = r < 8;
-  const uint16_t* w0 = a.w + (size_t)(TW == 2 ? c0 + r : (lo ? c0 + r : c1 + r - 8)) * K + lane_k;
-  const uint16_t* w1 = a.w + (size_t)(c1 + r) * K + lane_k;
-  const bool xval = r < M;
-
-  auto load = [&](Frag<U, TW>& f, int grp) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const size_t off = ((size_t)grp * NW * U + (size_t)u * NW) * 64;
-      const u32x4* p0 = reinterpret_cast<const u32x4*>(w0 + off);
-      f.w[u][0][0] = __builtin_nontemporal_load(p0);
-      f.w[u][0][1] = __builtin_nontemporal_load(p0 + 1);
-      if (TW == 2) {
-        const u32x4* p1 = reinterpret_cast<const u32x4*>(w1 + off);
-        f.w[u][TW - 1][0] = __builtin_nontemporal_load(p1);
-        f.w[u][TW - 1][1] = __builtin_nontemporal_load(p1 + 1);
-      }
-    }
-  };
-
-  // the first D groups stream while X is staged
-  Frag<U, TW> ring[D];
-#pragma unroll
-  for (int d = 0; d < D; ++d)
-    if (d < ngroups) load(ring[d], d);
-
-  // ---- stage X (residual add, norm) into LDS once per workgroup: only the
-  // M useful rows, spread over all threads (not 16 MFMA rows per lane)
   const int nchunk = K >> 3;
   for (int m = 0; m < M; ++m) {
     float ss = 0.f;
@@ -171,60 +128,13 @@ __global__ __launch_bounds__(NW * 64) void fused_skinny_kernel(FusedArgs a) {
     }
   }
   __syncthreads();
+}
 
-  const uint16_t* xl = xs + (xval ? r : 0) * ldx + lane_k;
-  f32x4 acc[TW];
-#pragma unroll
-  for (int nt = 0; nt < TW; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto compute = [&](const Frag<U, TW>& f, int grp) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int off = (grp * NW * U + u * NW) * 64;
-      u32x4 xa = u32x4{0u, 0u, 0u, 0u}, xb = u32x4{0u, 0u, 0u, 0u};
-      if (xval) {
-        xa = *reinterpret_cast<const u32x4*>(xl + off);
-        xb = *reinterpret_cast<const u32x4*>(xl + off + 8);
-      }
-#pragma unroll
-      for (int nt = 0; nt < TW; ++nt) {
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xa), as_bf16x8(f.w[u][nt][0]), acc[nt], 0, 0, 0);
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xb), as_bf16x8(f.w[u][nt][1]), acc[nt], 0, 0, 0);
-      }
-    }
-  };
-  for (int base = 0; base < ngroups; base += D) {
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      if (base + d < ngroups) {  // uniform; only the last round of a ragged ring is partial
-        compute(ring[d], base + d);
-        if (base + D + d < ngroups) load(ring[d], base + D + d);
-      }
-    }
-  }
-
-#pragma unroll
-  for (int nt = 0; nt < TW; ++nt) red[w][nt][lane] = acc[nt];
-  __syncthreads();
-  if (w != 0) return;
-  f32x4 v0 = red[0][0][lane], v1 = red[0][TW - 1][lane];
-#pragma unroll
-  for (int j = 1; j < NW; ++j) {
-    v0 += red[j][0][lane];
-    if (TW == 2) v1 += red[j][1][lane];
-  }
-  if (TW == 1) {
-    // this lane holds row c0 + r (r < 8) or c1 + r - 8; bring the other half of
-    // the pair over from lane ^ 8 (same row group g) so the epilogue below sees
-    // (v0, v1) = (row c0 + (r & 7), row c1 + (r & 7)) on every lane
-    const float bo = a.bias ? bf16_to_f32(a.bias[lo ? c0 + r : c1 + r - 8]) : 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float own = v0[i] + bo;
-      const float oth = __shfl_xor(own, 8);
-      v0[i] = lo ? own : oth;
-      v1[i] = lo ? oth : own;
-    }
-  }
+// Epilogue of one column pair on wave 0: (v0, v1) = rows (c0 + rr, c1 + rr) for the M
+// rows of lane group g; EPI 0 store, 1 SwiGLU, 2 RoPE + paged KV write.
+template <int TW, int EPI>
+__device__ __forceinline__ void store_pair(const FusedArgs& a, int c0, int c1, int r, int g, bool lo,
+                                           const f32x4& v0, const f32x4& v1) {
   const int rr = TW == 2 ? r : (r & 7);
   const float b0 = (TW == 2 && a.bias) ? bf16_to_f32(a.bias[c0 + r]) : 0.f;
   const float b1 = (TW == 2 && a.bias) ? bf16_to_f32(a.bias[c1 + r]) : 0.f;
@@ -282,6 +192,219 @@ __global__ __launch_bounds__(NW * 64) void fused_skinny_kernel(FusedArgs a) {
   }
 }
 
+// TW: 16-row weight tiles per workgroup.  TW = 2 is the pair (c0 + r, c1 + r);
+// TW = 1 packs both halves of a pair into one tile — lanes r < 8 read rows c0 + r,
+// lanes r >= 8 rows c1 + r - 8 — and swaps the halves with a lane shuffle in the
+// epilogue: half the rows per workgroup, twice the workgroups (qkv on 8B: 384
+// instead of 192 on 256 CUs).  D: load groups in flight (register ring); the
+// first D are issued before the X staging.
+template <int NW, int U, int TW, int D, int PRO, int EPI>
+__global__ __launch_bounds__(NW * 64) void fused_skinny_kernel(FusedArgs a) {
+  // normalised X rows live in LDS for the whole kernel: [M][K + 8] bf16 (16-byte
+  // row pad keeps the 16-row fragment reads off one bank)
+  extern __shared__ __attribute__((aligned(16))) uint16_t xs[];
+  __shared__ f32x4 red[NW][TW][64];
+  __shared__ float s_part[NW][16];
+  __shared__ float s_inv[16];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int r = lane & 15;
+  const int g = lane >> 4;
+  const int K = a.K;
+  const int M = a.M;
+  const int ldx = K + 8;
+  const int bid = blockIdx.x;
+  const int c0 = (bid / a.tpg) * a.gstride + (bid % a.tpg) * (TW == 2 ? 16 : 8);
+  const int c1 = c0 + a.pair_off;
+  const int ngroups = (K >> 6) / (NW * U);
+  const size_t lane_k = (size_t)g * 16 + (size_t)w * 64;
+  const bool lo = r < 8;
+  const uint16_t* w0 = a.w + (size_t)(TW == 2 ? c0 + r : (lo ? c0 + r : c1 + r - 8)) * K + lane_k;
+  const uint16_t* w1 = a.w + (size_t)(c1 + r) * K + lane_k;
+  const bool xval = r < M;
+
+  auto load = [&](Frag<U, TW>& f, int grp) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t off = ((size_t)grp * NW * U + (size_t)u * NW) * 64;
+      const u32x4* p0 = reinterpret_cast<const u32x4*>(w0 + off);
+      f.w[u][0][0] = __builtin_nontemporal_load(p0);
+      f.w[u][0][1] = __builtin_nontemporal_load(p0 + 1);
+      if (TW == 2) {
+        const u32x4* p1 = reinterpret_cast<const u32x4*>(w1 + off);
+        f.w[u][TW - 1][0] = __builtin_nontemporal_load(p1);
+        f.w[u][TW - 1][1] = __builtin_nontemporal_load(p1 + 1);
+      }
+    }
+  };
+
+  // the first D groups stream while X is staged
+  Frag<U, TW> ring[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (d < ngroups) load(ring[d], d);
+
+  stage_x<NW, PRO>(a, xs, s_part, s_inv, bid);
+
+  const uint16_t* xl = xs + (xval ? r : 0) * ldx + lane_k;
+  f32x4 acc[TW];
+#pragma unroll
+  for (int nt = 0; nt < TW; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](const Frag<U, TW>& f, int grp) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int off = (grp * NW * U + u * NW) * 64;
+      u32x4 xa = u32x4{0u, 0u, 0u, 0u}, xb = u32x4{0u, 0u, 0u, 0u};
+      if (xval) {
+        xa = *reinterpret_cast<const u32x4*>(xl + off);
+        xb = *reinterpret_cast<const u32x4*>(xl + off + 8);
+      }
+#pragma unroll
+      for (int nt = 0; nt < TW; ++nt) {
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xa), as_bf16x8(f.w[u][nt][0]), acc[nt], 0, 0, 0);
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xb), as_bf16x8(f.w[u][nt][1]), acc[nt], 0, 0, 0);
+      }
+    }
+  };
+  for (int base = 0; base < ngroups; base += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      if (base + d < ngroups) {  // uniform; only the last round of a ragged ring is partial
+        compute(ring[d], base + d);
+        if (base + D + d < ngroups) load(ring[d], base + D + d);
+      }
+    }
+  }
+
+#pragma unroll
+  for (int nt = 0; nt < TW; ++nt) red[w][nt][lane] = acc[nt];
+  __syncthreads();
+  if (w != 0) return;
+  f32x4 v0 = red[0][0][lane], v1 = red[0][TW - 1][lane];
+#pragma unroll
+  for (int j = 1; j < NW; ++j) {
+    v0 += red[j][0][lane];
+    if (TW == 2) v1 += red[j][1][lane];
+  }
+  if (TW == 1) {
+    // this lane holds row c0 + r (r < 8) or c1 + r - 8; bring the other half of
+    // the pair over from lane ^ 8 (same row group g) so the epilogue below sees
+    // (v0, v1) = (row c0 + (r & 7), row c1 + (r & 7)) on every lane
+    const float bo = a.bias ? bf16_to_f32(a.bias[lo ? c0 + r : c1 + r - 8]) : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float own = v0[i] + bo;
+      const float oth = __shfl_xor(own, 8);
+      v0[i] = lo ? own : oth;
+      v1[i] = lo ? oth : own;
+    }
+  }
+  store_pair<TW, EPI>(a, c0, c1, r, g, lo, v0, v1);
+}
+
+// Persistent variant (TW = 1): a workgroup owns `tpw` consecutive pair tiles and
+// streams their weights as ONE register ring — the next tile's first groups are in
+// flight while the current tile's last groups are consumed and its epilogue runs —
+// and stages X once per workgroup instead of once per tile.  With one workgroup per
+// CU (8B gate_up: 1792 tiles = 7 per CU) every CU reads one unbroken weight stream
+// instead of a launch's worth of short per-tile ramps and drains.  The cross-wave sum
+// uses two LDS buffers by tile parity, so one barrier per tile suffices.
+template <int NW, int U, int D, int PRO, int EPI>
+__global__ __launch_bounds__(NW * 64) void fused_skinny_persist_kernel(FusedArgs a, int tpw, int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t xs[];
+  __shared__ f32x4 red[2][NW][64];
+  __shared__ float s_part[NW][16];
+  __shared__ float s_inv[16];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int r = lane & 15;
+  const int g = lane >> 4;
+  const int K = a.K;
+  const int M = a.M;
+  const int ldx = K + 8;
+  const int bid = blockIdx.x;
+  const int t_first = bid * tpw;
+  const int nt_local = min(tpw, ntiles - t_first);   // >= 1: the host sizes the grid
+  const int ngroups = (K >> 6) / (NW * U);
+  const int total = nt_local * ngroups;
+  const size_t lane_k = (size_t)g * 16 + (size_t)w * 64;
+  const bool lo = r < 8;
+  const bool xval = r < M;
+  auto tile_c0 = [&](int ti) { return (ti / a.tpg) * a.gstride + (ti % a.tpg) * 8; };
+
+  // flattened group s of this workgroup: tile t_first + s / ngroups, K group s % ngroups
+  auto load = [&](Frag<U, 1>& f, int s) {
+    const int tl = s / ngroups;
+    const int grp = s - tl * ngroups;
+    const int c0 = tile_c0(t_first + tl);
+    const uint16_t* w0 = a.w + (size_t)(lo ? c0 + r : c0 + a.pair_off + r - 8) * K + lane_k;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t off = ((size_t)grp * NW * U + (size_t)u * NW) * 64;
+      const u32x4* p0 = reinterpret_cast<const u32x4*>(w0 + off);
+      f.w[u][0][0] = __builtin_nontemporal_load(p0);
+      f.w[u][0][1] = __builtin_nontemporal_load(p0 + 1);
+    }
+  };
+  Frag<U, 1> ring[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (d < total) load(ring[d], d);
+
+  stage_x<NW, PRO>(a, xs, s_part, s_inv, bid);
+
+  const uint16_t* xl = xs + (xval ? r : 0) * ldx + lane_k;
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  int parity = 0;
+  for (int base = 0; base < total; base += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int s = base + d;
+      if (s < total) {          // uniform
+        const int tl = s / ngroups;
+        const int grp = s - tl * ngroups;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int off = (grp * NW * U + u * NW) * 64;
+          u32x4 xa = u32x4{0u, 0u, 0u, 0u}, xb = u32x4{0u, 0u, 0u, 0u};
+          if (xval) {
+            xa = *reinterpret_cast<const u32x4*>(xl + off);
+            xb = *reinterpret_cast<const u32x4*>(xl + off + 8);
+          }
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xa), as_bf16x8(ring[d].w[u][0][0]), acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xb), as_bf16x8(ring[d].w[u][0][1]), acc, 0, 0, 0);
+        }
+        if (s + D < total) load(ring[d], s + D);
+        if (grp == ngroups - 1) {     // tile done: cross-wave sum, epilogue on wave 0
+          red[parity][w][lane] = acc;
+          __syncthreads();
+          if (w == 0) {
+            const int c0 = tile_c0(t_first + tl);
+            const int c1 = c0 + a.pair_off;
+            f32x4 v = red[parity][0][lane];
+#pragma unroll
+            for (int j = 1; j < NW; ++j) v += red[parity][j][lane];
+            const float bo = a.bias ? bf16_to_f32(a.bias[lo ? c0 + r : c1 + r - 8]) : 0.f;
+            f32x4 v0, v1;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float own = v[i] + bo;
+              const float oth = __shfl_xor(own, 8);
+              v0[i] = lo ? own : oth;
+              v1[i] = lo ? oth : own;
+            }
+            store_pair<1, EPI>(a, c0, c1, r, g, lo, v0, v1);
+          }
+          acc = f32x4{0.f, 0.f, 0.f, 0.f};
+          parity ^= 1;
+        }
+      }
+    }
+  }
+}
+
 template <int NW, int U, int TW, int D, int PRO, int EPI>
 int launch_cfg(FusedArgs a, int N, int ntiles, hipStream_t s) {
   if ((a.K / 64) % (NW * U)) return -7;
@@ -307,7 +430,37 @@ int launch_cfg(FusedArgs a, int N, int ntiles, hipStream_t s) {
   return 0;
 }
 
-// cfg: (waves per workgroup, K-steps per load group, tiles per workgroup, groups in flight)
+template <int NW, int U, int D, int PRO, int EPI>
+int launch_persist(FusedArgs a, int ntiles, hipStream_t s) {
+  if ((a.K / 64) % (NW * U)) return -7;
+  const size_t lds = (size_t)a.M * (a.K + 8) * 2;
+  const size_t lds_static = (size_t)2 * NW * 64 * 16 + (size_t)NW * 16 * 4 + 16 * 4;
+  if (lds + lds_static > 160 * 1024) return -6;
+  // TW = 1 pair geometry (as launch_cfg)
+  if (EPI == 0) {
+    a.gstride = 16;
+    a.pair_off = 8;
+  } else if (EPI == 1) {
+    a.gstride = 8;
+  } else {
+    a.tpg = 8;
+  }
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  const int tpw = (ntiles + cus - 1) / cus;
+  const int nblocks = (ntiles + tpw - 1) / tpw;
+  fused_skinny_persist_kernel<NW, U, D, PRO, EPI><<<dim3(nblocks), NW * 64, lds, s>>>(a, tpw, ntiles);
+  DGI_CHECK_LAUNCH();
+  return 0;
+}
+
+// cfg: (waves per workgroup, K-steps per load group, tiles per workgroup, groups in flight);
+// 12-16: persistent (waves, K-steps per group, groups in flight) with TW = 1
 template <int PRO, int EPI>
 int launch(const FusedArgs& a, int N, int ntiles, int cfg, hipStream_t s) {
   switch (cfg) {
@@ -322,6 +475,12 @@ int launch(const FusedArgs& a, int N, int ntiles, int cfg, hipStream_t s) {
     case 9: return launch_cfg<4, 2, 2, 4, PRO, EPI>(a, N, ntiles, s);
     case 10: return launch_cfg<8, 2, 1, 2, PRO, EPI>(a, N, ntiles, s);
     case 11: return launch_cfg<4, 1, 1, 8, PRO, EPI>(a, N, ntiles, s);
+    // persistent one-ring workgroups (TW = 1 pair tiles, ntiles of them)
+    case 12: return launch_persist<8, 1, 8, PRO, EPI>(a, ntiles, s);
+    case 13: return launch_persist<8, 2, 4, PRO, EPI>(a, ntiles, s);
+    case 14: return launch_persist<4, 2, 8, PRO, EPI>(a, ntiles, s);
+    case 15: return launch_persist<8, 2, 6, PRO, EPI>(a, ntiles, s);
+    case 16: return launch_persist<16, 1, 4, PRO, EPI>(a, ntiles, s);
     default: return -5;
   }
 }

@@ -19,6 +19,7 @@ re-normalises it, which is bit-identical to the fused add it replaces.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 from typing import Optional
@@ -40,6 +41,8 @@ TRIM_LAST_LAYER = os.environ.get("DGI_TRIM_LAST_LAYER", "1") != "0"
 # (1755 / 1743 vs 1761 / 1750 tok/s, profiles/r2_bench70b_qkvpad_ab.md)
 QKV_PAD = os.environ.get("DGI_QKV_PAD", "0") == "1"
 OPROJ_PAD = os.environ.get("DGI_OPROJ_PAD", "0") == "1"
+# mixed steps: decode-row attention on a side stream beside the prefill-row attention
+ATTN_OVERLAP = os.environ.get("DGI_ATTN_OVERLAP", "1") == "1"
 
 class LlamaLayerWeights:
     __slots__ = ("in_norm", "qkv", "o", "post_norm", "gate_up", "down", "qkv_bias")
@@ -86,6 +89,7 @@ class LlamaModel:
         self.mlp_pad = None
         self.mlp_impl = None     # rows -> (gate_up on the MFMA SwiGLU kernel, down on the MFMA kernel)
         self.proj_impl = None    # rows -> (QKV on the MFMA kernel, o-proj on the MFMA kernel)
+        self._attn_stream = None
         # called with the global layer id once that layer's KV is in the cache
         # (P/D layer-streamed migration sends finished layers while later ones compute)
         self.layer_hook = None
@@ -230,14 +234,27 @@ class LlamaModel:
         if out is None:
             out = torch.empty(T, c.q_size, device=qkv.device, dtype=qkv.dtype)
         nd = meta.num_decode
+        # mixed step: the decode rows' split-KV attention (HBM-latency bound) runs on a side
+        # stream beside the prefill rows' flash attention; joined before the o-proj
+        side = None
+        if ATTN_OVERLAP and nd > 0 and meta.num_prefill_tokens > 0 and qkv.is_cuda \
+                and not torch.cuda.is_current_stream_capturing():
+            side = self._attn_stream
+            if side is None or side.device != qkv.device:
+                side = self._attn_stream = torch.cuda.Stream(device=qkv.device)
+            main = torch.cuda.current_stream()
+            side.wait_stream(main)
         if nd > 0:
-            ops.paged_decode(qkv[:nd], kc, vc, meta.dec_block_tables, meta.dec_context_lens, c.num_heads,
-                             c.num_kv_heads, self.scale, meta.dec_max_splits, meta.dec_part_size,
-                             out=out[:nd], workspace=meta.dec_workspace)
+            with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                ops.paged_decode(qkv[:nd], kc, vc, meta.dec_block_tables, meta.dec_context_lens, c.num_heads,
+                                 c.num_kv_heads, self.scale, meta.dec_max_splits, meta.dec_part_size,
+                                 out=out[:nd], workspace=meta.dec_workspace)
         if meta.num_prefill_tokens > 0:
             ops.paged_prefill(qkv[nd:], kc, vc, meta.pre_block_tables, meta.pre_cu_seqlens, meta.pre_context_lens,
                               c.num_heads, c.num_kv_heads, self.scale, tiles=meta.pre_tiles,
                               tree_mask=meta.tree_mask, tree_n=meta.tree_n, out=out[nd:])
+        if side is not None:
+            main.wait_stream(side)
         return out
 
     def _mlp_rows(self, T: int, like: torch.Tensor) -> int:

@@ -403,18 +403,21 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
 
 # Fused decode GEMM (fused_decode.hip): RMSNorm prologue + SwiGLU / RoPE+KV epilogue.
 # Where it pays (profiles/r2_decode8b_fused.md, hipGraph-timed, weights cold):
-# the qkv projection at M <= 8 (15 vs 18 us at M = 1 on 8B) and gate_up at M <= 2;
-# above that the per-workgroup X staging outweighs the saved launches and the
-# unfused chain wins.  K <= 4096 (8B-class) like _use_skinny.
+# the qkv projection at M <= 8 (15 vs 18 us at M = 1 on 8B); gate_up on the persistent
+# one-ring workgroups (cfg 12-16: X staged once per CU, one weight stream per CU) at every
+# M <= 16 (55.5 vs 62.4 us unfused at M = 16, profiles/r3_decode/persistent_gemv.md).
+# K <= 4096 (8B-class) like _use_skinny.
 # DGI_FUSED_DECODE=0 disables, =force uses it for every M <= 16 and K.
 FUSED_DECODE = os.environ.get("DGI_FUSED_DECODE", "1")
-FUSED_MAX_M = {"qkv": 8, "gate_up": 4}
+FUSED_MAX_M = {"qkv": 8, "gate_up": 16}
 # launch config per projection and row count (fused_decode.hip cfg = waves, K-steps per load
 # group, tiles per workgroup, load ring depth: 6 = 8x1 one-tile ring 4, 7 = 8x1 two-tile ring 4,
-# 8 = 4x2 one-tile ring 4, 10 = 8x2 one-tile, 11 = 4x1 one-tile ring 8).  Fastest per M on the
-# 8B shapes, weights cold, hipGraph-timed (profiles/r3_decode_gemm/README.md): qkv 16.6 -> 15.0 us
-# and gate_up + SwiGLU 48.6 -> 43.8 us at M = 1 against round 2's fixed configs 4 / 5.
-FUSED_M_CFG = {"qkv": ((2, 10), (16, 7)), "gate_up": ((1, 6), (2, 8), (16, 11))}
+# 8 = 4x2 one-tile ring 4, 10 = 8x2 one-tile, 11 = 4x1 one-tile ring 8; persistent one-ring
+# workgroups 12 = 8x1 ring 8, 16 = 16x1 ring 4).  Fastest per M on the 8B shapes, weights cold,
+# hipGraph-timed (profiles/r3_decode_gemm/README.md, profiles/r3_decode/persistent_gemv.md): qkv
+# 16.6 -> 15.0 us at M = 1 against round 2's fixed config 4; gate_up + SwiGLU 48.6 -> 43.0 us at
+# M = 1, 56.2 -> 45.5 at M = 4, 66.1 -> 48.2 at M = 8 (cfg 16; 16 waves do not fit M = 16's LDS).
+FUSED_M_CFG = {"qkv": ((2, 10), (16, 7)), "gate_up": ((8, 16), (16, 12))}
 FUSED_KIND_CFG = {"qkv": int(os.environ.get("DGI_FUSED_QKV_CFG", "-1")),
                   "gate_up": int(os.environ.get("DGI_FUSED_GU_CFG", "-1"))}
 

@@ -450,18 +450,31 @@ def test_fused_skinny_matches_reference(pro, epi, M):
 @pytest.mark.parametrize("pro,epi", [(0, 0), (2, 0), (2, 1), (1, 2), (2, 2)])
 def test_fused_skinny_every_launch_config(pro, epi):
     """Every fused_decode.hip launch config (waves, K-steps per group, one- or
-    two-tile workgroups, load ring depth) against the reference, at M = 1 and 3."""
-    for cfg in range(12):
+    two-tile workgroups, load ring depth, persistent one-ring workgroups) against
+    the reference, at M = 1 and 3."""
+    for cfg in range(17):
         for M in (1, 3):
             _fused_skinny_case(pro, epi, M, cfg)
 
 
-def _fused_skinny_case(pro, epi, M, cfg):
+@pytest.mark.parametrize("pro,epi,R", [(2, 1, 2 * 14336), (2, 0, 8192), (0, 0, 8224), (2, 2, None)])
+def test_fused_skinny_persistent_multi_tile(pro, epi, R):
+    """Persistent configs at sizes where each workgroup streams several tiles through
+    one ring (8B gate_up: 7 tiles per workgroup; 8192 rows: 2; 8224: 3 with a 1-tile
+    last workgroup; qkv: 2), including the tile-parity double-buffered reduce."""
+    for cfg in (12, 13, 14, 15, 16):
+        for M in (1, 4):
+            _fused_skinny_case(pro, epi, M, cfg, R)
+
+
+def _fused_skinny_case(pro, epi, M, cfg, R=None):
     torch.manual_seed(M * 10 + pro * 3 + epi)
     K = 4096
     nh, nkv, bs, nb = 32, 8, 16, 64
     if epi == 2:
         R = (nh + 2 * nkv) * 128
+    elif R is not None:
+        pass
     elif epi == 1:
         R = 2 * 1024
     else:
