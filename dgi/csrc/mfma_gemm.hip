@@ -57,35 +57,54 @@ __device__ __forceinline__ void glds16(const uint16_t* src, char* lds) {
 __device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
 
 // Lane holds rows m0 + 128 wm + 16 i + (lane & 15), columns 4 (lane >> 4) + 0..3 of each 16x16 tile.
+// Two neighbouring tiles (A, B) are stored as ONE 16-byte store per lane: v_permlane16_swap
+// trades A's columns of the odd 16-lane rows for B's columns of the even rows, so lane group
+// g ends up with 8 consecutive columns — A 0-7 (g 0), B 0-7 (g 1), A 8-15 (g 2), B 8-15 (g 3) —
+// and every row of a store instruction writes 64 contiguous bytes (half the store
+// instructions of 8-byte stores; the store tail of a tile's epilogue is issue-bound).
+__device__ __forceinline__ void store_pair16(uint16_t* yrow, int n0, int g, const float (&a)[4], const float (&b)[4]) {
+  const uint32_t a01 = pack_bf16x2(a[0], a[1]), a23 = pack_bf16x2(a[2], a[3]);
+  const uint32_t b01 = pack_bf16x2(b[0], b[1]), b23 = pack_bf16x2(b[2], b[3]);
+  const auto s0 = __builtin_amdgcn_permlane16_swap(a01, b01, false, false);
+  const auto s1 = __builtin_amdgcn_permlane16_swap(a23, b23, false, false);
+  uint4 v;
+  v.x = s0[0];
+  v.y = s1[0];
+  v.z = s0[1];
+  v.w = s1[1];
+  *(uint4*)(yrow + n0 + 16 * (g & 1) + 4 * (g & 2)) = v;
+}
+
 template <int EPI>
 __device__ __forceinline__ void epilogue(const f32x4 (&acc)[8][4], uint16_t* __restrict__ Y, int ldy, int M, int m0,
                                          int tn, int wm, int wn, int lane) {
   const int r16 = lane & 15;
-  const int c4 = (lane >> 4) * 4;
+  const int g = lane >> 4;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int m = m0 + wm * 128 + i * 16 + r16;
+    // the swap partners (lanes l, l ^ 16) hold the same row, so a row past M drops both together
     if (m >= M) continue;
     uint16_t* yrow = Y + (size_t)m * ldy;
     if (EPI == 1) {
+      float o[2][4];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const f32x4 g = acc[i][j], u = acc[i][j + 2];
-        const int n = tn * 128 + wn * 32 + j * 16 + c4;
-        uint2 v;
-        v.x = pack_bf16x2(silu(g[0]) * u[0], silu(g[1]) * u[1]);
-        v.y = pack_bf16x2(silu(g[2]) * u[2], silu(g[3]) * u[3]);
-        *(uint2*)(yrow + n) = v;
+        const f32x4 gt = acc[i][j], u = acc[i][j + 2];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[j][e] = silu(gt[e]) * u[e];
       }
+      store_pair16(yrow, tn * 128 + wn * 32, g, o[0], o[1]);
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const f32x4 a = acc[i][j];
-        const int n = tn * 256 + wn * 64 + j * 16 + c4;
-        uint2 v;
-        v.x = pack_bf16x2(a[0], a[1]);
-        v.y = pack_bf16x2(a[2], a[3]);
-        *(uint2*)(yrow + n) = v;
+      for (int j = 0; j < 4; j += 2) {
+        float x0[4], x1[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          x0[e] = acc[i][j][e];
+          x1[e] = acc[i][j + 1][e];
+        }
+        store_pair16(yrow, tn * 256 + wn * 64 + j * 16, g, x0, x1);
       }
     }
   }
