@@ -460,7 +460,8 @@ struct PPArgs {
   float* ws;     // one 256 x 256 fp32 slab per block (hybrid launches)
   int* cnt;      // one arrival counter per split tile, zero between launches
   int ldx, ldy, M, I, K, tiles_m, tiles_total;
-  int rem, splits, full, P;
+  int rem, splits, full, P;   // P == 0: one tile per block (grid = tiles)
+  int ovl;                    // issue the next tile's prologue before the current epilogue
 };
 
 // buffer resource word 3 of a raw (stride 0, byte-addressed) buffer on gfx9, and the cache
@@ -469,14 +470,17 @@ constexpr int kRsrcWord3 = 0x00020000;
 constexpr int kSc1 = 16;
 
 // The work items of one block (see "Work decomposition" above): its one tile
-// (rem == 0), its split-K piece, then its whole tiles.  run(tm, tn, kb, L)
-// accumulates K tiles kb .. kb + L - 1 of output tile (tm, tn) into the
-// caller's registers; slab_store(store16) / slab_add(load16, first) move them to /
+// (P == 0), its split-K piece, then its whole tiles.  prologue(tm, tn, kb) issues the
+// staging loads of output tile (tm, tn) from K tile kb on, body(tm, tn, kb, L, ov) accumulates
+// L K tiles into the caller's registers; slab_store(store16) / slab_add(load16, first) move them to /
 // from a 256 x 256 fp32 slab through store16(e, v) / load16(e) (16-byte element e of
-// this thread; NT threads interleaved by 16 bytes); epi stores the bf16 tile.
-template <int NT, class Run, class Store, class Add, class Epi>
-__device__ __forceinline__ void drive(const PPArgs& a, char* smem, Run&& run, Store&& slab_store, Add&& slab_add,
-                                      Epi&& epi) {
+// this thread; NT threads interleaved by 16 bytes); epi stores the bf16 tile.  With a.ovl,
+// the next whole tile's prologue is issued before the current whole tile's epilogue
+// (which does not touch LDS: the body ends with every LDS read retired), so its first
+// K tiles load while the stores drain.
+template <int NT, class Pro, class Body, class Store, class Add, class Epi>
+__device__ __forceinline__ void drive(const PPArgs& a, char* smem, Pro&& prologue, Body&& body, Store&& slab_store,
+                                      Add&& slab_add, Epi&& epi) {
   const int tid = threadIdx.x;
   const int nt = a.K / kBK;
   const int nt2 = nt >> 1;                    // 128-deep units per tile
@@ -484,33 +488,42 @@ __device__ __forceinline__ void drive(const PPArgs& a, char* smem, Run&& run, St
   const int g = (blockIdx.x & 7) * (a.P >> 3) + (blockIdx.x >> 3);
   bool split = a.rem && g < a.rem * a.splits;
   int k = 0;
-  for (;;) {
-    int t, kb = 0, L = nt;
-    bool piece = false;
-    if (a.rem == 0) {
-      if (k++) break;
+  // next work item: tile t, K tiles kb .. kb + L - 1; t < 0 when the block is done
+  struct Item {
+    int t, kb, L;
+    bool piece;
+  };
+  auto next = [&]() -> Item {
+    if (a.P == 0) {
+      if (k++) return Item{-1, 0, 0, false};
       const int b = blockIdx.x, T = a.tiles_total;
       const int xcd = b & 7, li = b >> 3;
       const int q8 = T >> 3, r8 = T & 7;
-      t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + li;
-    } else if (split) {
+      return Item{(xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + li, 0, nt, false};
+    }
+    if (split) {
       split = false;
       const int j = g / a.rem;
-      t = g - j * a.rem;
       const int u0 = j * nt2 / a.splits, u1 = (j + 1) * nt2 / a.splits;
-      kb = 2 * u0;
-      L = 2 * (u1 - u0);
-      piece = true;
-    } else if (k < a.full) {
-      t = a.rem + k * a.P + g;
-      ++k;
-    } else {
-      break;
+      return Item{g - j * a.rem, 2 * u0, 2 * (u1 - u0), true};
     }
-    const int tm = t % a.tiles_m, tn = t / a.tiles_m;
-    run(tm, tn, kb, L);
+    if (k < a.full) return Item{a.rem + (k++) * a.P + g, 0, nt, false};
+    return Item{-1, 0, 0, false};
+  };
+  Item cur = next();
+  if (cur.t < 0) return;
+  prologue(cur.t % a.tiles_m, cur.t / a.tiles_m, cur.kb);
+  bool ov = false;
+  for (;;) {
+    const int tm = cur.t % a.tiles_m, tn = cur.t / a.tiles_m;
+    body(tm, tn, cur.kb, cur.L, ov);
+    const Item nx = next();
+    // overlap only between whole tiles whose epilogue stores every row (fixed store count)
+    ov = a.ovl && nx.t >= 0 && !cur.piece && !nx.piece && (tm + 1) * kBM <= a.M;
+    if (ov) prologue(nx.t % a.tiles_m, nx.t / a.tiles_m, nx.kb);
     bool store = true;
-    if (piece) {
+    if (cur.piece) {
+      const int t = cur.t;
       // slab offsets from a laundered thread id: otherwise hipcc hoists every per-lane
       // address out of the work-item loop and spills them
       int lt = tid;
@@ -547,9 +560,15 @@ __device__ __forceinline__ void drive(const PPArgs& a, char* smem, Run&& run, St
             return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rl, e * NT * 16 + lo, 0, 0));
           }, jj == 0);
         }
+        // a real s_waitcnt (not inline asm) so that the waitcnt pass knows the accumulators are
+        // written: otherwise it merges this path's pending loads into the epilogue as vmcnt(0)
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
       }
     }
     if (store) epi(tm, tn);
+    if (nx.t < 0) break;
+    if (!ov) prologue(nx.t % a.tiles_m, nx.t / a.tiles_m, nx.kb);
+    cur = nx;
   }
 }
 
@@ -571,8 +590,6 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
   const int wm = w >> 2, wn = w & 3;
   const int M = a.M, K = a.K, ldx = a.ldx;
 
-  const int q = tid >> 3;
-  const int lc = (tid & 7) ^ ((tid >> 4) & 7);
   char* const lds_x = smem + w * 1024;
   char* const lds_w = smem + kTileBytes + w * 1024;
   const int r16 = lane & 15;
@@ -623,14 +640,28 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  // acc = X[tile rows] . W[tile cols]^T over K tiles kb .. kb + L - 1 (L even, >= 2)
-  auto run = [&](int tm, int tn, int kb, int L) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // staging sources of the current work item (set by prologue)
+  const uint16_t* xs[4];
+  const uint16_t* wsrc = a.W;
+  size_t wslab = 0;
+  // slab i (rows 64 i .. 64 i + 63) of local K tile kt into LDS stage st
+  auto gx = [&](int kt, int i, int st) { glds16(xs[i] + kt * kBK, lds_x + st * kStageBytes + i * 8192); };
+  auto gw = [&](int kt, int i, int st) { glds16(wsrc + i * wslab + kt * kBK, lds_w + st * kStageBytes + i * 8192); };
+
+  // the staging loads that precede K tile 0 of output tile (tm, tn), K tiles from kb on
+  // (PH == 2: 9 loads, PH == 4: 12; the body retires the oldest 6 before its first read)
+  // per-lane terms of the prologue and epilogue from a laundered thread id: hipcc would otherwise
+  // keep them live across the K loop and spill them, and the reload's vmcnt(0) would drain the
+  // next tile's staging loads before the epilogue
+  auto fresh_tid = [&]() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+  };
+  auto set_src = [&](int tm, int tn, int kb) {
     const int m0 = tm * kBM;
-    const uint16_t* xs[4];
+    const int tq = fresh_tid();
+    const int q = tq >> 3, lc = (tq & 7) ^ ((tq >> 4) & 7);
 #pragma unroll
     for (int i = 0; i < 4; ++i) xs[i] = a.X + (size_t)min(m0 + q + i * 64, M - 1) * ldx + lc * 8 + kb * kBK;
     int wrow0, wstep;
@@ -641,11 +672,33 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
       wrow0 = tn * 256 + q;
       wstep = 64;
     }
-    const uint16_t* const wsrc = a.W + (size_t)wrow0 * K + lc * 8 + kb * kBK;
-    const size_t wslab = (size_t)wstep * K;
-    // slab i (rows 64 i .. 64 i + 63) of local K tile kt into LDS stage st
-    auto gx = [&](int kt, int i, int st) { glds16(xs[i] + kt * kBK, lds_x + st * kStageBytes + i * 8192); };
-    auto gw = [&](int kt, int i, int st) { glds16(wsrc + i * wslab + kt * kBK, lds_w + st * kStageBytes + i * 8192); };
+    wsrc = a.W + (size_t)wrow0 * K + lc * 8 + kb * kBK;
+    wslab = (size_t)wstep * K;
+  };
+  auto prologue = [&](int tm, int tn, int kb) {
+    set_src(tm, tn, kb);
+    if constexpr (PH == 2) {
+      gx(0, 0, 0); gw(0, 0, 0); gw(0, 1, 0); gw(0, 2, 0); gw(0, 3, 0); gx(0, 2, 0);
+      gx(0, 3, 0); gx(0, 1, 0); gx(1, 0, 1);
+    } else {
+      gx(0, 0, 0); gx(0, 2, 0); gw(0, 0, 0); gw(0, 1, 0); gw(0, 2, 0); gw(0, 3, 0);
+      gx(0, 3, 0); gx(1, 0, 1); gx(0, 1, 0); gx(1, 2, 1); gw(1, 0, 1); gw(1, 1, 1);
+    }
+  };
+
+  // acc = X[tile rows] . W[tile cols]^T over K tiles kb .. kb + L - 1 (L even, >= 4) after
+  // prologue(tm, tn, kb); the sources are recomputed here so that they are not live across an
+  // overlapped epilogue (whose register pressure otherwise makes hipcc reuse store-data
+  // registers, each reuse a vmcnt(0)).
+  // ov: the previous tile's epilogue (8 16-byte stores per thread for EPI 1, 16 for EPI 0; all its rows inside M) was
+  // issued between the prologue and this call, so the first wait counts those stores too
+  // (vector memory operations retire in issue order)
+  auto body = [&](int tm, int tn, int kb, int L, bool ov) {
+    set_src(tm, tn, kb);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     // one K tile; ST = its LDS stage, MODE 0: t + 2 < L, 1: t + 2 == L, 2: t + 1 == L
     auto tile = [&](int t, auto ST_, auto MODE_) {
@@ -716,10 +769,9 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
     using O = std::integral_constant<int, 1>;
     using T2 = std::integral_constant<int, 2>;
     if constexpr (PH == 2) {
-      // prologue: everything the steady state would have issued before tile 0
-      gx(0, 0, 0); gw(0, 0, 0); gw(0, 1, 0); gw(0, 2, 0); gw(0, 3, 0); gx(0, 2, 0);
-      gx(0, 3, 0); gx(0, 1, 0); gx(1, 0, 1);
-      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      if (!ov) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else if constexpr (EPI == 1) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(19)" ::: "memory");
       barrier();
       if (wm == 1) barrier();     // stagger: waves 4-7 run one section behind
       int t = 0;
@@ -730,10 +782,9 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
       tile2(t, Z{}, O{});
       tile2(t + 1, O{}, T2{});
     } else {
-      // prologue: everything the steady state would have issued before tile 0
-      gx(0, 0, 0); gx(0, 2, 0); gw(0, 0, 0); gw(0, 1, 0); gw(0, 2, 0); gw(0, 3, 0);
-      gx(0, 3, 0); gx(1, 0, 1); gx(0, 1, 0); gx(1, 2, 1); gw(1, 0, 1); gw(1, 1, 1);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      if (!ov) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if constexpr (EPI == 1) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
       barrier();
       if (wm == 1) barrier();     // stagger: waves 4-7 run one section behind
       int t = 0;
@@ -747,7 +798,7 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
     if (wm == 0) barrier();     // pairs with the last barrier of waves 4-7: every LDS read retired
   };
 
-  drive<512>(a, smem, run,
+  drive<512>(a, smem, prologue, body,
              [&](auto&& store16) {
 #pragma unroll
                for (int i = 0; i < 8; ++i)
@@ -755,15 +806,31 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
                  for (int j = 0; j < 4; ++j) store16(i * 4 + j, acc[i][j]);
              },
              [&](auto&& load16, bool first) {
+               if (first) {
 #pragma unroll
-               for (int i = 0; i < 8; ++i)
+                 for (int i = 0; i < 8; ++i)
 #pragma unroll
-                 for (int j = 0; j < 4; ++j) {
-                   const f32x4 v = load16(i * 4 + j);
-                   acc[i][j] = first ? v : acc[i][j] + v;
-                 }
+                   for (int j = 0; j < 4; ++j) acc[i][j] = load16(i * 4 + j);
+                 return;
+               }
+               // 8 loads in flight per batch (a load-add pair per element serialises on vmcnt(0))
+#pragma unroll
+               for (int i0 = 0; i0 < 8; i0 += 2) {
+                 f32x4 v[2][4];
+#pragma unroll
+                 for (int i = 0; i < 2; ++i)
+#pragma unroll
+                   for (int j = 0; j < 4; ++j) v[i][j] = load16((i0 + i) * 4 + j);
+#pragma unroll
+                 for (int i = 0; i < 2; ++i)
+#pragma unroll
+                   for (int j = 0; j < 4; ++j) acc[i0 + i][j] += v[i][j];
+               }
              },
-             [&](int tm, int tn) { epilogue<EPI>(acc, a.Y, a.ldy, M, tm * kBM, tn, wm, wn, lane); });
+             [&](int tm, int tn) {
+               const int te = fresh_tid();
+               epilogue<EPI>(acc, a.Y, a.ldy, M, tm * kBM, tn, (te >> 8) & 1, (te >> 6) & 3, te & 63);
+             });
 }
 
 // Per-device split-K workspace (one fp32 slab per block + one counter per tile),
@@ -811,17 +878,24 @@ void launch_pp(const void* x, int ldx, const void* w, void* y, int ldy, int M, i
                           : (prio & 3) == 2   ? mfma_gemm_pp_kernel<EPI, 2, 4>
                                               : mfma_gemm_pp_kernel<EPI, 0, 4>;
   PPArgs a{(const uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, nullptr, nullptr, ldx, ldy, M, I, K, tiles_m, total,
-           0, 0, 0, 0};
+           0, 0, 0, 0, !(prio & 8)};
   const int nt = K / kBK;
-  SkWorkspace* sk = (skmode && nt >= 8) ? sk_workspace(s) : nullptr;
+  SkWorkspace* sk = ((skmode || a.ovl) && nt >= 8) ? sk_workspace(s) : nullptr;
   if (sk) {
     const int full = total / sk->P, rem = total % sk->P;
     const int splits = rem ? min(4, sk->P / rem) : 0;
-    if (splits >= 2 && (full < 8 || skmode == 2)) {
+    if (skmode && splits >= 2 && (full < 8 || skmode == 2)) {
       a.ws = sk->ws;
       a.cnt = sk->cnt;
       a.rem = rem;
       a.splits = splits;
+      a.full = full;
+      a.P = sk->P;
+      kern<<<dim3(sk->P), 512, 0, s>>>(a);
+      return;
+    }
+    if (a.ovl && rem == 0 && full >= 2) {
+      // whole waves of tiles: persistent, so each block's next tile loads under this one's epilogue
       a.full = full;
       a.P = sk->P;
       kern<<<dim3(sk->P), 512, 0, s>>>(a);
@@ -851,7 +925,8 @@ void launch(const void* x, int ldx, const void* w, void* y, int ldy, int M, int 
 // 3 = ping-pong wave groups, 4 phases per K tile).  (epi >> 8) & 3: stream-K policy of schedule 3
 // (0 = auto, 1 = off, 2 = whenever the tiles leave the last wave part-empty).  (epi >> 10) & 3:
 // s_setprio variant of schedule 3, (epi >> 12) & 1: two 32-MFMA phases per K tile, (epi >> 13) & 1:
-// four 16-MFMA phases (default: two up to M = 2560, see mfma_gemm_pp_kernel).
+// four 16-MFMA phases (default: two up to M = 2560, see mfma_gemm_pp_kernel), (epi >> 14) & 1: no
+// cross-tile overlap (next tile's prologue after the epilogue; whole waves of tiles not persistent).
 extern "C" int dgi_mfma_gemm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K,
                              int epi, hipStream_t s) {
   if (M <= 0) return 0;
@@ -859,7 +934,7 @@ extern "C" int dgi_mfma_gemm(const void* x, int ldx, const void* w, void* y, int
   const int swiglu = epi & 15;
   int sched = (epi >> 4) & 15;
   const int skmode = ((epi >> 8) & 3) == 0 ? 1 : ((epi >> 8) & 3) == 1 ? 0 : 2;
-  int prio = (epi >> 10) & 7;
+  int prio = ((epi >> 10) & 7) | (((epi >> 14) & 1) << 3);
   // phases per K tile: (epi >> 13) & 1 forces 4; otherwise 2 up to 10 row tiles (M <= 2560: the
   // 2-phase body measured 2-4 % faster there) and 4 above (its deeper prefetch wins at M = 4096)
   if (!((epi >> 13) & 1) && !(prio & 4) && M <= 2560) prio |= 4;

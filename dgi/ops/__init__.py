@@ -520,7 +520,8 @@ MFMA_SCHED = int(os.environ.get("DGI_MFMA_SCHED", "3"))
 
 
 def mfma_gemm(x: torch.Tensor, w: torch.Tensor, epi: int = 0, out: Optional[torch.Tensor] = None,
-              sched: Optional[int] = None, streamk: int = 0, prio: int = 0, phases: int = 0) -> torch.Tensor:
+              sched: Optional[int] = None, streamk: int = 0, prio: int = 0, phases: int = 0,
+              overlap: bool = True) -> torch.Tensor:
     """Hand-written LDS-tiled MFMA GEMM (256x256 tiles, global_load_lds
     staging, XCD-aware tile order): ``epi`` 0 -> x @ w.T; 1 -> the fused
     SwiGLU of the MLP, silu(x @ gate.T) * (x @ up.T) with w = [gate; up],
@@ -528,7 +529,8 @@ def mfma_gemm(x: torch.Tensor, w: torch.Tensor, epi: int = 0, out: Optional[torc
     ``sched`` 3 is the ping-pong schedule; its ``streamk`` (split-K of the
     last partial wave) policy: 0 auto, 1 off, 2 whenever it applies;
     ``phases`` per K tile: 0 auto (2 up to M = 2560, else 4), 2 or 4;
-    ``prio``: s_setprio variant (benchmarking)."""
+    ``prio``: s_setprio variant (benchmarking); ``overlap`` False: no
+    cross-tile prologue / epilogue overlap (A/B)."""
     M = x.shape[0]
     N = w.shape[0] // 2 if epi == 1 else w.shape[0]
     if mfma_gemm_ok(x, w):
@@ -536,7 +538,8 @@ def mfma_gemm(x: torch.Tensor, w: torch.Tensor, epi: int = 0, out: Optional[torc
         if out is None:
             out = torch.empty(M, N, dtype=x.dtype, device=x.device)
         _call("mfma_gemm", out, x, w, epi | ((MFMA_SCHED if sched is None else sched) << 4) | (streamk << 8)
-              | (prio << 10) | ((1 if phases == 2 else 0) << 12) | ((1 if phases == 4 else 0) << 13))
+              | (prio << 10) | ((1 if phases == 2 else 0) << 12) | ((1 if phases == 4 else 0) << 13)
+              | ((0 if overlap else 1) << 14))
         return out
     r = mfma_gemm_ref(x, w, epi)
     if out is not None:

@@ -29,7 +29,8 @@ MS = [int(x) for x in os.environ.get("GEMM_MS", "512,1024,1536,1792,2048,4096").
 ROUNDS = int(os.environ.get("GEMM_ROUNDS", "7"))
 ITERS = int(os.environ.get("GEMM_ITERS", "10"))
 # schedule ids; "3k" = schedule 3 with split-K off, "3p1" / "3p2" = schedule 3 with s_setprio variant 1 / 2,
-# "3h" / "3f" = schedule 3 with two 32-MFMA / four 16-MFMA phases per K tile (default: by M)
+# "3h" / "3f" = schedule 3 with two 32-MFMA / four 16-MFMA phases per K tile (default: by M),
+# "3n" = schedule 3 without the cross-tile prologue / epilogue overlap
 SCHEDS = os.environ.get("GEMM_SCHEDS", "1,0,2,3").split(",")
 
 
@@ -59,7 +60,8 @@ def main():
                 variants[("mfma_swiglu" if fused else "mfma") + ("" if sc == SCHEDS[0] else f"_s{sc}")] = \
                     (lambda sc=sc: ops.mfma_gemm(x, w, epi, sched=int(sc[0]), streamk=int("k" in sc),
                                                  prio=int(sc.split("p")[1][0]) if "p" in sc else 0,
-                                                 phases=2 if "h" in sc else 4 if "f" in sc else 0))
+                                                 phases=2 if "h" in sc else 4 if "f" in sc else 0,
+                                                 overlap="n" not in sc))
             for f in variants.values():
                 f()
             torch.cuda.synchronize()

@@ -56,14 +56,18 @@ def test_mfma_gemm_strided_rows_and_asymmetric_operands(sched):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("M,N,K", [(2048, 1024, 256), (1920, 2560, 1024), (4096, 512, 8192)])
+@pytest.mark.parametrize("M,N,K", [(2048, 1024, 256), (1920, 2560, 1024), (4096, 512, 8192), (2048, 16384, 512),
+                                   (2000, 16384, 512)])
 @pytest.mark.parametrize("epi", [0, 1])
 @pytest.mark.parametrize("phases", [4, 2])
 def test_mfma_gemm_pingpong_bitwise_stable(M, N, K, epi, phases):
     """Race screen for the ping-pong schedule (sched 3): it accumulates in the same
     order as sched 1, so every one of repeated launches must match sched 1 bit for
     bit -- a slab read before its load landed (or overwritten before every wave
-    read it) shows up as a mismatch on some launch."""
+    read it) shows up as a mismatch on some launch.  N = 16384 at M = 2048 is two
+    whole waves of tiles: the persistent launch whose next tile's staging loads are
+    issued under the current tile's epilogue (M = 2000: the last row tile has a tail
+    and is not overlapped)."""
     ops.load_native(required=True)
     x = _rand(M, K, device="cuda", seed=M)
     w = _rand(N, K, device="cuda", scale=0.05, seed=K)
@@ -71,19 +75,21 @@ def test_mfma_gemm_pingpong_bitwise_stable(M, N, K, epi, phases):
     for _ in range(12):
         got = ops.mfma_gemm(x, w, epi, sched=3, streamk=1, phases=phases)
         assert torch.equal(got, ref)
+    assert torch.equal(ops.mfma_gemm(x, w, epi, sched=3, streamk=1, phases=phases, overlap=False), ref)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K", [(2048, 2560, 512), (1920, 10240, 8192), (1000, 768, 2048), (2432, 8192, 1024),
-                                   (300, 57344 // 8, 4096)])
+                                   (300, 57344 // 8, 4096), (2048, 19200, 1024)])
 @pytest.mark.parametrize("epi", [0, 1])
 @pytest.mark.parametrize("streamk", [0, 2])
 @pytest.mark.parametrize("phases", [4, 2])
 def test_mfma_gemm_splitk_matches_fp32_and_is_deterministic(M, N, K, epi, streamk, phases):
     """Hybrid split-K of the last partial wave (persistent launch, 2-4 K pieces per
     remainder tile reduced by the last arriving block through fp32 slabs; uneven
-    piece lengths at K = 512): matches the fp32 reference, and repeated launches
-    agree bit for bit (slabs are summed in piece order)."""
+    piece lengths at K = 512; N = 19200 at M = 2048: a split piece, then two whole
+    tiles whose second loads under the first's epilogue): matches the fp32 reference,
+    and repeated launches agree bit for bit (slabs are summed in piece order)."""
     ops.load_native(required=True)
     x = _rand(M, K, device="cuda", seed=M + 1)
     w = _rand(N, K, device="cuda", scale=0.05, seed=N + 1)
