@@ -192,33 +192,36 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void prefill_attn_kernel(
     // most tiles skip the 64 O multiplies (P stays <= 256, safe in f32 / bf16)
     if (__any(mx > m_run + 8.f)) {
       const float m_new = fmaxf(m_run, mx);
-      const float alpha = exp2f(m_run - m_new);
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
       l_run *= alpha;
 #pragma unroll
       for (int d = 0; d < ND; ++d) o[d] *= alpha;
       m_run = m_new;
     }
-    float psum = 0.f;
+    // raw v_exp_f32 (arguments <= 8; masked scores underflow to 0) and four partial row
+    // sums instead of one 32-long dependent add chain
+    float ps[4] = {0.f, 0.f, 0.f, 0.f};
     if (interior) {
       const float nm = -m_run;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float pv = exp2f(fmaf(sc[kb][r], scale_log2, nm));
+          const float pv = __builtin_amdgcn_exp2f(fmaf(sc[kb][r], scale_log2, nm));
           sc[kb][r] = pv;
-          psum += pv;
+          ps[r & 3] += pv;
         }
     } else {
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float pv = exp2f(sc[kb][r] - m_run);
+          const float pv = __builtin_amdgcn_exp2f(sc[kb][r] - m_run);
           sc[kb][r] = pv;
-          psum += pv;
+          ps[r & 3] += pv;
         }
     }
+    float psum = (ps[0] + ps[1]) + (ps[2] + ps[3]);
     psum += __shfl_xor(psum, 32, 64);
     l_run += psum;
 
