@@ -813,16 +813,17 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
                    for (int j = 0; j < 4; ++j) acc[i][j] = load16(i * 4 + j);
                  return;
                }
-               // 8 loads in flight per batch (a load-add pair per element serialises on vmcnt(0))
+               // 16 loads in flight per batch (a load-add pair per element serialises on vmcnt(0);
+               // the fragment registers are free here)
 #pragma unroll
-               for (int i0 = 0; i0 < 8; i0 += 2) {
-                 f32x4 v[2][4];
+               for (int i0 = 0; i0 < 8; i0 += 4) {
+                 f32x4 v[4][4];
 #pragma unroll
-                 for (int i = 0; i < 2; ++i)
+                 for (int i = 0; i < 4; ++i)
 #pragma unroll
                    for (int j = 0; j < 4; ++j) v[i][j] = load16((i0 + i) * 4 + j);
 #pragma unroll
-                 for (int i = 0; i < 2; ++i)
+                 for (int i = 0; i < 4; ++i)
 #pragma unroll
                    for (int j = 0; j < 4; ++j) acc[i0 + i][j] += v[i][j];
                }
