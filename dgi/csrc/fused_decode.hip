@@ -59,7 +59,16 @@ struct FusedArgs {
   uint16_t* k_cache;  // [blocks, nkv, bs, 128]
   uint16_t* v_cache;
   int nh, nkv, bs_log2;
+  // KS > 1: per-tile fp32 partials [tile][KS][64 lanes] and arrival counters (zero between launches)
+  float* ws;
+  int* cnt;
 };
+
+// buffer resource word 3 of a raw byte-addressed buffer, and the write-through (sc1) policy bit
+constexpr int kRsrcWord3 = 0x00020000;
+constexpr int kSc1 = 16;
+constexpr int kKsMaxTiles = 4096;
+constexpr int kKsMax = 2;
 
 template <int U, int TW>
 struct Frag {
@@ -198,8 +207,14 @@ __device__ __forceinline__ void store_pair(const FusedArgs& a, int c0, int c1, i
 // epilogue: half the rows per workgroup, twice the workgroups (qkv on 8B: 384
 // instead of 192 on 256 CUs).  D: load groups in flight (register ring); the
 // first D are issued before the X staging.
-template <int NW, int U, int TW, int D, int PRO, int EPI>
+// KS > 1 (TW = 1 only) splits K over KS workgroups per pair tile: 8B qkv has 384 pair
+// tiles, 1.5 per CU, so half the CUs stream twice the bytes of the other half; 768
+// half-K workgroups are 3 per CU.  Each part publishes its cross-wave sum (1 KB) with
+// write-through stores and bumps the tile's counter; the last part to arrive sums every
+// part in part order (deterministic) and runs the epilogue.
+template <int NW, int U, int TW, int D, int PRO, int EPI, int KS = 1>
 __global__ __launch_bounds__(NW * 64) void fused_skinny_kernel(FusedArgs a) {
+  static_assert(KS == 1 || TW == 1, "split-K pairs are one-tile workgroups");
   // normalised X rows live in LDS for the whole kernel: [M][K + 8] bf16 (16-byte
   // row pad keeps the 16-row fragment reads off one bank)
   extern __shared__ __attribute__((aligned(16))) uint16_t xs[];
@@ -215,10 +230,22 @@ __global__ __launch_bounds__(NW * 64) void fused_skinny_kernel(FusedArgs a) {
   const int M = a.M;
   const int ldx = K + 8;
   const int bid = blockIdx.x;
-  const int c0 = (bid / a.tpg) * a.gstride + (bid % a.tpg) * (TW == 2 ? 16 : 8);
+  // KS > 1: the parts of one tile are workgroups 8 apart (one XCD under round-robin
+  // dispatch, so the partials meet in that XCD's L2) when the grid is a multiple of 8 KS
+  int tile = bid, part = 0;
+  if (KS > 1) {
+    if ((gridDim.x % (8 * KS)) == 0) {
+      tile = (bid / (8 * KS)) * 8 + (bid & 7);
+      part = (bid >> 3) % KS;
+    } else {
+      tile = bid / KS;
+      part = bid % KS;
+    }
+  }
+  const int c0 = (tile / a.tpg) * a.gstride + (tile % a.tpg) * (TW == 2 ? 16 : 8);
   const int c1 = c0 + a.pair_off;
-  const int ngroups = (K >> 6) / (NW * U);
-  const size_t lane_k = (size_t)g * 16 + (size_t)w * 64;
+  const int ngroups = ((K / KS) >> 6) / (NW * U);
+  const size_t lane_k = (size_t)g * 16 + (size_t)w * 64 + (size_t)part * (K / KS);
   const bool lo = r < 8;
   const uint16_t* w0 = a.w + (size_t)(TW == 2 ? c0 + r : (lo ? c0 + r : c1 + r - 8)) * K + lane_k;
   const uint16_t* w1 = a.w + (size_t)(c1 + r) * K + lane_k;
@@ -286,6 +313,23 @@ __global__ __launch_bounds__(NW * 64) void fused_skinny_kernel(FusedArgs a) {
   for (int j = 1; j < NW; ++j) {
     v0 += red[j][0][lane];
     if (TW == 2) v1 += red[j][1][lane];
+  }
+  if (KS > 1) {
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.ws + (size_t)tile * KS * 256), 0, KS * 256 * 4, kRsrcWord3);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v0), rs, (part * 64 + lane) * 16, 0, kSc1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(a.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __shfl(old, 0);
+    if (old != KS - 1) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (lane == 0) __hip_atomic_store(a.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    v0 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < KS; ++j)
+      v0 += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (j * 64 + lane) * 16, 0, 0));
+    v1 = v0;
   }
   if (TW == 1) {
     // this lane holds row c0 + r (r < 8) or c1 + r - 8; bring the other half of
@@ -405,9 +449,45 @@ __global__ __launch_bounds__(NW * 64) void fused_skinny_persist_kernel(FusedArgs
   }
 }
 
-template <int NW, int U, int TW, int D, int PRO, int EPI>
+// Per-device split-K workspace (KS partial slabs + one counter per pair tile), allocated on
+// first use outside stream capture; the engine runs its decode projections on one stream.
+struct KsWorkspace {
+  float* ws = nullptr;
+  int* cnt = nullptr;
+};
+
+KsWorkspace* ks_workspace(hipStream_t s) {
+  static KsWorkspace per_dev[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  KsWorkspace& w = per_dev[dev];
+  if (w.ws) return &w;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  float* ws = nullptr;
+  int* cnt = nullptr;
+  if (hipMalloc(&ws, (size_t)kKsMaxTiles * kKsMax * 256 * sizeof(float)) != hipSuccess) return nullptr;
+  if (hipMalloc(&cnt, (size_t)kKsMaxTiles * sizeof(int)) != hipSuccess ||
+      hipMemset(cnt, 0, (size_t)kKsMaxTiles * sizeof(int)) != hipSuccess) {
+    hipFree(ws);
+    return nullptr;
+  }
+  w.ws = ws;
+  w.cnt = cnt;
+  return &w;
+}
+
+template <int NW, int U, int TW, int D, int PRO, int EPI, int KS = 1>
 int launch_cfg(FusedArgs a, int N, int ntiles, hipStream_t s) {
-  if ((a.K / 64) % (NW * U)) return -7;
+  static_assert(KS <= kKsMax, "workspace holds kKsMax parts");
+  if constexpr (KS > 1) {
+    KsWorkspace* ks = ntiles <= kKsMaxTiles ? ks_workspace(s) : nullptr;
+    // no workspace (first call inside a capture, huge N): the same launch without the split
+    if (!ks) return launch_cfg<NW, U, TW, D * KS <= 8 ? D * KS : D, PRO, EPI, 1>(a, N, ntiles, s);
+    a.ws = ks->ws;
+    a.cnt = ks->cnt;
+  }
+  if ((a.K / KS / 64) % (NW * U)) return -7;
   const size_t lds = (size_t)a.M * (a.K + 8) * 2;
   // static (reduce tiles + norm partials) + staged X must fit the 160 KB of LDS
   const size_t lds_static = (size_t)NW * TW * 64 * 16 + (size_t)NW * 16 * 4 + 16 * 4;
@@ -423,8 +503,8 @@ int launch_cfg(FusedArgs a, int N, int ntiles, hipStream_t s) {
       a.tpg = 8;
     }
   }
-  const int nblocks = TW == 2 ? ntiles / 2 : ntiles;
-  fused_skinny_kernel<NW, U, TW, D, PRO, EPI><<<dim3(nblocks), NW * 64, lds, s>>>(a);
+  const int nblocks = (TW == 2 ? ntiles / 2 : ntiles) * KS;
+  fused_skinny_kernel<NW, U, TW, D, PRO, EPI, KS><<<dim3(nblocks), NW * 64, lds, s>>>(a);
   DGI_CHECK_LAUNCH();
   (void)N;
   return 0;
@@ -481,6 +561,12 @@ int launch(const FusedArgs& a, int N, int ntiles, int cfg, hipStream_t s) {
     case 14: return launch_persist<4, 2, 8, PRO, EPI>(a, ntiles, s);
     case 15: return launch_persist<8, 2, 6, PRO, EPI>(a, ntiles, s);
     case 16: return launch_persist<16, 1, 4, PRO, EPI>(a, ntiles, s);
+    // K split over two workgroups per pair tile (one-tile workgroups, TW = 1)
+    case 17: return launch_cfg<8, 1, 1, 4, PRO, EPI, 2>(a, N, ntiles, s);
+    case 18: return launch_cfg<4, 1, 1, 4, PRO, EPI, 2>(a, N, ntiles, s);
+    case 19: return launch_cfg<8, 2, 1, 2, PRO, EPI, 2>(a, N, ntiles, s);
+    case 20: return launch_cfg<4, 2, 1, 4, PRO, EPI, 2>(a, N, ntiles, s);
+    case 21: return launch_cfg<4, 1, 1, 8, PRO, EPI, 2>(a, N, ntiles, s);
     default: return -5;
   }
 }

@@ -158,11 +158,38 @@ def bench_attn(nh, nkv, Bs, ctxs):
     return rows
 
 
+def bench_plain_fused(shapes, Ms, cfgs):
+    """Plain projections (no prologue / epilogue: o-proj, down) through fused_skinny's
+    launch configs (incl. the split-K ones) vs ops.linear (skinny_gemm / hipBLASLt)."""
+    dev, bf = "cuda", torch.bfloat16
+    rows = []
+    for name, N, K in shapes:
+        nbuf = max(2, int(2.5e9 // (N * K * 2)))
+        ws = [torch.randn(N, K, device=dev, dtype=bf) * 0.02 for _ in range(nbuf)]
+        for M in Ms:
+            x = torch.randn(M, K, device=dev, dtype=bf)
+            y = torch.empty(M, N, device=dev, dtype=bf)
+            row = {"proj": name, "M": M, "linear": round(graph_time(lambda i: ops.linear(x, ws[i % nbuf])), 2)}
+            for cfg in cfgs:
+                try:
+                    ops.fused_skinny(y, x, None, None, None, 0.0, ws[0], None, 0, 0, cfg=cfg)
+                    torch.cuda.synchronize()
+                except RuntimeError as e:
+                    print(f"skip {name} cfg {cfg} M={M}: {e}", flush=True)
+                    continue
+                row[f"c{cfg}"] = round(graph_time(lambda i: ops.fused_skinny(
+                    y, x, None, None, None, 0.0, ws[i % nbuf], None, 0, 0, cfg=cfg)), 2)
+            print(json.dumps(row), flush=True)
+            rows.append(row)
+    return rows
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--cfgs", type=int, nargs="+", default=[0, 2, 3, 4, 5])
     ap.add_argument("--skip-attn", action="store_true")
+    ap.add_argument("--plain-fused", action="store_true", help="also o-proj / down through fused_skinny configs")
     ap.add_argument("--plain", action="store_true", help="only the plain skinny-vs-hipBLASLt table")
     a = ap.parse_args()
     if a.plain:
@@ -174,6 +201,8 @@ def main():
                 json.dump(res, f, indent=1)
         return
     res = {"gemm_8b": bench_gemms(4096, 14336, 32, 8, [1, 2, 4, 8, 16], a.cfgs)}
+    if a.plain_fused:
+        res["plain_fused_8b"] = bench_plain_fused([("o", 4096, 4096), ("down", 4096, 14336)], [1, 4, 8], a.cfgs)
     if not a.skip_attn:
         res["attn_8b"] = bench_attn(32, 8, [1, 4, 16], [256, 384, 1024, 4096])
     if a.out:

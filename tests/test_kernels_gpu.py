@@ -452,7 +452,7 @@ def test_fused_skinny_every_launch_config(pro, epi):
     """Every fused_decode.hip launch config (waves, K-steps per group, one- or
     two-tile workgroups, load ring depth, persistent one-ring workgroups) against
     the reference, at M = 1 and 3."""
-    for cfg in range(17):
+    for cfg in range(22):
         for M in (1, 3):
             _fused_skinny_case(pro, epi, M, cfg)
 
@@ -465,6 +465,19 @@ def test_fused_skinny_persistent_multi_tile(pro, epi, R):
     for cfg in (12, 13, 14, 15, 16):
         for M in (1, 4):
             _fused_skinny_case(pro, epi, M, cfg, R)
+
+
+@pytest.mark.parametrize("pro,epi,R", [(2, 2, None), (0, 0, 2080), (2, 1, 2 * 1040)])
+def test_fused_skinny_split_k(pro, epi, R):
+    """Split-K configs (two workgroups per pair tile, last arriver reduces): against the
+    reference, bit-identical on a repeat (the tile counters reset themselves, the parts are
+    summed in part order), on XCD-paired grids (qkv: 384 tiles) and on grids that are not a
+    multiple of 16 workgroups (2080 rows, 1040 gate rows: 130 tiles each)."""
+    for cfg in (17, 18, 19, 20, 21):
+        for M in (1, 4):
+            y1 = _fused_skinny_case(pro, epi, M, cfg, R)
+            y2 = _fused_skinny_case(pro, epi, M, cfg, R)
+            assert torch.equal(y1, y2), cfg
 
 
 def _fused_skinny_case(pro, epi, M, cfg, R=None):
@@ -513,6 +526,7 @@ def _fused_skinny_case(pro, epi, M, cfg, R=None):
             assert float((a_.float() - b_.float()).abs().max()) <= 0.02 * s2
         if M > 2:
             assert int((kc.view(-1, 128).abs().sum(1) > 0).sum()) == (M - 1) * nkv
+    return y
 
 
 def test_fused_decode_model_matches_unfused():
