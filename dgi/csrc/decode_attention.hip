@@ -38,6 +38,8 @@ __device__ __forceinline__ int v_lds_off(int row, int col) {
 // per-wave LDS: the V tile (32 x HD bf16), reused after the loop for the wave's
 // partial O (16 queries x HD fp32, rows padded by 4 floats so the 16 query rows
 // of one store land in different banks) plus m / l
+__device__ __forceinline__ int o_swz(int q) { return ((q & 3) << 4) | (q >> 2); }
+
 template <int HD>
 constexpr int decode_wave_lds() {
   return (32 * HD * 2 > 16 * (HD + 4) * 4 ? 32 * HD * 2 : 16 * (HD + 4) * 4) + 128;
@@ -54,7 +56,11 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_kernel(
   constexpr int NC = HD / 16;   // 16-wide dim blocks of the PV product
   constexpr int VCH = HD / 8;   // 16-byte chunks per V row
   constexpr int WREG = decode_wave_lds<HD>();  // per-wave LDS bytes (V tile, then O/m/l)
-  constexpr int OROW = HD + 4;                 // padded fp32 row of the merged partial O
+  // fp32 row of the merged partial O: unpadded, columns XOR-swizzled per query row
+  // (bits 0-1 ^= q >> 2, bits 4-5 ^= q & 3) so the 64 lanes of each scalar store
+  // (16 queries x 4 dim groups) hit 64 different banks; a padded row (HD + 4) put
+  // 4 lanes on one bank (profiles/r2_pmc_attention_kernels.md: 15 % conflict cycles)
+  constexpr int OROW = HD;
   constexpr int NT = 64 * NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -217,7 +223,7 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_kernel(
 #pragma unroll
     for (int c = 0; c < NC; ++c)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) ow[qi * OROW + 16 * c + 4 * g + i] = o[c][i];
+      for (int i = 0; i < 4; ++i) ow[qi * OROW + ((16 * c + 4 * g + i) ^ o_swz(qi))] = o[c][i];
     if (g == 0) {
       ml[qi] = m_run;
       ml[16 + qi] = l_run;
@@ -236,7 +242,7 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_kernel(
       const float* mlw = reinterpret_cast<float*>(smem + ww * WREG + MLOFF);
       const float sc = exp2f(mlw[qq] - M);
       L += mlw[16 + qq] * sc;
-      acc += reinterpret_cast<float*>(smem + ww * WREG)[qq * OROW + d] * sc;
+      acc += reinterpret_cast<float*>(smem + ww * WREG)[qq * OROW + (d ^ o_swz(qq))] * sc;
     }
     const int head = h * G + qq;
     const float r = acc / L;

@@ -139,31 +139,27 @@ __device__ __forceinline__ void stage_x(const FusedArgs& a, uint16_t* xs, float 
   __syncthreads();
 }
 
-// Epilogue of one column pair on wave 0: (v0, v1) = rows (c0 + rr, c1 + rr) for the M
-// rows of lane group g; EPI 0 store, 1 SwiGLU, 2 RoPE + paged KV write.
-template <int TW, int EPI>
-__device__ __forceinline__ void store_pair(const FusedArgs& a, int c0, int c1, int r, int g, bool lo,
-                                           const f32x4& v0, const f32x4& v1) {
-  const int rr = TW == 2 ? r : (r & 7);
-  const float b0 = (TW == 2 && a.bias) ? bf16_to_f32(a.bias[c0 + r]) : 0.f;
-  const float b1 = (TW == 2 && a.bias) ? bf16_to_f32(a.bias[c1 + r]) : 0.f;
-  // TW 1: lanes r < 8 store the pair's first half, r >= 8 the second
-  const bool st0 = TW == 2 || lo, st1 = TW == 2 || !lo;
+// Epilogue rows on wave 0: (v0, v1) = output rows (row0, row1) for the M rows of lane
+// group g; st0 / st1: this lane stores row0 / row1.  EPI 0 store, 1 SwiGLU (row0 a gate
+// row, row1 its up row), 2 RoPE + paged KV write (row0 = d, row1 = d + 64 of one head).
+template <int EPI>
+__device__ __forceinline__ void store_rows(const FusedArgs& a, int row0, int row1, int g, bool st0, bool st1,
+                                           float b0, float b1, const f32x4& v0, const f32x4& v1) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = g * 4 + i;
     if (m >= a.M) break;
     uint16_t* yrow = a.y + (size_t)m * a.ldy;
     if (EPI == 0) {
-      if (st0) yrow[c0 + rr] = f32_to_bf16(v0[i] + b0);
-      if (st1) yrow[c1 + rr] = f32_to_bf16(v1[i] + b1);
+      if (st0) yrow[row0] = f32_to_bf16(v0[i] + b0);
+      if (st1) yrow[row1] = f32_to_bf16(v1[i] + b1);
     } else if (EPI == 1) {
       const float gt = bf16_to_f32(f32_to_bf16(v0[i] + b0));
       const float up = bf16_to_f32(f32_to_bf16(v1[i] + b1));
-      if (st0) yrow[c0 + rr] = f32_to_bf16(gt * __builtin_amdgcn_rcpf(1.f + __expf(-gt)) * up);
+      if (st0) yrow[row0] = f32_to_bf16(gt * __builtin_amdgcn_rcpf(1.f + __expf(-gt)) * up);
     } else {
-      const int head = c0 >> 7;
-      const int d = (c0 & 127) + rr;  // 0..63
+      const int head = row0 >> 7;
+      const int d = row0 & 127;  // 0..63
       const uint16_t x1 = f32_to_bf16(v0[i] + b0), x2 = f32_to_bf16(v1[i] + b1);
       if (head < a.nh + a.nkv) {
         const float* cs = a.cos_sin + (size_t)a.positions[m] * 128;
@@ -172,11 +168,11 @@ __device__ __forceinline__ void store_pair(const FusedArgs& a, int c0, int c1, i
         const uint16_t o1 = f32_to_bf16(f1 * cv - f2 * sv);
         const uint16_t o2 = f32_to_bf16(f2 * cv + f1 * sv);
         if (head < a.nh) {
-          if (st0) yrow[c0 + rr] = o1;
-          if (st1) yrow[c1 + rr] = o2;
+          if (st0) yrow[row0] = o1;
+          if (st1) yrow[row1] = o2;
         } else {
-          if (st0) yrow[c0 + rr] = x1;
-          if (st1) yrow[c1 + rr] = x2;
+          if (st0) yrow[row0] = x1;
+          if (st1) yrow[row1] = x2;
           const int slot = a.slots[m];
           if (slot >= 0) {
             const int bs = 1 << a.bs_log2;
@@ -186,8 +182,8 @@ __device__ __forceinline__ void store_pair(const FusedArgs& a, int c0, int c1, i
           }
         }
       } else {
-        if (st0) yrow[c0 + rr] = x1;
-        if (st1) yrow[c1 + rr] = x2;
+        if (st0) yrow[row0] = x1;
+        if (st1) yrow[row1] = x2;
         const int slot = a.slots[m];
         if (slot >= 0) {
           const int bs = 1 << a.bs_log2;
@@ -199,6 +195,17 @@ __device__ __forceinline__ void store_pair(const FusedArgs& a, int c0, int c1, i
       }
     }
   }
+}
+
+// Epilogue of one column pair on wave 0: (v0, v1) = rows (c0 + rr, c1 + rr).
+template <int TW, int EPI>
+__device__ __forceinline__ void store_pair(const FusedArgs& a, int c0, int c1, int r, int g, bool lo,
+                                           const f32x4& v0, const f32x4& v1) {
+  const int rr = TW == 2 ? r : (r & 7);
+  const float b0 = (TW == 2 && a.bias) ? bf16_to_f32(a.bias[c0 + r]) : 0.f;
+  const float b1 = (TW == 2 && a.bias) ? bf16_to_f32(a.bias[c1 + r]) : 0.f;
+  // TW 1: lanes r < 8 store the pair's first half, r >= 8 the second
+  store_rows<EPI>(a, c0 + rr, c1 + rr, g, TW == 2 || lo, TW == 2 || !lo, b0, b1, v0, v1);
 }
 
 // TW: 16-row weight tiles per workgroup.  TW = 2 is the pair (c0 + r, c1 + r);
@@ -449,6 +456,147 @@ __global__ __launch_bounds__(NW * 64) void fused_skinny_persist_kernel(FusedArgs
   }
 }
 
+// Balanced persistent variant ("quarter pairs"): the rows are cut into quarter pairs of
+// 4 + 4 rows (half of a TW = 1 pair tile) and every workgroup streams qpw consecutive
+// quarters, two per MFMA step (lanes r & 7 < 4 hold the step's first quarter, >= 4 its
+// second; a step with one quarter leaves the upper lanes idle: no loads, no stores).
+// 8B qkv: 384 pair tiles are 1.5 per CU, so the one-tile workgroups put 262 KB on half of
+// the CUs and 131 KB on the rest; 768 quarters = 3 per CU stream 196 KB on every CU.
+template <int NW, int U, int D, int PRO, int EPI>
+__global__ __launch_bounds__(NW * 64) void fused_skinny_quarter_kernel(FusedArgs a, int qpw, int nq) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t xs[];
+  __shared__ f32x4 red[2][NW][64];
+  __shared__ float s_part[NW][16];
+  __shared__ float s_inv[16];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int r = lane & 15;
+  const int g = lane >> 4;
+  const int K = a.K;
+  const int M = a.M;
+  const int ldx = K + 8;
+  const int bid = blockIdx.x;
+  const int q_first = bid * qpw;
+  const int nq_local = min(qpw, nq - q_first);   // >= 1: the host sizes the grid
+  const int nsteps = (nq_local + 1) >> 1;
+  const int ngroups = (K >> 6) / (NW * U);
+  const int total = nsteps * ngroups;
+  const size_t lane_k = (size_t)g * 16 + (size_t)w * 64;
+  const bool lo = r < 8;
+  const int j = r & 7;
+  const bool xval = r < M;
+  // c0-side weight row of this lane in step st; -1 when the step has no second quarter
+  auto lane_row = [&](int st) -> int {
+    const int qq = 2 * st + (j >> 2);
+    if (qq >= nq_local) return -1;
+    const int qp = q_first + qq;
+    const int ti = qp >> 1;
+    return (ti / a.tpg) * a.gstride + (ti % a.tpg) * 8 + (qp & 1) * 4 + (j & 3);
+  };
+  auto load = [&](Frag<U, 1>& f, int s) {
+    const int st = s / ngroups;
+    const int grp = s - st * ngroups;
+    const int row = lane_row(st);
+    if (row < 0) return;   // idle lanes: their MFMA columns are never stored
+    const uint16_t* w0 = a.w + (size_t)(lo ? row : row + a.pair_off) * K + lane_k;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t off = ((size_t)grp * NW * U + (size_t)u * NW) * 64;
+      const u32x4* p0 = reinterpret_cast<const u32x4*>(w0 + off);
+      f.w[u][0][0] = __builtin_nontemporal_load(p0);
+      f.w[u][0][1] = __builtin_nontemporal_load(p0 + 1);
+    }
+  };
+  Frag<U, 1> ring[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) ring[d].w[u][0][0] = ring[d].w[u][0][1] = u32x4{0u, 0u, 0u, 0u};
+    if (d < total) load(ring[d], d);
+  }
+
+  stage_x<NW, PRO>(a, xs, s_part, s_inv, bid);
+
+  const uint16_t* xl = xs + (xval ? r : 0) * ldx + lane_k;
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  int parity = 0;
+  for (int base = 0; base < total; base += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int s = base + d;
+      if (s < total) {          // uniform
+        const int st = s / ngroups;
+        const int grp = s - st * ngroups;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int off = (grp * NW * U + u * NW) * 64;
+          u32x4 xa = u32x4{0u, 0u, 0u, 0u}, xb = u32x4{0u, 0u, 0u, 0u};
+          if (xval) {
+            xa = *reinterpret_cast<const u32x4*>(xl + off);
+            xb = *reinterpret_cast<const u32x4*>(xl + off + 8);
+          }
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xa), as_bf16x8(ring[d].w[u][0][0]), acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xb), as_bf16x8(ring[d].w[u][0][1]), acc, 0, 0, 0);
+        }
+        if (s + D < total) load(ring[d], s + D);
+        if (grp == ngroups - 1) {     // step done: cross-wave sum, epilogue on wave 0
+          red[parity][w][lane] = acc;
+          __syncthreads();
+          if (w == 0) {
+            const int row = lane_row(st);
+            f32x4 v = red[parity][0][lane];
+#pragma unroll
+            for (int jj = 1; jj < NW; ++jj) v += red[parity][jj][lane];
+            const float bo = (a.bias && row >= 0) ? bf16_to_f32(a.bias[lo ? row : row + a.pair_off]) : 0.f;
+            f32x4 v0, v1;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float own = v[i] + bo;
+              const float oth = __shfl_xor(own, 8);
+              v0[i] = lo ? own : oth;
+              v1[i] = lo ? oth : own;
+            }
+            if (row >= 0) store_rows<EPI>(a, row, row + a.pair_off, g, lo, !lo, 0.f, 0.f, v0, v1);
+          }
+          acc = f32x4{0.f, 0.f, 0.f, 0.f};
+          parity ^= 1;
+        }
+      }
+    }
+  }
+}
+
+template <int NW, int U, int D, int PRO, int EPI>
+int launch_quarter(FusedArgs a, int ntiles, hipStream_t s) {
+  if ((a.K / 64) % (NW * U)) return -7;
+  const size_t lds = (size_t)a.M * (a.K + 8) * 2;
+  const size_t lds_static = (size_t)2 * NW * 64 * 16 + (size_t)NW * 16 * 4 + 16 * 4;
+  if (lds + lds_static > 160 * 1024) return -6;
+  // TW = 1 pair geometry (as launch_cfg)
+  if (EPI == 0) {
+    a.gstride = 16;
+    a.pair_off = 8;
+  } else if (EPI == 1) {
+    a.gstride = 8;
+  } else {
+    a.tpg = 8;
+  }
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  const int nq = 2 * ntiles;
+  const int qpw = (nq + cus - 1) / cus;
+  const int nblocks = (nq + qpw - 1) / qpw;
+  fused_skinny_quarter_kernel<NW, U, D, PRO, EPI><<<dim3(nblocks), NW * 64, lds, s>>>(a, qpw, nq);
+  DGI_CHECK_LAUNCH();
+  return 0;
+}
+
 // Per-device split-K workspace (KS partial slabs + one counter per pair tile), allocated on
 // first use outside stream capture; the engine runs its decode projections on one stream.
 struct KsWorkspace {
@@ -567,6 +715,12 @@ int launch(const FusedArgs& a, int N, int ntiles, int cfg, hipStream_t s) {
     case 19: return launch_cfg<8, 2, 1, 2, PRO, EPI, 2>(a, N, ntiles, s);
     case 20: return launch_cfg<4, 2, 1, 4, PRO, EPI, 2>(a, N, ntiles, s);
     case 21: return launch_cfg<4, 1, 1, 8, PRO, EPI, 2>(a, N, ntiles, s);
+    // balanced persistent quarter-pair workgroups (waves, K-steps per group, groups in flight)
+    case 22: return launch_quarter<8, 1, 8, PRO, EPI>(a, ntiles, s);
+    case 23: return launch_quarter<8, 2, 4, PRO, EPI>(a, ntiles, s);
+    case 24: return launch_quarter<16, 1, 4, PRO, EPI>(a, ntiles, s);
+    case 25: return launch_quarter<4, 2, 8, PRO, EPI>(a, ntiles, s);
+    case 26: return launch_quarter<8, 1, 4, PRO, EPI>(a, ntiles, s);
     default: return -5;
   }
 }

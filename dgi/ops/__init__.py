@@ -413,11 +413,14 @@ FUSED_MAX_M = {"qkv": 8, "gate_up": 16}
 # launch config per projection and row count (fused_decode.hip cfg = waves, K-steps per load
 # group, tiles per workgroup, load ring depth: 6 = 8x1 one-tile ring 4, 7 = 8x1 two-tile ring 4,
 # 8 = 4x2 one-tile ring 4, 10 = 8x2 one-tile, 11 = 4x1 one-tile ring 8; persistent one-ring
-# workgroups 12 = 8x1 ring 8, 16 = 16x1 ring 4).  Fastest per M on the 8B shapes, weights cold,
+# workgroups 12 = 8x1 ring 8, 16 = 16x1 ring 4; balanced quarter-pair workgroups 24 = 16x1 ring 4).  Fastest per M on the 8B shapes, weights cold,
 # hipGraph-timed (profiles/r3_decode_gemm/README.md, profiles/r3_decode/persistent_gemv.md): qkv
 # 16.6 -> 15.0 us at M = 1 against round 2's fixed config 4; gate_up + SwiGLU 48.6 -> 43.0 us at
 # M = 1, 56.2 -> 45.5 at M = 4, 66.1 -> 48.2 at M = 8 (cfg 16; 16 waves do not fit M = 16's LDS).
-FUSED_M_CFG = {"qkv": ((2, 10), (16, 7)), "gate_up": ((8, 16), (16, 12))}
+# qkv + RoPE/KV at M <= 8: balanced quarter-pair workgroups, 16 waves (cfg 24: 384 pair tiles
+# = 768 quarters, 3 per CU instead of 1.5 whole tiles): 14.96 -> 13.16 us at M = 1, 18.52 -> 17.40
+# at M = 4, 21.37 -> 20.23 at M = 8 (profiles/r3_decode/quarter_gemv.md).
+FUSED_M_CFG = {"qkv": ((8, 24), (16, 7)), "gate_up": ((8, 16), (16, 12))}
 FUSED_KIND_CFG = {"qkv": int(os.environ.get("DGI_FUSED_QKV_CFG", "-1")),
                   "gate_up": int(os.environ.get("DGI_FUSED_GU_CFG", "-1"))}
 

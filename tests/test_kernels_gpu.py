@@ -452,17 +452,17 @@ def test_fused_skinny_every_launch_config(pro, epi):
     """Every fused_decode.hip launch config (waves, K-steps per group, one- or
     two-tile workgroups, load ring depth, persistent one-ring workgroups) against
     the reference, at M = 1 and 3."""
-    for cfg in range(22):
+    for cfg in range(27):
         for M in (1, 3):
             _fused_skinny_case(pro, epi, M, cfg)
 
 
 @pytest.mark.parametrize("pro,epi,R", [(2, 1, 2 * 14336), (2, 0, 8192), (0, 0, 8224), (2, 2, None)])
 def test_fused_skinny_persistent_multi_tile(pro, epi, R):
-    """Persistent configs at sizes where each workgroup streams several tiles through
-    one ring (8B gate_up: 7 tiles per workgroup; 8192 rows: 2; 8224: 3 with a 1-tile
+    """Persistent configs (whole pair tiles: 12-16; quarter pairs: 22-26) at sizes where
+    each workgroup streams several tiles through one ring (8B gate_up: 7 tiles per workgroup; 8192 rows: 2; 8224: 3 with a 1-tile
     last workgroup; qkv: 2), including the tile-parity double-buffered reduce."""
-    for cfg in (12, 13, 14, 15, 16):
+    for cfg in (12, 13, 14, 15, 16, 22, 23, 24, 25, 26):
         for M in (1, 4):
             _fused_skinny_case(pro, epi, M, cfg, R)
 
