@@ -38,7 +38,7 @@ __device__ __forceinline__ int v_lds_off(int row, int col) {
 // per-wave LDS: the V tile (32 x HD bf16), reused after the loop for the wave's
 // partial O (16 queries x HD fp32, rows padded by 4 floats so the 16 query rows
 // of one store land in different banks) plus m / l
-__device__ __forceinline__ int o_swz(int q) { return ((q & 3) << 4) | (q >> 2); }
+__device__ __forceinline__ int o_swz(int q) { return ((q & 3) << 3) | (q >> 2); }
 
 template <int HD>
 constexpr int decode_wave_lds() {
@@ -57,9 +57,9 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_kernel(
   constexpr int VCH = HD / 8;   // 16-byte chunks per V row
   constexpr int WREG = decode_wave_lds<HD>();  // per-wave LDS bytes (V tile, then O/m/l)
   // fp32 row of the merged partial O: unpadded, columns XOR-swizzled per query row
-  // (bits 0-1 ^= q >> 2, bits 4-5 ^= q & 3) so the 64 lanes of each scalar store
-  // (16 queries x 4 dim groups) hit 64 different banks; a padded row (HD + 4) put
-  // 4 lanes on one bank (profiles/r2_pmc_attention_kernels.md: 15 % conflict cycles)
+  // (bits 0-1 ^= q >> 2, bits 3-4 ^= q & 3) so each 32-lane half of a ds_write_b32
+  // (16 queries x 2 dim groups; banks (a/4) mod 32) hits 32 different banks; a padded
+  // row (HD + 4) put 4 lanes on one bank
   constexpr int OROW = HD;
   constexpr int NT = 64 * NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
