@@ -257,10 +257,14 @@ class LLMEngine:
         return ops.kv_gather(self.pool.kv, ids).cpu()
 
     def import_prefilled(self, prompt: list[int], first_token: int, kv: torch.Tensor,
-                         params: Optional[SamplingParams] = None, rid=None) -> Request:
+                         params: Optional[SamplingParams] = None, rid=None, seed: Optional[int] = None) -> Request:
         """Adopt a sequence another worker prefilled: its pages ``kv`` (``export_request_kv``
         layout) go into fresh pages of this pool and decoding continues from
-        ``first_token`` — no prompt recompute."""
+        ``first_token`` — no prompt recompute.  ``seed``: the exporting request's
+        sampling seed (a seeded request then draws the same tokens as on one
+        worker).  The first token goes through the same stop checks as a local
+        one: a sequence that ended there (EOS / stop id / max_tokens) comes back
+        FINISHED with its pages released."""
         from dgi import ops
         L, two, n, nkv, bs, hd = kv.shape
         pool = self.pool
@@ -273,10 +277,17 @@ class LLMEngine:
         ops.kv_scatter(pool.kv, torch.tensor(ids, dtype=torch.int32, device=self.device),
                        kv.to(self.device, pool.dtype))
         req = Request(prompt, params or SamplingParams(), rid=rid)
+        if seed is not None:
+            req.seed = int(seed) & 0x7FFFFFFF
         req.output = [int(first_token)]
         req.first_token_time = time.perf_counter()
         req.token_times.append(req.first_token_time)
         self.scheduler.add_prefilled(req, ids)
+        reason = self._check_stop(req, int(first_token))
+        if reason is not None:
+            self.scheduler.finish(req, reason)
+            self.stats["finished"] += 1
+            return req
         self.requests[req.rid] = req
         return req
 

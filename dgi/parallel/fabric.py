@@ -170,6 +170,7 @@ class Fabric:
         self._rings_in: dict = {}
         self.ctrl_kind = os.environ.get("DGI_CTRL", "shm")
         self.sent_msgs = 0
+        self.ring_bytes = 0                  # shared memory of the rings this rank created
         self.pairs_connected = 0
         atexit.register(self._unlink_rings)
         # liveness watchdog over the rendezvous store (dgi.parallel.fault)
@@ -354,9 +355,16 @@ class Fabric:
         key = (peer, tag)
         r = self._rings_out.get(key)
         if r is None:
-            from dgi.parallel.shm import create_ring
+            from dgi.parallel.shm import create_ring, shm_free_bytes
+            free = shm_free_bytes()
+            if free is not None and free < capacity:
+                raise RuntimeError(
+                    f"rank {self.rank}: /dev/shm has {free >> 20} MiB free, the {tag} control ring to rank {peer} "
+                    f"needs {capacity >> 20} MiB ({self.ring_bytes >> 20} MiB already mapped by this rank): give "
+                    f"the container a larger /dev/shm (docker --shm-size, e.g. 1g for an 8-GPU node)")
             r = create_ring(self._ring_name(self.rank, peer, tag), capacity)
             self._rings_out[key] = r
+            self.ring_bytes += capacity
         return r
 
     def ring_in(self, peer: int, tag: str, wait_s: float = 0.0):

@@ -11,7 +11,8 @@
   ``,``) at named sites of the step loops:
 
   ``kill``     the rank exits with status 17 at that step
-  ``delay``    sleep ``arg`` ms (default 200) at that step
+  ``delay``    sleep ``arg`` ms (default 200) at that step (a site that passes
+               ``idle`` keeps calling it meanwhile: slow compute, live comms)
   ``raise``    raise ``InjectedFault`` (exercises the failure record path)
   ``corrupt``  the site's ``corrupt`` hook flips bytes of the payload it owns
                (P/D: the migrated KV buffer)
@@ -48,7 +49,7 @@ class FaultPlan:
     def __bool__(self) -> bool:
         return bool(self.rules)
 
-    def check(self, rank: int, step: int, corrupt=None) -> None:
+    def check(self, rank: int, step: int, corrupt=None, idle=None) -> None:
         for i, (r, s, kind, arg) in enumerate(self.rules):
             if r != rank or s != step or i in self.fired:
                 continue
@@ -58,7 +59,12 @@ class FaultPlan:
                 sys.stderr.flush()
                 os._exit(17)
             elif kind == "delay":
-                time.sleep(float(arg or 200) / 1000.0)
+                end = time.perf_counter() + float(arg or 200) / 1000.0
+                if idle is None:
+                    time.sleep(max(0.0, end - time.perf_counter()))
+                while idle is not None and time.perf_counter() < end:
+                    idle()
+                    time.sleep(0.0005)
             elif kind == "raise":
                 raise InjectedFault(f"injected fault on rank {rank} at step {step}")
             elif kind == "corrupt" and corrupt is not None:

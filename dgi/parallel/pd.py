@@ -15,10 +15,12 @@ SURVEY §3.5).  Here:
 * **Decode replicas**: the node runs R decode replicas (``NodeLayout.
   decode_groups``), each a whole-model decode GPU or a decode layer pipeline.
   A replica's **driver** (``DecodeDriver``) allocates pages when a migration
-  is announced, tells its later stages the page ids (each stage receives its
-  own slice straight from the prefill rank) and admits the requests once the
-  driver's slice has landed; a stage installs every announced migration before
-  the first micro-step that can read it.
+  is announced and tells its later stages the page ids (each stage receives its
+  own slice straight from the prefill rank, installs it when it lands and
+  reports LANDED); the driver admits the requests once its own slice has landed
+  and every stage has reported, so sequences already decoding never wait for a
+  migration in flight (reference semantics: a job moves to decode and is
+  placed independently of its transfer, pd_scheduler.py:207-232).
 * **Placement**: each prefill rank runs a node-local instance of the
   reference's ``PrefillDecodeScheduler`` (server/app/services/pd_scheduler.py
   API, reference :274-323): every replica is a registered DECODE worker whose
@@ -322,6 +324,9 @@ class PrefillServer:
         self.engine.model.layer_hook = self._layer_done
 
     def _layer_done(self, li: int) -> None:
+        from dgi.parallel.fault import plan
+        if plan():      # fault site 200000 + layer: a slow layer mid-migration (handshakes stay live)
+            plan().check(self.f.rank, 200000 + li, idle=self.sender.service)
         kv = self.engine.pool.kv
         for d, _rs, ids_t, by_end, _t0, key, nblk in self._streams:
             for si, c0, c1, gi, ng in by_end.get(li, ()):
@@ -471,11 +476,13 @@ class PrefillServer:
 
 
 class _Migration:
-    __slots__ = ("p", "key", "ids", "ids_t", "meta", "toks", "first_known")
+    __slots__ = ("p", "key", "ids", "ids_t", "meta", "toks", "first_known", "installed", "t_announced")
 
     def __init__(self, p, key, ids, ids_t, meta, toks, first_known):
         self.p, self.key, self.ids, self.ids_t = p, key, ids, ids_t
         self.meta, self.toks, self.first_known = meta, toks, first_known
+        self.installed = False          # the driver's own slice is in its pool
+        self.t_announced = time.perf_counter()
 
 
 class DecodeDriver:
@@ -543,6 +550,7 @@ class DecodeDriver:
         self.await_first: dict = {p: collections.deque() for p in self.prefill}
         self.received = 0
         self.recv_bytes = 0
+        self.admit_ms: list = []    # MIGRATE -> admitted (whole replica landed), ms
 
     # ------------------------------------------------------------------ migrations
     def _announced(self, p: int, msg) -> None:
@@ -572,25 +580,42 @@ class DecodeDriver:
         item.first_known = True
 
     def _admit_arrived(self, block: bool = False) -> None:
-        """Install every migration whose slice has landed (and whose first tokens
-        are known) into the pool and admit its requests."""
+        """Admit every migration that is complete on the whole replica: the driver's
+        own slice has landed and is installed, its first tokens are known and every
+        later stage has reported its slice installed (``PipelineEngine.
+        stages_landed``).  Migrations still in flight hold nothing up: the replica
+        keeps stepping the sequences it has."""
         keep = []
         self.kvr.service()
+        pipe = self.engine if isinstance(self.engine, PipelineEngine) else None
+        if pipe is not None:
+            pipe.poll_landed()
         for item in self.inflight:
-            if block:
-                while not item.first_known:      # FIRST follows its MIGRATE on the same channel
-                    self._poll_ctrl(item.p)
+            if not item.installed:
+                if block:
+                    while not item.first_known:      # FIRST follows its MIGRATE on the same channel
+                        self._poll_ctrl(item.p)
+                        self.kvr.service()
+                        time.sleep(0.0002)
+                    groups = self.kvr.wait_landed(item.p, item.key) if self.L_local else []
+                elif item.first_known and (self.L_local == 0 or self.kvr.is_landed(item.p, item.key)):
+                    groups = self.kvr.take(item.p, item.key)
+                else:
+                    keep.append(item)
+                    continue
+                scatter_groups(self.engine.pool.kv, item.ids_t, groups)
+                self.recv_bytes += sum(b.numel() * b.element_size() for _a, _b, b in groups)
+                item.installed = True
+            if pipe is not None and not pipe.stages_landed(item.p, item.key):
+                if not block:
+                    keep.append(item)
+                    continue
+                while not pipe.stages_landed(item.p, item.key):
                     self.kvr.service()
+                    pipe.poll_landed()
                     time.sleep(0.0002)
-                groups = self.kvr.wait_landed(item.p, item.key) if self.L_local else []
-            elif item.first_known and (self.L_local == 0 or self.kvr.is_landed(item.p, item.key)):
-                groups = self.kvr.take(item.p, item.key)
-            else:
-                keep.append(item)
-                continue
             mark("kv_migration_landed", len(item.meta))
-            scatter_groups(self.engine.pool.kv, item.ids_t, groups)
-            self.recv_bytes += sum(b.numel() * b.element_size() for _a, _b, b in groups)
+            self.admit_ms.append((time.perf_counter() - item.t_announced) * 1e3)
             self._admit(item.p, item.ids, item.meta, item.toks)
         self.inflight = keep
 
@@ -755,7 +780,10 @@ class DecodeDriver:
         self.f.flush()
 
     def stats(self) -> dict:
-        return {"kv_transport": self.kvr.stats()}
+        a = sorted(self.admit_ms)
+        return {"kv_transport": self.kvr.stats(),
+                "announce_to_admit_ms_p50": round(a[len(a) // 2], 3) if a else None,
+                "announce_to_admit_ms_p95": round(a[int(0.95 * (len(a) - 1))], 3) if a else None}
 
 
 def build_engine_config(model: str, **kw) -> EngineConfig:

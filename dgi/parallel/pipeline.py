@@ -25,8 +25,14 @@ the shards and has one stage busy at a time (worker/distributed/session.py:
   (``idle_hook``);
 * P/D migrations into a decode pipeline: the driver sends each later stage the
   page ids of an announced migration directly (``send_kv_notice``); the stage
-  receives its own layer slice from the prefill rank (``KVReceiver``) and
-  installs it before the first micro-step that follows the notice.
+  receives its own layer slice from the prefill rank (``KVReceiver``), installs
+  it as soon as it lands — whatever microbatch is flowing — and reports LANDED
+  back to the driver (``poll_landed``).  The driver admits the migration's
+  requests only once every stage has reported, so the first hop that reads
+  those pages follows the install on each stage's stream, and no stage ever
+  blocks a microbatch on a migration it does not contain (round 3 installed
+  every announced migration before every hop: a decode pipeline stalled for up
+  to a prefill step whenever any migration was in flight).
 """
 from __future__ import annotations
 
@@ -177,6 +183,24 @@ class StageGraphs:
         return self.outs[b]
 
 
+def hop_ring_bytes(mb_cap: int, max_tokens: int, max_blocks: int) -> int:
+    """Capacity of a stage's hop ring: room for two of the largest hop messages
+    (``ModelRunner.build_host``: header + packed int32 metadata, whose dense block
+    tables grow with rows x max_model_len / page), rounded up to a power of two —
+    a 512-row microbatch at a 32k context needs ~17 MiB, more than a fixed ring
+    held."""
+    T = max(mb_cap, max_tokens) + mb_cap            # decode rows (bucket-padded) + prefill tokens
+    nb = mb_cap                                     # prefill chunks
+    nlog = mb_cap + nb
+    ntiles = T // max(1, ops.PREFILL_TILE) + nb
+    words = 3 * T + (mb_cap + nb) * max_blocks + mb_cap + (nb + 1) + nb + 2 * ntiles + 5 * nlog
+    need = 2 * (HDR * 8 + 4 * words) + 4096
+    cap = 1 << 20
+    while cap < need:
+        cap <<= 1
+    return cap
+
+
 def stage_split(mc: ModelConfig, stages: int) -> list[tuple[int, int]]:
     # embedding gather is cheap; the LM head GEMM is ~1.9 layers of 70B decode weight traffic
     head = (mc.vocab_size * mc.hidden_size) / max(1, (mc.qkv_size + mc.q_size + 3 * mc.intermediate_size) * mc.hidden_size)
@@ -259,10 +283,14 @@ class PipelineEngine(LLMEngine):
         self.pp = fabric.pp_group(self.ranks)
         # control plane: hop headers to stage 1, tokens back from the last stage,
         # KV-migration notices straight to every later stage
-        self.hop = CtrlChannel(fabric, self.next_rank, HDR, tag="pp", capacity=1 << 23) if self.next_rank is not None \
+        ring = hop_ring_bytes(self.mb_cap, cfg.max_num_batched_tokens, self.runner.max_blocks)
+        self.hop = CtrlChannel(fabric, self.next_rank, HDR, tag="pp", capacity=ring) if self.next_rank is not None \
             else None
         self.tok = CtrlChannel(fabric, self.last_rank, 1, tag="tok") if self.next_rank is not None else None
         self.notice = {r: CtrlChannel(fabric, r, 1, tag="kvn") for r in self.ranks[1:]} if kv_sources else {}
+        # stage -> driver: (src, key) of every migration slice a stage has installed
+        self.landed_in = {r: CtrlChannel(fabric, r, 2, tag="kvl") for r in self.ranks[1:]} if kv_sources else {}
+        self.stage_landed: collections.Counter = collections.Counter()
         self.idle_hook = None       # called while waiting for a microbatch's tokens (P/D: KV handshakes)
         self.wait_s = 0.0
         # decode micro-steps of this stage replay hipGraphs (same buckets on every stage)
@@ -359,6 +387,26 @@ class PipelineEngine(LLMEngine):
         for ch in self.notice.values():
             ch.send_var(msg)
 
+    def poll_landed(self) -> None:
+        """Take in the stages' LANDED reports."""
+        for ch in self.landed_in.values():
+            while True:
+                m = ch.poll()
+                if m is None:
+                    break
+                self.stage_landed[(int(m[0]), int(m[1]))] += 1
+
+    def stages_landed(self, src: int, key: int) -> bool:
+        """Every later stage has installed its slice of migration ``key`` from ``src``
+        (its scatter is on the stage's stream ahead of any hop sent from now on)."""
+        if not self.landed_in:
+            return True
+        k = (src, key)
+        if self.stage_landed[k] >= len(self.landed_in):
+            del self.stage_landed[k]
+            return True
+        return False
+
     def _ctl(self, kind: int) -> None:
         self.drain()
         if self.hop is not None:
@@ -407,20 +455,24 @@ class StageWorker:
         self.n_layers = b - a
         self.steps = 0
         self.pp = fabric.pp_group(self.ranks)
-        self.hop_in = CtrlChannel(fabric, self.prev, HDR, tag="pp", capacity=1 << 23)
-        self.hop_out = CtrlChannel(fabric, self.next, HDR, tag="pp", capacity=1 << 23) if self.next is not None \
+        ring = hop_ring_bytes(self.mb_cap, cfg.max_num_batched_tokens, self.runner.max_blocks)
+        self.hop_in = CtrlChannel(fabric, self.prev, HDR, tag="pp")
+        self.hop_out = CtrlChannel(fabric, self.next, HDR, tag="pp", capacity=ring) if self.next is not None \
             else None
         self.tok = CtrlChannel(fabric, self.driver, 1, tag="tok") if self.is_last else None
         self.tok_pending: collections.deque = collections.deque()   # (event, pinned tokens, n) in order
         # P/D: page-id notices from the driver, slices from the prefill ranks
         self.kvr = None
         self.notice = None
-        self.kv_pending: collections.deque = collections.deque()    # (src, key, ids_t) not installed yet
+        self.kv_pending: list = []                                  # [src, key, ids_t] not installed yet
+        self.landed_out = None
         if kv_sources:
             from dgi.parallel.kv_transfer import KVReceiver
             self.notice = CtrlChannel(fabric, self.driver, 1, tag="kvn")
+            self.landed_out = CtrlChannel(fabric, self.driver, 2, tag="kvl")
             self.kvr = KVReceiver(fabric, kv_sources, (2, mc.num_kv_heads, cfg.block_size, mc.head_dim), cfg.dtype)
         self.installed = 0
+        self.kv_block_s = 0.0          # host time a stage spent blocked on KV (only at PAUSE / STOP)
         self.sgraphs = None
         if cfg.use_graphs and dev.type == "cuda":
             self.sgraphs = StageGraphs(self.model, self.runner, pipeline_buckets(self.mb_cap), first=False,
@@ -439,31 +491,45 @@ class StageWorker:
             self.kv_pending.append((int(m[0]), int(m[1]), ids_t))
 
     def _service(self) -> None:
-        """Everything a stage does while it waits: KV handshakes, notices, token
-        publication, and installing migrations whose slices have landed."""
+        """Everything a stage does between hops and while it waits: KV handshakes,
+        notices, token publication, and installing every migration whose slice
+        has landed (in landing order, not announcement order: slices from
+        different prefill ranks land independently)."""
         self._take_notices()
         if self.kvr is not None:
             self.kvr.service()
-            while self.kv_pending and (self.n_layers == 0 or
-                                       self.kvr.is_landed(self.kv_pending[0][0], self.kv_pending[0][1])):
-                self._install_one()
+            if self.kv_pending:
+                keep = []
+                for item in self.kv_pending:
+                    if self.n_layers == 0 or self.kvr.is_landed(item[0], item[1]):
+                        self._install(item, block=False)
+                    else:
+                        keep.append(item)
+                self.kv_pending = keep
         self._publish_tokens()
 
-    def _install_one(self, block: bool = False) -> None:
+    def _install(self, item, block: bool) -> None:
         from dgi.parallel.kv_transfer import scatter_groups
-        src, key, ids_t = self.kv_pending.popleft()
-        if self.n_layers == 0:          # a layer-less stage (more stages than layers): nothing is sent to it
-            return
-        groups = self.kvr.wait_landed(src, key, idle=self._publish_tokens) if block else self.kvr.take(src, key)
-        scatter_groups(self.pool.kv, ids_t, groups)
-        self.installed += 1
+        src, key, ids_t = item
+        if self.n_layers:               # a layer-less stage (more stages than layers) is sent nothing
+            if block:
+                t0 = time.perf_counter()
+                groups = self.kvr.wait_landed(src, key, idle=self._publish_tokens)
+                self.kv_block_s += time.perf_counter() - t0
+            else:
+                groups = self.kvr.take(src, key)
+            scatter_groups(self.pool.kv, ids_t, groups)
+            self.installed += 1
+        # the driver admits the migration's requests once every stage has reported
+        self.landed_out.send([src, key])
 
     def _install_all(self) -> None:
-        """Every migration the driver announced before this point is in the pool
-        (its notice was written before the hop that follows it)."""
+        """Phase boundary (PAUSE / STOP): every announced migration is installed.
+        The driver quiesces migrations before pausing, so this normally finds
+        nothing to wait for."""
         self._take_notices()
         while self.kv_pending:
-            self._install_one(block=True)
+            self._install(self.kv_pending.pop(0), block=True)
 
     # ------------------------------------------------------------------ tokens (last stage)
     def _publish_tokens(self, block: bool = False) -> None:
@@ -517,7 +583,9 @@ class StageWorker:
             from dgi.parallel.fault import plan
             if plan():
                 plan().check(f.rank, self.steps)
-            self._install_all()
+            # installs whatever has landed; never waits (a hop only carries requests the
+            # driver admitted after every stage reported their pages installed)
+            self._service()
             h = [int(x) for x in hdr]
             if self.hop_out is not None:           # the next stage can post its receive now
                 self.hop_out.send_bytes(b)

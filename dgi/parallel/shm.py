@@ -26,6 +26,16 @@ def _shm():
     return _mod
 
 
+def shm_free_bytes(path: str = "/dev/shm") -> Optional[int]:
+    """Free bytes of the shared-memory file system the rings live in (None if unknown)."""
+    import os
+    try:
+        st = os.statvfs(path)
+    except OSError:
+        return None
+    return st.f_bavail * st.f_frsize
+
+
 def create_ring(name: str, capacity: int):
     return _shm().Ring.create(name, int(capacity))
 

@@ -43,6 +43,8 @@ logger = logging.getLogger(__name__)
 # defaults when a worker does not report capabilities (one MI355X: ~2.5 PF dense bf16, 8 TB/s)
 DEFAULT_TFLOPS = 2500.0
 DEFAULT_HBM_GBPS = 8000.0
+# decode-job params the coordinator owns (stripped from what the client sent)
+CLIENT_STRIP = ("kv_url", "kv_token", "kv_source", "pd_phase", "first_token", "prefill_text", "kv_cache_key")
 
 
 def _run(coro):
@@ -149,7 +151,9 @@ class PDCoordinator:
                 # the byte move itself is the decode worker's (dgi RCCL in-node, re-prefill across nodes)
                 self.migrator.record(kv_key, a.migration_source, a.worker_id, int(res.get("kv_bytes", 0)),
                                      (time.perf_counter() - t0) * 1000.0)
-        params = dict(job.params or {})
+        # fields only the coordinator may set: a client-supplied kv_url / kv_token /
+        # kv_source never reaches the decode worker
+        params = {k: v for k, v in (job.params or {}).items() if k not in CLIENT_STRIP}
         params["pd_phase"] = "decode"
         params["first_token"] = res.get("first_token")
         params["prefill_text"] = res.get("response", "")
@@ -160,6 +164,8 @@ class PDCoordinator:
             # instead of re-running the prompt, when the prefill worker exported them
             if res.get("kv_url"):
                 params["kv_url"] = res["kv_url"]
+                if res.get("kv_token"):
+                    params["kv_token"] = res["kv_token"]
         return {"phase": "decode", "target_worker_id": a.worker_id if a is not None else None, "params": params,
                 "estimated_latency_ms": a.estimated_latency_ms if a is not None else None}
 

@@ -15,11 +15,14 @@ import threading
 import time
 from typing import Any, Dict, Optional
 
-from fastapi import FastAPI, HTTPException
+from fastapi import FastAPI, HTTPException, Request
 from fastapi.responses import StreamingResponse
 from pydantic import BaseModel
 
 logger = logging.getLogger(__name__)
+
+# params of the coordinator's cluster P/D job path, never taken from a direct caller
+DIRECT_STRIP = ("pd", "pd_phase", "kv_url", "kv_token", "kv_source", "first_token")
 
 
 class DirectInferenceRequest(BaseModel):
@@ -80,24 +83,31 @@ class DirectServer:
                     "engines": {k: e.get_status() for k, e in w.engines.items()}}
 
         @app.get("/kv/{key}")
-        async def kv_pull(key: str):
+        async def kv_pull(key: str, request: Request):
             """Cluster P/D: the pages of a sequence this worker prefilled (dgi.kv.transfer
-            blob), pulled once by the decode worker the scheduler placed it on."""
+            blob), pulled once by the decode worker the scheduler placed it on.  The
+            pull must present the export's secret (``X-KV-Token``), which the
+            coordinator hands only to that decode worker; anything else gets 404 and
+            leaves the blob in place."""
             from fastapi.responses import Response
             eng = self.worker.engines.get("llm")
             store = getattr(eng, "kv_exports", None)
-            blob = store.take(key) if store is not None else None
+            token = request.headers.get("X-KV-Token")
+            blob = await asyncio.to_thread(store.take, key, token) if (store is not None and token) else None
             if blob is None:
-                raise HTTPException(404, f"no exported KV under {key}")
+                raise HTTPException(404, "no exported KV under that key for this token")
             return Response(content=blob, media_type="application/octet-stream")
 
         @app.post("/inference", response_model=DirectInferenceResponse)
         async def direct_inference(req: DirectInferenceRequest):
             self._admit(req.type)
             t0 = time.time()
+            # cluster P/D phases only come from the coordinator's job path: a direct caller
+            # cannot make this worker pull KV from a URL of its choosing
+            params = {k: v for k, v in (req.params or {}).items() if k not in DIRECT_STRIP}
             try:
                 result = await asyncio.wait_for(
-                    asyncio.to_thread(self.worker.execute, req.type, req.params, "direct"),
+                    asyncio.to_thread(self.worker.execute, req.type, params, "direct"),
                     timeout=req.timeout_seconds)
                 return DirectInferenceResponse(success=True, result=result,
                                                processing_time_ms=int((time.time() - t0) * 1000))

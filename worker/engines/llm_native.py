@@ -44,11 +44,12 @@ def _merged(config: Dict[str, Any]) -> Dict[str, Any]:
 
 
 class _Pending:
-    __slots__ = ("req", "loop", "future", "stream_q", "sent", "cfg", "prompt_len", "export_key")
+    __slots__ = ("req", "loop", "future", "stream_q", "sent", "cfg", "prompt_len", "export_key", "export_token")
 
-    def __init__(self, loop, future, stream_q, cfg, prompt_len, export_key=None):
+    def __init__(self, loop, future, stream_q, cfg, prompt_len, export_key=None, export_token=None):
         self.req = None
         self.export_key = export_key    # cluster P/D prefill phase: export the KV at the first token
+        self.export_token = export_token  # secret the decode worker presents to pull it
         self.loop = loop
         self.future = future
         self.stream_q = stream_q
@@ -149,7 +150,7 @@ class NativeLLMEngine(LLMBaseEngine):
 
     # ------------------------------------------------------------------ engine thread
     def _loop(self) -> None:
-        from dgi.sched.request import SamplingParams
+        from dgi.sched.request import SamplingParams, Status
         eng = self.engine
         while not self._stop.is_set():
             while True:
@@ -161,13 +162,12 @@ class NativeLLMEngine(LLMBaseEngine):
                     sp = SamplingParams(max_tokens=cfg.max_tokens, temperature=cfg.temperature, top_p=cfg.top_p,
                                         top_k=cfg.top_k)
                     if imported is not None:       # decode phase of a cluster P/D job: KV pulled from its prefill worker
-                        first, kv = imported
-                        p.req = eng.import_prefilled(prompt, first, kv, sp)
+                        first, kv, seed = imported
+                        p.req = eng.import_prefilled(prompt, first, kv, sp, seed=seed)
                         self.stats["kv_imported"] += 1
                         if p.stream_q is not None:
                             p.loop.call_soon_threadsafe(p.stream_q.put_nowait, first)
-                        if sp.max_tokens <= 1:
-                            eng.abort(p.req.rid)
+                        if p.req.status is Status.FINISHED:   # EOS / stop id / max_tokens at the first token
                             self._resolve(p, p.req)
                             continue
                     else:
@@ -199,17 +199,44 @@ class NativeLLMEngine(LLMBaseEngine):
 
     def _on_first_token(self, req) -> None:
         """Engine thread, first token of ``req`` sampled and its pages still held:
-        a P/D prefill-phase request exports them for its decode worker."""
+        a P/D prefill-phase request exports them for its decode worker.  Only the
+        page gather is enqueued here (a fresh tensor, so the pages may be freed
+        right after); the device-to-host copy waits on an event and the packing
+        runs on the export thread, so the other sequences of the batch never wait
+        for it (``KVExportStore.put_pending``)."""
         p = self._pending.get(req.rid)
         if p is None or p.export_key is None:
             return
+        from dgi import ops
         from dgi.kv.transfer import pack_kv
-        mc = self.engine.model_cfg
-        blob = pack_kv(self.engine.export_request_kv(req),
-                       {"prompt": list(req.prompt), "first_token": int(req.output[0]), "model": mc.name,
-                        "num_layers": mc.num_layers, "seed": int(req.seed)})
-        self.kv_exports.put(p.export_key, blob)
+        eng = self.engine
+        mc = eng.model_cfg
+        meta = {"prompt": list(req.prompt), "first_token": int(req.output[0]), "model": mc.name,
+                "num_layers": mc.num_layers, "seed": int(req.seed)}
+        nb = (req.num_computed + eng.pool.block_size - 1) // eng.pool.block_size
+        ids = torch.tensor(req.blocks[:nb], dtype=torch.int32, device=eng.device)
+        pages = ops.kv_gather(eng.pool.kv, ids)
+        ev = None
+        if pages.is_cuda:
+            host = torch.empty(pages.shape, dtype=pages.dtype, pin_memory=True)
+            host.copy_(pages, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            host = pages
+
+        def pack():
+            if ev is not None:
+                ev.synchronize()
+            return pack_kv(host, meta)
+        self.kv_exports.put_pending(p.export_key, self._export_pool().submit(pack), token=p.export_token)
         self.stats["kv_exported"] += 1
+
+    def _export_pool(self):
+        if getattr(self, "_exporter", None) is None:
+            from concurrent.futures import ThreadPoolExecutor
+            self._exporter = ThreadPoolExecutor(max_workers=1, thread_name_prefix="kv-export")
+        return self._exporter
 
     def _resolve(self, p: _Pending, req) -> None:
         text = self.tokenizer.decode(req.output, skip_special_tokens=True)
@@ -237,13 +264,14 @@ class NativeLLMEngine(LLMBaseEngine):
         p.loop.call_soon_threadsafe(_set)
 
     def _submit(self, messages, cfg: GenerationConfig, stream: bool = False, export_key: Optional[str] = None,
-                prompt: Optional[List[int]] = None, imported=None) -> _Pending:
+                prompt: Optional[List[int]] = None, imported=None, export_token: Optional[str] = None) -> _Pending:
         if not self.loaded:
             raise RuntimeError("model not loaded")
         loop = asyncio.get_running_loop()
         if prompt is None:
             prompt = chat_prompt_ids(self.tokenizer, messages)
-        p = _Pending(loop, loop.create_future(), asyncio.Queue() if stream else None, cfg, len(prompt), export_key)
+        p = _Pending(loop, loop.create_future(), asyncio.Queue() if stream else None, cfg, len(prompt), export_key,
+                     export_token)
         self.stats["requests"] += 1
         self._inbox.put((prompt, p, cfg, imported))
         self._wake.set()
@@ -252,15 +280,20 @@ class NativeLLMEngine(LLMBaseEngine):
     # ------------------------------------------------------------------ cluster P/D (server services/pd_runtime.py)
     def prefill_export(self, params: Dict[str, Any], key: str) -> Dict[str, Any]:
         """Prefill phase: sample the first token and keep the sequence's KV pages under
-        ``key`` (``kv_exports``) for the decode worker to pull (``GET /kv/{key}``)."""
+        ``key`` (``kv_exports``) for the decode worker to pull (``GET /kv/{key}`` with
+        the returned ``kv_token``, or straight from the store when the decode phase
+        lands on this worker)."""
+        from dgi.kv.transfer import new_token
         from .llm_base import generation_config_from_params, result_to_response
         cfg = generation_config_from_params({**params, "max_tokens": 1})
+        token = new_token()
 
         async def run():
-            return await self._submit(self._messages_of(params), cfg, export_key=key).future
+            return await self._submit(self._messages_of(params), cfg, export_key=key, export_token=token).future
         res = self._run_sync(run())
         out = result_to_response(res)
         out["kv_cache_key"] = key
+        out["kv_token"] = token
         return out
 
     def decode_import(self, params: Dict[str, Any], blob: bytes) -> Dict[str, Any]:
@@ -272,9 +305,11 @@ class NativeLLMEngine(LLMBaseEngine):
             raise ValueError(f"KV of model {meta.get('model')} offered to a {self.engine.model_cfg.name} engine")
         cfg = generation_config_from_params(params)
 
+        seed = meta.get("seed")
+
         async def run():
             return await self._submit(None, cfg, prompt=list(meta["prompt"]),
-                                      imported=(int(meta["first_token"]), kv)).future
+                                      imported=(int(meta["first_token"]), kv, seed)).future
         return result_to_response(self._run_sync(run()))
 
     def _run_sync(self, coro):

@@ -281,27 +281,67 @@ class Worker:
         if phase == "prefill":
             if engine is not None and hasattr(engine, "prefill_export"):
                 out = engine.prefill_export({**params, "max_tokens": 1}, key)
-                base = getattr(self, "direct_url", None)
+                base = self._kv_pull_base()
                 return {**out, "phase": "prefill", "first_token": out.get("response", ""), "kv_cache_key": key,
                         "kv_url": f"{base.rstrip('/')}/kv/{key}" if base else None}
             out = self._execute("llm", {**params, "max_tokens": 1}, job_id)
             return {**out, "phase": "prefill", "first_token": out.get("response", ""), "kv_cache_key": key}
-        clean = {k: v for k, v in params.items() if k not in ("pd_phase", "first_token", "kv_url")}
-        url = params.get("kv_url")
-        if url and engine is not None and hasattr(engine, "decode_import"):
-            try:
-                import httpx
-                t0 = time.perf_counter()
-                r = httpx.get(url, timeout=60.0)
-                r.raise_for_status()
-                pull_ms = (time.perf_counter() - t0) * 1000.0
-                out = engine.decode_import(clean, r.content)
-                return {**out, "phase": "decode", "kv_source": params.get("kv_source"), "reprefilled": False,
-                        "kv_bytes": len(r.content), "kv_pull_ms": round(pull_ms, 2)}
-            except Exception as e:     # source gone / evicted: fall back to recomputing the prompt
-                logger.warning("KV pull from %s failed (%s): re-prefilling", url, e)
+        clean = {k: v for k, v in params.items() if k not in ("pd_phase", "first_token", "kv_url", "kv_token")}
+        if engine is not None and hasattr(engine, "decode_import"):
+            # decode placed on the worker that prefilled: the pages are in our own store
+            store = getattr(engine, "kv_exports", None)
+            own = store.take(key, check_token=False) if store is not None else None
+            if own is not None:
+                out = engine.decode_import(clean, own)
+                return {**out, "phase": "decode", "kv_source": "local", "reprefilled": False,
+                        "kv_bytes": len(own), "kv_pull_ms": 0.0}
+            url = params.get("kv_url")
+            if url and self._kv_url_ok(url, job_id):
+                try:
+                    import httpx
+                    t0 = time.perf_counter()
+                    r = httpx.get(url, timeout=60.0, follow_redirects=False,
+                                  headers={"X-KV-Token": str(params.get("kv_token") or "")})
+                    r.raise_for_status()
+                    pull_ms = (time.perf_counter() - t0) * 1000.0
+                    out = engine.decode_import(clean, r.content)
+                    return {**out, "phase": "decode", "kv_source": params.get("kv_source"), "reprefilled": False,
+                            "kv_bytes": len(r.content), "kv_pull_ms": round(pull_ms, 2)}
+                except Exception as e:     # source gone / evicted: fall back to recomputing the prompt
+                    logger.warning("KV pull from %s failed (%s): re-prefilling", url, e)
         out = self._execute("llm", clean, job_id)
         return {**out, "phase": "decode", "kv_source": params.get("kv_source"), "reprefilled": True}
+
+    def _kv_pull_base(self) -> Optional[str]:
+        """Base URL decode workers pull this worker's exported KV from: the direct
+        server's public URL.  A loopback address is only reachable from this host,
+        so it is advertised only when the operator set it explicitly (a decode
+        worker elsewhere would pull from its own localhost and silently re-prefill)."""
+        base = getattr(self, "direct_url", None)
+        if not base:
+            return None
+        from urllib.parse import urlparse
+        host = (urlparse(base).hostname or "").lower()
+        explicit = bool(getattr(getattr(getattr(self, "config", None), "direct", None), "public_url", None))
+        if host in ("127.0.0.1", "localhost", "::1") and not explicit and not getattr(self, "kv_loopback_ok", False):
+            if not getattr(self, "_warned_loopback", False):
+                logger.warning("direct server has no public URL (set GPU_DIRECT_PUBLIC_URL): exported KV is not "
+                               "advertised to decode workers on other hosts")
+                self._warned_loopback = True
+            return None
+        return base
+
+    @staticmethod
+    def _kv_url_ok(url: str, job_id: str) -> bool:
+        """Only pull what the coordinator can have handed us: an http(s) ``/kv/<worker>:<job>``
+        URL of THIS job, no query, no credentials (a client-supplied URL is stripped by the
+        coordinator; this refuses anything else that reaches the worker)."""
+        from urllib.parse import unquote, urlparse
+        u = urlparse(url)
+        if u.scheme not in ("http", "https") or not u.hostname or u.username or u.password or u.query:
+            return False
+        path = unquote(u.path)
+        return path.startswith("/kv/") and path.endswith(f":{job_id}") and "/" not in path[4:]
 
     def _execute(self, job_type: str, params: Dict[str, Any], job_id: str = "direct") -> Dict[str, Any]:
         engine = self.engines.get(job_type)
