@@ -6,11 +6,12 @@ Layouts (dgi.parallel.plan):
   pdpp  P prefill ranks + a decode layer pipeline (KV over RCCL, then
         layer-sliced down the pipeline)  — the BASELINE north-star layout
 
-The decode driver is the clock: its steps are the benchmark steps.  Phase
-boundaries (end of warmup, end of timed window) are broadcast to prefill
-ranks over the control store and to pipeline stages as PAUSE messages, then
-every rank meets in a barrier, so the timed window is [barrier, barrier] on
-all ranks; tokens are summed over ranks and the elapsed time is the max.
+The decode driver is the clock: its micro-steps make the benchmark steps, and
+the timed window is a timestamp window on the node's shared monotonic clock
+(section "timed window" below): every rank keeps serving across both edges,
+counts the tokens it produced inside [t0, t1], and only after t1 fences its KV
+transfers, pauses its pipeline, synchronises and meets the others in a
+barrier.  Tokens are summed over ranks; the elapsed time is t1 - t0.
 """
 from __future__ import annotations
 
@@ -153,6 +154,83 @@ def run_distributed(args, layout_kind: str, dist):
                                   "tpots": all_tpots, "e2es": all_e2es, "ranks": per_rank}
 
 
+# ---------------------------------------------------------------------------- timed window
+#
+# Multi-rank serving runs are timed by a TIMESTAMP window on the node's shared
+# monotonic clock (``time.perf_counter`` is CLOCK_MONOTONIC: one clock for every
+# process of the node).  The clock rank (a decode driver) steps through ramp +
+# warm-up, takes t0 and tells every rank; after K node steps it takes t1 and
+# tells every rank again.  Every rank counts the tokens IT produced whose
+# application timestamp (``Request.token_times``) lies in [t0, t1]; nothing is
+# drained, fenced or paused inside the window (pipelines stay full across both
+# edges) — fences, pipeline pauses, the device synchronise and the barrier all
+# happen after t1.  A node step is ``micro`` decode micro-steps of the clock
+# replica, enough to cover one prefill step (``node_step_micro``), so a
+# --steps 20 window holds ~20 prefill steps of every prefill rank.
+
+MSG_T0, MSG_T1 = 1, 2
+
+
+def _ns(t: float) -> int:
+    return int(round(t * 1e9))
+
+
+def _sec(ns) -> float:
+    return int(ns) / 1e9
+
+
+def node_step_micro(cap, k: int, n_mb: int) -> int:
+    """Decode micro-steps of the clock replica per node step: at least one full
+    pipeline round (``n_mb``) and at least one prefill step's worth of micro-steps
+    under the capacity table (70B 5P+PP3: 202 ms prefill step / 42.5 ms stage step
+    -> 5)."""
+    micro = max(1, n_mb)
+    if cap is not None and cap.prefill_step_ms and cap.decode_step_ms.get(k):
+        micro = max(micro, -(-int(cap.prefill_step_ms * 1000) // int(cap.decode_step_ms[k] * 1000)))
+    return micro
+
+
+class TokenLog:
+    """Tokens this rank produced, by application time; filtered once the window is known."""
+
+    def __init__(self):
+        self.times: list = []          # one timestamp per produced token
+        self.firsts: list = []         # (time, ttft) of first tokens produced here
+        self.finished: list = []       # requests finished here
+        self.steps: list = []          # end time of every engine step that ran
+
+    def outputs(self, outs, count_first: bool = True) -> int:
+        for o in outs:
+            r = o.request
+            t = r.token_times[-1] if r.token_times else time.perf_counter()
+            self.times.append(t)
+            if count_first and len(r.output) == 1 and r.ttft is not None:
+                self.firsts.append((t, r.ttft))
+            if o.finished:
+                self.finished.append(r)
+        return len(outs)
+
+    def window(self, t0: float, t1: float) -> dict:
+        inw = lambda t: t0 <= t <= t1   # noqa: E731
+        fin = [r for r in self.finished if r.finish_time is not None and inw(r.finish_time)]
+        return {"tokens": sum(1 for t in self.times if inw(t)),
+                "ttfts": [v for t, v in self.firsts if inw(t)],
+                "tpots": _tpots(fin), "e2es": [r.finish_time - r.arrival for r in fin],
+                "steps_in_window": sum(1 for t in self.steps if inw(t))}
+
+
+def recount(reqs, t0: float, t1: float) -> int:
+    """Independent count for the tests: tokens of ``reqs`` (the requests whose tokens this
+    rank produced) with a timestamp in the window, read from the requests themselves
+    after the run (``DGI_BENCH_RECOUNT=1``)."""
+    return sum(1 for r in reqs for t in r.token_times if t0 <= t <= t1)
+
+
+def _bcast(chans, kind: int, t: float) -> None:
+    for ch in chans:
+        ch.send([MSG_PHASE, kind, _ns(t)])
+
+
 # ---------------------------------------------------------------------------- layer pipeline only
 
 def _run_pp(args, f, cfg, layout, role, sp, rng, conc):
@@ -162,59 +240,48 @@ def _run_pp(args, f, cfg, layout, role, sp, rng, conc):
         eng = PipelineEngine(cfg, f, ranks)
         vocab = eng.model_cfg.vocab_size
         inflight = set()
+        log = TokenLog()
+        micro = max(1, eng.n_mb)          # node step: one full pipeline round
 
         def top(limit):
             while len(inflight) < limit:
                 inflight.add(eng.add_request(_prompt(rng, args.prompt_len, vocab), sp).rid)
 
         def step():
-            n, firsts = 0, []
-            for o in eng.step():
-                n += 1
-                if len(o.request.output) == 1:
-                    firsts.append(o.request.ttft)
+            outs = eng.step()
+            log.outputs(outs)
+            for o in outs:
                 if o.finished:
                     inflight.discard(o.rid)
-            return n, firsts
 
         ramp = args.ramp_steps if args.ramp_steps >= 0 else args.output_len
         per = max(1, -(-conc // max(1, ramp)))
         for i in range(ramp):
             top(min(conc, (i + 1) * per))
             step()
-        for _ in range(args.warmup):
+        for _ in range(args.warmup * micro):
             top(conc)
             step()
-        eng.pause_stages()
-        torch.cuda.synchronize() if f.device.type == "cuda" else None
-        f.barrier()
         t0 = time.perf_counter()
-        toks, ttfts = 0, []
-        for _ in range(args.steps):
+        for _ in range(args.steps * micro):
             top(conc)
-            n, fs = step()
-            toks += n
-            ttfts += fs
-        for o in eng.drain():
-            toks += 1
+            step()
+        t1 = time.perf_counter()
         eng.pause_stages()
         torch.cuda.synchronize() if f.device.type == "cuda" else None
         f.barrier()
-        el = time.perf_counter() - t0
         eng.stop_stages()
-        return toks, el, ttfts, {"tokens": toks, "steps": eng.stats["steps"],
-                                 "token_wait_s": round(eng.wait_s, 3)}
+        w = log.window(t0, t1)
+        return w["tokens"], t1 - t0, w["ttfts"], {"tokens": w["tokens"], "steps": eng.stats["steps"],
+                                                   "micro_per_step": micro, "tpots": w["tpots"], "e2es": w["e2es"],
+                                                   "window": {"t0_ns": _ns(t0), "t1_ns": _ns(t1)},
+                                                   "token_wait_s": round(eng.wait_s, 3)}
     w = StageWorker(cfg, f, ranks)
     w.run()
     torch.cuda.synchronize() if f.device.type == "cuda" else None
     f.barrier()
-    t0 = time.perf_counter()
     w.run()
-    torch.cuda.synchronize() if f.device.type == "cuda" else None
-    f.barrier()
-    el = time.perf_counter() - t0
-    w.run()
-    return 0, el, [], {"stage_steps": w.steps}
+    return 0, 0.0, [], {"stage_steps": w.steps}
 
 
 # ---------------------------------------------------------------------------- P/D (+ decode pipelines)
@@ -230,22 +297,21 @@ def _tpots(reqs) -> list:
 
 
 def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
-    """P prefill ranks + R decode replicas.  The first replica's driver is the
-    clock: its productive steps are the benchmark steps, and it broadcasts the
-    phase boundaries (end of warm-up, end of the timed window) to every
+    """P prefill ranks + R decode replicas, timed by the timestamp window above.
+    The first replica's driver is the clock: it broadcasts t0 / t1 to every
     prefill rank and every other replica driver."""
     from dgi.parallel.fabric import CtrlChannel
     from dgi.parallel.pd import DecodeDriver, PrefillServer
     from dgi.parallel.pipeline import StageWorker
-    from dgi.parallel.plan import decode_local_fraction, prefill_overflow_cap
+    from dgi.parallel.plan import capacity_for, decode_local_fraction, prefill_overflow_cap
 
     clock = layout.drivers[0]
+    cap = capacity_for(args.model)
+    debug_counts = os.environ.get("DGI_BENCH_RECOUNT") == "1"
     if role == "prefill":
         lc = getattr(args, "prefill_local_cap", -1)
         lc = prefill_overflow_cap(layout, model=args.model) if lc < 0 else lc
         # prefill step size: the capacity table's (TTFT: a prompt admitted just in time waits ~1 step)
-        from dgi.parallel.plan import capacity_for
-        cap = capacity_for(args.model)
         pmbt = getattr(args, "prefill_mbt", 0) or (cap.prefill_mbt if cap is not None else args.max_batched_tokens)
         pcfg = EngineConfig(**{**cfg.__dict__, "max_num_seqs": 64 + lc, "max_num_batched_tokens": pmbt})
         srv = PrefillServer(pcfg, f, layout, local_cap=lc)
@@ -253,50 +319,59 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
         vocab = srv.engine.model_cfg.vocab_size
         # one step's worth of prompts, topped up right before each step
         depth = max(1, pmbt // max(1, args.prompt_len))
+        log = TokenLog()
+        submitted = []
 
         # open loop (--arrival-rate, node-wide req/s): this rank's Poisson share; the prompt's
         # arrival is its scheduled time, so TTFT includes every wait (queue, credit, prefill)
         rate = float(getattr(args, "arrival_rate", 0.0) or 0.0) / max(1, len(layout.prefill_ranks))
         nxt = {"t": time.perf_counter()}
 
+        def submit():
+            r = srv.submit(_prompt(rng, args.prompt_len, vocab), sp)
+            if debug_counts:
+                submitted.append(r)
+            return r
+
         def top_up():
             if rate > 0:
                 now = time.perf_counter()
                 while nxt["t"] <= now:
-                    r = srv.submit(_prompt(rng, args.prompt_len, vocab), sp)
-                    r.arrival = nxt["t"]
+                    submit().arrival = nxt["t"]
                     nxt["t"] += rng.expovariate(rate)
                 return
             while len(srv.pending) + len(srv.engine.scheduler.waiting) < depth:
-                srv.submit(_prompt(rng, args.prompt_len, vocab), sp)
+                submit()
 
-        def serve_until_phase():
-            n, ttfts = 0, []
-            while ph.poll() is None:
-                top_up()
-                before = len(srv.ttfts)
-                n += len(srv.step())
-                ttfts += srv.ttfts[before:]
-            return n, ttfts
-
-        # at each phase boundary: fence = drain every KV transfer this rank started (the
-        # decode ranks keep servicing their handshakes) and report the migration count;
-        # afterwards nothing is in flight and the device can be synchronised
-        serve_until_phase()
+        t0 = t1 = None
+        while t1 is None:
+            m = ph.poll()
+            if m is not None:
+                if int(m[1]) == MSG_T0:
+                    t0 = _sec(m[2])
+                else:
+                    t1 = _sec(m[2])
+                continue
+            top_up()
+            s0 = srv.engine.stats["steps"]
+            log.outputs(srv.step())
+            if srv.engine.stats["steps"] > s0:
+                log.steps.append(time.perf_counter())
+        # after the window: drain every KV transfer this rank started (the decode ranks keep
+        # servicing their handshakes) and report the migration count; then synchronise
         srv.fence()
         torch.cuda.synchronize() if f.device.type == "cuda" else None
         f.barrier()
-        t0 = time.perf_counter()
-        n, ttfts = serve_until_phase()
-        srv.fence()
-        torch.cuda.synchronize() if f.device.type == "cuda" else None
-        f.barrier()
-        el = time.perf_counter() - t0
         srv.finish()
-        return n, el, ttfts, {"tokens": n, "prompts": len(ttfts), "prefill_mbt": pmbt, "migrated": srv.migrated, "migrate_s": round(srv.migrate_time, 3),
-                              "sent_GB": round(srv.sent_bytes / 1e9, 3), "local_cap": lc,
-                              "local_tokens": srv.local_tokens, "pd_scheduler": srv.pd_stats(),
-                              "migration_ms_p50": srv.pd_stats()["migration_ms_p50"]}
+        w = log.window(t0, t1)
+        ex = {"tokens": w["tokens"], "prompts": len(w["ttfts"]), "prefill_steps_in_window": w["steps_in_window"],
+              "prefill_mbt": pmbt, "migrated": srv.migrated, "migrate_s": round(srv.migrate_time, 3),
+              "sent_GB": round(srv.sent_bytes / 1e9, 3), "local_cap": lc, "local_tokens": srv.local_tokens,
+              "pd_scheduler": srv.pd_stats(), "migration_ms_p50": srv.pd_stats()["migration_ms_p50"],
+              "tpots": w["tpots"], "e2es": w["e2es"]}
+        if debug_counts:
+            ex["recount"] = recount(submitted, t0, t1)
+        return w["tokens"], t1 - t0, w["ttfts"], ex
 
     if role == "decode_driver":
         # a replica the prefill side cannot saturate also serves local prompts with a slice of its pool
@@ -309,93 +384,93 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
         phases = [CtrlChannel(f, p, 4, tag="phase") for p in others] if is_clock else \
             [CtrlChannel(f, clock, 4, tag="phase")]
         vocab = drv.engine.model_cfg.vocab_size
-        local_ttfts, finished = [], []
+        log = TokenLog()
+        seen = {}
+        k = len(layout.group_of(f.rank))
+        micro = node_step_micro(cap, k, getattr(drv.engine, "n_mb", 1))
 
         def top_local():
             while local_frac > 0 and drv.admit_local(_prompt(rng, args.prompt_len, vocab), sp) is not None:
                 pass
 
-        def one_step():
-            n = 0
-            for o in drv.step():
-                n += 1
-                if o.rid in drv.local_used and len(o.request.output) == 1:
-                    local_ttfts.append(o.request.ttft)
+        def one_step() -> bool:
+            top_local()
+            if not drv.engine.has_unfinished():
+                drv.poll()
+                if not drv.engine.has_unfinished():
+                    time.sleep(0.0005)
+                    return False
+            outs = drv.step()
+            # first tokens of locally admitted prompts are produced here; a migrated request's
+            # first token was produced (and is counted) on its prefill rank
+            for o in outs:
+                if debug_counts:
+                    seen[o.rid] = o.request
+                r = o.request
+                log.times.append(r.token_times[-1] if r.token_times else time.perf_counter())
+                if o.rid in drv.local_used and len(r.output) == 1 and r.ttft is not None:
+                    log.firsts.append((log.times[-1], r.ttft))
                 if o.finished:
-                    finished.append(o.request)
-            return n
+                    log.finished.append(r)
+            log.steps.append(time.perf_counter())
+            return True
 
-        def run_steps(k):
-            """k productive decode steps (idle polling while nothing has arrived does not count)."""
-            n = done = 0
-            while done < k:
-                top_local()
-                if not drv.engine.has_unfinished():
-                    drv.poll()
-                    if not drv.engine.has_unfinished():
-                        time.sleep(0.0005)
-                        continue
-                n += one_step()
-                done += 1
-            return n
+        def run_steps(n):
+            done = 0
+            while done < n:
+                done += one_step()
 
-        def run_until_phase():
-            n = 0
-            while phases[0].poll() is None:
-                top_local()
-                if not drv.engine.has_unfinished():
-                    drv.poll()
-                    if not drv.engine.has_unfinished():
-                        time.sleep(0.0005)
-                        continue
-                n += one_step()
-            return n
-
-        def boundary():
-            if is_clock:
-                for ph in phases:
-                    ph.send([MSG_PHASE])
-            drv.await_fences()       # receives of every announced migration are posted
-            if hasattr(drv.engine, "pause_stages"):
-                drv.engine.pause_stages()
-            torch.cuda.synchronize() if f.device.type == "cuda" else None
-            f.barrier()
-
-        ramp = args.ramp_steps if args.ramp_steps >= 0 else 2 * args.output_len
+        t0 = t1 = None
         if is_clock:
-            run_steps(ramp + args.warmup)
+            ramp = args.ramp_steps if args.ramp_steps >= 0 else 2 * args.output_len
+            run_steps(ramp + args.warmup * micro)
+            t0 = time.perf_counter()
+            _bcast(phases, MSG_T0, t0)
+            run_steps(args.steps * micro)
+            t1 = time.perf_counter()
+            _bcast(phases, MSG_T1, t1)
         else:
-            run_until_phase()
-        boundary()
-        t0 = time.perf_counter()
-        local_ttfts.clear()
-        finished.clear()
-        n = run_steps(args.steps) if is_clock else run_until_phase()
-        boundary()
-        el = time.perf_counter() - t0
+            while t1 is None:
+                m = phases[0].poll()
+                if m is not None:
+                    if int(m[1]) == MSG_T0:
+                        t0 = _sec(m[2])
+                    else:
+                        t1 = _sec(m[2])
+                    continue
+                one_step()
+        # after the window: receive every announced migration (prefill ranks fence), drain
+        # the decode pipeline, synchronise, barrier
+        drv.await_fences()
+        if hasattr(drv.engine, "pause_stages"):
+            drv.engine.pause_stages()
+        torch.cuda.synchronize() if f.device.type == "cuda" else None
+        f.barrier()
         running = len(drv.engine.scheduler.running)
         # receive migrations still in flight so every prefill send completes
         while not drv.all_prefill_done():
             drv.poll()
             time.sleep(0.001)
         drv.finish()
-        return n, el, list(local_ttfts), {"tokens": n, "received": drv.received, "running_at_end": running,
-                                          "recv_GB": round(drv.recv_bytes / 1e9, 3), "local_fraction": local_frac,
-                                          "steps": drv.engine.stats["steps"], "tpots": _tpots(finished),
-                                          "kv_transport": drv.kvr.stats(),
-                                          "e2es": [r.finish_time - r.arrival for r in finished
-                                                   if r.finish_time is not None]}
+        w = log.window(t0, t1)
+        ex = {"tokens": w["tokens"], "received": drv.received, "running_at_end": running,
+              "recv_GB": round(drv.recv_bytes / 1e9, 3), "local_fraction": local_frac,
+              "steps": drv.engine.stats["steps"], "micro_per_step": micro,
+              "micro_steps_in_window": w["steps_in_window"], "tpots": w["tpots"], "e2es": w["e2es"],
+              "window": {"t0_ns": _ns(t0), "t1_ns": _ns(t1)}, **drv.stats(),
+              "token_wait_s": round(getattr(drv.engine, "wait_s", 0.0), 3)}
+        if debug_counts:
+            # a migrated request's token_times hold only what this replica produced (its first
+            # token was produced on the prefill rank); a local prompt's hold all of its tokens
+            ex["recount"] = recount(seen.values(), t0, t1)
+        return w["tokens"], t1 - t0, w["ttfts"], ex
 
     # later stages of a decode pipeline replica (receive their KV slices from the prefill ranks)
     w = StageWorker(cfg, f, layout.group_of(f.rank), kv_sources=layout.prefill_ranks)
     w.run()
     torch.cuda.synchronize() if f.device.type == "cuda" else None
     f.barrier()
-    t0 = time.perf_counter()
     w.run()
-    torch.cuda.synchronize() if f.device.type == "cuda" else None
-    f.barrier()
-    el = time.perf_counter() - t0
-    w.run()
-    return 0, el, [], {"tokens": 0, "stage_steps": w.steps, "installed": w.installed,
-                       "kv_transport": w.kvr.stats() if w.kvr is not None else None}
+    return 0, 0.0, [], {"tokens": 0, "stage_steps": w.steps, "installed": w.installed,
+                        "kv_block_s": round(w.kv_block_s, 4),
+                        "kv_transport": w.kvr.stats() if w.kvr is not None else None}

@@ -57,3 +57,40 @@ def test_pd_separation_cli_runs_config4_as_2p_6d(tmp_path):
     d = json.loads(out.read_text())["separated"]
     assert d["prefill_workers"] == 2 and d["decode_workers"] == 6 and d["tokens_per_second"] > 0
     assert "2P+6D[1+1+1+1+1+1]" in r.stdout + r.stderr or d["mode"] == "separated"
+
+
+@pytest.mark.parametrize("n,args", [
+    (3, ["--layout", "pdpp", "--prefill-ranks", "1", "--decode-stages", "2", "--decode-local-frac", "0.3"]),
+    (3, ["--layout", "pd", "--prefill-ranks", "2", "--decode-replicas", "1", "--prefill-local-cap", "4"]),
+    (2, ["--layout", "pp"]),
+])
+def test_bench_window_counts_exactly_the_tokens_inside_it(n, args):
+    """Timestamp window (dgi.parallel.bench_dist): every rank keeps serving across
+    both edges and counts the tokens it produced inside [t0, t1].  The reported
+    total equals an independent recount from the requests' own token timestamps,
+    the rate is that total over t1 - t0, and prefill ranks step inside it."""
+    env = {**os.environ, "OMP_NUM_THREADS": "1", "DGI_WATCHDOG": "0", "DGI_BENCH_RECOUNT": "1"}
+    env.pop("DGI_STAGED_GPU", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(n),
+           "--model", "llama-tiny", "--steps", "12", "--warmup", "2", "--ramp-steps", "4", "--concurrency", "8",
+           "--output-len", "4", "--prompt-len", "32", "--max-batched-tokens", "256", *args]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith('{"metric"')][-1])
+    ranks = d["extra"]["ranks"]
+    total = sum(int(o.get("tokens", 0)) for o in ranks)
+    assert total > 0
+    win = d["steps"] * d["ms_per_step"] / 1000.0
+    assert abs(d["value"] * win - total) <= 0.02 * total + 1
+    if args[1] == "pp":
+        drv = [o for o in ranks if o["role"] == "decode_driver"][0]
+        assert drv["micro_per_step"] >= 2
+        return
+    for o in ranks:
+        if o["role"] in ("prefill", "decode_driver"):
+            assert o["recount"] == o["tokens"], o
+    pre = [o for o in ranks if o["role"] == "prefill"]
+    assert all(o["prefill_steps_in_window"] >= 1 for o in pre)
+    drv = [o for o in ranks if o["role"] == "decode_driver"][0]
+    assert drv["micro_steps_in_window"] >= d["steps"] * drv["micro_per_step"] - 1
