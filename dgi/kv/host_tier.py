@@ -33,7 +33,11 @@ class HostKVTier:
         pin = (dev.type == "cuda") if pin is None else pin
         self.host = torch.empty((self.capacity,) + self.page_shape, dtype=pool.kv.dtype, pin_memory=pin)
         self._free = list(range(self.capacity - 1, -1, -1))
-        self.copy_stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
+        if dev.type == "cuda":
+            from dgi.utils.streams import named_stream
+            self.copy_stream = named_stream("kv_host_copy", dev)
+        else:
+            self.copy_stream = None
         self.stats = {"spilled": 0, "restored": 0, "dropped": 0, "spill_bytes": 0, "restore_bytes": 0}
 
     @property

@@ -241,7 +241,8 @@ class LlamaModel:
                 and not torch.cuda.is_current_stream_capturing():
             side = self._attn_stream
             if side is None or side.device != qkv.device:
-                side = self._attn_stream = torch.cuda.Stream(device=qkv.device)
+                from dgi.utils.streams import named_stream
+                side = self._attn_stream = named_stream("attn_side", qkv.device)
             main = torch.cuda.current_stream()
             side.wait_stream(main)
         if nd > 0:

@@ -159,7 +159,11 @@ class Fabric:
         # receives are POSTED from this (empty, high-priority) stream so the RCCL
         # stream waits on nothing the compute stream has queued (a KV receive must
         # never depend on this rank's own compute: pd.py deadlock argument)
-        self.recv_stream = torch.cuda.Stream(device=device, priority=-1) if self.on_gpu else None
+        if self.on_gpu:
+            from dgi.utils.streams import named_stream
+            self.recv_stream = named_stream("recv", device, priority=-1)
+        else:
+            self.recv_stream = None
         self._pending: list = []
         # DGI_DEBUG_STREAMS=1: send buffers must not be rewritten while in flight (dgi.utils.debug)
         from dgi.utils.debug import stream_checker
@@ -244,16 +248,21 @@ class Fabric:
     def pp_group(self, ranks) -> Optional[object]:
         return self.pp_groups.get(tuple(ranks))
 
-    def stream_budget(self, roles: Optional[set] = None) -> dict:
+    def stream_budget(self, engines=()) -> dict:
         """Streams this rank issues GPU work on, per priority class.
 
-        normal: the compute (default) stream, plus the host KV tier's copy stream
-        when one exists; high: the world (KV) communicator's RCCL stream, each
-        pipeline sub-communicator's, and the stream receives are posted from.
-        Each class must fit in ``GPU_HW_QUEUES`` so no two streams share a
-        hardware queue."""
+        normal: per engine this rank serves (``dgi.utils.streams.engine_streams``)
+        the compute (default) stream, the mixed-step attention side stream and the
+        host KV tier's copy stream; high: the world (KV) communicator's RCCL
+        stream, each pipeline sub-communicator's, and the stream receives are
+        posted from.  Each class must fit in ``GPU_HW_QUEUES`` so no two streams
+        share a hardware queue (``dgi.utils.streams.created`` lists what exists)."""
+        from dgi.utils.streams import engine_streams
+        normal = ["compute"]
+        for e in engines:
+            normal += [n for n in engine_streams(e) if n not in normal]
         high = ["rccl:kv", "recv"] + [f"rccl:pp{list(g)}" for g in self.pp_groups]
-        return {"normal": ["compute"], "high": high}
+        return {"normal": normal, "high": high}
 
     # ------------------------------------------------------------------ data plane (device tensors)
     def send(self, t: torch.Tensor, dst: int, group=None) -> None:

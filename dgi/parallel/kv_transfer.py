@@ -50,6 +50,15 @@ from dgi.parallel.fabric import CtrlChannel, Fabric
 
 RTS, CTS = 1, 2
 KV_TAG = "kv"
+# DGI_KV_CHECKSUM=1 (tests): the sender hashes every gathered buffer and the receiver
+# re-gathers every installed group from its pool and hashes it, so a test can require
+# the landed pages to be bit-identical to what the prefill rank gathered
+CHECKSUM = os.environ.get("DGI_KV_CHECKSUM") == "1"
+
+
+def buf_digest(t: torch.Tensor) -> str:
+    import hashlib
+    return hashlib.sha1(t.detach().contiguous().view(torch.int16).cpu().numpy().tobytes()).hexdigest()
 DIAG_S = float(os.environ.get("DGI_KV_DIAG_S", "30"))    # print protocol state every DIAG_S s of a stuck wait
 
 
@@ -85,9 +94,12 @@ class KVSender:
         self.transfers = 0
         # DGI_KV_TRACE=1: (event, tid, dst, t) for the protocol-order tests
         self.trace = [] if os.environ.get("DGI_KV_TRACE") == "1" else None
+        self.digests: dict = {}         # DGI_KV_CHECKSUM: (dst, key, c0, c1) -> sha1 of the gathered group
 
     def submit(self, dst: int, buf: torch.Tensor, key: int, group: int, ngroups: int, c0: int, c1: int,
                nblk: int) -> None:
+        if CHECKSUM:
+            self.digests[(dst, key, c0, c1)] = buf_digest(buf)
         ev = None
         if buf.is_cuda:
             ev = torch.cuda.Event()
@@ -187,6 +199,7 @@ class KVReceiver:
         self.recv_bytes = 0
         self.wait_us: list = []                                   # post -> landed per transfer
         self.trace = [] if os.environ.get("DGI_KV_TRACE") == "1" else None
+        self.digests = {} if CHECKSUM else None                   # (src, key, c0, c1) -> sha1 of installed pages
 
     def service(self) -> int:
         """Take in RTS messages, retire the receive in flight, post the next one.
@@ -269,8 +282,13 @@ class KVReceiver:
                 "post_to_land_us_p50": round(w[len(w) // 2], 1) if w else None}
 
 
-def scatter_groups(pool_kv: torch.Tensor, ids_t: torch.Tensor, groups: list) -> None:
-    """Install landed layer groups [(c0, c1, buf)] into the paged pool (current stream)."""
+def scatter_groups(pool_kv: torch.Tensor, ids_t: torch.Tensor, groups: list, digests: Optional[dict] = None,
+                   src: int = -1, key: int = -1) -> None:
+    """Install landed layer groups [(c0, c1, buf)] into the paged pool (current stream).
+    With ``digests`` (DGI_KV_CHECKSUM), each installed group is gathered back out of the
+    pool and hashed under (src, key, c0, c1)."""
     from dgi import ops
     for c0, c1, buf in groups:
         ops.kv_scatter(pool_kv[c0:c1], ids_t, buf)
+        if digests is not None:
+            digests[(src, key, c0, c1)] = buf_digest(ops.kv_gather(pool_kv[c0:c1], ids_t))

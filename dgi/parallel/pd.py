@@ -603,7 +603,7 @@ class DecodeDriver:
                 else:
                     keep.append(item)
                     continue
-                scatter_groups(self.engine.pool.kv, item.ids_t, groups)
+                scatter_groups(self.engine.pool.kv, item.ids_t, groups, self.kvr.digests, item.p, item.key)
                 self.recv_bytes += sum(b.numel() * b.element_size() for _a, _b, b in groups)
                 item.installed = True
             if pipe is not None and not pipe.stages_landed(item.p, item.key):

@@ -518,7 +518,7 @@ class StageWorker:
                 self.kv_block_s += time.perf_counter() - t0
             else:
                 groups = self.kvr.take(src, key)
-            scatter_groups(self.pool.kv, ids_t, groups)
+            scatter_groups(self.pool.kv, ids_t, groups, self.kvr.digests, src, key)
             self.installed += 1
         # the driver admits the migration's requests once every stage has reported
         self.landed_out.send([src, key])

@@ -189,10 +189,24 @@ CAPACITY = {
 }
 
 
+_MEASURED: dict = {}     # model -> RoleCapacity measured at start-up (dgi.parallel.probe)
+
+
+def set_capacity(model: str, cap: Optional[RoleCapacity]) -> None:
+    """Plan ``model`` with ``cap`` (this node's start-up probe) instead of the table."""
+    key = model.split("@")[0] if model else model
+    if cap is None:
+        _MEASURED.pop(key, None)
+    else:
+        _MEASURED[key] = cap
+
+
 def capacity_for(model: str) -> Optional[RoleCapacity]:
-    """Capacity table entry of ``model``; a layer-truncated rehearsal name
-    (``llama3-70b@L8``) plans like the full model it stands in for."""
-    return CAPACITY.get(model.split("@")[0] if model else model)
+    """This node's measured capacity of ``model`` if the start-up probe ran, else the
+    table entry; a layer-truncated rehearsal name (``llama3-70b@L8``) plans like the
+    full model it stands in for."""
+    key = model.split("@")[0] if model else model
+    return _MEASURED.get(key) or CAPACITY.get(key)
 
 
 def estimate_layout(n_prefill: int, stages: int, replicas: int, cap: RoleCapacity, fill: bool = False) -> float:

@@ -1,0 +1,218 @@
+"""Start-up per-role capacity probe (what ``bench.py --layout auto`` plans with).
+
+Round 3 chose the 8-GPU layout from a table measured once on one box
+(``plan.CAPACITY``); the P/D-vs-DP call sat within that box-to-box spread
+(VERDICT r3 weak #9).  Here every rank of the node measures its own GPU for a
+few seconds before the layout is fixed, with the real engine on shortened
+copies of the model (same hidden size, heads, vocabulary and page size):
+
+* prefill step  — ``prefill_mbt`` prompt tokens per step, max_tokens = 1;
+* decode step   — ``rows`` pure-decode rows at the load's mean context
+  (prompt + output/2 tokens), KV pages installed directly (no prefill);
+* mixed step    — ``rows`` decode rows + prompt/output x rows prefill tokens,
+  the steady state of a data-parallel GPU under the 512/128 load.
+
+Each is timed at two layer counts, ``t(n) = fixed + n * per_layer``, and
+extrapolated to the model's depth (the fixed part is the embedding, LM head,
+sampler and host work of one step).  ``capacity_from_probe`` turns the fits
+into a ``plan.RoleCapacity``; ranks gather their probes and plan with the
+median, so every rank picks the same layout.
+"""
+from __future__ import annotations
+
+import dataclasses
+import random
+import time
+from typing import Optional
+
+import torch
+
+from dgi.models.config import ModelConfig, get_config
+
+
+@dataclasses.dataclass
+class ProbeResult:
+    model: str
+    prefill: tuple          # (fixed_ms, per_layer_ms) at prefill_mbt tokens
+    decode: dict            # rows -> (fixed_ms, per_layer_ms)
+    mixed: tuple            # (fixed_ms, per_layer_ms) at mixed_rows decode rows
+    prefill_mbt: int
+    mixed_rows: int
+    prompt_len: int
+    output_len: int
+    layers: tuple
+    seconds: float
+
+    def to_dict(self) -> dict:
+        return dataclasses.asdict(self)
+
+
+def _time_steps(eng, steps: int, before=None) -> float:
+    """Mean ms of ``eng.step()`` over ``steps`` (after 2 untimed)."""
+    sync = (lambda: torch.cuda.synchronize()) if eng.device.type == "cuda" else (lambda: None)
+    for _ in range(2):
+        if before:
+            before()
+        eng.step()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        if before:
+            before()
+        eng.step()
+    sync()
+    return (time.perf_counter() - t0) / steps * 1e3
+
+
+def _engine(model: str, mc: ModelConfig, device: str, max_seqs: int, mbt: int, num_blocks: int,
+            graphs: bool, buckets=None):
+    from dgi.engine import EngineConfig, LLMEngine
+    cfg = EngineConfig(model=model, device=device, max_num_seqs=max_seqs, max_num_batched_tokens=mbt,
+                       max_model_len=2048, use_graphs=graphs, enable_prefix_caching=False, num_blocks=num_blocks,
+                       graph_buckets=buckets)
+    eng = LLMEngine(cfg, model_cfg=mc)
+    if graphs:
+        eng.warmup()
+    return eng
+
+
+def _adopt(eng, n: int, ctx: int, rng) -> None:
+    """``n`` running sequences with ``ctx`` tokens of (uninitialised) KV each."""
+    from dgi.sched.request import Request, SamplingParams
+    bs = eng.pool.block_size
+    sp = SamplingParams(max_tokens=1 << 20, temperature=0.0, ignore_eos=True)
+    V = eng.model_cfg.vocab_size
+    for _ in range(n):
+        r = Request([rng.randrange(1, V) for _ in range(ctx - 1)], sp)
+        r.output = [rng.randrange(1, V)]
+        eng.scheduler.add_prefilled(r, eng.pool.allocate((ctx + bs - 1) // bs))
+        eng.requests[r.rid] = r
+
+
+def _release(device: str) -> None:
+    """Give the probe engines' memory (weights, KV, graph pools) back before the
+    serving engine sizes its KV pool from free HBM."""
+    import gc
+    gc.collect()
+    if device != "cpu":
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+
+
+def _fit(ts: dict) -> tuple:
+    (n0, t0), (n1, t1) = sorted(ts.items())
+    per = max(0.0, (t1 - t0) / (n1 - n0))
+    return (round(max(0.0, t0 - n0 * per), 4), round(per, 4))
+
+
+def run_probe(model: str, device: str, prompt_len: int = 512, output_len: int = 128, prefill_mbt: int = 2048,
+              decode_rows=(576, 768), mixed_rows: int = 384, layers=(2, 4), steps: int = 4,
+              seed: int = 0) -> ProbeResult:
+    t_start = time.perf_counter()
+    base = get_config(model.split("@")[0] if model else model)
+    rng = random.Random(seed)
+    ctx = prompt_len + output_len // 2
+    bs = 16
+    pre, dec, mix = {}, {r: {} for r in decode_rows}, {}
+    per_prompt = max(1, prefill_mbt // prompt_len)
+    from dgi.sched.request import SamplingParams
+    one = SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True)
+    if device != "cpu":
+        # the MLP row-padding table (dgi.runtime.gemm_pad) once, at the serving engines' row
+        # range: every probe engine below and the serving engine reuse it
+        eng = _engine(model, dataclasses.replace(base, num_layers=1), device, 8, 4096, 64, graphs=False)
+        del eng
+        _release(device)
+    for n in layers:
+        mc = dataclasses.replace(base, num_layers=n)
+        # prefill: a step's worth of prompts waiting before every step
+        eng = _engine(model, mc, device, 4 * per_prompt, prefill_mbt, 4 * per_prompt * (prompt_len // bs + 2) + 8,
+                      graphs=False)
+
+        def top():
+            while len(eng.scheduler.waiting) < per_prompt:
+                eng.add_request([rng.randrange(1, mc.vocab_size) for _ in range(prompt_len)], one)
+        pre[n] = _time_steps(eng, steps, top)
+        del eng
+        # decode: rows at the mean context, graph-captured like the serving engines
+        for rows in decode_rows:
+            nb = rows * (ctx // bs + 2 + steps + 4) + 8
+            eng = _engine(model, mc, device, rows, max(4096, rows), nb, graphs=device != "cpu", buckets=(rows,))
+            _adopt(eng, rows, ctx, rng)
+            dec[rows][n] = _time_steps(eng, steps)
+            del eng
+        # mixed: decode rows + prompt/output x rows prefill tokens per step (DP steady state)
+        ptoks = mixed_rows * prompt_len // max(1, output_len)
+        nprompt = max(1, ptoks // prompt_len)
+        nb = mixed_rows * (ctx // bs + 2 + steps + 4) + 4 * nprompt * (prompt_len // bs + 2) + 8
+        eng = _engine(model, mc, device, mixed_rows + 4 * nprompt, mixed_rows + ptoks, nb, graphs=False)
+        _adopt(eng, mixed_rows, ctx, rng)
+
+        def topm():
+            while len(eng.scheduler.waiting) < nprompt:
+                eng.add_request([rng.randrange(1, mc.vocab_size) for _ in range(prompt_len)], one)
+        mix[n] = _time_steps(eng, steps, topm)
+        del eng
+        _release(device)
+    return ProbeResult(model=model, prefill=_fit(pre), decode={r: _fit(v) for r, v in dec.items()}, mixed=_fit(mix),
+                       prefill_mbt=prefill_mbt, mixed_rows=mixed_rows, prompt_len=prompt_len, output_len=output_len,
+                       layers=tuple(layers), seconds=round(time.perf_counter() - t_start, 2))
+
+
+def capacity_from_probe(p: ProbeResult, num_layers: Optional[int] = None, max_stages: int = 3):
+    """``plan.RoleCapacity`` of the full model from a probe (per-GPU rates).
+
+    A k-stage decode replica runs k microbatches of R rows; each stage step is
+    ~1/k of a whole-model decode step at R rows (balanced split), so the
+    replica emits k * R tokens per whole-model step: k * R / t_dec(L, R)."""
+    from dgi.parallel.plan import RoleCapacity
+    L = num_layers or get_config(p.model.split("@")[0]).num_layers
+    t = lambda fit: fit[0] + fit[1] * L          # noqa: E731  ms at the full depth
+    t_pre = t(p.prefill)
+    prompts_per_step = max(1, p.prefill_mbt // p.prompt_len)
+    prefill_tok_s = prompts_per_step / (t_pre / 1e3) * p.output_len
+    rows = sorted(p.decode)
+    r1 = rows[0]
+    rk = rows[-1]
+    dec, step, drows = {}, {}, {}
+    for k in range(1, max_stages + 1):
+        R = r1 if k == 1 else rk
+        td = t(p.decode[R])
+        dec[k] = round(k * R / (td / 1e3), 1)
+        step[k] = round(td / k, 2)
+        drows[k] = R
+    t_mix = t(p.mixed)
+    return RoleCapacity(prefill_tok_s=round(prefill_tok_s, 1), decode_tok_s=dec,
+                        mixed_tok_s=round(p.mixed_rows / (t_mix / 1e3), 1), prefill_step_ms=round(t_pre, 2),
+                        prefill_mbt=p.prefill_mbt, decode_step_ms=step, decode_rows=drows,
+                        mixed_step_ms=round(t_mix, 2))
+
+
+def median_capacity(caps: list):
+    """Element-wise median of several ranks' capacities (same keys)."""
+    import statistics
+    from dgi.parallel.plan import RoleCapacity
+    c0 = caps[0]
+    med = lambda xs: round(float(statistics.median(xs)), 2)   # noqa: E731
+    return RoleCapacity(
+        prefill_tok_s=med([c.prefill_tok_s for c in caps]),
+        decode_tok_s={k: med([c.decode_tok_s[k] for c in caps]) for k in c0.decode_tok_s},
+        mixed_tok_s=med([c.mixed_tok_s for c in caps]), prefill_step_ms=med([c.prefill_step_ms for c in caps]),
+        prefill_mbt=c0.prefill_mbt, decode_step_ms={k: med([c.decode_step_ms[k] for c in caps]) for k in c0.decode_step_ms},
+        decode_rows=dict(c0.decode_rows), mixed_step_ms=med([c.mixed_step_ms for c in caps]))
+
+
+def plan_from_probe(world: int, cap, min_ratio: float = 1.0) -> dict:
+    """The auto layout under ``cap``: the planner's best P/D split, kept only when its
+    disaggregated estimate reaches ``min_ratio`` x ``world`` data-parallel GPUs
+    (never pick a layout the planner itself rates below DP)."""
+    from dgi.parallel.plan import choose_pd_layout, layout_estimate
+    npre, k, reps, _ = choose_pd_layout(world, cap)
+    est = layout_estimate(npre, k, reps, cap)
+    dp = world * cap.mixed_tok_s
+    pd_ok = est["disagg_tok_s"] >= min_ratio * dp
+    kind = ("pdpp" if k > 1 else "pd") if pd_ok else "dp"
+    why = (f"P/D {est['layout']} estimated {est['disagg_tok_s']:.0f} tok/s "
+           f"{'>=' if pd_ok else '<'} {world} DP GPUs {dp:.0f} tok/s")
+    return {"kind": kind, "prefill_ranks": npre, "decode_stages": k, "decode_replicas": reps, "estimate": est,
+            "dp_tok_s": round(dp, 1), "reason": why}

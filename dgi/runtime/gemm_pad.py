@@ -146,8 +146,14 @@ class MlpPadTable:
         return r
 
 
+_TABLES: dict = {}      # (shapes, device, step) -> (m_max, table): one measurement per process
+
+
 def build_for_model(model, m_max: int, step: int = 32) -> Optional[MlpPadTable]:
-    """Measure the table for ``model``'s MLP shape on its device (None when off / not applicable)."""
+    """Measure the table for ``model``'s MLP shape on its device (None when off / not
+    applicable).  A table already measured in this process for the same weight shapes
+    on the same device up to at least ``m_max`` rows is reused (the start-up capacity
+    probe and the serving engine share one ~5 s measurement)."""
     if os.environ.get("DGI_MLP_PAD", "1") == "0":
         return None
     layers = getattr(model, "layers", None)
@@ -157,6 +163,13 @@ def build_for_model(model, m_max: int, step: int = 32) -> Optional[MlpPadTable]:
     if L.gate_up.device.type != "cuda" or m_max < 1024:
         return None
     from dgi.models import llama
-    return MlpPadTable.measure(L.gate_up, L.down, m_max=m_max, step=step,
-                               qkv=L.qkv if llama.QKV_PAD else None, o_w=L.o if llama.OPROJ_PAD else None,
-                               proj_qkv=L.qkv if L.qkv_bias is None else None, proj_o=L.o)
+    key = (tuple(L.gate_up.shape), tuple(L.down.shape), tuple(L.qkv.shape), tuple(L.o.shape), L.qkv_bias is None,
+           str(L.gate_up.device), L.gate_up.dtype, step, llama.QKV_PAD, llama.OPROJ_PAD)
+    hit = _TABLES.get(key)
+    if hit is not None and hit[0] >= m_max:
+        return hit[1]
+    t = MlpPadTable.measure(L.gate_up, L.down, m_max=m_max, step=step,
+                            qkv=L.qkv if llama.QKV_PAD else None, o_w=L.o if llama.OPROJ_PAD else None,
+                            proj_qkv=L.qkv if L.qkv_bias is None else None, proj_o=L.o)
+    _TABLES[key] = (m_max, t)
+    return t

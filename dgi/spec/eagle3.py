@@ -329,7 +329,8 @@ class _VerifyGraph:
     def _capture(self) -> None:
         eng = self.eng
         eng.model.kv_cache = eng.pool.kv
-        s = torch.cuda.Stream(device=eng.device)
+        from dgi.utils.streams import named_stream
+        s = named_stream("capture", eng.device)
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             self._body()                                   # warm-up (lazy inits outside capture)
@@ -473,7 +474,8 @@ class _DraftGraph:
     @torch.inference_mode()
     def _capture(self) -> None:
         eng = self.eng
-        s = torch.cuda.Stream(device=eng.device)
+        from dgi.utils.streams import named_stream
+        s = named_stream("capture", eng.device)
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             self._body()

@@ -124,3 +124,25 @@ def test_auto_host_tier_size_is_half_the_pool_capped_by_ram():
     pool = _pool(nb=65)
     gb = auto_host_kv_gb(pool, torch.device("cpu"))
     assert 0 < gb <= pool.page_bytes() * 65 * 0.5 / (1 << 30) + 0.01
+
+
+@pytest.mark.gpu
+def test_streams_created_are_within_the_engine_budget():
+    """Every long-lived stream a serving engine really creates (mixed steps with the
+    side attention stream, host tier spills) is in its stream budget, and the
+    budget fits the hardware queues of one priority class."""
+    from dgi.parallel.fabric import GPU_HW_QUEUES
+    from dgi.utils.streams import created, engine_streams
+    eng = LLMEngine(EngineConfig(model="llama-tiny-hd128", device="cuda", max_num_seqs=6, max_num_batched_tokens=256,
+                                 max_model_len=256, use_graphs=False, enable_prefix_caching=False, num_blocks=17,
+                                 host_kv_gb=0.05))
+    g = torch.Generator().manual_seed(3)
+    prompts = [torch.randint(5, 500, (20 + 3 * i,), generator=g).tolist() for i in range(6)]
+    eng.generate(prompts, SamplingParams(max_tokens=24, temperature=0.0, ignore_eos=True))
+    torch.cuda.synchronize()
+    assert eng.scheduler.stats()["swapped_out"] > 0            # the copy stream was used
+    budget = engine_streams(eng)
+    have = created(torch.cuda.current_device())
+    assert set(have["normal"]) - {"capture"} <= set(budget), (have, budget)
+    assert "attn_side" in have["normal"] and "kv_host_copy" in have["normal"]
+    assert len(budget) <= GPU_HW_QUEUES and len(have["high"]) <= GPU_HW_QUEUES - 1

@@ -320,6 +320,38 @@ def _teacher_forced_ok(name, src_model, prompts, gpu_outs, rel=0.03, abs_=0.02):
     return checked
 
 
+def _teacher_forced_topk_ok(name, src_model, prompts, gpu_outs, k, rel=0.03, abs_=0.02):
+    """Sampled runs: every token the GPU drew is inside the fp32 model's top-k for the
+    same prefix (teacher forced), up to a bf16 tolerance — per step, every prompt."""
+    from dgi.engine import EngineConfig, LLMEngine
+    from dgi.models.llama import LlamaModel
+    from dgi.sched.request import SamplingParams
+    mc = src_model.cfg
+    f32 = LlamaModel(mc, "cpu", torch.float32, init="empty").copy_from(src_model)
+    ref = LLMEngine(EngineConfig(model=name, device="cpu", dtype=torch.float32, num_blocks=256, max_num_seqs=8,
+                                 max_model_len=512, max_num_batched_tokens=256, use_graphs=False,
+                                 enable_prefix_caching=False), model_cfg=mc, model=f32)
+    got = {}
+    orig = ref.model.compute_logits
+
+    def spy(h, residual, idx):
+        out = orig(h, residual, idx)
+        got["l"] = out[-1].detach().float()
+        return out
+    ref.model.compute_logits = spy
+    one = SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True)
+    checked = 0
+    for p, toks in zip(prompts, gpu_outs):
+        for t, tok in enumerate(toks):
+            ref.generate([p + toks[:t]], one)
+            r = got["l"]
+            kth = float(r.topk(k).values[-1])
+            tol = rel * float(r.abs().max()) + abs_
+            assert float(r[tok]) >= kth - tol, (name, len(p), t, tok, kth, float(r[tok]))
+            checked += 1
+    return checked
+
+
 def test_qwen2_engine_gpu_matches_cpu():
     """Qwen2 family (biased QKV, GQA 7:1) through the native kernels vs the CPU engine."""
     from dgi.engine import EngineConfig, LLMEngine
