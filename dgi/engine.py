@@ -45,6 +45,8 @@ class EngineConfig:
     model_path: Optional[str] = None   # HF safetensors checkpoint dir (None: ``model`` if it is one, else random init)
     token_align: int = -1              # round mixed-step row counts down to a multiple of this (the GEMM
                                        # row tile; -1 = 256 on GPU engines, 0 = off): SchedulerConfig
+    tpot_slo_ms: float = 0.0           # > 0: cap each step's rows so a step (= a decode token's wait)
+                                       # stays under this (dgi.sched.slo.StepBudget)
 
 
 @dataclasses.dataclass
@@ -139,6 +141,10 @@ class LLMEngine:
         self.runner = ModelRunner(self.model, self.pool, cfg.max_num_seqs, cfg.max_model_len,
                                   cfg.max_num_batched_tokens, cfg.use_graphs, **rkw)
         self.requests: dict = {}
+        self.step_budget = None
+        if cfg.tpot_slo_ms > 0:
+            from dgi.sched.slo import StepBudget
+            self.step_budget = StepBudget(cfg.tpot_slo_ms)
         # optional callback(ScheduledBatch) between scheduling and execution (P/D streaming)
         self.pre_execute = None
         # optional callback(Request) when a request's first token is sampled, BEFORE any
@@ -182,7 +188,9 @@ class LLMEngine:
         t0 = time.perf_counter()
         self.model.kv_cache = self.pool.kv   # engines may share one model object
         with phase("schedule"):
-            sb = self.scheduler.schedule()
+            sbud = self.step_budget
+            cap = None if sbud is None else sbud.budget(self.cfg.max_num_batched_tokens, len(self.scheduler.running))
+            sb = self.scheduler.schedule(max_tokens=cap)
         if sb.empty:
             return []
         if self.pre_execute is not None:
@@ -191,7 +199,10 @@ class LLMEngine:
             res = self.runner.execute(sb)
         with phase("apply"):
             outs = self._apply(sb, res.rows, res.tokens)
-        self.stats["step_time"] += time.perf_counter() - t0
+        dt = time.perf_counter() - t0
+        self.stats["step_time"] += dt
+        if sbud is not None and sb.prefill:       # mixed / prefill steps set the per-row cost
+            sbud.observe(sb.num_tokens, dt * 1e3)
         return outs
 
     def _apply(self, sb, rows, tokens) -> list[StepOutput]:

@@ -165,10 +165,13 @@ def run_distributed(args, layout_kind: str, dist):
 # drained, fenced or paused inside the window (pipelines stay full across both
 # edges) — fences, pipeline pauses, the device synchronise and the barrier all
 # happen after t1.  A node step is ``micro`` decode micro-steps of the clock
-# replica, enough to cover one prefill step (``node_step_micro``), so a
-# --steps 20 window holds ~20 prefill steps of every prefill rank.
+# replica, enough to cover one prefill step: the prefill ranks report their
+# measured step time to the clock during the ramp (``MSG_STEPMS``) and the clock
+# sizes ``micro`` from it and its own micro-step time (``node_step_micro`` falls
+# back to the capacity table), so a --steps 20 window holds ~20 prefill steps of
+# every prefill rank.
 
-MSG_T0, MSG_T1 = 1, 2
+MSG_T0, MSG_T1, MSG_STEPMS = 1, 2, 3
 
 
 def _ns(t: float) -> int:
@@ -179,12 +182,15 @@ def _sec(ns) -> float:
     return int(ns) / 1e9
 
 
-def node_step_micro(cap, k: int, n_mb: int) -> int:
+def node_step_micro(cap, k: int, n_mb: int, prefill_ms: float = 0.0, micro_ms: float = 0.0) -> int:
     """Decode micro-steps of the clock replica per node step: at least one full
     pipeline round (``n_mb``) and at least one prefill step's worth of micro-steps
-    under the capacity table (70B 5P+PP3: 202 ms prefill step / 42.5 ms stage step
-    -> 5)."""
+    — from measured times when given (the slowest prefill rank's step, the clock's
+    own micro-step), else from the capacity table (70B 5P+PP3: 202 ms prefill
+    step / 42.5 ms stage step -> 5)."""
     micro = max(1, n_mb)
+    if prefill_ms > 0 and micro_ms > 0:
+        return max(micro, -(-int(prefill_ms * 1000) // max(1, int(micro_ms * 1000))))
     if cap is not None and cap.prefill_step_ms and cap.decode_step_ms.get(k):
         micro = max(micro, -(-int(cap.prefill_step_ms * 1000) // int(cap.decode_step_ms[k] * 1000)))
     return micro
@@ -344,6 +350,7 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
                 submit()
 
         t0 = t1 = None
+        step_ms = None
         while t1 is None:
             m = ph.poll()
             if m is not None:
@@ -354,9 +361,14 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
                 continue
             top_up()
             s0 = srv.engine.stats["steps"]
+            ts = time.perf_counter()
             log.outputs(srv.step())
             if srv.engine.stats["steps"] > s0:
                 log.steps.append(time.perf_counter())
+                ms = (log.steps[-1] - ts) * 1e3
+                step_ms = ms if step_ms is None else 0.8 * step_ms + 0.2 * ms
+                if t0 is None and len(log.steps) % 4 == 0:        # the clock sizes its node step from it
+                    ph.send([MSG_PHASE, MSG_STEPMS, int(step_ms * 1000)])
         # after the window: drain every KV transfer this rank started (the decode ranks keep
         # servicing their handshakes) and report the migration count; then synchronise
         srv.fence()
@@ -387,7 +399,10 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
         log = TokenLog()
         seen = {}
         k = len(layout.group_of(f.rank))
-        micro = node_step_micro(cap, k, getattr(drv.engine, "n_mb", 1))
+        n_mb = getattr(drv.engine, "n_mb", 1)
+        micro = node_step_micro(cap, k, n_mb)
+        reported: dict = {}          # prefill rank -> its latest step time (ms)
+        my_ms = {"ema": None}
 
         def top_local():
             while local_frac > 0 and drv.admit_local(_prompt(rng, args.prompt_len, vocab), sp) is not None:
@@ -400,7 +415,10 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
                 if not drv.engine.has_unfinished():
                     time.sleep(0.0005)
                     return False
+            ts = time.perf_counter()
             outs = drv.step()
+            ms = (time.perf_counter() - ts) * 1e3
+            my_ms["ema"] = ms if my_ms["ema"] is None else 0.8 * my_ms["ema"] + 0.2 * ms
             # first tokens of locally admitted prompts are produced here; a migrated request's
             # first token was produced (and is counted) on its prefill rank
             for o in outs:
@@ -420,10 +438,24 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
             while done < n:
                 done += one_step()
 
+        def take_reports():
+            for p, ch in zip(others, phases):
+                while True:
+                    m = ch.poll()
+                    if m is None:
+                        break
+                    if int(m[1]) == MSG_STEPMS:
+                        reported[p] = int(m[2]) / 1000.0
+
         t0 = t1 = None
         if is_clock:
             ramp = args.ramp_steps if args.ramp_steps >= 0 else 2 * args.output_len
-            run_steps(ramp + args.warmup * micro)
+            run_steps(ramp)
+            take_reports()
+            if reported and my_ms["ema"]:
+                micro = node_step_micro(cap, k, n_mb, max(reported.values()), my_ms["ema"])
+            run_steps(args.warmup * micro)
+            take_reports()
             t0 = time.perf_counter()
             _bcast(phases, MSG_T0, t0)
             run_steps(args.steps * micro)
@@ -456,6 +488,8 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
         ex = {"tokens": w["tokens"], "received": drv.received, "running_at_end": running,
               "recv_GB": round(drv.recv_bytes / 1e9, 3), "local_fraction": local_frac,
               "steps": drv.engine.stats["steps"], "micro_per_step": micro,
+              "prefill_step_ms_reported": {str(p): round(v, 2) for p, v in reported.items()},
+              "micro_step_ms": round(my_ms["ema"], 3) if my_ms["ema"] else None,
               "micro_steps_in_window": w["steps_in_window"], "tpots": w["tpots"], "e2es": w["e2es"],
               "window": {"t0_ns": _ns(t0), "t1_ns": _ns(t1)}, **drv.stats(),
               "token_wait_s": round(getattr(drv.engine, "wait_s", 0.0), 3)}

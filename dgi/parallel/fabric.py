@@ -318,6 +318,26 @@ class Fabric:
             return AsyncRecv(self, w, t)
         return AsyncRecv(self, dist.irecv(t, src, group=group), t)
 
+    def irecv_batch(self, items: list, group=None) -> list:
+        """Post several receives (``[(tensor, src), ...]``, distinct sources) as ONE
+        RCCL group from ``recv_stream``: they progress concurrently over their own
+        links and none waits behind another (``dgi.parallel.kv_transfer`` deadlock
+        argument).  One ``AsyncRecv`` per item."""
+        if len(items) == 1:
+            t, src = items[0]
+            return [self.irecv_async(t, src, group=group)]
+        if self.staged:
+            hs = [torch.empty(t.shape, dtype=t.dtype) for t, _s in items]
+            works = dist.batch_isend_irecv([dist.P2POp(dist.irecv, h, s, group=group) for h, (_t, s) in zip(hs, items)])
+            return [AsyncRecv(self, w, t, host=h) for w, h, (t, _s) in zip(works, hs, items)]
+        ops_ = [dist.P2POp(dist.irecv, t, s, group=group) for t, s in items]
+        if self.on_gpu:
+            with torch.cuda.stream(self.recv_stream):
+                works = dist.batch_isend_irecv(ops_)
+        else:
+            works = dist.batch_isend_irecv(ops_)
+        return [AsyncRecv(self, w, t) for w, (t, _s) in zip(works, items)]
+
     def alloc_recv(self, shape, dtype) -> torch.Tensor:
         """A receive buffer owned by ``recv_stream`` (caching-allocator safe for
         ``irecv_async``)."""

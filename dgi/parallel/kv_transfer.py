@@ -10,23 +10,34 @@ plane, and the data moves only once both ends are committed:
 
     prefill rank P                                    decode rank X
     gather pages (compute stream), event
-    event complete  --RTS(tid, group, shape)------->  queue (FIFO over all P)
-                                                      when X has NO receive in flight:
-                                                        post irecv (own stream, waits on nothing)
-                    <-------------------CTS(tid)---
+    event complete  --RTS(tid, group, shape)------->  queue (FIFO per source)
+                                                      when X has NO batch in flight:
+                                                        post ONE batch: the oldest queued
+                                                        RTS of each source, as one RCCL
+                                                        group (own stream, waits on nothing)
+                    <-------------------CTS(tid)---   (one CTS per receive of the batch)
     enqueue the send (batched with the other
     CTS'd sends of this poll: one RCCL group)
-                                                      poll: landed -> scatter into the pool
+                                                      poll: batch landed -> scatter into the pool
+
+A batch holds at most one receive per source (``DGI_KV_RECV_BATCH`` caps its
+size; 1 = round 3's single receive in flight), so a decode rank pulls from up
+to P prefill ranks at once, each over its own xGMI link (round 3: one receive
+at a time per decode rank).
 
 Why it cannot deadlock (on the KV communicator's FIFO stream of every rank):
-  (1) a decode rank has at most ONE receive posted, and posts it from an empty
-      stream, so the receive kernel is running from the moment it is posted
-      (communicators live on their own high-priority hardware queues,
-      dgi.parallel.fabric);
+  (1) a decode rank has at most ONE batch posted, and posts it from an empty
+      stream as one RCCL group, so every receive of the batch is running (a
+      group's point-to-point operations progress independently of each other)
+      from the moment it is posted (communicators live on their own
+      high-priority hardware queues, dgi.parallel.fabric);
   (2) a prefill rank enqueues a send only after its receiver's CTS, i.e. the
       partner of EVERY send in a prefill rank's stream is a running receive;
   (3) so the head of each prefill stream completes as soon as its own compute
-      (the gather) is done, and by induction every send and receive completes.
+      (the gather) is done, and by induction every send and every batch
+      completes.  (Two SEPARATELY posted receives on one stream would break
+      (1): the second would wait behind the first while its sender's stream
+      waits on it — the cycle the single group avoids.)
 Nothing on either side waits on the other's compute or on another transfer.
 The decode side never blocks its host on a transfer it has not posted; a
 prefill rank drains (``KVSender.drain``) only at phase boundaries, while every
@@ -54,6 +65,8 @@ KV_TAG = "kv"
 # re-gathers every installed group from its pool and hashes it, so a test can require
 # the landed pages to be bit-identical to what the prefill rank gathered
 CHECKSUM = os.environ.get("DGI_KV_CHECKSUM") == "1"
+# receives per posted batch (at most one per source); 0 = one per source
+RECV_BATCH = int(os.environ.get("DGI_KV_RECV_BATCH", "0"))
 
 
 def buf_digest(t: torch.Tensor) -> str:
@@ -184,61 +197,81 @@ class KVSender:
 
 
 class KVReceiver:
-    """Decode-rank end: one receive in flight at a time, FIFO over every source."""
+    """Decode-rank end: one batch of receives in flight (at most one per source),
+    each source's transfers in FIFO order."""
 
-    def __init__(self, fabric: Fabric, sources: list, page_shape: tuple, dtype: torch.dtype):
+    def __init__(self, fabric: Fabric, sources: list, page_shape: tuple, dtype: torch.dtype,
+                 max_batch: Optional[int] = None):
         self.f = fabric
         self.ch = {p: CtrlChannel(fabric, p, 8, tag=KV_TAG) for p in sorted(set(sources))}
         self.page_shape = tuple(page_shape)      # (2, nkv, bs, hd): one page of one layer
         self.dtype = dtype
-        self.queue: collections.deque = collections.deque()      # (src, rts fields)
-        self.cur = None                                           # (src, fields, AsyncRecv, buf)
+        self.queue: dict = {p: collections.deque() for p in self.ch}   # src -> RTS fields, FIFO
+        mb = RECV_BATCH if max_batch is None else max_batch
+        self.max_batch = max(1, mb) if mb else len(self.ch)
+        self.cur: list = []                                       # the batch in flight: (src, fields, AsyncRecv, buf)
+        self.batches = 0
         self.landed: dict = collections.defaultdict(list)         # (src, key) -> [(c0, c1, buf)]
         self.expected: dict = {}                                  # (src, key) -> ngroups
         self.received = 0
         self.recv_bytes = 0
         self.wait_us: list = []                                   # post -> landed per transfer
+        self.batch_sizes: list = []
         self.trace = [] if os.environ.get("DGI_KV_TRACE") == "1" else None
         self.digests = {} if CHECKSUM else None                   # (src, key, c0, c1) -> sha1 of installed pages
+        self._rr = 0                                              # round-robin start over sources
+
+    def _queued(self) -> int:
+        return sum(len(q) for q in self.queue.values())
 
     def service(self) -> int:
-        """Take in RTS messages, retire the receive in flight, post the next one.
-        Returns the number of transfers that landed."""
+        """Take in RTS messages, retire the batch in flight once all of it has landed,
+        post the next batch.  Returns the number of transfers that landed."""
         for p, ch in self.ch.items():
             while True:
                 m = ch.poll()
                 if m is None:
                     break
                 assert m[0] == RTS, m
-                self.queue.append((p, [int(x) for x in m[1:8]]))
+                self.queue[p].append([int(x) for x in m[1:8]])
         n = 0
         while True:
-            if self.cur is not None:
-                src, fl, rec, buf = self.cur
-                if not rec.ready():
+            if self.cur:
+                if not all(rec.ready() for _s, _f, rec, _b in self.cur):
                     break
-                rec.complete()
-                self.wait_us.append((time.perf_counter() - rec.t_post) * 1e6)
-                tid, key, group, ng, c0, c1, nblk = fl
-                self.landed[(src, key)].append((c0, c1, buf))
-                self.expected[(src, key)] = ng
-                self.received += 1
-                self.recv_bytes += buf.numel() * buf.element_size()
-                self.cur = None
-                n += 1
-                if self.trace is not None:
-                    self.trace.append(("land", tid, src, time.perf_counter()))
-            if not self.queue:
+                for src, fl, rec, buf in self.cur:
+                    rec.complete()
+                    self.wait_us.append((time.perf_counter() - rec.t_post) * 1e6)
+                    tid, key, group, ng, c0, c1, nblk = fl
+                    self.landed[(src, key)].append((c0, c1, buf))
+                    self.expected[(src, key)] = ng
+                    self.received += 1
+                    self.recv_bytes += buf.numel() * buf.element_size()
+                    n += 1
+                    if self.trace is not None:
+                        self.trace.append(("land", tid, src, time.perf_counter(), self.batches))
+                self.cur = []
+            srcs = [p for p in self.queue if self.queue[p]]
+            if not srcs:
                 break
-            src, fl = self.queue.popleft()
-            tid, key, group, ng, c0, c1, nblk = fl
-            nkv_2 = self.page_shape
-            buf = self.f.alloc_recv((c1 - c0, nkv_2[0], nblk) + nkv_2[1:], self.dtype)
-            rec = self.f.irecv_async(buf, src, group=self.f.kv_group)
-            self.cur = (src, fl, rec, buf)
-            if self.trace is not None:
-                self.trace.append(("post", tid, src, time.perf_counter()))
-            self.ch[src].send([CTS, tid])
+            # the oldest RTS of up to max_batch sources, rotating the start so no source waits
+            k = self._rr % len(srcs)
+            pick = (srcs[k:] + srcs[:k])[: self.max_batch]
+            self._rr += 1
+            items = []
+            for src in pick:
+                fl = self.queue[src].popleft()
+                tid, key, group, ng, c0, c1, nblk = fl
+                nkv_2 = self.page_shape
+                items.append((src, fl, self.f.alloc_recv((c1 - c0, nkv_2[0], nblk) + nkv_2[1:], self.dtype)))
+            recs = self.f.irecv_batch([(buf, src) for src, _fl, buf in items], group=self.f.kv_group)
+            self.batches += 1
+            self.batch_sizes.append(len(items))
+            self.cur = [(src, fl, rec, buf) for (src, fl, buf), rec in zip(items, recs)]
+            for src, fl, _buf in items:
+                if self.trace is not None:
+                    self.trace.append(("post", fl[0], src, time.perf_counter(), self.batches))
+                self.ch[src].send([CTS, fl[0]])
         return n
 
     def is_landed(self, src: int, key: int) -> bool:
@@ -261,25 +294,27 @@ class KVReceiver:
                     idle()
                 if time.perf_counter() - t0 > timeout_s:
                     raise TimeoutError(f"rank {self.f.rank}: KV of migration {key} from rank {src} "
-                                       f"not landed in {timeout_s}s (queue {len(self.queue)})")
+                                       f"not landed in {timeout_s}s (queue {self._queued()})")
                 time.sleep(0.0001)
         return self.take(src, key)
 
     def busy(self) -> bool:
-        return self.cur is not None or bool(self.queue)
+        return bool(self.cur) or self._queued() > 0
 
     def describe(self) -> str:
-        cur = None
-        if self.cur is not None:
-            src, fl, rec, _buf = self.cur
-            cur = (src, fl[0], round(time.perf_counter() - rec.t_post, 1), rec.work.is_completed() if self.f.on_gpu else None)
-        return (f"KVReceiver rank {self.f.rank}: in flight (src, tid, s, done) {cur}, queued "
-                f"{[(p, fl[0]) for p, fl in list(self.queue)[:8]]}, landed {self.received}")
+        cur = [(src, fl[0], round(time.perf_counter() - rec.t_post, 1),
+                rec.work.is_completed() if self.f.on_gpu else None) for src, fl, rec, _buf in self.cur]
+        q = [(p, fl[0]) for p, dq in self.queue.items() for fl in list(dq)[:2]]
+        return (f"KVReceiver rank {self.f.rank}: batch in flight (src, tid, s, done) {cur}, queued "
+                f"{q[:8]}, landed {self.received}")
 
     def stats(self) -> dict:
         w = sorted(self.wait_us)
+        b = self.batch_sizes
         return {"received": self.received, "bytes": self.recv_bytes,
-                "post_to_land_us_p50": round(w[len(w) // 2], 1) if w else None}
+                "post_to_land_us_p50": round(w[len(w) // 2], 1) if w else None,
+                "batches": self.batches, "mean_batch": round(sum(b) / len(b), 2) if b else None,
+                "max_batch": self.max_batch}
 
 
 def scatter_groups(pool_kv: torch.Tensor, ids_t: torch.Tensor, groups: list, digests: Optional[dict] = None,

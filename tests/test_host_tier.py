@@ -138,7 +138,15 @@ def test_streams_created_are_within_the_engine_budget():
                                  host_kv_gb=0.05))
     g = torch.Generator().manual_seed(3)
     prompts = [torch.randint(5, 500, (20 + 3 * i,), generator=g).tolist() for i in range(6)]
-    eng.generate(prompts, SamplingParams(max_tokens=24, temperature=0.0, ignore_eos=True))
+    sp = SamplingParams(max_tokens=24, temperature=0.0, ignore_eos=True)
+    for p in prompts[:3]:
+        eng.add_request(p, sp)
+    for _ in range(2):
+        eng.step()
+    for p in prompts[3:]:                 # admitted while the first three decode: mixed steps
+        eng.add_request(p, sp)
+    while eng.has_unfinished():
+        eng.step()
     torch.cuda.synchronize()
     assert eng.scheduler.stats()["swapped_out"] > 0            # the copy stream was used
     budget = engine_streams(eng)

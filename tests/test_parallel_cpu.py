@@ -672,14 +672,16 @@ def _pd_trace_body(rank, world):
     return {"role": "stage", "trace": w.kvr.trace, "installed": w.installed, "budget": budget}
 
 
-def test_kv_handshake_order_and_one_receive_in_flight(monkeypatch):
+def test_kv_handshake_order_and_one_receive_batch_in_flight(monkeypatch):
     """Clear-to-send protocol (dgi.parallel.kv_transfer): every send is enqueued
-    only after its RTS went out and its CTS came back, and no decode rank ever
-    has two receives posted at once."""
+    only after its RTS went out and its CTS came back; a decode rank has at most
+    ONE batch of receives posted, with at most one receive per source, and posts
+    the next batch only after the whole previous one landed."""
     monkeypatch.setenv("DGI_KV_TRACE", "1")
     monkeypatch.setenv("DGI_TEST_MODEL", "llama-tiny-hd128")
     out = _spawn("_pd_trace_body", 6)
     sends = 0
+    multi = 0
     for r, o in out.items():
         tr = o["trace"]
         if o["role"] == "prefill":
@@ -689,16 +691,40 @@ def test_kv_handshake_order_and_one_receive_in_flight(monkeypatch):
             assert seen and all(v == ["rts", "cts", "send"] for v in seen.values()), seen
             sends += len(seen)
         else:
-            evs = [e for e, *_ in tr]
-            assert evs[0::2] == ["post"] * len(evs[0::2]) and evs[1::2] == ["land"] * len(evs[1::2]), evs
-            assert len(evs) % 2 == 0
+            batches = {}
+            order = []
+            for ev, tid, src, _t, b in tr:
+                batches.setdefault(b, {"post": [], "land": []})[ev].append(src)
+                order.append((ev, b))
+            for b, d in batches.items():
+                assert len(d["post"]) == len(set(d["post"])) <= 2, d      # one receive per source (2 sources)
+                assert sorted(d["post"]) == sorted(d["land"]), d
+                multi += len(d["post"]) > 1
+            # posts of batch b+1 only after every land of batch b
+            last_land = {}
+            for i, (ev, b) in enumerate(order):
+                if ev == "land":
+                    last_land[b] = i
+            for i, (ev, b) in enumerate(order):
+                if ev == "post" and b - 1 in last_land:
+                    assert i > last_land[b - 1], (r, order)
         # communication streams of every role fit the hardware queues of one priority class
         from dgi.parallel.fabric import GPU_HW_QUEUES
         assert len(o["budget"]["high"]) <= GPU_HW_QUEUES - 1 and len(o["budget"]["normal"]) <= GPU_HW_QUEUES
-    received = sum(len(o["trace"]) // 2 for o in out.values() if o["role"] != "prefill")
+    received = sum(sum(1 for e in o["trace"] if e[0] == "land") for o in out.values() if o["role"] != "prefill")
     assert received == sends > 0
     assert out[2]["finished"] + out[4]["finished"] == 2 * len(PROMPTS)
     assert out[3]["installed"] >= 1 and out[5]["installed"] >= 1
+
+
+def test_kv_single_receive_mode_matches(monkeypatch):
+    """DGI_KV_RECV_BATCH=1 (round 3's one receive in flight): same outputs."""
+    monkeypatch.setenv("DGI_KV_RECV_BATCH", "1")
+    monkeypatch.setenv("DGI_TEST_MODEL", "llama-tiny-hd128")
+    monkeypatch.setenv("DGI_TEST_PREFILL", "2")
+    ref = _reference_outputs(model="llama-tiny-hd128")
+    out = _spawn("_pd_body", 4)
+    assert _merged(out, 2) == ref
 
 
 def test_streams_per_rank_fit_hardware_queues():

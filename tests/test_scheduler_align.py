@@ -83,3 +83,38 @@ def test_pure_prefill_steps_are_not_rounded():
     for _ in range(3):
         s.add(Request(list(range(1, 301)), SamplingParams(max_tokens=8)))
     assert s.schedule().num_tokens == 900
+
+
+def test_tpot_slo_step_budget_caps_rows():
+    """dgi.sched.slo.StepBudget: learns ms per row from executed steps and caps the next
+    step at slo / cost rows, never below the decode rows + a minimum prefill chunk."""
+    from dgi.sched.slo import StepBudget
+    b = StepBudget(100.0, min_prefill=128)
+    assert b.budget(4096, 300) == 4096                 # nothing learned yet: no cap
+    b.observe(100, 50.0)                               # too few rows to be GEMM-bound: ignored
+    assert b.ms_per_row is None
+    b.observe(2000, 200.0)                             # 0.1 ms per row
+    assert b.budget(4096, 300) == 1000 and b.capped == 1
+    assert b.budget(4096, 950) == 1078                 # decode rows + the minimum prefill
+    assert b.budget(512, 300) == 512
+    st = b.stats()
+    assert st["budget_rows"] == 1000 and st["steps_observed"] == 1
+
+
+def test_engine_with_tpot_slo_runs_smaller_mixed_steps():
+    """An engine with a TPOT SLO schedules mixed steps below the SLO's row budget once it
+    has measured its step cost; outputs are unchanged (only the chunking differs)."""
+    import torch
+    from dgi.engine import EngineConfig, LLMEngine
+    from dgi.sched.request import SamplingParams
+    g = torch.Generator().manual_seed(0)
+    prompts = [torch.randint(5, 500, (120,), generator=g).tolist() for _ in range(12)]
+    sp = SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True)
+    base = dict(model="llama-tiny", device="cpu", num_blocks=512, max_num_seqs=16, max_model_len=256,
+                max_num_batched_tokens=1024, use_graphs=False, enable_prefix_caching=False)
+    ref = [r.output for r in LLMEngine(EngineConfig(**base)).generate(prompts, sp)]
+    eng = LLMEngine(EngineConfig(**base, tpot_slo_ms=1e-3))     # unreachable: always the minimum step
+    eng.step_budget.min_rows = 1
+    got = [r.output for r in eng.generate(prompts, sp)]
+    assert got == ref
+    assert eng.step_budget.capped > 0 and eng.step_budget.steps > 0

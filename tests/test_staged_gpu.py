@@ -130,3 +130,14 @@ def test_rccl_tensor_parallel_on_shared_gpu(shared_rccl):
     out = tpc._spawn("_tp_gpu_body", 2, timeout=150)
     assert out[0]["out"] == out[1]["out"]                  # SPMD: both ranks emit the same tokens
     _check(out[0]["out"], prompts=out[0]["prompts"], model="llama-tiny-tp")
+
+
+def test_rccl_two_prefill_sources_batched_receives_on_shared_gpu(shared_rccl, monkeypatch):
+    """2 prefill ranks feeding one decode rank over RCCL: the decode rank posts its
+    receives from both sources as one RCCL group (dgi.parallel.kv_transfer); the
+    migrated pages land bit-identical and every token is right."""
+    monkeypatch.setenv("DGI_TEST_PREFILL", "2")
+    monkeypatch.setenv("DGI_KV_CHECKSUM", "1")
+    out = tpc._spawn("_pd_body", 3, timeout=150)
+    _check(tpc._merged(out, 2))
+    assert tpc.check_kv_digests(out) >= 2
