@@ -201,6 +201,8 @@ class LLMEngine:
             outs = self._apply(sb, res.rows, res.tokens)
         dt = time.perf_counter() - t0
         self.stats["step_time"] += dt
+        rh = self.stats.setdefault("rows_hist", {})         # step row counts (GEMM M): tile alignment / SLO
+        rh[sb.num_tokens] = rh.get(sb.num_tokens, 0) + 1
         if sbud is not None and sb.prefill:       # mixed / prefill steps set the per-row cost
             sbud.observe(sb.num_tokens, dt * 1e3)
         return outs

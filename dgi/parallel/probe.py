@@ -48,20 +48,25 @@ class ProbeResult:
 
 
 def _time_steps(eng, steps: int, before=None) -> float:
-    """Mean ms of ``eng.step()`` over ``steps`` (after 2 untimed)."""
+    """Median ms of one ``eng.step()`` over ``steps`` (after 2 untimed; each step ends on its
+    sampled tokens, so its wall time is its device time plus the host work of the step).  The
+    median keeps one slow step (a late allocation, a clock transition) out of the fit."""
+    import statistics
     sync = (lambda: torch.cuda.synchronize()) if eng.device.type == "cuda" else (lambda: None)
     for _ in range(2):
         if before:
             before()
         eng.step()
-    sync()
-    t0 = time.perf_counter()
+    ts = []
     for _ in range(steps):
         if before:
             before()
+        sync()
+        t0 = time.perf_counter()
         eng.step()
-    sync()
-    return (time.perf_counter() - t0) / steps * 1e3
+        sync()
+        ts.append((time.perf_counter() - t0) * 1e3)
+    return statistics.median(ts)
 
 
 def _engine(model: str, mc: ModelConfig, device: str, max_seqs: int, mbt: int, num_blocks: int,
@@ -106,7 +111,7 @@ def _fit(ts: dict) -> tuple:
 
 
 def run_probe(model: str, device: str, prompt_len: int = 512, output_len: int = 128, prefill_mbt: int = 2048,
-              decode_rows=(576, 768), mixed_rows: int = 384, layers=(2, 4), steps: int = 4,
+              decode_rows=(576, 768), mixed_rows: int = 384, layers=(4, 8), steps: int = 8,
               seed: int = 0) -> ProbeResult:
     t_start = time.perf_counter()
     base = get_config(model.split("@")[0] if model else model)
