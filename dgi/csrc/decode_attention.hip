@@ -20,13 +20,21 @@
 //   tile through ds_read_b64_tr_b16 (hardware transpose) with an XOR swizzle
 //   that makes the transposed reads bank-conflict free.
 //   The 4 waves merge (m, l, O) through LDS; with more than one split the
-//   partial results (normalised O and log2-sum-exp) go to a workspace and a
-//   small reduce kernel combines them.
+//   partial results (normalised O and log2-sum-exp) go to a workspace and
+//   either the last-arriving split of each (sequence, kv head) combines them
+//   in the same launch (ticket counters in the workspace: write-through
+//   partials, one relaxed ticket, one acquire on the last arriver) or a small
+//   reduce kernel does.
 #include "common.h"
 
 using namespace dgi;
 
 namespace {
+
+// buffer resource word 3 of a raw (stride 0, byte-addressed) buffer on gfx9, and the cache
+// policy bit of a write-through (sc1) access
+constexpr int kRsrcWord3 = 0x00020000;
+constexpr int kSc1 = 16;
 
 template <int HD>
 __device__ __forceinline__ int v_lds_off(int row, int col) {
@@ -68,6 +76,11 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_kernel(
   const int h = blockIdx.y;
   const int b = blockIdx.z;
   const int ctx = context_lens[b];
+  // write-through views of the split workspace (fused reduce); byte ranges cover the launch
+  const __amdgpu_buffer_rsrc_t po_rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)part_o, 0, (int)min((size_t)gridDim.z * nh * max_splits * HD * 4, (size_t)0x7fffffff), kRsrcWord3);
+  const __amdgpu_buffer_rsrc_t pl_rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)part_lse, 0, (int)min((size_t)gridDim.z * nh * max_splits * 4, (size_t)0x7fffffff), kRsrcWord3);
   // part_size <= 0: device-side split plan from this sequence's own context —
   // up to max_splits parts of at least -part_size tokens (32-token multiples),
   // so a graph captured for the longest context does not leave short ones
@@ -248,6 +261,15 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_kernel(
     const float r = acc / L;
     if (nsplit == 1) {
       out[(size_t)b * out_stride + head * HD + d] = f32_to_bf16(r);
+    } else if (counters != nullptr) {
+      // fused reduce: partials leave with write-through (sc1) stores, so no release fence
+      // (an agent release writes back the whole L2) is needed before the ticket below
+      const size_t pi = ((size_t)b * nh + head) * max_splits + split;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, r), po_rs,
+                                            (int)((pi * HD + d) * 4), 0, kSc1);
+      if (d == 0)
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, M + log2f(L)), pl_rs, (int)(pi * 4), 0,
+                                              kSc1);
     } else {
       const size_t pi = ((size_t)b * nh + head) * max_splits + split;
       part_o[pi * HD + d] = r;
@@ -255,31 +277,38 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_kernel(
     }
   }
   if (nsplit == 1 || counters == nullptr) return;
-  // ---- fused split reduce: the last of the nsplit workgroups of (b, kv-head)
-  // combines all partials (release: fence before the ticket; acquire: fence after)
+  // ---- fused split reduce (MI355X_MICROARCH "Valid forms"): every wave drains its sc1 stores,
+  // the workgroup meets at a barrier, one lane takes a relaxed agent-scope ticket; the workgroup
+  // that draws nsplit - 1 acquires once (invalidates its CU's L1) and combines every split in
+  // split order (deterministic).  No workgroup waits for another: placement-independent.
   __shared__ int s_last;
-  __threadfence();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
-    const int ticket = atomicAdd(&counters[b * nkv + h], 1);
-    s_last = ticket == nsplit - 1;
-    if (s_last) counters[b * nkv + h] = 0;  // ready for the next launch (stream-ordered)
+    const int ticket = __hip_atomic_fetch_add(&counters[b * nkv + h], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = ticket == nsplit - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // ready for the next launch (stream-ordered after this one)
+      __hip_atomic_store(&counters[b * nkv + h], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_last = last;
   }
   __syncthreads();
   if (!s_last) return;
-  __threadfence();
   for (int idx = tid; idx < G * HD; idx += NT) {
     const int qq = idx / HD;
     const int d = idx - qq * HD;
     const int head = h * G + qq;
     const size_t base = ((size_t)b * nh + head) * max_splits;
     float M = -1e30f;
-    for (int sp = 0; sp < nsplit; ++sp) M = fmaxf(M, __builtin_nontemporal_load(part_lse + base + sp));
+    for (int sp = 0; sp < nsplit; ++sp) M = fmaxf(M, part_lse[base + sp]);
     float W = 0.f, acc = 0.f;
     for (int sp = 0; sp < nsplit; ++sp) {
-      const float wgt = exp2f(__builtin_nontemporal_load(part_lse + base + sp) - M);
+      const float wgt = exp2f(part_lse[base + sp] - M);
       W += wgt;
-      acc += wgt * __builtin_nontemporal_load(part_o + (base + sp) * HD + d);
+      acc += wgt * part_o[(base + sp) * HD + d];
     }
     out[(size_t)b * out_stride + head * HD + d] = f32_to_bf16(acc / W);
   }
@@ -326,6 +355,8 @@ extern "C" int dgi_paged_decode(const void* q, int q_stride, const void* k_cache
   // fixed parts: multiples of 128 tokens; dynamic (part_size <= 0): minimum part a multiple of 32
   if ((part_size > 0 && part_size % 128) || (part_size <= 0 && (part_size == 0 || (-part_size) % 32))) return -3;
   if (max_splits <= 1) counters = nullptr;
+  // the fused reduce addresses the partials through 32-bit buffer offsets
+  if ((size_t)B * nh * max_splits * hd * 4 >= ((size_t)1 << 31)) counters = nullptr;
   int bs_log2 = 0;
   while ((1 << bs_log2) < block_size) ++bs_log2;
   if ((1 << bs_log2) != block_size) return -4;

@@ -285,7 +285,9 @@ class Fabric:
                 self.send(t, d, group=group)
             return
         ops_ = [dist.P2POp(dist.isend, t, d, group=group) for t, d in items]
-        works = dist.batch_isend_irecv(ops_)
+        works = list(dist.batch_isend_irecv(ops_) or [])
+        if len(works) != len(items):        # RCCL: one coalesced work for the whole group
+            works = [works[-1]] * len(items)
         for w, (t, _d) in zip(works, items):
             self._track(w, t)
 
@@ -336,6 +338,12 @@ class Fabric:
                 works = dist.batch_isend_irecv(ops_)
         else:
             works = dist.batch_isend_irecv(ops_)
+        works = list(works or [])
+        if len(works) != len(items):
+            # RCCL coalesces the group into ONE work (torch's _coalescing_manager): every
+            # receive of the batch completes with it
+            assert works, "batch_isend_irecv returned no work handle"
+            works = [works[-1]] * len(items)
         return [AsyncRecv(self, w, t) for w, (t, _s) in zip(works, items)]
 
     def alloc_recv(self, shape, dtype) -> torch.Tensor:

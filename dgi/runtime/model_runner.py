@@ -119,12 +119,13 @@ class ModelRunner:
         maxb = max(max_num_seqs, max(graph_buckets) if graph_buckets else 1)
         self.dec_ws = None
         if self.is_cuda:
-            # partial O / log-sum-exp per split (+ with DGI_DECODE_FUSED_REDUCE=1 one ticket counter
-            # per (sequence, kv-head) for the in-kernel split reduce; off by default: its
-            # device-scope fences write back L2 and cost more than the reduce kernel on MI355X)
+            # partial O / log-sum-exp per split + one ticket counter per (sequence, kv-head) for the
+            # in-kernel split reduce (write-through partials, one acquire on the last arriver; round 3's
+            # form fenced every workgroup, which wrote back L2 and cost more than a reduce kernel);
+            # DGI_DECODE_FUSED_REDUCE=0: the separate reduce kernel
             self.dec_ws = (torch.empty(maxb * nh * self.ws_splits * hd, dtype=torch.float32, device=self.device),
                            torch.empty(maxb * nh * self.ws_splits, dtype=torch.float32, device=self.device))
-            if os.environ.get("DGI_DECODE_FUSED_REDUCE", "0") == "1":
+            if os.environ.get("DGI_DECODE_FUSED_REDUCE", "1") == "1":
                 self.dec_ws += (torch.zeros(maxb * model.cfg.num_kv_heads, dtype=torch.int32, device=self.device),)
         # called while the host waits for a step's sampled tokens (P/D ranks keep
         # their KV handshakes moving instead of blocking in a stream synchronize)

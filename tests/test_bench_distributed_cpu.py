@@ -94,3 +94,17 @@ def test_bench_window_counts_exactly_the_tokens_inside_it(n, args):
     assert all(o["prefill_steps_in_window"] >= 1 for o in pre)
     drv = [o for o in ranks if o["role"] == "decode_driver"][0]
     assert drv["micro_steps_in_window"] >= d["steps"] * drv["micro_per_step"] - 1
+
+
+def test_node_step_covers_one_prefill_step():
+    """A P/D node step is enough decode micro-steps of the clock replica to cover one
+    prefill step: from the measured times when the prefill ranks reported them, else
+    from the capacity table, never less than one pipeline round."""
+    sys.path.insert(0, ROOT)
+    from dgi.parallel.bench_dist import node_step_micro
+    from dgi.parallel.plan import CAPACITY
+    cap = CAPACITY["llama3-70b"]
+    assert node_step_micro(cap, 3, 3) == 5                       # 202.1 ms / 42.5 ms -> 5
+    assert node_step_micro(cap, 3, 3, prefill_ms=500.0, micro_ms=40.0) == 13
+    assert node_step_micro(cap, 3, 3, prefill_ms=50.0, micro_ms=40.0) == 3   # one pipeline round at least
+    assert node_step_micro(None, 1, 1) == 1

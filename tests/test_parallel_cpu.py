@@ -251,7 +251,41 @@ def _pd_hol_body(rank, world):
     return {"kv_block_s": w.kv_block_s, "installed": w.installed}
 
 
+def _recv_batch_body(rank, world):
+    """Ranks 1..world-1 each send a distinct tensor to rank 0, which posts ALL the
+    receives as one batch (``Fabric.irecv_batch``) and checks every buffer."""
+    import time as _t
+    from dgi.parallel.fabric import Fabric
+    f = Fabric()
+    dev = f.device if f.on_gpu else torch.device("cpu")
+    n = 1 << 16
+    if rank == 0:
+        bufs = [f.alloc_recv((n,), torch.float32) for _ in range(1, world)]
+        recs = f.irecv_batch([(b, src) for b, src in zip(bufs, range(1, world))], group=f.kv_group)
+        f.barrier()                      # every receive is posted before any send
+        assert len(recs) == world - 1
+        for r in recs:
+            t0 = _t.time()
+            while not r.ready():
+                assert _t.time() - t0 < 60
+                _t.sleep(0.001)
+            r.complete()
+        if f.on_gpu:
+            torch.cuda.synchronize()
+        return [float(b[0]) for b in bufs] + [float(b[-1]) for b in bufs]
+    f.barrier()
+    t = torch.full((n,), float(rank), device=dev)
+    f.send(t, 0)
+    f.flush()
+    return None
+
+
 # ---------------------------------------------------------------------------- tests
+
+def test_receive_batch_completes_every_receive():
+    out = _spawn("_recv_batch_body", 3)
+    assert out[0] == [1.0, 2.0, 1.0, 2.0]
+
 
 def test_decode_pipeline_keeps_stepping_while_a_migration_is_stuck(monkeypatch):
     """Head-of-line: a migration whose last-stage slice is late (2 s) must not stop

@@ -141,3 +141,11 @@ def test_rccl_two_prefill_sources_batched_receives_on_shared_gpu(shared_rccl, mo
     out = tpc._spawn("_pd_body", 3, timeout=150)
     _check(tpc._merged(out, 2))
     assert tpc.check_kv_digests(out) >= 2
+
+
+def test_rccl_receive_batch_completes_every_receive(shared_rccl):
+    """One RCCL group of receives from two sources: RCCL coalesces it into a single work
+    handle, and every receive of the batch must be reported complete with it (a batch
+    that tracked only one handle lost the other transfers)."""
+    out = tpc._spawn("_recv_batch_body", 3, timeout=120)
+    assert out[0] == [1.0, 2.0, 1.0, 2.0]
