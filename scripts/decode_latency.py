@@ -41,15 +41,18 @@ def main():
         for _ in range(4):
             eng.step()
         torch.cuda.synchronize()
+        from dgi.utils.trace import phase_summary
+        phase_summary(reset=True)
         t0 = time.perf_counter()
         for _ in range(a.steps):
             eng.step()
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) / a.steps * 1000
+        ph = {k: v["ms_avg"] for k, v in phase_summary().items()}
         while eng.has_unfinished():
             eng.step()
         rows.append({"model": a.model, "batch": B, "tpot_ms": round(ms, 3), "tok_s": round(B / ms * 1000, 1),
-                     "skinny_max_m": int(os.environ.get("DGI_SKINNY_MAX_M", "32"))})
+                     "skinny_max_m": int(os.environ.get("DGI_SKINNY_MAX_M", "32")), "host_phases_ms": ph})
         print(json.dumps(rows[-1]), flush=True)
     if a.out:
         with open(a.out, "w") as f:

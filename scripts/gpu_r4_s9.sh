@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0 PYTHONUNBUFFERED=1
-timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -k "paged_decode or decode_matches or fused" -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/r4_s9_tests.log 2>&1 || { tail -30 gpurun_out/r4_s9_tests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/r4_s9_tests.log 2>&1 || { tail -30 gpurun_out/r4_s9_tests.log; exit 1; }
 tail -3 gpurun_out/r4_s9_tests.log
 timeout -k 10 300 python -u -m pytest tests/test_staged_gpu.py -m gpu -k "receive_batch or two_prefill" -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/r4_s9_rccl.log 2>&1 || { tail -30 gpurun_out/r4_s9_rccl.log; exit 1; }
 tail -3 gpurun_out/r4_s9_rccl.log

@@ -108,3 +108,21 @@ def test_node_step_covers_one_prefill_step():
     assert node_step_micro(cap, 3, 3, prefill_ms=500.0, micro_ms=40.0) == 13
     assert node_step_micro(cap, 3, 3, prefill_ms=50.0, micro_ms=40.0) == 3   # one pipeline round at least
     assert node_step_micro(None, 1, 1) == 1
+
+
+def test_bench_auto_layout_plans_from_the_startup_probe():
+    """--layout auto on 2 gloo ranks with the start-up probe forced on: every rank probes,
+    the ranks agree on one plan from the median capacity, the run completes, and the
+    JSON carries the planner's source and reason."""
+    env = {**os.environ, "OMP_NUM_THREADS": "1", "DGI_WATCHDOG": "0", "DGI_PROBE": "1"}
+    env.pop("DGI_STAGED_GPU", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
+           "--model", "llama-tiny", "--steps", "4", "--warmup", "1", "--ramp-steps", "2", "--concurrency", "8",
+           "--output-len", "8", "--prompt-len", "32", "--max-batched-tokens", "256"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith('{"metric"')][-1])
+    pl = d["extra"]["planner"]
+    assert pl["source"] == "probe" and pl["kind"] in ("dp", "pd", "pdpp") and pl["reason"]
+    assert d["value"] > 0 and "auto:" in d["metric_scope"]
