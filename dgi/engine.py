@@ -47,6 +47,8 @@ class EngineConfig:
                                        # row tile; -1 = 256 on GPU engines, 0 = off): SchedulerConfig
     tpot_slo_ms: float = 0.0           # > 0: cap each step's rows so a step (= a decode token's wait)
                                        # stays under this (dgi.sched.slo.StepBudget)
+    decode_lookahead: bool = True      # pure-decode graph steps: launch step N+1 before step N's
+                                       # tokens are back (``LLMEngine._lookahead``); DGI_DECODE_LOOKAHEAD=0
 
 
 @dataclasses.dataclass
@@ -141,6 +143,10 @@ class LLMEngine:
         self.runner = ModelRunner(self.model, self.pool, cfg.max_num_seqs, cfg.max_model_len,
                                   cfg.max_num_batched_tokens, cfg.use_graphs, **rkw)
         self.requests: dict = {}
+        # decode lookahead: (ScheduledBatch, launch handle) of a step in flight, not applied yet
+        import os as _os
+        self._la = None
+        self.lookahead = bool(cfg.decode_lookahead) and _os.environ.get("DGI_DECODE_LOOKAHEAD", "1") == "1"
         self.step_budget = None
         if cfg.tpot_slo_ms > 0:
             from dgi.sched.slo import StepBudget
@@ -177,7 +183,7 @@ class LLMEngine:
         return self.scheduler.abort(rid)
 
     def has_unfinished(self) -> bool:
-        return self.scheduler.has_work()
+        return self._la is not None or self.scheduler.has_work()
 
     def warmup(self) -> None:
         """Capture decode graphs ahead of serving."""
@@ -185,6 +191,8 @@ class LLMEngine:
             self.runner.graphs.capture()
 
     def step(self) -> list[StepOutput]:
+        if self._la is not None:
+            return self._step_lookahead()
         t0 = time.perf_counter()
         self.model.kv_cache = self.pool.kv   # engines may share one model object
         with phase("schedule"):
@@ -195,6 +203,13 @@ class LLMEngine:
             return []
         if self.pre_execute is not None:
             self.pre_execute(sb)
+        if self._lookahead_ok(sb):
+            # pure decode on the graphs: launch it, then (while it runs) the step after it
+            self.runner.step_id += 1
+            self._la = (sb, self.runner.graphs.launch(sb.decode))
+            out = self._step_lookahead()
+            self.stats["step_time"] += time.perf_counter() - t0
+            return out
         with phase("execute", decode=len(sb.decode), prefill=len(sb.prefill)):
             res = self.runner.execute(sb)
         with phase("apply"):
@@ -206,6 +221,49 @@ class LLMEngine:
         if sbud is not None and sb.prefill:       # mixed / prefill steps set the per-row cost
             sbud.observe(sb.num_tokens, dt * 1e3)
         return outs
+
+    # ------------------------------------------------------------------ decode lookahead
+    def _lookahead_ok(self, sb) -> bool:
+        """Decode lookahead applies to pure-decode steps on the captured graphs of a plain
+        engine with nothing else to schedule (no waiting prompt, no prefill chunk, no swap)."""
+        g = self.runner.graphs
+        return (self.lookahead and g is not None and type(self) is LLMEngine and not sb.prefill and sb.decode
+                and not sb.preempted and len(sb.decode) <= g.max_bucket and not self.scheduler.waiting
+                and self.pre_execute is None and self.step_budget is None
+                and all(r.swapped is None for r in sb.decode))
+
+    def _step_lookahead(self) -> list[StepOutput]:
+        """Collect and apply the step in flight — after launching the next one when every
+        row continues (no length stop due, nothing waiting to be scheduled): the host work
+        of applying step N and packing step N+1 overlaps step N+1 on the GPU instead of
+        leaving the GPU idle between graph replays.  A row whose step-N token ends it
+        (EOS / stop id) still runs in step N+1; that token is discarded when applied."""
+        sb, h = self._la
+        self._la = None
+        g = self.runner.graphs
+        nxt = None
+        cap = self.cfg.max_model_len - 1
+        live = [r for r in sb.decode if r.status is Status.RUNNING]
+        # the running set must be exactly these rows: a sequence admitted meanwhile (P/D import,
+        # swap-in) ends the chain so the next step schedules it
+        if live and len(live) == len(sb.decode) == len(self.scheduler.running) and not self.scheduler.waiting and all(
+                len(r.output) + 1 < r.params.max_tokens and len(r.prompt) + len(r.output) + 1 < cap for r in live):
+            try:
+                for r in live:                       # the page of position num_computed + 1
+                    self.scheduler._grow(r, r.num_computed + 2)
+                nxt = live
+            except Exception:                        # out of pages: no lookahead this step
+                nxt = None
+        if nxt is not None:
+            self.runner.step_id += 1
+            self._la = (type(sb)(list(nxt), [], []), g.launch(nxt, ahead=1))
+        with phase("execute", decode=len(sb.decode), prefill=0):
+            toks = g.collect(h)
+        with phase("apply"):
+            keep = [(r, t) for r, t in zip(sb.decode, toks) if r.status is Status.RUNNING]
+            if len(keep) != len(sb.decode):          # finished at the previous step: tokens discarded
+                sb = type(sb)([r for r, _t in keep], [], [])
+            return self._apply(sb, [r for r, _t in keep], [t for _r, t in keep])
 
     def _apply(self, sb, rows, tokens) -> list[StepOutput]:
         """Commit one executed batch: advance KV cursors, append tokens, stop checks."""

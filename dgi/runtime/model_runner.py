@@ -65,13 +65,15 @@ def graph_capture(g, pool=None):
             gc.enable()
 
 
-def decode_rows(reqs: list, bs: int, bt_out: np.ndarray):
+def decode_rows(reqs: list, bs: int, bt_out: np.ndarray, ahead: int = 0):
     """Per-row decode metadata of ``reqs``, vectorised (the per-request Python work is
     one attribute read per field): returns (input token, position, KV slot, context
     length) int32 arrays and fills ``bt_out[:n]`` (zeroed by the caller) with the
-    block tables."""
+    block tables.  ``ahead``: tokens each row has in flight that are not applied yet
+    (decode lookahead: positions move on by that many; the input token then comes
+    from the device, the returned ids are placeholders)."""
     n = len(reqs)
-    pos = np.fromiter((r.num_computed for r in reqs), np.int32, n)
+    pos = np.fromiter((r.num_computed + ahead for r in reqs), np.int32, n)
     ids = np.fromiter((r.output[-1] if r.output else r.prompt[-1] for r in reqs), np.int32, n)
     lens = np.fromiter((len(r.blocks) for r in reqs), np.int64, n)
     tot = int(lens.sum())
@@ -84,12 +86,12 @@ def decode_rows(reqs: list, bs: int, bt_out: np.ndarray):
     return ids, pos, slots.astype(np.int32), pos + 1
 
 
-def sampling_rows(sampled: list):
+def sampling_rows(sampled: list, ahead: int = 0):
     """(temperature bits, seed, top-k, top-p bits, any filtered) of the sampled rows."""
     n = len(sampled)
     nf = [r.params.needs_filter for r in sampled]
     temps = np.fromiter((r.params.temperature for r in sampled), np.float32, n).view(np.int32)
-    seeds = np.fromiter((r.sample_seed() for r in sampled), np.int64, n).astype(np.int32)
+    seeds = np.fromiter((r.sample_seed(ahead) for r in sampled), np.int64, n).astype(np.int32)
     topk = np.fromiter((max(0, r.params.top_k) if f else 0 for r, f in zip(sampled, nf)), np.int32, n)
     topp = np.fromiter((r.params.top_p if f else 1.0 for r, f in zip(sampled, nf)), np.float32, n).view(np.int32)
     return temps, seeds, topk, topp, any(nf)
@@ -329,10 +331,11 @@ class GraphRunner:
         # with ONE H2D copy and each bucket's graph reads its inputs straight out of it (round 3
         # copied nine device views into separate static tensors: nine copy launches per step)
         self.NSEG = 8
-        self.host_in = torch.zeros(maxb * (self.NSEG + maxw), dtype=torch.int32).pin_memory()
+        self.host_in2 = [torch.zeros(maxb * (self.NSEG + maxw), dtype=torch.int32).pin_memory() for _ in range(2)]
+        self.host_out2 = [torch.zeros(maxb, dtype=torch.long).pin_memory() for _ in range(2)]
+        self._flip = 0
         self.dev_in = torch.zeros(maxb * (self.NSEG + maxw), dtype=torch.int32, device=dev)
         self.out = torch.zeros(maxb, dtype=torch.long, device=dev)
-        self.host_out = torch.zeros(maxb, dtype=torch.long).pin_memory()
         self.captured = False
         # optional EAGLE-3 feature tap captured with the step: (layer ids, fuse fn) -> [b, H] per bucket
         self.features = None
@@ -418,15 +421,26 @@ class GraphRunner:
         self.captured = True
 
     def run(self, sb: ScheduledBatch) -> list:
+        return self.collect(self.launch(sb.decode))
+
+    def launch(self, dec: list, ahead: int = 0) -> tuple:
+        """Enqueue one decode step of rows ``dec`` (H2D of the packed inputs, graph replay,
+        async D2H of the sampled tokens) without waiting for it; ``collect`` returns its
+        tokens.  ``ahead=1``: every row has one token in flight from the previous launch
+        (decode lookahead) — positions move on by one and the input tokens are that
+        launch's sampled tokens, copied on the device in stream order.  Staging buffers
+        alternate, so a launch never rewrites the host buffers of the one before it."""
         if not self.captured:
             self.capture()
-        n = len(sb.decode)
+        n = len(dec)
         b = next(x for x in self.buckets if x >= n)
         r = self.r
         bs = r.bs
         maxw = r.max_blocks
         S = self.NSEG
-        h = self.host_in.numpy()
+        self._flip ^= 1
+        host_in, host_out = self.host_in2[self._flip], self.host_out2[self._flip]
+        h = host_in.numpy()
         seg = h[: S * b].reshape(S, b)
         ids, pos, slots, ctx = seg[0], seg[1], seg[2], seg[3]
         temps, seeds, topk = seg[4].view(np.float32), seg[5], seg[6]
@@ -436,20 +450,35 @@ class GraphRunner:
         ctx[:] = 1
         topp[:] = 1.0
         bt[:] = 0
-        dec = sb.decode
-        ids[:n], pos[:n], slots[:n], ctx[:n] = decode_rows(dec, bs, bt)
-        tb, seeds[:n], topk[:n], pb, _f = sampling_rows(dec)
+        ids[:n], pos[:n], slots[:n], ctx[:n] = decode_rows(dec, bs, bt, ahead)
+        tb, seeds[:n], topk[:n], pb, _f = sampling_rows(dec, ahead)
         temps[:n] = tb.view(np.float32)
         topp[:n] = pb.view(np.float32)
         max_ctx = int(ctx[:n].max()) if n else 0
         k = S * b + b * maxw
-        self.dev_in[:k].copy_(self.host_in[:k], non_blocking=True)
+        self.dev_in[:k].copy_(host_in[:k], non_blocking=True)
+        if ahead:
+            self.dev_in[:n].copy_(self.out[:n])        # the previous launch's tokens (same rows, same order)
         gs = self.short_graphs.get(b)
         short = gs is not None and max_ctx <= self.short_ctx
         (gs if short else self.graphs[b]).replay()
         self.last_bucket = b
         self.last_key = (b, short)
-        return self.r.fetch(self.out[:n], self.host_out[:n])
+        host_out[:n].copy_(self.out[:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return (ev, host_out, n)
+
+    def collect(self, handle: tuple) -> list:
+        ev, host_out, n = handle
+        wh = self.r.wait_hook
+        if wh is None:
+            ev.synchronize()
+        else:
+            while not ev.query():
+                wh()
+                time.sleep(0.00002)
+        return host_out[:n].tolist()
 
     def last_features(self, n: int) -> torch.Tensor:
         """Fused EAGLE-3 features of the last replay's first ``n`` rows (feature tap on)."""

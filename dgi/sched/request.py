@@ -72,12 +72,12 @@ class Request:
     def all_tokens(self) -> list[int]:
         return self.prompt + self.output
 
-    def sample_seed(self) -> int:
+    def sample_seed(self, ahead: int = 0) -> int:
         """Seed of the next sampled token: a function of the request alone (its seed
-        and how many tokens it has produced), so a seeded request draws the same
-        tokens whatever the batching, the engine's step count or the parallel
-        layout (single GPU, pipeline, P/D, graph or eager)."""
-        return (self.seed * 1000003 + len(self.output)) & 0x7FFFFFFF
+        and how many tokens it has produced, ``ahead`` of them still in flight), so a
+        seeded request draws the same tokens whatever the batching, the engine's step
+        count or the parallel layout (single GPU, pipeline, P/D, graph or eager)."""
+        return (self.seed * 1000003 + len(self.output) + ahead) & 0x7FFFFFFF
 
     @property
     def in_prefill(self) -> bool:

@@ -586,3 +586,40 @@ def test_fused_decode_model_matches_unfused():
     # both paths pick, at every step, an argmax of the fp32 model's logits (up to bf16 tolerance)
     for o in outs:
         assert _teacher_forced_ok("llama-tiny-hd128", src, prompts, o) == 64
+
+
+@pytest.mark.parametrize("sampled", [False, True])
+def test_decode_lookahead_matches_plain_decode(sampled, monkeypatch):
+    """Decode lookahead (step N+1 launched before step N's tokens are back) gives the same
+    tokens as plain graph decoding, with length stops at different steps, an EOS stop that
+    lands while the next step is already in flight, and seeded sampling."""
+    from dgi.engine import EngineConfig, LLMEngine
+    from dgi.models.config import get_config
+    from dgi.models.llama import LlamaModel
+    from dgi.sched.request import SamplingParams
+    mc = get_config("llama-tiny-hd128")
+    src = LlamaModel(mc, "cuda", seed=7)
+    prompts = [[1] + list(range(3, 3 + n)) for n in (5, 40, 130, 7)]
+
+    def sp(i, eos_ok):
+        return SamplingParams(max_tokens=9 + 4 * i, temperature=0.8 if sampled else 0.0, top_k=20 if sampled else 0,
+                              seed=100 + i, ignore_eos=not eos_ok)
+
+    def run(lookahead, eos=None):
+        cfg = EngineConfig(model="llama-tiny-hd128", device="cuda", num_blocks=256, max_num_seqs=8, max_model_len=512,
+                           max_num_batched_tokens=512, use_graphs=True, decode_lookahead=lookahead)
+        e = LLMEngine(cfg, model_cfg=get_config("llama-tiny-hd128"), model=src)
+        if eos is not None:
+            e.model_cfg.eos_token_id = eos
+        reqs = [e.add_request(p, sp(i, eos is not None)) for i, p in enumerate(prompts)]
+        while e.has_unfinished():
+            e.step()
+        return [r.output for r in reqs], [r.finish_reason for r in reqs]
+
+    plain, _ = run(False)
+    la, _ = run(True)
+    assert la == plain
+    eos = plain[2][5]                       # the third prompt's 6th token ends it (and maybe others)
+    p2, f2 = run(False, eos)
+    l2, g2 = run(True, eos)
+    assert l2 == p2 and g2 == f2 and "stop" in f2
