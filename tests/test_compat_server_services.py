@@ -188,7 +188,7 @@ class _W:
 
 @pytest.mark.parametrize("worker,token,err", [
     (None, "x", "worker_not_found"),
-    (_W(locked_until=datetime.utcnow() + timedelta(minutes=1)), "good", "account_locked"),
+    (_W(locked_until=datetime.utcnow() + timedelta(days=1)), "good", "account_locked"),
     (_W(), "bad", "invalid_token"),
     (_W(token_expires_at=datetime.utcnow() - timedelta(seconds=1)), "good", "token_expired"),
     (_W(failed_auth_attempts=2), "good", ""),

@@ -259,6 +259,9 @@ def _recv_batch_body(rank, world):
     f = Fabric()
     dev = f.device if f.on_gpu else torch.device("cpu")
     n = 1 << 16
+    # RCCL connects a pair on its first transfer, with both ends inside the call: the
+    # serving paths connect every pair up front (Fabric.connect_pairs), so does this
+    f.connect_pairs([(0, s) for s in range(1, world)])
     if rank == 0:
         bufs = [f.alloc_recv((n,), torch.float32) for _ in range(1, world)]
         recs = f.irecv_batch([(b, src) for b, src in zip(bufs, range(1, world))], group=f.kv_group)
