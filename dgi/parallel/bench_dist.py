@@ -94,7 +94,7 @@ def run_distributed(args, layout_kind: str, dist):
     conc = args.concurrency or (rows * k if k > 1 else 1024)
     # staged rehearsal: every rank shares one GPU, so each takes a slice of its memory
     from dgi.parallel.fabric import shared_gpu
-    kv_frac = float(os.environ.get("DGI_KV_FRACTION", 0.5 / world if (f.staged or shared_gpu()) else 0.9))
+    kv_frac = float(os.environ.get("DGI_KV_FRACTION", 0.35 / world if (f.staged or shared_gpu()) else 0.9))
     cfg = EngineConfig(model=args.model, device=str(f.device), max_num_seqs=conc,
                        max_num_batched_tokens=args.max_batched_tokens,
                        max_model_len=max(2048, args.prompt_len + args.output_len + 64),

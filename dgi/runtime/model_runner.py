@@ -123,11 +123,13 @@ class ModelRunner:
         if self.is_cuda:
             # partial O / log-sum-exp per split + one ticket counter per (sequence, kv-head) for the
             # in-kernel split reduce (write-through partials, one acquire on the last arriver; round 3's
-            # form fenced every workgroup, which wrote back L2 and cost more than a reduce kernel);
-            # DGI_DECODE_FUSED_REDUCE=0: the separate reduce kernel
+            # form fenced every workgroup, which wrote back L2 and cost more than a reduce kernel).
+            # Opt-in (DGI_DECODE_FUSED_REDUCE=1): 8B TPOT ties the reduce kernel at batch 1-4 and
+            # loses 0.09-0.23 ms at batch 16-64, where the last arriver's serial combine is the
+            # tail of the launch (profiles/r4_decode/README.md)
             self.dec_ws = (torch.empty(maxb * nh * self.ws_splits * hd, dtype=torch.float32, device=self.device),
                            torch.empty(maxb * nh * self.ws_splits, dtype=torch.float32, device=self.device))
-            if os.environ.get("DGI_DECODE_FUSED_REDUCE", "1") == "1":
+            if os.environ.get("DGI_DECODE_FUSED_REDUCE", "0") == "1":
                 self.dec_ws += (torch.zeros(maxb * model.cfg.num_kv_heads, dtype=torch.int32, device=self.device),)
         # called while the host waits for a step's sampled tokens (P/D ranks keep
         # their KV handshakes moving instead of blocking in a stream synchronize)
