@@ -47,7 +47,10 @@ def main():
     ap.add_argument("--batch", type=int, nargs="+", default=[1, 4])
     ap.add_argument("--ctx", type=int, nargs="+", default=[128, 256, 384, 512, 1024, 2048])
     ap.add_argument("--chain", type=int, default=32)
+    ap.add_argument("--heads", type=int, nargs=2, default=[nh, nkv])
     a = ap.parse_args()
+    globals().update(nh=a.heads[0], nkv=a.heads[1])
+    ops.load_native(required=True)
     dev = "cuda"
     scale = 1 / math.sqrt(hd)
     for B in a.batch:
@@ -66,18 +69,21 @@ def main():
             wsc = ws + (torch.zeros(B * nkv, dtype=torch.int32, device=dev),)
             want = max(1, -(-4 * 256 // (B * nkv)))
             splits = min(ms, want)
-            ref = ops.paged_decode(q, kc, vc, bt, ctx, nh, nkv, scale, max_splits=1, part_size=1 << 20).float()
-            row = {"batch": B, "ctx": C}
-            for name, kw in (("one_split", dict(max_splits=1, part_size=1 << 20)),
-                             ("split_reduce", dict(max_splits=splits, part_size=-128, workspace=ws)),
-                             ("split_fused", dict(max_splits=splits, part_size=-128, workspace=wsc))):
-                fn = lambda kw=kw: ops.paged_decode(q, kc, vc, bt, ctx, nh, nkv, scale, out=out, **kw)  # noqa: E731
-                row[name + "_us"] = round(graph_us(fn, a.chain), 2)
-                err = (out.float() - ref).abs().max().item()
-                row[name + "_err"] = round(err, 4)
+            ref = ops.paged_decode_ref(q, kc, vc, bt, ctx, nh, nkv, scale).float()
+            row = {"batch": B, "ctx": C, "heads": [nh, nkv]}
+            _variants(row, q, kc, vc, bt, ctx, out, ref, ws, wsc, splits, scale, a.chain)
             src = torch.randn(B, nh * hd, device=dev, dtype=torch.bfloat16)
             row["copy_floor_us"] = round(graph_us(lambda: out.copy_(src), a.chain), 2)
             print(json.dumps(row), flush=True)
+
+
+def _variants(row, q, kc, vc, bt, ctx, out, ref, ws, wsc, splits, scale, chain):
+    for name, kw in (("one_split", dict(max_splits=1, part_size=1 << 20)),
+                     ("split_reduce", dict(max_splits=splits, part_size=-128, workspace=ws)),
+                     ("split_fused", dict(max_splits=splits, part_size=-128, workspace=wsc))):
+        fn = lambda kw=kw: ops.paged_decode(q, kc, vc, bt, ctx, nh, nkv, scale, out=out, **kw)  # noqa: E731
+        row[name + "_us"] = round(graph_us(fn, chain), 2)
+        row[name + "_err"] = round((out.float() - ref).abs().max().item(), 4)
 
 
 if __name__ == "__main__":

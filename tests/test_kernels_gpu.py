@@ -88,8 +88,18 @@ def _block_tables(ctx_lens, bs, nblocks, maxw):
                                        (14, 2, 64)])
 @pytest.mark.parametrize("ctx_lens", [[1], [17, 300, 64, 1000], [4097, 33]])
 def test_paged_decode(nh, nkv, hd, ctx_lens):
-    bs = 16
-    maxw = 300
+    """Every plan: one split, split + reduce kernel, fixed parts, device-side plan + ticket reduce."""
+    _paged_decode_case(nh, nkv, hd, ctx_lens)
+
+
+@pytest.mark.parametrize("bs", [8, 32, 64])
+def test_paged_decode_block_sizes(bs):
+    """32-token tiles over 4 / 1 / half a block of the paged pool."""
+    _paged_decode_case(32, 8, 128, [1, 33, 700, 2100], bs=bs)
+
+
+def _paged_decode_case(nh, nkv, hd, ctx_lens, bs=16):
+    maxw = max(300, max((c + bs - 1) // bs for c in ctx_lens))
     nblocks = sum((c + bs - 1) // bs for c in ctx_lens) + 8
     kc, vc = _make_cache(nblocks, nkv, bs, hd)
     bt = _block_tables(ctx_lens, bs, nblocks, maxw)
