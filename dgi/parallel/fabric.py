@@ -45,9 +45,11 @@ import torch
 import torch.distributed as dist
 
 GPU_HW_QUEUES = 4          # HIP default hardware queues per priority class per process
-# DGI_BATCH_P2P=1: CTS'd sends to several peers leave as one RCCL group (concurrent links);
-# default 0: one ordered send each on the world communicator's stream
-BATCH_P2P = os.environ.get("DGI_BATCH_P2P", "0") == "1"
+# CTS'd sends to several peers leave as one RCCL group (concurrent links; every receive of the
+# group is already posted, so the group cannot wait on anything).  DGI_BATCH_P2P=0: one ordered
+# send each on the world communicator's stream (round 3).  Shared-GPU rehearsals, 2P+6D:
+# prefill RTS->CTS p50 131 ms batched vs 427 ms one by one (profiles/r4_rccl_rehearsal/)
+BATCH_P2P = os.environ.get("DGI_BATCH_P2P", "1") == "1"
 
 
 def shared_gpu() -> bool:
@@ -280,7 +282,7 @@ class Fabric:
         different peers progress concurrently over their own xGMI links."""
         if not items:
             return
-        if self.staged or len(items) == 1 or not BATCH_P2P:
+        if self.staged or not self.on_gpu or len(items) == 1 or not BATCH_P2P:
             for t, d in items:
                 self.send(t, d, group=group)
             return
