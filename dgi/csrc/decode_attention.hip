@@ -59,7 +59,7 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_kernel(
     const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ context_lens, uint16_t* __restrict__ out, int out_stride,
     float* __restrict__ part_o, float* __restrict__ part_lse, int* __restrict__ counters, int max_splits, int nh,
-    int nkv, int bs_log2, int part_size, float scale_log2) {
+    int nkv, int bs_log2, int part_size, float scale_log2, bool page16) {
   constexpr int KS = HD / 32;   // k-steps of the QK^T product
   constexpr int NC = HD / 16;   // 16-wide dim blocks of the PV product
   constexpr int VCH = HD / 8;   // 16-byte chunks per V row
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_kernel(
   const int bs = 1 << bs_log2;
 
   const int tid = threadIdx.x;
-  const int w = tid >> 6;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: tile bases in SGPRs
   const int lane = tid & 63;
   const int qi = lane & 15;
   const int g = lane >> 4;
@@ -129,29 +129,58 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_kernel(
   const int ntiles = (end - start + 31) >> 5;
   for (int t = w; t < ntiles; t += NW) {
     const int tb = start + (t << 5);
-    // ---- K fragments straight to VGPRs (A operand: row = token, k = dims)
     u32x4 kf[2][KS];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      int tok = tb + 16 * u + qi;
-      tok = min(tok, end - 1);
-      const int blk = bt[tok >> bs_log2];
-      const uint16_t* kp = k_cache + ((size_t)blk * nkv + h) * head_stride + (size_t)(tok & (bs - 1)) * HD;
-#pragma unroll
-      for (int s = 0; s < KS; ++s) kf[u][s] = *reinterpret_cast<const u32x4*>(kp + 32 * s + 8 * g);
-    }
-    // ---- V tile -> registers -> swizzled LDS
     u32x4 vr[VCH / 2];
+    if (page16 && tb + 32 <= end) {
+      // full tile of 16-token pages (the engine's page size): its two pages come from two
+      // scalar block-table reads, every lane's offset inside a page is a constant, so each
+      // load is an SGPR base + a fixed VGPR offset (no per-load 64-bit address arithmetic:
+      // at small batch the tile loop is VALU-issue-bound)
+      const int fb = tb >> 4;
+      const uint16_t* kp[2];
+      const uint16_t* vp[2];
 #pragma unroll
-    for (int k = 0; k < VCH / 2; ++k) {
-      // 32 rows x VCH chunks; each pass covers 64/VCH rows
-      const int idx = k * 64 + lane;
-      const int row = idx / VCH;
-      const int ch = idx % VCH;
-      int tok = min(tb + row, end - 1);
-      const int blk = bt[tok >> bs_log2];
-      const uint16_t* vp = v_cache + ((size_t)blk * nkv + h) * head_stride + (size_t)(tok & (bs - 1)) * HD;
-      vr[k] = *reinterpret_cast<const u32x4*>(vp + ch * 8);
+      for (int j = 0; j < 2; ++j) {
+        const size_t page = ((size_t)bt[fb + j] * nkv + h) * head_stride;
+        kp[j] = k_cache + page;
+        vp[j] = v_cache + page;
+      }
+      // ---- K fragments straight to VGPRs (A operand: row = token, k = dims)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+          kf[u][s] = *reinterpret_cast<const u32x4*>(kp[u] + qi * HD + 32 * s + 8 * g);
+      // ---- V tile -> registers (row 4k + lane / VCH of the tile; rows 16-31 on the second page)
+#pragma unroll
+      for (int k = 0; k < VCH / 2; ++k) {
+        const int idx = k * 64 + lane;
+        const int row = idx / VCH;
+        vr[k] = *reinterpret_cast<const u32x4*>(vp[row >> 4] + (row & 15) * HD + (idx % VCH) * 8);
+      }
+    } else {
+      // ---- K fragments straight to VGPRs (A operand: row = token, k = dims)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        int tok = tb + 16 * u + qi;
+        tok = min(tok, end - 1);
+        const int blk = bt[tok >> bs_log2];
+        const uint16_t* kpl = k_cache + ((size_t)blk * nkv + h) * head_stride + (size_t)(tok & (bs - 1)) * HD;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) kf[u][s] = *reinterpret_cast<const u32x4*>(kpl + 32 * s + 8 * g);
+      }
+      // ---- V tile -> registers -> swizzled LDS
+#pragma unroll
+      for (int k = 0; k < VCH / 2; ++k) {
+        // 32 rows x VCH chunks; each pass covers 64/VCH rows
+        const int idx = k * 64 + lane;
+        const int row = idx / VCH;
+        const int ch = idx % VCH;
+        int tok = min(tb + row, end - 1);
+        const int blk = bt[tok >> bs_log2];
+        const uint16_t* vpl = v_cache + ((size_t)blk * nkv + h) * head_stride + (size_t)(tok & (bs - 1)) * HD;
+        vr[k] = *reinterpret_cast<const u32x4*>(vpl + ch * 8);
+      }
     }
     // ---- S^T = K Q^T
     f32x4 sacc[2];
@@ -171,30 +200,42 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_kernel(
       const int ch = idx % VCH;
       *reinterpret_cast<u32x4*>(vt + v_lds_off<HD>(row, ch * 8)) = vr[k];
     }
-    // ---- online softmax (lane owns query qi; tokens 16u + 4g + i)
+    // ---- online softmax (lane owns query qi; tokens 16u + 4g + i); only the sequence's last
+    // tile has tokens past its end to mask
+    const bool full = tb + 32 <= end;
     float x[2][4];
     float mx = -1e30f;
+    if (full) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int tok = tb + 16 * u + 4 * g + i;
-        const float v = (tok < end) ? sacc[u][i] * scale_log2 : -1e30f;
-        x[u][i] = v;
-        mx = fmaxf(mx, v);
-      }
+        for (int i = 0; i < 4; ++i) {
+          x[u][i] = sacc[u][i] * scale_log2;
+          mx = fmaxf(mx, x[u][i]);
+        }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int tok = tb + 16 * u + 4 * g + i;
+          const float v = (tok < end) ? sacc[u][i] * scale_log2 : -1e30f;
+          x[u][i] = v;
+          mx = fmaxf(mx, v);
+        }
+    }
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float m_new = fmaxf(m_run, mx);
-    const float alpha = exp2f(m_run - m_new);
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
     float psum = 0.f;
     float p[2][4];
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int tok = tb + 16 * u + 4 * g + i;
-        p[u][i] = (tok < end) ? exp2f(x[u][i] - m_new) : 0.f;
+        // masked tokens hold -1e30: exp2 of (-1e30 - m_new) is exactly 0
+        p[u][i] = __builtin_amdgcn_exp2f(x[u][i] - m_new);
         psum += p[u][i];
       }
     psum += __shfl_xor(psum, 16, 64);
@@ -361,6 +402,12 @@ extern "C" int dgi_paged_decode(const void* q, int q_stride, const void* k_cache
   while ((1 << bs_log2) < block_size) ++bs_log2;
   if ((1 << bs_log2) != block_size) return -4;
   const float scale_log2 = scale * 1.4426950408889634f;
+  // full tiles of 16-token pages take the scalar-page-base load path (DGI_DECODE_PAGE16=0: off)
+  static const bool page16_on = [] {
+    const char* e = getenv("DGI_DECODE_PAGE16");
+    return !(e && e[0] == '0');
+  }();
+  const bool page16 = page16_on && bs_log2 == 4;
   dim3 grid(max_splits, nkv, B);
   // few workgroups (small batch, one split: every (sequence, kv head) walks its whole
   // context): 8 waves per workgroup halve the serial tile chain of each wave
@@ -370,12 +417,12 @@ extern "C" int dgi_paged_decode(const void* q, int q_stride, const void* k_cache
       paged_decode_kernel<128, 8><<<grid, 512, 8 * decode_wave_lds<128>(), s>>>(
           (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,
           block_tables, bt_stride, context_lens, (uint16_t*)out, out_stride, part_o, part_lse,
-          counters, max_splits, nh, nkv, bs_log2, part_size, scale_log2);
+          counters, max_splits, nh, nkv, bs_log2, part_size, scale_log2, page16);
     } else {
       paged_decode_kernel<128, 4><<<grid, 256, 4 * decode_wave_lds<128>(), s>>>(
           (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,
           block_tables, bt_stride, context_lens, (uint16_t*)out, out_stride, part_o, part_lse,
-          counters, max_splits, nh, nkv, bs_log2, part_size, scale_log2);
+          counters, max_splits, nh, nkv, bs_log2, part_size, scale_log2, page16);
     }
     DGI_CHECK_LAUNCH();
     if (max_splits > 1 && counters == nullptr) {
@@ -389,12 +436,12 @@ extern "C" int dgi_paged_decode(const void* q, int q_stride, const void* k_cache
       paged_decode_kernel<64, 8><<<grid, 512, 8 * decode_wave_lds<64>(), s>>>(
           (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,
           block_tables, bt_stride, context_lens, (uint16_t*)out, out_stride, part_o, part_lse,
-          counters, max_splits, nh, nkv, bs_log2, part_size, scale_log2);
+          counters, max_splits, nh, nkv, bs_log2, part_size, scale_log2, page16);
     } else {
       paged_decode_kernel<64, 4><<<grid, 256, 4 * decode_wave_lds<64>(), s>>>(
           (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,
           block_tables, bt_stride, context_lens, (uint16_t*)out, out_stride, part_o, part_lse,
-          counters, max_splits, nh, nkv, bs_log2, part_size, scale_log2);
+          counters, max_splits, nh, nkv, bs_log2, part_size, scale_log2, page16);
     }
     DGI_CHECK_LAUNCH();
     if (max_splits > 1 && counters == nullptr) {
