@@ -21,6 +21,7 @@ median, so every rank picks the same layout.
 from __future__ import annotations
 
 import dataclasses
+import os
 import random
 import time
 from typing import Optional
@@ -207,10 +208,18 @@ def median_capacity(caps: list):
         decode_rows=dict(c0.decode_rows), mixed_step_ms=med([c.mixed_step_ms for c in caps]))
 
 
-def plan_from_probe(world: int, cap, min_ratio: float = 1.0) -> dict:
+# auto picks P/D only when its estimate beats data parallel by more than the measured
+# box-to-box spread of one GPU's throughput (~4-5 %, profiles/r4_slo/, BASELINE.md): a pick
+# inside the noise would trade a well-rehearsed layout for a coin flip
+PD_MIN_RATIO = float(os.environ.get("DGI_PD_MIN_RATIO", "1.05"))
+
+
+def plan_from_probe(world: int, cap, min_ratio: Optional[float] = None) -> dict:
     """The auto layout under ``cap``: the planner's best P/D split, kept only when its
-    disaggregated estimate reaches ``min_ratio`` x ``world`` data-parallel GPUs
-    (VERDICT r3 #8: never pick a layout the planner itself rates below DP)."""
+    disaggregated estimate reaches ``min_ratio`` (default ``PD_MIN_RATIO``) x ``world``
+    data-parallel GPUs (VERDICT r3 #8: never pick a layout the planner itself rates below DP)."""
+    if min_ratio is None:
+        min_ratio = PD_MIN_RATIO
     from dgi.parallel.plan import choose_pd_layout, layout_estimate
     npre, k, reps, _ = choose_pd_layout(world, cap)
     est = layout_estimate(npre, k, reps, cap)
@@ -218,6 +227,6 @@ def plan_from_probe(world: int, cap, min_ratio: float = 1.0) -> dict:
     pd_ok = est["disagg_tok_s"] >= min_ratio * dp
     kind = ("pdpp" if k > 1 else "pd") if pd_ok else "dp"
     why = (f"P/D {est['layout']} estimated {est['disagg_tok_s']:.0f} tok/s "
-           f"{'>=' if pd_ok else '<'} {world} DP GPUs {dp:.0f} tok/s")
+           f"{'>=' if pd_ok else '<'} {min_ratio:g} x {world} DP GPUs {dp:.0f} tok/s")
     return {"kind": kind, "prefill_ranks": npre, "decode_stages": k, "decode_replicas": reps, "estimate": est,
             "dp_tok_s": round(dp, 1), "reason": why}

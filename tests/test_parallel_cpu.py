@@ -827,11 +827,21 @@ def test_auto_layout_never_runs_a_pd_split_rated_below_dp():
     assert d["kind"] == "dp" and "<" in d["reason"] and d["estimate"]["disagg_tok_s"] < d["dp_tok_s"]
     fast = dataclasses.replace(tab, decode_tok_s={k: v * 1.35 for k, v in tab.decode_tok_s.items()},
                                decode_step_ms={k: v / 1.35 for k, v in tab.decode_step_ms.items()})
-    d = plan_from_probe(8, fast)
+    d = plan_from_probe(8, fast, min_ratio=1.0)
     assert d["kind"] in ("pd", "pdpp") and d["estimate"]["disagg_tok_s"] >= d["dp_tok_s"]
+    # 2.3 % above DP is inside the box-to-box spread: the default margin (PD_MIN_RATIO 1.05) keeps DP
+    ratio = d["estimate"]["disagg_tok_s"] / d["dp_tok_s"]
+    assert 1.0 <= ratio < 1.05
+    tie = plan_from_probe(8, fast)
+    assert tie["kind"] == "dp" and "<" in tie["reason"]
+    faster = dataclasses.replace(fast, prefill_tok_s=tab.prefill_tok_s * 1.25)
+    d = plan_from_probe(8, faster)
+    assert d["kind"] in ("pd", "pdpp") and d["estimate"]["disagg_tok_s"] >= 1.05 * d["dp_tok_s"]
     try:
-        set_capacity("llama3-70b", fast)          # what the start-up probe does with its measurement
+        set_capacity("llama3-70b", faster)        # what the start-up probe does with its measurement
         assert bench.auto_layout(8, "llama3-70b@L8") == d["kind"]
+        set_capacity("llama3-70b", fast)
+        assert bench.auto_layout(8, "llama3-70b@L8") == "dp"
     finally:
         set_capacity("llama3-70b", None)
     assert bench.auto_layout(8, "llama3-70b") == "dp"
