@@ -318,9 +318,9 @@ class GraphRunner:
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         # small buckets also get a one-split variant (8-wave workgroups walk each
         # sequence's whole context: no partials, no reduce kernel) replayed when
-        # every context is short (DGI_DECODE_SHORT_CTX tokens, 0 = off; at ~900 tokens the split
-        # plan is faster again: profiles/r3_decode8b_short_ctx.md)
-        self.short_ctx = int(os.environ.get("DGI_DECODE_SHORT_CTX", "512"))
+        # every context is short (DGI_DECODE_SHORT_CTX tokens, 0 = off; the one-split plan wins up to
+        # ~700 tokens, the split plan from ~1k: profiles/r4_decode/attn_b1_plans.jsonl, page16 rows)
+        self.short_ctx = int(os.environ.get("DGI_DECODE_SHORT_CTX", "640"))
         self.short_max_b = int(os.environ.get("DGI_DECODE_SHORT_B", "8"))
         self.short_graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self._short = False
