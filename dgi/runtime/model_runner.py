@@ -319,7 +319,7 @@ class GraphRunner:
         # small buckets also get a one-split variant (8-wave workgroups walk each
         # sequence's whole context: no partials, no reduce kernel) replayed when
         # every context is short (DGI_DECODE_SHORT_CTX tokens, 0 = off; the one-split plan wins up to
-        # ~700 tokens, the split plan from ~1k: profiles/r4_decode/attn_b1_plans.jsonl, page16 rows)
+        # ~700 tokens, the split plan from ~1k: profiles/r4_decode/attn8b_p16_1.jsonl)
         self.short_ctx = int(os.environ.get("DGI_DECODE_SHORT_CTX", "640"))
         self.short_max_b = int(os.environ.get("DGI_DECODE_SHORT_B", "8"))
         self.short_graphs: dict[int, torch.cuda.CUDAGraph] = {}

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4, session 19: decode attention with block ids loaded one tile ahead: numerics, small-batch plan
+# Round 4, session 19: decode attention (scalar page bases for full 16-token-page tiles, hardware exp2): numerics, small-batch plan
 # timings, 70B batch-384 check, 8B decode TPOT.
 set -o pipefail
 mkdir -p gpurun_out
