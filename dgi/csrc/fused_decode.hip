@@ -383,26 +383,38 @@ __global__ __launch_bounds__(NW * 64) void fused_skinny_persist_kernel(FusedArgs
   const size_t lane_k = (size_t)g * 16 + (size_t)w * 64;
   const bool lo = r < 8;
   const bool xval = r < M;
-  auto tile_c0 = [&](int ti) { return (ti / a.tpg) * a.gstride + (ti % a.tpg) * 8; };
-
-  // flattened group s of this workgroup: tile t_first + s / ngroups, K group s % ngroups
-  auto load = [&](Frag<U, 1>& f, int s) {
-    const int tl = s / ngroups;
-    const int grp = s - tl * ngroups;
-    const int c0 = tile_c0(t_first + tl);
+  // Walk the flattened groups s (tile t_first + s / ngroups, K group s % ngroups) with
+  // incremental cursors: a runtime integer division is ~30 scalar instructions, and with
+  // two per group (consumer and loader) the scalar unit, shared by the CU's 16 waves, was
+  // issuing more than the vector units (PMC, profiles/r4_decode/pmc_decode8b_b1_step.md)
+  struct Cursor { int grp, tq, tr; };       // K group, (tile / tpg, tile % tpg)
+  auto c0_of = [&](const Cursor& c) { return c.tq * a.gstride + c.tr * 8; };
+  auto advance = [&](Cursor& c) {
+    if (++c.grp == ngroups) {
+      c.grp = 0;
+      if (++c.tr == a.tpg) { c.tr = 0; ++c.tq; }
+    }
+  };
+  auto load = [&](Frag<U, 1>& f, const Cursor& c) {
+    const int c0 = c0_of(c);
     const uint16_t* w0 = a.w + (size_t)(lo ? c0 + r : c0 + a.pair_off + r - 8) * K + lane_k;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const size_t off = ((size_t)grp * NW * U + (size_t)u * NW) * 64;
+      const size_t off = ((size_t)c.grp * NW * U + (size_t)u * NW) * 64;
       const u32x4* p0 = reinterpret_cast<const u32x4*>(w0 + off);
       f.w[u][0][0] = __builtin_nontemporal_load(p0);
       f.w[u][0][1] = __builtin_nontemporal_load(p0 + 1);
     }
   };
+  Cursor cons{0, t_first / a.tpg, t_first % a.tpg};   // the group being consumed
+  Cursor ld = cons;                                      // the next group to load
   Frag<U, 1> ring[D];
 #pragma unroll
   for (int d = 0; d < D; ++d)
-    if (d < total) load(ring[d], d);
+    if (d < total) {
+      load(ring[d], ld);
+      advance(ld);
+    }
 
   stage_x<NW, PRO>(a, xs, s_part, s_inv, bid);
 
@@ -414,8 +426,7 @@ __global__ __launch_bounds__(NW * 64) void fused_skinny_persist_kernel(FusedArgs
     for (int d = 0; d < D; ++d) {
       const int s = base + d;
       if (s < total) {          // uniform
-        const int tl = s / ngroups;
-        const int grp = s - tl * ngroups;
+        const int grp = cons.grp;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int off = (grp * NW * U + u * NW) * 64;
@@ -427,12 +438,15 @@ __global__ __launch_bounds__(NW * 64) void fused_skinny_persist_kernel(FusedArgs
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xa), as_bf16x8(ring[d].w[u][0][0]), acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xb), as_bf16x8(ring[d].w[u][0][1]), acc, 0, 0, 0);
         }
-        if (s + D < total) load(ring[d], s + D);
+        if (s + D < total) {
+          load(ring[d], ld);
+          advance(ld);
+        }
         if (grp == ngroups - 1) {     // tile done: cross-wave sum, epilogue on wave 0
           red[parity][w][lane] = acc;
           __syncthreads();
           if (w == 0) {
-            const int c0 = tile_c0(t_first + tl);
+            const int c0 = c0_of(cons);
             const int c1 = c0 + a.pair_off;
             f32x4 v = red[parity][0][lane];
 #pragma unroll
@@ -451,6 +465,7 @@ __global__ __launch_bounds__(NW * 64) void fused_skinny_persist_kernel(FusedArgs
           acc = f32x4{0.f, 0.f, 0.f, 0.f};
           parity ^= 1;
         }
+        advance(cons);
       }
     }
   }
@@ -494,26 +509,37 @@ __global__ __launch_bounds__(NW * 64) void fused_skinny_quarter_kernel(FusedArgs
     const int ti = qp >> 1;
     return (ti / a.tpg) * a.gstride + (ti % a.tpg) * 8 + (qp & 1) * 4 + (j & 3);
   };
-  auto load = [&](Frag<U, 1>& f, int s) {
-    const int st = s / ngroups;
-    const int grp = s - st * ngroups;
-    const int row = lane_row(st);
-    if (row < 0) return;   // idle lanes: their MFMA columns are never stored
-    const uint16_t* w0 = a.w + (size_t)(lo ? row : row + a.pair_off) * K + lane_k;
+  // incremental cursor over the flattened groups (step s / ngroups, K group s % ngroups): no
+  // integer division per group; the lane's row is recomputed once per step
+  struct Cursor { int grp, st, row; };
+  auto advance = [&](Cursor& c) {
+    if (++c.grp == ngroups) {
+      c.grp = 0;
+      c.row = lane_row(++c.st);
+    }
+  };
+  auto load = [&](Frag<U, 1>& f, const Cursor& c) {
+    if (c.row < 0) return;   // idle lanes: their MFMA columns are never stored
+    const uint16_t* w0 = a.w + (size_t)(lo ? c.row : c.row + a.pair_off) * K + lane_k;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const size_t off = ((size_t)grp * NW * U + (size_t)u * NW) * 64;
+      const size_t off = ((size_t)c.grp * NW * U + (size_t)u * NW) * 64;
       const u32x4* p0 = reinterpret_cast<const u32x4*>(w0 + off);
       f.w[u][0][0] = __builtin_nontemporal_load(p0);
       f.w[u][0][1] = __builtin_nontemporal_load(p0 + 1);
     }
   };
+  Cursor cons{0, 0, lane_row(0)};
+  Cursor ld = cons;
   Frag<U, 1> ring[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
 #pragma unroll
     for (int u = 0; u < U; ++u) ring[d].w[u][0][0] = ring[d].w[u][0][1] = u32x4{0u, 0u, 0u, 0u};
-    if (d < total) load(ring[d], d);
+    if (d < total) {
+      load(ring[d], ld);
+      advance(ld);
+    }
   }
 
   stage_x<NW, PRO>(a, xs, s_part, s_inv, bid);
@@ -526,8 +552,7 @@ __global__ __launch_bounds__(NW * 64) void fused_skinny_quarter_kernel(FusedArgs
     for (int d = 0; d < D; ++d) {
       const int s = base + d;
       if (s < total) {          // uniform
-        const int st = s / ngroups;
-        const int grp = s - st * ngroups;
+        const int grp = cons.grp;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int off = (grp * NW * U + u * NW) * 64;
@@ -539,12 +564,15 @@ __global__ __launch_bounds__(NW * 64) void fused_skinny_quarter_kernel(FusedArgs
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xa), as_bf16x8(ring[d].w[u][0][0]), acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(xb), as_bf16x8(ring[d].w[u][0][1]), acc, 0, 0, 0);
         }
-        if (s + D < total) load(ring[d], s + D);
+        if (s + D < total) {
+          load(ring[d], ld);
+          advance(ld);
+        }
         if (grp == ngroups - 1) {     // step done: cross-wave sum, epilogue on wave 0
           red[parity][w][lane] = acc;
           __syncthreads();
           if (w == 0) {
-            const int row = lane_row(st);
+            const int row = cons.row;
             f32x4 v = red[parity][0][lane];
 #pragma unroll
             for (int jj = 1; jj < NW; ++jj) v += red[parity][jj][lane];
@@ -562,6 +590,7 @@ __global__ __launch_bounds__(NW * 64) void fused_skinny_quarter_kernel(FusedArgs
           acc = f32x4{0.f, 0.f, 0.f, 0.f};
           parity ^= 1;
         }
+        advance(cons);
       }
     }
   }
