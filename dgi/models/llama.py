@@ -323,7 +323,7 @@ class LlamaModel:
                 else:
                     ops.fused_add_rmsnorm(h, residual, L.in_norm, eps)
                 attn = self.attention(i, ops.linear(h, L.qkv, L.qkv_bias), meta)
-            h = ops.linear(attn, L.o)
+            h = ops.decode_proj(attn, L.o)
             if self.reduce is not None:
                 self.reduce(h)
             if fuse_gu:

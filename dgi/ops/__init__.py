@@ -484,6 +484,24 @@ def fused_skinny(y, x, res, res_out, gamma, eps, w, bias, pro: int, epi: int, po
                             k_cache, v_cache, nh, nkv)
 
 
+# batch-1 decode o-proj (no prologue / epilogue) through the persistent fused GEMV config 16:
+# 8.35 vs 8.80 us for the skinny kernel on Llama-3-8B (profiles/r4_decode/plain_proj_fused_configs.json);
+# at M >= 2 the skinny kernel is as fast or faster.  DGI_OPROJ_FUSED=0: always ops.linear
+OPROJ_FUSED = os.environ.get("DGI_OPROJ_FUSED", "1") == "1"
+
+
+def decode_proj(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """A decode step's plain projection (o-proj): the persistent fused GEMV at one row,
+    ``linear`` otherwise."""
+    M, K = x.shape
+    if (OPROJ_FUSED and M == 1 and _native(x) and x.dtype == torch.bfloat16 and x.is_contiguous()
+            and fused_decode_ok(M, K, "qkv") and w.shape[0] % 16 == 0):
+        y = torch.empty(M, w.shape[0], dtype=x.dtype, device=x.device)
+        _call("fused_skinny", y, x, None, None, None, 0.0, w, None, 0, 0, None, None, None, None, None, 0, 0, 16)
+        return y
+    return linear(x, w)
+
+
 def silu_mul_ref(gu: torch.Tensor) -> torch.Tensor:
     I = gu.shape[-1] // 2
     g = gu[..., :I].float()
