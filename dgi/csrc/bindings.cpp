@@ -30,6 +30,7 @@ int dgi_skinny_gemm(const void* x, int ldx, const void* w, const void* bias, voi
                     int N, int K, int nw, hipStream_t s);
 int dgi_mfma_gemm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int epi,
                   hipStream_t s);
+void dgi_set_gemm_cus(int cus);
 int dgi_fused_skinny(const void* x, int ldx, const void* res, int ldr, void* res_out, const void* gamma,
                      float eps, const void* w, const void* bias, void* y, int ldy, int M, int N, int K, int pro,
                      int epi, const int* positions, const float* cos_sin, const int* slots, void* k_cache,
@@ -433,9 +434,14 @@ void tree_verify(at::Tensor accept_len, at::Tensor path, at::Tensor out_tokens,
                            cur_stream()), "tree_verify");
 }
 
+// CUs the MFMA GEMM's persistent launches size their grid for (0 = the device's; a CU-masked
+// two-batch-overlap step sets the GEMM stream's share)
+void set_gemm_cus(int64_t cus) { dgi_set_gemm_cus(static_cast<int>(cus)); }
+
 }  // namespace
 
 TORCH_LIBRARY(dgi, m) {
+  m.def("set_gemm_cus(int cus) -> ()", &set_gemm_cus);
   m.def("rmsnorm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
   m.def("fused_add_rmsnorm(Tensor(a!) x, Tensor(b!) residual, Tensor w, float eps) -> ()");
   m.def("rope_cache(Tensor(a!) qkv, Tensor positions, Tensor cos_sin, int nh, int nkv, int hd, "

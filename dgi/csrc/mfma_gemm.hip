@@ -867,6 +867,12 @@ SkWorkspace* sk_workspace(hipStream_t s) {
   return &w;
 }
 
+// CUs the persistent / split-K launches size their grid for (0 = all of the device's): a GEMM
+// issued on a CU-masked stream (two-batch-overlap decode steps keep a few CUs of every XCD for
+// attention) must not launch one block per device CU, or the blocks past the mask run as a
+// second round.  Set by the host around such a step (dgi_set_gemm_cus).
+int g_cu_limit = 0;
+
 // skmode 0: whole tiles only; 1: hybrid split-K when the tiles leave the last wave at most half
 // full (and fewer than 8 full waves); 2: hybrid whenever tiles % CUs leaves room for 2 splits
 template <int EPI>
@@ -883,23 +889,24 @@ void launch_pp(const void* x, int ldx, const void* w, void* y, int ldy, int M, i
   const int nt = K / kBK;
   SkWorkspace* sk = ((skmode || a.ovl) && nt >= 8) ? sk_workspace(s) : nullptr;
   if (sk) {
-    const int full = total / sk->P, rem = total % sk->P;
-    const int splits = rem ? min(4, sk->P / rem) : 0;
+    const int P = (g_cu_limit >= 8 && g_cu_limit < sk->P) ? (g_cu_limit & ~7) : sk->P;
+    const int full = total / P, rem = total % P;
+    const int splits = rem ? min(4, P / rem) : 0;
     if (skmode && splits >= 2 && (full < 8 || skmode == 2)) {
       a.ws = sk->ws;
       a.cnt = sk->cnt;
       a.rem = rem;
       a.splits = splits;
       a.full = full;
-      a.P = sk->P;
-      kern<<<dim3(sk->P), 512, 0, s>>>(a);
+      a.P = P;
+      kern<<<dim3(P), 512, 0, s>>>(a);
       return;
     }
     if (a.ovl && rem == 0 && full >= 2) {
       // whole waves of tiles: persistent, so each block's next tile loads under this one's epilogue
       a.full = full;
-      a.P = sk->P;
-      kern<<<dim3(sk->P), 512, 0, s>>>(a);
+      a.P = P;
+      kern<<<dim3(P), 512, 0, s>>>(a);
       return;
     }
   }
@@ -928,6 +935,8 @@ void launch(const void* x, int ldx, const void* w, void* y, int ldy, int M, int 
 // s_setprio variant of schedule 3, (epi >> 12) & 1: two 32-MFMA phases per K tile, (epi >> 13) & 1:
 // four 16-MFMA phases (default: two up to M = 2560, see mfma_gemm_pp_kernel), (epi >> 14) & 1: no
 // cross-tile overlap (next tile's prologue after the epilogue; whole waves of tiles not persistent).
+extern "C" void dgi_set_gemm_cus(int cus) { g_cu_limit = cus; }
+
 extern "C" int dgi_mfma_gemm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K,
                              int epi, hipStream_t s) {
   if (M <= 0) return 0;

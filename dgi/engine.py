@@ -13,7 +13,7 @@ from typing import Iterable, Optional
 
 import torch
 
-from dgi.kv.block_pool import BlockPool, num_blocks_for_budget
+from dgi.kv.block_pool import BlockPool, OutOfBlocks, num_blocks_for_budget
 from dgi.models.config import ModelConfig, get_config
 from dgi.models.llama import LlamaModel
 from dgi.runtime.model_runner import ModelRunner
@@ -182,6 +182,22 @@ class LLMEngine:
         self.requests.pop(rid, None)
         return self.scheduler.abort(rid)
 
+    def admission_limit(self) -> Optional[int]:
+        """Sequences this engine keeps in flight (running + one step of queued prompts)
+        without missing its TPOT SLO; None without an SLO or before it has measured
+        enough.  A closed-loop client sizes its concurrency to it."""
+        sbud = self.step_budget
+        if sbud is None:
+            return None
+        cap = sbud.admission_cap(self.cfg.max_num_batched_tokens)
+        if cap is None:
+            return None
+        rows = sbud.rows_at_slo() or 0
+        queued = max(1, int((rows - rows * (sbud.output_avg or 0) / max(1.0, (sbud.prompt_avg or 0) +
+                                                                         (sbud.output_avg or 0)))
+                            / max(1.0, sbud.prompt_avg or 1.0)))
+        return cap + queued
+
     def has_unfinished(self) -> bool:
         return self._la is not None or self.scheduler.has_work()
 
@@ -191,13 +207,19 @@ class LLMEngine:
             self.runner.graphs.capture()
 
     def step(self) -> list[StepOutput]:
-        if self._la is not None:
-            return self._step_lookahead()
         t0 = time.perf_counter()
+        if self._la is not None:
+            n = len(self._la[0].decode)
+            outs = self._step_lookahead()
+            self._account(n, time.perf_counter() - t0)
+            return outs
         self.model.kv_cache = self.pool.kv   # engines may share one model object
         with phase("schedule"):
             sbud = self.step_budget
-            cap = None if sbud is None else sbud.budget(self.cfg.max_num_batched_tokens, len(self.scheduler.running))
+            cap = None
+            if sbud is not None:
+                cap = sbud.budget(self.cfg.max_num_batched_tokens, len(self.scheduler.running))
+                self.scheduler.admit_cap = sbud.admission_cap(self.cfg.max_num_batched_tokens)
             sb = self.scheduler.schedule(max_tokens=cap)
         if sb.empty:
             return []
@@ -208,18 +230,36 @@ class LLMEngine:
             self.runner.step_id += 1
             self._la = (sb, self.runner.graphs.launch(sb.decode))
             out = self._step_lookahead()
-            self.stats["step_time"] += time.perf_counter() - t0
+            self._account(sb.num_tokens, time.perf_counter() - t0)
             return out
         with phase("execute", decode=len(sb.decode), prefill=len(sb.prefill)):
             res = self.runner.execute(sb)
         with phase("apply"):
             outs = self._apply(sb, res.rows, res.tokens)
         dt = time.perf_counter() - t0
-        self.stats["step_time"] += dt
-        rh = self.stats.setdefault("rows_hist", {})         # step row counts (GEMM M): tile alignment / SLO
-        rh[sb.num_tokens] = rh.get(sb.num_tokens, 0) + 1
+        self._account(sb.num_tokens, dt)
         if sbud is not None and sb.prefill:       # mixed / prefill steps set the per-row cost
             sbud.observe(sb.num_tokens, dt * 1e3)
+        return outs
+
+    def _account(self, rows: int, dt: float) -> None:
+        """Step wall time and row-count histogram (every step, lookahead chains included)."""
+        self.stats["step_time"] += dt
+        rh = self.stats.setdefault("rows_hist", {})         # step row counts (GEMM M): tile alignment / SLO
+        rh[rows] = rh.get(rows, 0) + 1
+
+    def drain(self) -> list[StepOutput]:
+        """Collect and apply a lookahead step still in flight (teardown, or before the
+        running set is changed from outside the engine)."""
+        outs = []
+        if self._la is not None:
+            sb, h = self._la
+            self._la = None
+            toks = self.runner.graphs.collect(h)
+            keep = [(r, t) for r, t in zip(sb.decode, toks) if r.status is Status.RUNNING]
+            if keep:
+                outs = self._apply(type(sb)([r for r, _t in keep], [], []), [r for r, _t in keep],
+                                   [t for _r, t in keep])
         return outs
 
     # ------------------------------------------------------------------ decode lookahead
@@ -252,8 +292,8 @@ class LLMEngine:
                 for r in live:                       # the page of position num_computed + 1
                     self.scheduler._grow(r, r.num_computed + 2)
                 nxt = live
-            except Exception:                        # out of pages: no lookahead this step
-                nxt = None
+            except OutOfBlocks:                      # out of pages: no lookahead this step (pages grown
+                nxt = None                           # for earlier rows are the ones they need next step)
         if nxt is not None:
             self.runner.step_id += 1
             self._la = (type(sb)(list(nxt), [], []), g.launch(nxt, ahead=1))
@@ -263,7 +303,12 @@ class LLMEngine:
             keep = [(r, t) for r, t in zip(sb.decode, toks) if r.status is Status.RUNNING]
             if len(keep) != len(sb.decode):          # finished at the previous step: tokens discarded
                 sb = type(sb)([r for r, _t in keep], [], [])
-            return self._apply(sb, [r for r, _t in keep], [t for _r, t in keep])
+            outs = self._apply(sb, [r for r, _t in keep], [t for _r, t in keep])
+        if self._la is not None and not any(r.status is Status.RUNNING for r in self._la[0].decode):
+            # every row of the launch in flight stopped at this step (EOS / stop id): collect it now
+            # (its tokens are discarded) instead of leaving the engine with work and no requests
+            self.drain()
+        return outs
 
     def _apply(self, sb, rows, tokens) -> list[StepOutput]:
         """Commit one executed batch: advance KV cursors, append tokens, stop checks."""
@@ -304,6 +349,8 @@ class LLMEngine:
                 finish(req, reason)
                 st["finished"] += 1
                 self.requests.pop(req.rid, None)
+                if self.step_budget is not None:
+                    self.step_budget.observe_finished(len(req.prompt), len(out))
             outs.append(StepOutput(req.rid, tok, reason is not None, reason, req))
         st["generated"] += len(outs)
         return outs

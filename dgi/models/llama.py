@@ -43,6 +43,44 @@ QKV_PAD = os.environ.get("DGI_QKV_PAD", "0") == "1"
 OPROJ_PAD = os.environ.get("DGI_OPROJ_PAD", "0") == "1"
 # mixed steps: decode-row attention on a side stream beside the prefill-row attention
 ATTN_OVERLAP = os.environ.get("DGI_ATTN_OVERLAP", "1") == "1"
+# Two-batch overlap (TBO) of large pure-decode steps (``LlamaModel._forward_layers_tbo``): the
+# rows are cut in two tile-aligned halves whose decode attention runs on a few CUs of every
+# XCD (``DGI_TBO_SIDE`` per XCD) while the other half's GEMM chain runs on the rest.  Two
+# plain streams do not overlap (a full-chip GEMM holds every CU: graph-forked GEMM + HBM stream
+# 0.713 vs 0.751 ms serial); CU-masked streams do for a plain HBM stream (1.56 vs 1.70 ms
+# eagerly), and a captured graph drops the masks, so TBO steps run eagerly.  OFF by default:
+# on the 27-layer 70B decode stage at 768 rows it MEASURED 67.0 ms against 41.9 eager / 39.8
+# graph-replayed (profiles/r5_pd/README.md) — split-KV decode attention is latency-bound per
+# CU (32 CUs ran it 3.1x slower than 256, not 8x) and the half-size GEMMs beside it ran 1.85x
+# slower than their share; DGI_TBO=1 turns it on for experiments.
+TBO = os.environ.get("DGI_TBO", "0") == "1"
+TBO_MIN_ROWS = int(os.environ.get("DGI_TBO_MIN_ROWS", "512"))
+TBO_SIDE_PER_XCD = int(os.environ.get("DGI_TBO_SIDE", "4"))
+
+
+def tbo_split(T: int) -> Optional[tuple]:
+    """(rows of half A, rows of half B) of a T-row TBO step: B is half of T rounded down to the
+    256-row GEMM tile (at least one tile), A the rest; None below ``TBO_MIN_ROWS``."""
+    if T < max(512, TBO_MIN_ROWS):
+        return None
+    b = max(256, (T // 2) // 256 * 256)
+    return T - b, b
+
+
+class TboStreams:
+    """The CU-masked stream pair of a device's TBO steps (created once per process)."""
+
+    def __init__(self, device: torch.device, side_per_xcd: int):
+        from dgi.utils.streams import cu_masked_stream, xcd_split
+        n = torch.cuda.get_device_properties(device).multi_processor_count
+        main, side = xcd_split(n, side_per_xcd)
+        self.gemm = cu_masked_stream("tbo_gemm", device, main)
+        self.attn = cu_masked_stream("tbo_attn", device, side)
+        self.gemm_cus = len(main)
+        self.events = [torch.cuda.Event() for _ in range(4)]     # q ready / attention done, per half
+
+
+_TBO_STREAMS: dict = {}
 
 class LlamaLayerWeights:
     __slots__ = ("in_norm", "qkv", "o", "post_norm", "gate_up", "down", "qkv_bias")
@@ -343,6 +381,103 @@ class LlamaModel:
                 self.layer_hook(self.layer_start + i)
         return h, residual
 
+    # ------------------------------------------------------------------ two-batch overlap
+    def _tbo_ok(self, h: torch.Tensor, meta: AttnMeta, trim_last) -> Optional[tuple]:
+        if not (TBO and h.is_cuda and self.layers and meta.num_prefill_tokens == 0 and trim_last is None
+                and self.reduce is None and not self.capture_layers and self.layer_hook is None
+                and h.dtype == torch.bfloat16 and not torch.cuda.is_current_stream_capturing()):
+            return None
+        return tbo_split(h.shape[0])
+
+    @staticmethod
+    def _rows_meta(meta: AttnMeta, a: int, b: int) -> AttnMeta:
+        """Decode metadata of rows [a, b) of a pure-decode step."""
+        return AttnMeta(positions=meta.positions[a:b], slot_mapping=meta.slot_mapping[a:b], num_decode=b - a,
+                        dec_block_tables=meta.dec_block_tables[a:b], dec_context_lens=meta.dec_context_lens[a:b],
+                        dec_max_splits=meta.dec_max_splits, dec_part_size=meta.dec_part_size,
+                        dec_workspace=meta.dec_workspace, num_prefill_tokens=0, logits_indices=None)
+
+    def _forward_layers_tbo(self, h: torch.Tensor, meta: AttnMeta, residual: Optional[torch.Tensor], split: tuple):
+        """Pure-decode layers as two halves A | B: half X's attention (RoPE + paged KV write +
+        split-KV decode attention) runs on the side stream's CUs while the GEMM stream runs
+        the other half's o-proj, MLP and next QKV, so the attention (~23 % of a 768-row 70B
+        stage step) hides under GEMMs instead of following them.  Per layer, in issue order::
+
+            gemm: pre(A, i+1) | post(B, i) pre(B, i+1) | post(A, i+1) ...
+            attn:        attn(A, i+1) ->         attn(B, i+1) -> ...
+
+        pre = (add +) RMSNorm + QKV GEMM; post = o-proj + add + RMSNorm + gate_up (SwiGLU) + down.
+        Row-independent, so the outputs equal the one-batch step's up to GEMM blocking."""
+        dev = h.device
+        st = _TBO_STREAMS.get(dev.index)
+        if st is None:
+            st = _TBO_STREAMS[dev.index] = TboStreams(dev, TBO_SIDE_PER_XCD)
+        G, S = st.gemm, st.attn
+        eq = st.events[:2]
+        ea = st.events[2:]
+        c = self.cfg
+        eps = c.rms_eps
+        T = h.shape[0]
+        na = split[0]
+        bounds = ((0, na), (na, T))
+        metas = [self._rows_meta(meta, a, b) for a, b in bounds]
+        main = torch.cuda.current_stream()
+        G.wait_stream(main)
+        S.wait_stream(main)
+        hs = [h[a:b] for a, b in bounds]
+        res = [None if residual is None else residual[a:b] for a, b in bounds]
+        rows = [b - a for a, b in bounds]
+        impl = [(self.mlp_impl(r) if self.mlp_impl is not None else (False, False)) +
+                (self.proj_impl(r) if self.proj_impl is not None else (False, False)) for r in rows]
+        qkv = [None, None]
+        att = [None, None]
+        n = len(self.layers)
+        ops.set_gemm_cus(st.gemm_cus)
+        try:
+            def pre(x, i):
+                L = self.layers[i]
+                if res[x] is None:
+                    res[x] = hs[x]
+                    hs[x] = ops.rmsnorm(hs[x], L.in_norm, eps)
+                else:
+                    ops.fused_add_rmsnorm(hs[x], res[x], L.in_norm, eps)
+                q = ops.mfma_gemm(hs[x], L.qkv, 0) if (impl[x][2] and L.qkv_bias is None) else \
+                    ops.linear(hs[x], L.qkv, L.qkv_bias)
+                o = torch.empty(rows[x], c.q_size, device=dev, dtype=h.dtype)
+                q.record_stream(S)
+                o.record_stream(S)
+                qkv[x], att[x] = q, o
+                eq[x].record(G)
+                with torch.cuda.stream(S):
+                    S.wait_event(eq[x])
+                    self.attention(i, q, metas[x], out=o)
+                    ea[x].record(S)
+
+            def post(x, i):
+                L = self.layers[i]
+                G.wait_event(ea[x])
+                hh = ops.mfma_gemm(att[x], L.o, 0) if impl[x][3] else ops.linear(att[x], L.o)
+                ops.fused_add_rmsnorm(hh, res[x], L.post_norm, eps)
+                act = ops.mfma_gemm(hh, L.gate_up, 1) if impl[x][0] else ops.silu_mul(ops.linear(hh, L.gate_up))
+                hs[x] = ops.mfma_gemm(act, L.down, 0) if impl[x][1] else ops.linear(act, L.down)
+
+            with torch.cuda.stream(G):
+                pre(0, 0)
+                pre(1, 0)
+                for i in range(n):
+                    for x in (0, 1):
+                        post(x, i)
+                        if i + 1 < n:
+                            pre(x, i + 1)
+                out_h = torch.cat(hs, 0)
+                out_r = torch.cat(res, 0)
+        finally:
+            ops.set_gemm_cus(0)
+        main.wait_stream(G)
+        out_h.record_stream(main)
+        out_r.record_stream(main)
+        return out_h, out_r
+
     def forward_layers(self, h: torch.Tensor, meta: AttnMeta, residual: Optional[torch.Tensor] = None,
                        trim_last: Optional[torch.Tensor] = None):
         """Run the local layers.  ``trim_last`` (row indices): the last layer's
@@ -353,6 +488,9 @@ class LlamaModel:
         eps = c.rms_eps
         T = h.shape[0]
         if self.layers:
+            split = self._tbo_ok(h, meta, trim_last)
+            if split is not None:
+                return self._forward_layers_tbo(h, meta, residual, split)
             fq, fg = self._fused_decode(h, meta)
             if fq or fg:
                 h, residual = self._forward_layers_fused(h, meta, residual, fq, fg)

@@ -495,6 +495,7 @@ def decode_proj(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     ``linear`` otherwise."""
     M, K = x.shape
     if (OPROJ_FUSED and M == 1 and _native(x) and x.dtype == torch.bfloat16 and x.is_contiguous()
+            and w.dtype == torch.bfloat16 and w.is_contiguous() and w.shape[1] == K
             and fused_decode_ok(M, K, "qkv") and w.shape[0] % 16 == 0):
         y = torch.empty(M, w.shape[0], dtype=x.dtype, device=x.device)
         _call("fused_skinny", y, x, None, None, None, 0.0, w, None, 0, 0, None, None, None, None, None, 0, 0, 16)
@@ -538,6 +539,13 @@ def mfma_gemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
 
 
 MFMA_SCHED = int(os.environ.get("DGI_MFMA_SCHED", "3"))
+
+
+def set_gemm_cus(cus: int) -> None:
+    """CUs the MFMA GEMM's persistent / split-K launches size their grid for (0 = all of the
+    device's): GEMMs issued on a CU-masked stream (two-batch overlap) set its CU count."""
+    if native_available():
+        torch.ops.dgi.set_gemm_cus(int(cus))
 
 
 def mfma_gemm(x: torch.Tensor, w: torch.Tensor, epi: int = 0, out: Optional[torch.Tensor] = None,

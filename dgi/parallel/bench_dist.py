@@ -28,6 +28,27 @@ from dgi.parallel.plan import plan_node_layout
 from dgi.sched.request import SamplingParams
 
 MSG_PHASE = 9
+# serving-phase deadline (ramp + warm-up + window) of the watchdog's phase clock
+SERVE_S = float(os.environ.get("DGI_SERVE_S", "420"))
+
+
+class _FirstHop:
+    """``first_hop`` phase until this rank completed its first step, then ``serve``."""
+
+    def __init__(self):
+        from dgi.parallel.fault import phase
+        self._phase = phase
+        self.done = False
+        phase("first_hop")
+
+    def step_done(self) -> None:
+        if not self.done:
+            self.done = True
+            self._phase("serve", SERVE_S)
+
+    def teardown(self) -> None:
+        self.step_done()
+        self._phase("teardown")
 
 
 def _prompt(rng, n, vocab):
@@ -75,6 +96,7 @@ def capacity_check(cap, layout, per_rank: list, el: float) -> Optional[dict]:
 
 
 def run_distributed(args, layout_kind: str, dist):
+    from dgi.parallel.fault import phase
     f = Fabric()
     rank, world = f.rank, f.world
     layout = plan_node_layout(world, layout_kind, getattr(args, "prefill_ranks", None) or None,
@@ -82,8 +104,13 @@ def run_distributed(args, layout_kind: str, dist):
                               decode_replicas=getattr(args, "decode_replicas", None) or None, model=args.model)
     # every communicator of the layout up front (world KV pairs + pipeline sub-communicators),
     # each warmed with one transfer per pair in a deadlock-free order
+    phase("pair_warmup")
     t_pairs = f.setup_layout(layout)
+    from dgi.parallel.fabric import rccl_transports
+    rccl = rccl_transports() if f.on_gpu else None
     ctrl_rtt = ctrl_ping(f, 0, world - 1)
+    # model load (+ graph capture) of this rank's role
+    phase("engine_build", float(os.environ.get("DGI_BUILD_S", "300")))
     # decode-side concurrency: one microbatch of 768 rows per decode stage keeps the
     # decode GEMMs out of the small-M regime (70B down-proj: 0.76 PF/s at M=512,
     # 1.28 at 1024); a single decode GPU is capped by its KV pool (credits) instead
@@ -115,6 +142,8 @@ def run_distributed(args, layout_kind: str, dist):
             f.watchdog.report_failure(f"{role}: {type(e).__name__}: {e}")
         raise
     tokens, elapsed, ttfts, extra = res
+    phase("report")
+    extra["rccl"] = rccl
     t = torch.tensor([tokens, elapsed], dtype=torch.float64, device=f.device if f.on_gpu else "cpu")
     tl = [torch.zeros_like(t) for _ in range(world)]
     dist.all_gather(tl, t)
@@ -126,7 +155,22 @@ def run_distributed(args, layout_kind: str, dist):
     all_ttfts = [v for o in obj for v in o["ttfts"]]
     all_tpots = [v for o in obj for v in o.get("tpots", [])]
     all_e2es = [v for o in obj for v in o.get("e2es", [])]
-    per_rank = [{k: v for k, v in o.items() if k not in ("ttfts", "tpots", "e2es")} for o in obj]
+    per_rank = [{k: v for k, v in o.items() if k not in ("ttfts", "tpots", "e2es", "rccl")} for o in obj]
+    # RCCL transports of the node: each rank's connections (P2P/IPC over xGMI expected on a real
+    # node, NET/Socket in the shared-GPU rehearsal)
+    rc = [o.get("rccl") for o in obj]
+    rccl_node = None
+    if any(rc):
+        by: dict = {}
+        peers: dict = {}
+        for o in rc:
+            if not o:
+                continue
+            for k, v in o["by_transport"].items():
+                by[k] = by.get(k, 0) + v
+            peers.update(o["peers"])
+        rccl_node = {"by_transport": by, "peers": dict(sorted(peers.items())),
+                     "ranks_logged": sum(1 for o in rc if o)}
     roles = {}
     for o in per_rank:
         r = roles.setdefault(o["role"], {"ranks": 0, "tokens": 0})
@@ -149,7 +193,7 @@ def run_distributed(args, layout_kind: str, dist):
                                   "layout": {"kind": layout.kind, "describe": layout.describe(),
                                              "prefill": layout.prefill_ranks, "decode_groups": layout.decode_groups},
                                   "concurrency": conc, "pair_setup_s": round(t_pairs, 3), "roles": roles,
-                                  "ctrl_rtt_us": ctrl_rtt,
+                                  "ctrl_rtt_us": ctrl_rtt, "rccl": rccl_node,
                                   "migration_ms_p50": round(float(sorted(mig)[len(mig) // 2]), 3) if mig else None,
                                   "tpots": all_tpots, "e2es": all_e2es, "ranks": per_rank}
 
@@ -244,6 +288,7 @@ def _run_pp(args, f, cfg, layout, role, sp, rng, conc):
     ranks = layout.decode_ranks
     if role == "decode_driver":
         eng = PipelineEngine(cfg, f, ranks)
+        hop = _FirstHop()
         vocab = eng.model_cfg.vocab_size
         inflight = set()
         log = TokenLog()
@@ -255,6 +300,8 @@ def _run_pp(args, f, cfg, layout, role, sp, rng, conc):
 
         def step():
             outs = eng.step()
+            if outs:
+                hop.step_done()
             log.outputs(outs)
             for o in outs:
                 if o.finished:
@@ -273,6 +320,7 @@ def _run_pp(args, f, cfg, layout, role, sp, rng, conc):
             top(conc)
             step()
         t1 = time.perf_counter()
+        hop.teardown()
         eng.pause_stages()
         torch.cuda.synchronize() if f.device.type == "cuda" else None
         f.barrier()
@@ -283,7 +331,10 @@ def _run_pp(args, f, cfg, layout, role, sp, rng, conc):
                                                    "window": {"t0_ns": _ns(t0), "t1_ns": _ns(t1)},
                                                    "token_wait_s": round(eng.wait_s, 3)}
     w = StageWorker(cfg, f, ranks)
+    hop = _FirstHop()
+    w.on_hop = hop.step_done
     w.run()
+    hop.teardown()
     torch.cuda.synchronize() if f.device.type == "cuda" else None
     f.barrier()
     w.run()
@@ -321,6 +372,7 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
         pmbt = getattr(args, "prefill_mbt", 0) or (cap.prefill_mbt if cap is not None else args.max_batched_tokens)
         pcfg = EngineConfig(**{**cfg.__dict__, "max_num_seqs": 64 + lc, "max_num_batched_tokens": pmbt})
         srv = PrefillServer(pcfg, f, layout, local_cap=lc)
+        hop = _FirstHop()
         ph = CtrlChannel(f, clock, 4, tag="phase")
         vocab = srv.engine.model_cfg.vocab_size
         # one step's worth of prompts, topped up right before each step
@@ -364,6 +416,7 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
             ts = time.perf_counter()
             log.outputs(srv.step())
             if srv.engine.stats["steps"] > s0:
+                hop.step_done()
                 log.steps.append(time.perf_counter())
                 ms = (log.steps[-1] - ts) * 1e3
                 step_ms = ms if step_ms is None else 0.8 * step_ms + 0.2 * ms
@@ -371,6 +424,7 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
                     ph.send([MSG_PHASE, MSG_STEPMS, int(step_ms * 1000)])
         # after the window: drain every KV transfer this rank started (the decode ranks keep
         # servicing their handshakes) and report the migration count; then synchronise
+        hop.teardown()
         srv.fence()
         torch.cuda.synchronize() if f.device.type == "cuda" else None
         f.barrier()
@@ -391,6 +445,7 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
         if local_frac < 0:
             local_frac = decode_local_fraction(layout, model=args.model)
         drv = DecodeDriver(cfg, f, layout, local_fraction=local_frac)
+        hop = _FirstHop()
         is_clock = f.rank == clock
         others = [p for p in layout.prefill_ranks] + [d for d in layout.drivers if d != clock]
         phases = [CtrlChannel(f, p, 4, tag="phase") for p in others] if is_clock else \
@@ -417,6 +472,8 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
                     return False
             ts = time.perf_counter()
             outs = drv.step()
+            if outs:
+                hop.step_done()
             ms = (time.perf_counter() - ts) * 1e3
             my_ms["ema"] = ms if my_ms["ema"] is None else 0.8 * my_ms["ema"] + 0.2 * ms
             # first tokens of locally admitted prompts are produced here; a migrated request's
@@ -473,6 +530,7 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
                 one_step()
         # after the window: receive every announced migration (prefill ranks fence), drain
         # the decode pipeline, synchronise, barrier
+        hop.teardown()
         drv.await_fences()
         if hasattr(drv.engine, "pause_stages"):
             drv.engine.pause_stages()
@@ -501,7 +559,10 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
 
     # later stages of a decode pipeline replica (receive their KV slices from the prefill ranks)
     w = StageWorker(cfg, f, layout.group_of(f.rank), kv_sources=layout.prefill_ranks)
+    hop = _FirstHop()
+    w.on_hop = hop.step_done
     w.run()
+    hop.teardown()
     torch.cuda.synchronize() if f.device.type == "cuda" else None
     f.barrier()
     w.run()

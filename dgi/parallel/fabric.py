@@ -80,6 +80,13 @@ def prepare_rccl_env() -> None:
     connect is a blocking host handshake with the peer in the middle of
     serving)."""
     os.environ.setdefault("NCCL_RUNTIME_CONNECT", "0")
+    # which transport each connection uses (P2P/IPC over xGMI vs a network fallback) goes into
+    # the bench JSON: RCCL's INIT log, one file per rank, parsed by ``rccl_transports``
+    # (DGI_RCCL_LOG=0, or a NCCL_DEBUG set by the user, leaves RCCL's logging alone)
+    if os.environ.get("DGI_RCCL_LOG", "1") != "0" and "NCCL_DEBUG" not in os.environ:
+        os.environ["NCCL_DEBUG"] = "INFO"
+        os.environ.setdefault("NCCL_DEBUG_SUBSYS", "INIT")
+        os.environ["NCCL_DEBUG_FILE"] = rccl_log_path()
     # eager init already serialises unbatched p2p on the world communicator: that
     # is the point, so the one-time warning is noise
     os.environ.setdefault("TORCH_NCCL_SHOW_EAGER_INIT_P2P_SERIALIZATION_WARNING", "0")
@@ -87,6 +94,37 @@ def prepare_rccl_env() -> None:
         os.environ["NCCL_HOSTID"] = f"dgi-shared-rank{os.environ.get('RANK', '0')}"
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         os.environ.setdefault("NCCL_IB_DISABLE", "1")
+
+
+def rccl_log_path() -> str:
+    d = os.environ.get("TMPDIR", "/tmp")
+    return os.path.join(d, f"dgi_rccl_{os.environ.get('MASTER_PORT', '0')}_{os.environ.get('RANK', '0')}.log")
+
+
+_VIA = None
+
+
+def rccl_transports(path: Optional[str] = None) -> Optional[dict]:
+    """Transport of every RCCL connection this rank set up, from its INIT log:
+    ``{"by_transport": {"P2P/IPC": n, ...}, "peers": {"0->3": "P2P/IPC", ...}}``
+    (None when no log was written: gloo, or logging left to the user)."""
+    import re
+    global _VIA
+    path = path or os.environ.get("NCCL_DEBUG_FILE") or rccl_log_path()
+    if not os.path.exists(path):
+        return None
+    if _VIA is None:
+        _VIA = re.compile(r"(\d+)\[[^\]]*\]\s*->\s*(\d+)\[[^\]]*\]\s*(?:\[(?:send|receive)\]\s*)?via\s+(\S+)")
+    by, peers = {}, {}
+    with open(path, errors="replace") as fh:
+        for line in fh:
+            m = _VIA.search(line)
+            if m is None:
+                continue
+            a, b, via = m.group(1), m.group(2), m.group(3)
+            by[via] = by.get(via, 0) + 1
+            peers[f"{a}->{b}"] = via
+    return {"by_transport": by, "peers": peers, "log": path}
 
 
 def _nccl_options():
@@ -99,7 +137,7 @@ def _nccl_options():
         return None
 
 
-def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0) -> str:
+def init_distributed(backend: Optional[str] = None, timeout_s: float = 300.0) -> str:
     """Initialise the default process group for this process (idempotent).
 
     RCCL: eager init bound to this rank's GPU (``device_id``) with
@@ -128,7 +166,7 @@ class Fabric:
     """Per-rank view of the node: communicators, streams and control rings."""
 
     def __init__(self, backend: Optional[str] = None, device: Optional[torch.device] = None,
-                 timeout_s: float = 1800.0):
+                 timeout_s: float = 300.0):
         self.owns_pg = not dist.is_initialized()
         init_distributed(backend, timeout_s)
         self.rank = dist.get_rank()
@@ -182,8 +220,8 @@ class Fabric:
         # liveness watchdog over the rendezvous store (dgi.parallel.fault)
         self.watchdog = None
         if self.world > 1 and os.environ.get("DGI_WATCHDOG", "1") != "0":
-            from dgi.parallel.fault import Watchdog
-            self.watchdog = Watchdog(self.rank, self.world).start()
+            from dgi.parallel.fault import Watchdog, current_watchdog
+            self.watchdog = current_watchdog() or Watchdog(self.rank, self.world).start()
 
     # ------------------------------------------------------------------ set-up
     def _job_id(self) -> str:
@@ -522,7 +560,7 @@ class CtrlChannel:
         self.rseq += 1
         return v
 
-    def wait_bytes(self, timeout_s: float = 1800.0) -> bytes:
+    def wait_bytes(self, timeout_s: float = 300.0) -> bytes:
         if self.shm:
             r = self._inbox(timeout_s)
             if r is None:
@@ -553,5 +591,5 @@ class CtrlChannel:
         v = self.poll_bytes()
         return None if v is None else np.frombuffer(v, dtype=np.int64).copy()
 
-    def wait(self, timeout_s: float = 1800.0) -> np.ndarray:
+    def wait(self, timeout_s: float = 300.0) -> np.ndarray:
         return np.frombuffer(self.wait_bytes(timeout_s), dtype=np.int64).copy()

@@ -7,6 +7,17 @@
   Python stacks and exit non-zero — a dead or wedged rank can no longer
   leave the node hanging in an RCCL wait forever (the reference had no
   data-plane failure handling at all: its ``_handle_failure`` raised).
+* **Phase deadlines** (``Watchdog.phase``): a multi-rank run moves
+  through named phases (rendezvous, pair warm-up, start-up probe, engine build,
+  first hop, serving window, teardown), each with a time budget (``DGI_PHASE_S``,
+  default 120 s; the serving phase scales with the steps).  Every rank publishes
+  its current phase in the store.  The first rank whose phase overruns prints ONE
+  JSON line on stdout — ``{"status": "timeout", ...}`` with the stuck rank, its
+  phase and every rank's phase — records a failure (so every other rank exits
+  too) and exits with status 4: a wedged first contact with a real node ends in
+  minutes with evidence, instead of a silent lease-long hang (the reference's
+  ``DistributedInferenceSession._handle_failure`` raised with no state:
+  worker/distributed/session.py:339-365).
 * **Fault injection** (``DGI_FAULT=rank:step:kind[:arg]``, several separated by
   ``,``) at named sites of the step loops:
 
@@ -16,6 +27,9 @@
   ``raise``    raise ``InjectedFault`` (exercises the failure record path)
   ``corrupt``  the site's ``corrupt`` hook flips bytes of the payload it owns
                (P/D: the migrated KV buffer)
+  ``stall``    sleep ``arg`` s (default 3600) without servicing anything: a wedged
+               rank (phase-deadline tests; site ``PHASE_SITES[name]`` stalls in
+               that start-up phase)
 
 The multi-process tests (tests/test_parallel_cpu.py) drive each kind.
 """
@@ -69,7 +83,13 @@ class FaultPlan:
                 raise InjectedFault(f"injected fault on rank {rank} at step {step}")
             elif kind == "corrupt" and corrupt is not None:
                 corrupt()
+            elif kind == "stall":
+                time.sleep(float(arg or 3600))
 
+
+# fault-injection step ids of the start-up phases (``DGI_FAULT=rank:<site>:stall``)
+PHASE_SITES = {"pair_warmup": 300001, "probe": 300002, "engine_build": 300003, "first_hop": 300004}
+DEFAULT_PHASE_S = float(os.environ.get("DGI_PHASE_S", "120"))
 
 _plan: Optional[FaultPlan] = None
 
@@ -94,9 +114,14 @@ class Watchdog:
         self._stop = threading.Event()
         self._t = threading.Thread(target=self._run, name="dgi-watchdog", daemon=True)
         self.last_seen = {r: time.time() for r in range(world)}
+        self.phase_name: Optional[str] = None
+        self.phase_t0 = time.time()
+        self.deadline: Optional[float] = None
+        self.timeout_info: dict = {}            # extra fields of the timeout JSON line
 
     def start(self) -> "Watchdog":
         import atexit
+        _WATCHDOG.append(self)
         self.beat()
         self._t.start()
         atexit.register(self.stop)
@@ -104,6 +129,52 @@ class Watchdog:
 
     def beat(self) -> None:
         self.store.set(f"dgi/hb/{self.rank}", repr(time.time()))
+
+    def phase(self, name: str, budget_s: Optional[float] = None) -> None:
+        """Enter phase ``name``: it must end (the next ``phase`` call) within ``budget_s``
+        seconds (``DGI_PHASE_S`` by default; <= 0: no deadline)."""
+        b = DEFAULT_PHASE_S if budget_s is None else float(budget_s)
+        self.phase_name, self.phase_t0 = name, time.time()
+        self.deadline = self.phase_t0 + b if b > 0 else None
+        try:
+            self.store.set(f"dgi/phase/{self.rank}", f"{name}@{self.phase_t0:.3f}")
+        except Exception:
+            pass
+
+    def _phases(self) -> dict:
+        out = {}
+        now = time.time()
+        for r in range(self.world):
+            k = f"dgi/phase/{r}"
+            try:
+                if self.store.check([k]):
+                    name, _, t = self.store.get(k).decode().partition("@")
+                    out[str(r)] = {"phase": name, "s": round(now - float(t), 1) if t else None}
+                else:
+                    out[str(r)] = None
+            except Exception:
+                out[str(r)] = "?"
+        return out
+
+    def _timeout(self) -> None:
+        """This rank overran its phase: one JSON line (first rank only), failure record, exit 4."""
+        import json
+        waited = time.time() - self.phase_t0
+        msg = {"status": "timeout", "value": None, "n_gpus": self.world,
+               "stuck": {"rank": self.rank, "phase": self.phase_name, "waited_s": round(waited, 1)},
+               "phases": self._phases(), **self.timeout_info}
+        first = True
+        try:
+            first = self.store.add("dgi/timeout_json", 1) == 1
+        except Exception:
+            pass
+        if first:
+            os.write(1, (json.dumps(msg) + "\n").encode())
+        self.report_failure(f"phase {self.phase_name} timed out after {waited:.0f}s")
+        sys.stderr.write(f"[dgi watchdog] rank {self.rank}: phase {self.phase_name} timed out after {waited:.0f}s\n")
+        faulthandler.dump_traceback(all_threads=True)
+        sys.stderr.flush()
+        os._exit(4)
 
     def report_failure(self, msg: str) -> None:
         try:
@@ -119,13 +190,15 @@ class Watchdog:
             pass
 
     def _abort(self, why: str) -> None:
-        sys.stderr.write(f"[dgi watchdog] rank {self.rank}: {why}; aborting\n")
+        sys.stderr.write(f"[dgi watchdog] rank {self.rank} (phase {self.phase_name}): {why}; aborting\n")
         faulthandler.dump_traceback(all_threads=True)
         sys.stderr.flush()
         os._exit(3)
 
     def _run(self) -> None:
         while not self._stop.wait(self.interval):
+            if self.deadline is not None and time.time() > self.deadline:
+                self._timeout()
             try:
                 self.beat()
                 if self.store.check(["dgi/failed"]):
@@ -146,3 +219,22 @@ class Watchdog:
                 # the store itself is gone: the job is tearing down (rank 0 left);
                 # never turn a normal shutdown into a failure exit
                 return
+
+
+def phase(name: str, budget_s: Optional[float] = None) -> None:
+    """Enter start-up / serving phase ``name`` on this rank's watchdog (no-op without
+    one: single-rank runs), and fire any ``stall`` fault injected at that phase."""
+    w = current_watchdog()
+    if w is not None:
+        w.phase(name, budget_s)
+    site = PHASE_SITES.get(name)
+    if site is not None and plan():
+        rank = w.rank if w is not None else int(os.environ.get("RANK", "0"))
+        plan().check(rank, site)
+
+
+_WATCHDOG: list = []
+
+
+def current_watchdog() -> Optional[Watchdog]:
+    return _WATCHDOG[-1] if _WATCHDOG else None

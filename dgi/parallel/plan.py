@@ -166,6 +166,22 @@ class RoleCapacity:
     decode_step_ms: dict = dataclasses.field(default_factory=dict)
     decode_rows: dict = dataclasses.field(default_factory=dict)
     mixed_step_ms: float = 0.0
+    # prefill step time (ms) per prefill step size (tokens): the planner picks the step size
+    # for TTFT (a prompt admitted just in time waits ~one step); {prefill_mbt: prefill_step_ms}
+    # when only that point was measured
+    prefill_steps: dict = dataclasses.field(default_factory=dict)
+    prompt_len: int = 512
+    output_len: int = 128
+
+    def steps(self) -> dict:
+        return dict(self.prefill_steps) or {self.prefill_mbt: self.prefill_step_ms}
+
+    def prefill_rate(self, mbt: Optional[int] = None) -> float:
+        """Decode demand (output tok/s) one prefill GPU creates at ``mbt`` tokens per step."""
+        st = self.steps()
+        if mbt is None or mbt not in st or not st[mbt]:
+            return self.prefill_tok_s
+        return max(1, mbt // self.prompt_len) / (st[mbt] / 1e3) * self.output_len
 
 
 # Measured on one MI355X with scripts/pd_capacity.py (profiles/r2_pd_capacity.md,
@@ -178,10 +194,14 @@ CAPACITY = {
     # Re-measured after the ping-pong MFMA GEMM + tile-aligned mixed steps
     # (profiles/r3_gemm/pd_capacity_70b.jsonl, bench70b_token_align256.json): the mixed (DP) GPU
     # gained 5.5 % (1760 -> 1857 tok/s), the prefill and decode roles ~1 %.
-    "llama3-70b": RoleCapacity(prefill_tok_s=19.79 * 128, decode_tok_s={1: 5723.0, 2: 12189.0, 3: 18088.0},
-                               mixed_tok_s=1857.0, prefill_step_ms=202.1, prefill_mbt=2048,
-                               decode_step_ms={1: 100.6, 2: 63.0, 3: 42.5}, decode_rows={1: 576, 2: 768, 3: 768},
-                               mixed_step_ms=189.7),
+    # r5 (profiles/r5_pd/probe70b_r5.json): start-up probe on one MI355X — prefill at 2048 and
+    # 1024 tokens per step (201.5 / 109.1 ms), decode replicas at 576 / 768-row microbatches;
+    # the mixed (DP) rate and step are the 1-GPU bench's (1,871 tok/s, 204.7 ms: the probe's
+    # short-model extrapolation reads mixed steps ~5 % fast, 1,968 tok/s / 195.1 ms).
+    "llama3-70b": RoleCapacity(prefill_tok_s=2540.5, decode_tok_s={1: 5885.8, 2: 12937.6, 3: 19406.5},
+                               mixed_tok_s=1871.0, prefill_step_ms=201.5, prefill_mbt=2048,
+                               decode_step_ms={1: 97.9, 2: 59.4, 3: 39.6}, decode_rows={1: 576, 2: 768, 3: 768},
+                               mixed_step_ms=204.7, prefill_steps={2048: 201.5, 1024: 109.1}),
     "llama3-8b": RoleCapacity(prefill_tok_s=176.2 * 128, decode_tok_s={1: 31566.0, 2: 58028.0, 3: 69373.0},
                               mixed_tok_s=11842.0, prefill_step_ms=45.4, prefill_mbt=4096,
                               decode_step_ms={1: 32.4, 2: 18.2, 3: 11.2}, decode_rows={1: 1024, 2: 1024, 3: 768},
@@ -286,6 +306,72 @@ def choose_pd_layout(n_gpus: int, cap: RoleCapacity, max_stages: int = 3, prefer
     return npre, k, reps, est
 
 
+# P/D planning objective: the disaggregated layout exists for latency at throughput
+# parity — on a compute-bound GPU it cannot out-run data parallel.  Among P/D candidates whose
+# TTFT AND TPOT are at most LATENCY_FRAC of a data-parallel GPU's, the highest node rate (the
+# slack filler counted at FILL_WEIGHT: it runs mixed steps with DP-like latency); the pick runs
+# unless its rate falls below PD_MIN_RATIO x data parallel.
+LATENCY_FRAC = float(os.environ.get("DGI_PD_LATENCY_FRAC", "0.7"))
+FILL_WEIGHT = 0.8
+# 0.85: below the ~0.9 x DP the kernels allow a P/D node on 70B (a decode row costs 1.86 us per
+# layer vs a mixed row's 1.33: profiles/r5_pd/README.md) and below the start-up probe's ~5 %
+# optimism about DP mixed steps
+PD_MIN_RATIO = float(os.environ.get("DGI_PD_MIN_RATIO", "0.85"))
+# a split that needs the slack filler for more than this share of its output is a DP-like hybrid
+# (2-4 GPUs of 70B: ~30 %), not disaggregation: data parallel runs there
+MAX_FILLER_SHARE = float(os.environ.get("DGI_PD_MAX_FILLER", "0.15"))
+
+
+def dp_reference(n_gpus: int, cap: RoleCapacity) -> dict:
+    """N data-parallel GPUs under ``cap``: every token waits one mixed step (TTFT ~ TPOT ~ step)."""
+    return {"layout": f"dp{n_gpus}", "tok_s": round(n_gpus * cap.mixed_tok_s, 1),
+            "ttft_ms": cap.mixed_step_ms or None, "tpot_ms": cap.mixed_step_ms or None}
+
+
+def pd_candidate(n_prefill: int, stages: int, replicas: int, mbt: int, cap: RoleCapacity) -> dict:
+    """Rate and latency of nP (``mbt``-token prefill steps) + replicas x (stages-deep decode)."""
+    pre = n_prefill * cap.prefill_rate(mbt)
+    dec = replicas * cap.decode_tok_s.get(stages, 0.0)
+    base = min(pre, dec)
+    if dec >= pre:        # decode slack: replicas admit local prompts (mixed microbatches)
+        fill = (1.0 - pre / dec) * replicas * stages * cap.mixed_tok_s if dec > 0 else 0.0
+    else:                 # prefill slack: prefill ranks decode overflow sequences themselves
+        fill = (1.0 - dec / pre) * n_prefill * cap.mixed_tok_s
+    tot = base + FILL_WEIGHT * fill
+    return {"layout": f"{n_prefill}P+{replicas}D[" + "+".join([f"pp{stages}" if stages > 1 else "1"] * replicas) + "]",
+            "prefill_ranks": n_prefill, "decode_stages": stages, "decode_replicas": replicas, "prefill_mbt": mbt,
+            "tok_s": round(tot, 1), "disagg_tok_s": round(base, 1),
+            "bound": "prefill" if pre < dec else "decode",
+            "ttft_ms": round(cap.steps().get(mbt, cap.prefill_step_ms), 1) or None,
+            "tpot_ms": round(stages * cap.decode_step_ms.get(stages, 0.0), 1) or None,
+            "filler_share": round(FILL_WEIGHT * fill / tot, 3) if tot > 0 else 0.0}
+
+
+def plan_pd(n_gpus: int, cap: RoleCapacity, max_stages: int = 3, lat_frac: Optional[float] = None) -> tuple:
+    """(best P/D candidate, DP reference, every candidate): see LATENCY_FRAC above.  Without a
+    candidate meeting the latency bound the fastest candidate is returned with
+    ``latency_ok`` False."""
+    lat = LATENCY_FRAC if lat_frac is None else lat_frac
+    dp = dp_reference(n_gpus, cap)
+    cands = []
+    for npre in range(1, n_gpus):
+        left = n_gpus - npre
+        for k in range(1, max_stages + 1):
+            if left % k or k not in cap.decode_tok_s:
+                continue
+            for mbt in sorted(cap.steps()):
+                c = pd_candidate(npre, k, left // k, mbt, cap)
+                c["latency_ok"] = bool(dp["ttft_ms"] and c["ttft_ms"] and c["tpot_ms"]
+                                       and c["ttft_ms"] <= lat * dp["ttft_ms"] and c["tpot_ms"] <= lat * dp["tpot_ms"])
+                cands.append(c)
+    if not cands:
+        return None, dp, []
+    ok = [c for c in cands if c["latency_ok"]] or cands
+    best = max(ok, key=lambda c: (c["tok_s"], -(c["tpot_ms"] or 0), -(c["ttft_ms"] or 0)))
+    best = dict(best, vs_dp=round(best["tok_s"] / dp["tok_s"], 3) if dp["tok_s"] else None)
+    return best, dp, cands
+
+
 def _groups(first: int, stages: int, replicas: int) -> list:
     return [list(range(first + i * stages, first + (i + 1) * stages)) for i in range(replicas)]
 
@@ -312,8 +398,8 @@ def plan_node_layout(n_gpus: int, kind: str = "pdpp", prefill_ranks: Optional[in
         decode_stages = 1
     if prefill_ranks is None and decode_replicas is None and cap is not None and \
             (decode_stages is None or kind == "pd"):
-        npre, k, reps, _est = choose_pd_layout(n_gpus, cap, max_stages=decode_stages or 3,
-                                               prefer_pipeline=kind == "pdpp")
+        best, _dp, _c = plan_pd(n_gpus, cap, max_stages=decode_stages or 3)
+        npre, k, reps = best["prefill_ranks"], best["decode_stages"], best["decode_replicas"]
     else:
         k = decode_stages or (3 if (kind == "pdpp" and n_gpus >= 8) else 1)
         reps = decode_replicas

@@ -43,6 +43,7 @@ class ProbeResult:
     output_len: int
     layers: tuple
     seconds: float
+    prefill_more: dict = dataclasses.field(default_factory=dict)   # other step sizes: mbt -> fit
 
     def to_dict(self) -> dict:
         return dataclasses.asdict(self)
@@ -113,13 +114,18 @@ def _fit(ts: dict) -> tuple:
 
 def run_probe(model: str, device: str, prompt_len: int = 512, output_len: int = 128, prefill_mbt: int = 2048,
               decode_rows=(576, 768), mixed_rows: int = 384, layers=(4, 8), steps: int = 8,
-              seed: int = 0) -> ProbeResult:
+              seed: int = 0, prefill_more=(1024,)) -> ProbeResult:
+    """Also times prefill steps of each size in ``prefill_more`` (the planner picks the step
+    size for TTFT).  Decode rows that take two-batch overlap (``llama.tbo_split``) are timed
+    eagerly on the CU-masked streams, as the decode roles run them."""
+    from dgi.models import llama
     t_start = time.perf_counter()
     base = get_config(model.split("@")[0] if model else model)
     rng = random.Random(seed)
     ctx = prompt_len + output_len // 2
     bs = 16
     pre, dec, mix = {}, {r: {} for r in decode_rows}, {}
+    more = {m: {} for m in prefill_more if m != prefill_mbt}
     per_prompt = max(1, prefill_mbt // prompt_len)
     from dgi.sched.request import SamplingParams
     one = SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True)
@@ -140,10 +146,21 @@ def run_probe(model: str, device: str, prompt_len: int = 512, output_len: int = 
                 eng.add_request([rng.randrange(1, mc.vocab_size) for _ in range(prompt_len)], one)
         pre[n] = _time_steps(eng, steps, top)
         del eng
-        # decode: rows at the mean context, graph-captured like the serving engines
+        for mbt in more:
+            pp = max(1, mbt // prompt_len)
+            eng = _engine(model, mc, device, 4 * pp, mbt, 4 * pp * (prompt_len // bs + 2) + 8, graphs=False)
+
+            def topm_(eng=eng, pp=pp):
+                while len(eng.scheduler.waiting) < pp:
+                    eng.add_request([rng.randrange(1, mc.vocab_size) for _ in range(prompt_len)], one)
+            more[mbt][n] = _time_steps(eng, steps, topm_)
+            del eng
+        # decode: rows at the mean context, graph-captured like the serving engines (two-batch
+        # overlap steps eagerly: a graph would drop the CU masks)
         for rows in decode_rows:
             nb = rows * (ctx // bs + 2 + steps + 4) + 8
-            eng = _engine(model, mc, device, rows, max(4096, rows), nb, graphs=device != "cpu", buckets=(rows,))
+            graphs = device != "cpu" and not (llama.TBO and llama.tbo_split(rows) is not None)
+            eng = _engine(model, mc, device, rows, max(4096, rows), nb, graphs=graphs, buckets=(rows,))
             _adopt(eng, rows, ctx, rng)
             dec[rows][n] = _time_steps(eng, steps)
             del eng
@@ -162,7 +179,8 @@ def run_probe(model: str, device: str, prompt_len: int = 512, output_len: int = 
         _release(device)
     return ProbeResult(model=model, prefill=_fit(pre), decode={r: _fit(v) for r, v in dec.items()}, mixed=_fit(mix),
                        prefill_mbt=prefill_mbt, mixed_rows=mixed_rows, prompt_len=prompt_len, output_len=output_len,
-                       layers=tuple(layers), seconds=round(time.perf_counter() - t_start, 2))
+                       layers=tuple(layers), seconds=round(time.perf_counter() - t_start, 2),
+                       prefill_more={m: _fit(v) for m, v in more.items()})
 
 
 def capacity_from_probe(p: ProbeResult, num_layers: Optional[int] = None, max_stages: int = 3):
@@ -188,10 +206,14 @@ def capacity_from_probe(p: ProbeResult, num_layers: Optional[int] = None, max_st
         step[k] = round(td / k, 2)
         drows[k] = R
     t_mix = t(p.mixed)
+    psteps = {p.prefill_mbt: round(t_pre, 2)}
+    for m, fit in (p.prefill_more or {}).items():
+        psteps[int(m)] = round(t(fit), 2)
     return RoleCapacity(prefill_tok_s=round(prefill_tok_s, 1), decode_tok_s=dec,
                         mixed_tok_s=round(p.mixed_rows / (t_mix / 1e3), 1), prefill_step_ms=round(t_pre, 2),
                         prefill_mbt=p.prefill_mbt, decode_step_ms=step, decode_rows=drows,
-                        mixed_step_ms=round(t_mix, 2))
+                        mixed_step_ms=round(t_mix, 2), prefill_steps=psteps, prompt_len=p.prompt_len,
+                        output_len=p.output_len)
 
 
 def median_capacity(caps: list):
@@ -205,28 +227,34 @@ def median_capacity(caps: list):
         decode_tok_s={k: med([c.decode_tok_s[k] for c in caps]) for k in c0.decode_tok_s},
         mixed_tok_s=med([c.mixed_tok_s for c in caps]), prefill_step_ms=med([c.prefill_step_ms for c in caps]),
         prefill_mbt=c0.prefill_mbt, decode_step_ms={k: med([c.decode_step_ms[k] for c in caps]) for k in c0.decode_step_ms},
-        decode_rows=dict(c0.decode_rows), mixed_step_ms=med([c.mixed_step_ms for c in caps]))
+        decode_rows=dict(c0.decode_rows), mixed_step_ms=med([c.mixed_step_ms for c in caps]),
+        prefill_steps={m: med([c.steps()[m] for c in caps]) for m in c0.steps()},
+        prompt_len=c0.prompt_len, output_len=c0.output_len)
 
 
-# auto picks P/D only when its estimate beats data parallel by more than the measured
-# box-to-box spread of one GPU's throughput (~4-5 %, profiles/r4_slo/, BASELINE.md): a pick
-# inside the noise would trade a well-rehearsed layout for a coin flip
-PD_MIN_RATIO = float(os.environ.get("DGI_PD_MIN_RATIO", "1.05"))
-
-
-def plan_from_probe(world: int, cap, min_ratio: Optional[float] = None) -> dict:
-    """The auto layout under ``cap``: the planner's best P/D split, kept only when its
-    disaggregated estimate reaches ``min_ratio`` (default ``PD_MIN_RATIO``) x ``world``
-    data-parallel GPUs (VERDICT r3 #8: never pick a layout the planner itself rates below DP)."""
+def plan_from_probe(world: int, cap, min_ratio: Optional[float] = None, lat_frac: Optional[float] = None) -> dict:
+    """The auto layout under ``cap``: the planner's best P/D split — the
+    fastest whose TTFT and TPOT are at most ``lat_frac`` of a data-parallel GPU's, with the
+    prefill step size chosen for TTFT — unless its node rate falls below ``min_ratio`` x
+    ``world`` data-parallel GPUs (``plan.PD_MIN_RATIO``) or no split meets the latency bound:
+    then data parallel.  The DP estimate is reported next to the pick (``dp_reference``)."""
+    from dgi.parallel.plan import MAX_FILLER_SHARE, PD_MIN_RATIO, plan_pd
     if min_ratio is None:
         min_ratio = PD_MIN_RATIO
-    from dgi.parallel.plan import choose_pd_layout, layout_estimate
-    npre, k, reps, _ = choose_pd_layout(world, cap)
-    est = layout_estimate(npre, k, reps, cap)
-    dp = world * cap.mixed_tok_s
-    pd_ok = est["disagg_tok_s"] >= min_ratio * dp
-    kind = ("pdpp" if k > 1 else "pd") if pd_ok else "dp"
-    why = (f"P/D {est['layout']} estimated {est['disagg_tok_s']:.0f} tok/s "
-           f"{'>=' if pd_ok else '<'} {min_ratio:g} x {world} DP GPUs {dp:.0f} tok/s")
-    return {"kind": kind, "prefill_ranks": npre, "decode_stages": k, "decode_replicas": reps, "estimate": est,
-            "dp_tok_s": round(dp, 1), "reason": why}
+    best, dp, _cands = plan_pd(world, cap, lat_frac=lat_frac)
+    if best is None:
+        return {"kind": "dp", "dp_reference": dp, "reason": "no P/D candidate", "estimate": None}
+    ratio = best["tok_s"] / dp["tok_s"] if dp["tok_s"] else 0.0
+    hybrid = best["filler_share"] > MAX_FILLER_SHARE
+    pd_ok = best["latency_ok"] and ratio >= min_ratio and not hybrid
+    kind = ("pdpp" if best["decode_stages"] > 1 else "pd") if pd_ok else "dp"
+    why = (f"P/D {best['layout']} at {best['prefill_mbt']}-token prefill steps: est {best['tok_s']:.0f} tok/s = "
+           f"{ratio:.2f} x DP {dp['tok_s']:.0f}, TTFT {best['ttft_ms']} vs {dp['ttft_ms']} ms, TPOT "
+           f"{best['tpot_ms']} vs {dp['tpot_ms']} ms -> {kind}"
+           + ("" if best["latency_ok"] else " (no split meets the latency bound)")
+           + ("" if ratio >= min_ratio else f" (below {min_ratio:g} x DP)")
+           + (f" (filler share {best['filler_share']:.2f} > {MAX_FILLER_SHARE:g}: a hybrid, not a split)"
+              if hybrid else ""))
+    return {"kind": kind, "prefill_ranks": best["prefill_ranks"], "decode_stages": best["decode_stages"],
+            "decode_replicas": best["decode_replicas"], "prefill_mbt": best["prefill_mbt"], "estimate": best,
+            "dp_reference": dp, "dp_tok_s": dp["tok_s"], "reason": why}

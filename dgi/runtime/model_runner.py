@@ -146,8 +146,32 @@ class ModelRunner:
     H_LEN, H_T, H_NDP, H_NPRE, H_NB, H_MAXW, H_SPLITS, H_PART, H_NTILES, H_NLOG, H_STEP, H_FILT = range(1, 13)
     HEADER_SIZE = 16
 
-    def build_host(self, sb: ScheduledBatch, pad_decode_to: int = 0):
-        """Pack one step's metadata into a flat int32 array + int64 header."""
+    def prebuild_decode(self, reqs: list, ahead: int = 1) -> dict:
+        """Per-row decode metadata of ``reqs`` for the step AFTER the one in flight (positions
+        ``ahead`` further on; the input tokens are filled in when that step's tokens are
+        back): what ``build_host(..., dec_pre=...)`` takes for the first rows of its batch.
+        The pipeline driver builds it while it waits for the tokens (``PipelineEngine``)."""
+        n = len(reqs)
+        bt = np.zeros((n, self.max_blocks), np.int32)
+        _ids, pos, slots, ctx = decode_rows(reqs, self.bs, bt, ahead)
+        temps, seeds, topk, topp, filt = sampling_rows(reqs, ahead)
+        return {"rows": list(reqs), "pos": pos, "slots": slots, "ctx": ctx, "bt": bt,
+                "samp": (temps, seeds, topk, topp), "filt": filt}
+
+    @staticmethod
+    def subset_prebuilt(pre: dict, keep: np.ndarray) -> dict:
+        """The rows of a ``prebuild_decode`` result where ``keep`` is True."""
+        idx = np.flatnonzero(keep)
+        samp = tuple(a[idx] for a in pre["samp"])
+        return {"rows": [pre["rows"][i] for i in idx], "pos": pre["pos"][idx], "slots": pre["slots"][idx],
+                "ctx": pre["ctx"][idx], "bt": pre["bt"][idx], "samp": samp,
+                "filt": bool((samp[2] > 0).any() or (samp[3].view(np.float32) < 1.0).any())}
+
+    def build_host(self, sb: ScheduledBatch, pad_decode_to: int = 0, dec_pre: Optional[dict] = None,
+                   pre_ids: Optional[np.ndarray] = None):
+        """Pack one step's metadata into a flat int32 array + int64 header.  ``dec_pre``
+        (``prebuild_decode``) holds the first decode rows' metadata, built ahead; their input
+        tokens are ``pre_ids``."""
         bs = self.bs
         nd = len(sb.decode)
         ndp = max(nd, pad_decode_to)
@@ -160,8 +184,13 @@ class ModelRunner:
         maxw = self.max_blocks
         dec_bt = np.zeros((ndp, maxw), np.int32)
         dec_ctx = np.ones(ndp, np.int32)
-        if nd:
-            ids[:nd], pos[:nd], slots[:nd], dec_ctx[:nd] = decode_rows(sb.decode, bs, dec_bt)
+        k = len(dec_pre["rows"]) if dec_pre is not None else 0
+        if k:
+            ids[:k] = pre_ids
+            pos[:k], slots[:k], dec_ctx[:k] = dec_pre["pos"], dec_pre["slots"], dec_pre["ctx"]
+            dec_bt[:k] = dec_pre["bt"]
+        if nd > k:
+            ids[k:nd], pos[k:nd], slots[k:nd], dec_ctx[k:nd] = decode_rows(sb.decode[k:], bs, dec_bt[k:nd])
         # padded decode rows write into reserved block 0 and read it back
         nb = len(chunks)
         pre_bt = np.zeros((nb, maxw), np.int32)
@@ -193,7 +222,12 @@ class ModelRunner:
         nlog = len(logit_rows)
         lidx = np.asarray(logit_rows, np.int32)
         # top-k / top-p ride in the same flat buffer (one H2D copy; pipeline stages get them too)
-        temps, seeds, topk, topp, filt = sampling_rows(sampled)
+        if k:
+            rest = sampling_rows(sampled[k:])
+            temps, seeds, topk, topp = (np.concatenate([a, b]) for a, b in zip(dec_pre["samp"], rest[:4]))
+            filt = dec_pre["filt"] or rest[4]
+        else:
+            temps, seeds, topk, topp, filt = sampling_rows(sampled)
         parts = [ids, pos, slots, dec_bt.ravel(), dec_ctx, pre_bt.ravel(), cu, pctx, tiles_np.ravel(), lidx,
                  temps, seeds, topk, topp]
         flat = np.concatenate(parts)

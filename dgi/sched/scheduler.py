@@ -120,6 +120,9 @@ class Scheduler:
         self.host_tier = None          # HostKVTier: swap preempted sequences out instead of recomputing
         self.num_swapped_out = 0
         self.num_swapped_in = 0
+        # running sequences admitted at most (None: max_num_seqs); the TPOT-SLO budget sets it
+        # to what the engine sustains at the SLO (dgi.sched.slo.StepBudget.admission_cap)
+        self.admit_cap: Optional[int] = None
 
     # ------------------------------------------------------------------ queue
     def add(self, req: Request) -> None:
@@ -277,7 +280,8 @@ class Scheduler:
             prefill.append(PrefillChunk(req, req.num_computed, n, req.num_computed + n == req.prefill_target))
             budget -= n
             n_seqs += 1
-        while self.waiting and budget > 0 and len(self.running) < self.cfg.max_num_seqs and n_seqs < seq_cap:
+        max_running = self.cfg.max_num_seqs if self.admit_cap is None else min(self.cfg.max_num_seqs, self.admit_cap)
+        while self.waiting and budget > 0 and len(self.running) < max_running and n_seqs < seq_cap:
             req = self.waiting[0]
             if req.swapped is not None:
                 # back in the next step's batch (decode row or its remaining prefill chunk)

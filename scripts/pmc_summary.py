@@ -29,6 +29,9 @@ def _key(name: str) -> str:
     return n[:60]
 
 
+BY_GRID = "--by-grid" in sys.argv
+
+
 def load(path):
     files = [path] if os.path.isfile(path) else glob.glob(os.path.join(path, "**", "*counter_collection.csv"),
                                                            recursive=True)
@@ -37,7 +40,7 @@ def load(path):
     seen = set()
     for f in files:
         for r in csv.DictReader(open(f)):
-            key = _key(r.get("Kernel_Name", "?"))
+            key = _key(r.get("Kernel_Name", "?")) + (f" grid={r.get('Grid_Size')}" if BY_GRID else "")
             disp = (f, r.get("Dispatch_Id"))
             per[key][r["Counter_Name"]] += float(r["Counter_Value"])
             if disp not in seen and r.get("Start_Timestamp") and r.get("End_Timestamp"):
@@ -86,4 +89,5 @@ def main(path, title=""):
 
 
 if __name__ == "__main__":
+    sys.argv = [a for a in sys.argv if a != "--by-grid"]
     main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "")

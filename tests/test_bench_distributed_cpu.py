@@ -40,6 +40,65 @@ def test_bench_pd_layouts_on_gloo(n, args):
     d = json.loads(line)
     assert d["n_gpus"] == n and d["value"] > 0
     assert d["extra"]["layout"]["kind"] in ("pd", "pdpp")
+    _check_metric_fields(d)
+
+
+def _check_metric_fields(d):
+    """VERDICT r4 #8: metric / metric_scope / vs_baseline agree with config.parallelism."""
+    sys.path.insert(0, ROOT)
+    from bench import HEADLINE_METRIC
+    kind = d["config"]["parallelism"].rstrip("0123456789")
+    n = d["n_gpus"]
+    assert d["config"]["parallelism"] == f"{kind}{n}"
+    headline = n == 8 and d["config"]["model"] == "llama3-70b" and kind in ("pd", "pdpp")
+    if headline:
+        assert d["metric"] == HEADLINE_METRIC and d["metric_scope"].startswith("headline")
+        assert d["vs_baseline"] is not None
+    else:
+        assert d["metric"].startswith(HEADLINE_METRIC + " [this run: ") and d["vs_baseline"] is None
+        assert not d["metric_scope"].startswith("headline")
+        assert f"{n}-GPU" in d["metric_scope"]
+        if kind not in ("pd", "pdpp"):
+            assert "not the P/D-split headline layout" in d["metric"]
+
+
+def test_metric_fields_match_the_layout():
+    sys.path.insert(0, ROOT)
+    from bench import HEADLINE_METRIC, metric_fields
+    h = metric_fields(8, "pdpp", "llama3-70b", "5P+1D[pp3]")
+    assert h["headline"] and h["metric"] == HEADLINE_METRIC
+    for world, kind, model in ((8, "dp", "llama3-70b"), (1, "single", "llama3-70b"), (8, "pd", "llama3-8b"),
+                               (4, "pdpp", "llama3-70b")):
+        m = metric_fields(world, kind, model)
+        assert not m["headline"] and m["metric"] != HEADLINE_METRIC and m["metric"].startswith(HEADLINE_METRIC)
+        assert (kind in ("pd", "pdpp")) == ("not the P/D-split" not in m["metric"])
+
+
+def test_stalled_pair_warmup_ends_the_run_with_a_timeout_line():
+    """VERDICT r4 #3: a rank wedged in pair warm-up (``DGI_FAULT`` stall at the phase's
+    site) ends the run within the phase budget: ONE JSON line with status "timeout",
+    the stuck phase per rank, and a non-zero exit — not a lease-long hang."""
+    import time
+    env = {**os.environ, "OMP_NUM_THREADS": "1", "DGI_PHASE_S": "6", "DGI_FAULT": "1:300001:stall:120"}
+    env.pop("DGI_STAGED_GPU", None)
+    env.pop("DGI_WATCHDOG", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
+           "--model", "llama-tiny", "--steps", "4", "--warmup", "1", "--ramp-steps", "2", "--concurrency", "8",
+           "--output-len", "8", "--prompt-len", "32", "--max-batched-tokens", "256", "--layout", "pd",
+           "--prefill-ranks", "1", "--decode-replicas", "1"]
+    t0 = time.time()
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=200)
+    took = time.time() - t0
+    assert r.returncode != 0
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{") and '"status"' in x]
+    assert len(lines) == 1, r.stdout[-2000:] + r.stderr[-2000:]
+    d = lines[0]
+    assert d["status"] == "timeout" and d["value"] is None and d["n_gpus"] == 2
+    assert d["stuck"]["phase"] == "pair_warmup"
+    assert d["phases"]["1"]["phase"] == "pair_warmup"
+    assert d["metric"].startswith("output tokens/sec")
+    assert took < 100, took
 
 
 def test_pd_separation_cli_runs_config4_as_2p_6d(tmp_path):
@@ -104,7 +163,7 @@ def test_node_step_covers_one_prefill_step():
     from dgi.parallel.bench_dist import node_step_micro
     from dgi.parallel.plan import CAPACITY
     cap = CAPACITY["llama3-70b"]
-    assert node_step_micro(cap, 3, 3) == 5                       # 202.1 ms / 42.5 ms -> 5
+    assert node_step_micro(cap, 3, 3) == 6                       # 201.5 ms / 39.6 ms -> 6
     assert node_step_micro(cap, 3, 3, prefill_ms=500.0, micro_ms=40.0) == 13
     assert node_step_micro(cap, 3, 3, prefill_ms=50.0, micro_ms=40.0) == 3   # one pipeline round at least
     assert node_step_micro(None, 1, 1) == 1

@@ -633,3 +633,162 @@ def test_decode_lookahead_matches_plain_decode(sampled, monkeypatch):
     p2, f2 = run(False, eos)
     l2, g2 = run(True, eos)
     assert l2 == p2 and g2 == f2 and "stop" in f2
+
+
+@pytest.mark.parametrize("K,N", [(4096, 4096), (1024, 8192), (8192, 8192)])
+def test_decode_proj_matches_linear_without_bias(K, N):
+    """decode_proj at M = 1 (the persistent fused GEMV, config 16, no prologue / epilogue / bias)
+    vs ops.linear and the fp32 reference, on the 8B o-proj, a TP-sharded o-proj and the 70B o-proj;
+    a non-contiguous weight falls back to ops.linear."""
+    torch.manual_seed(K + N)
+    x = (torch.randn(1, K, device=DEV) * 0.5).bfloat16()
+    w = (torch.randn(N, K, device=DEV) * 0.02).bfloat16()
+    y = ops.decode_proj(x, w)
+    ref = x.float() @ w.float().t()
+    lin = ops.linear(x, w)
+    torch.cuda.synchronize()
+    scale = float(ref.abs().max()) + 1e-3
+    assert float((y.float() - ref).abs().max()) <= 0.02 * scale
+    assert float((y.float() - lin.float()).abs().max()) <= 0.02 * scale
+    wt = torch.empty(K, N, device=DEV, dtype=torch.bfloat16).t()      # [N, K] view, not contiguous
+    wt.copy_(w)
+    y2 = ops.decode_proj(x, wt)
+    assert float((y2.float() - ref).abs().max()) <= 0.02 * scale
+
+
+def test_decode_lookahead_admission_abort_and_page_exhaustion():
+    """A lookahead chain broken by a request admitted mid-chain (add_request and
+    import_prefilled), an abort while a launch is in flight, and a pool too small for the
+    lookahead page growth: every output equals plain (non-lookahead) decoding, nothing
+    stays in flight once the work is done, and every page returns to the pool."""
+    from dgi.engine import EngineConfig, LLMEngine
+    from dgi.models.config import get_config
+    from dgi.models.llama import LlamaModel
+    from dgi.sched.request import SamplingParams
+    mc = get_config("llama-tiny-hd128")
+    src = LlamaModel(mc, "cuda", seed=9)
+    prompts = [[1] + list(range(3, 3 + n)) for n in (5, 40, 17, 7)]
+    sp = SamplingParams(max_tokens=24, temperature=0.0, ignore_eos=True)
+
+    def run(lookahead, num_blocks=256):
+        cfg = EngineConfig(model="llama-tiny-hd128", device="cuda", num_blocks=num_blocks, max_num_seqs=8,
+                           max_model_len=512, max_num_batched_tokens=512, use_graphs=True, decode_lookahead=lookahead,
+                           enable_prefix_caching=False)
+        e = LLMEngine(cfg, model_cfg=get_config("llama-tiny-hd128"), model=src)
+        free0 = e.pool.num_free
+        reqs = [e.add_request(p, sp) for p in prompts[:2]]
+        for _ in range(6):
+            e.step()
+        reqs.append(e.add_request(prompts[2], sp))          # admitted while a launch may be in flight
+        for _ in range(4):
+            e.step()
+        victim = reqs[0]
+        e.abort(victim.rid)                                  # aborted with a step in flight
+        for _ in range(3):
+            e.step()
+        # a sequence prefilled elsewhere joins the running set mid-chain
+        donor = LLMEngine(EngineConfig(model="llama-tiny-hd128", device="cuda", num_blocks=64, max_num_seqs=2,
+                                       max_model_len=512, max_num_batched_tokens=512, use_graphs=False,
+                                       enable_prefix_caching=False), model_cfg=get_config("llama-tiny-hd128"),
+                          model=src)
+        got = []
+        donor.first_token_hook = lambda r: got.append(donor.export_request_kv(r))   # before its pages are freed
+        d = donor.add_request(prompts[3], SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True))
+        donor.step()
+        kv = got[0]
+        reqs.append(e.import_prefilled(prompts[3], d.output[0], kv, sp))
+        while e.has_unfinished():
+            e.step()
+        assert e._la is None
+        assert e.pool.num_free == free0, (e.pool.num_free, free0)
+        return [r.output for r in reqs[1:]]
+
+    plain = run(False)
+    assert run(True) == plain
+    # a pool with barely enough pages: lookahead growth runs out and falls back to plain steps
+    need = sum((len(p) + 24 + 15) // 16 for p in prompts) + 1
+    assert run(True, num_blocks=need) == run(False, num_blocks=need) == plain
+
+
+@pytest.mark.parametrize("rows", [768, 1024])
+def test_two_batch_overlap_decode_step_matches_one_batch(rows, monkeypatch):
+    """Two-batch overlap (CU-masked GEMM and attention streams, dgi.models.llama
+    _forward_layers_tbo) on a pure-decode step gives the logits of the one-batch step
+    (same KV, same rows) up to GEMM blocking, and both are within bf16 tolerance of the
+    fp32 CPU model on a sample of rows."""
+    import random
+    from dgi.engine import EngineConfig, LLMEngine
+    from dgi.models import llama
+    from dgi.models.config import get_config
+    from dgi.models.llama import LlamaModel
+    from dgi.parallel.probe import _adopt
+    mc = get_config("llama-tiny-hd128")
+    src = LlamaModel(mc, "cpu", seed=21)
+    gm = LlamaModel(mc, "cuda", init="empty").copy_from(src)
+    eng = LLMEngine(EngineConfig(model="llama-tiny-hd128", device="cuda", num_blocks=rows * 8 + 16,
+                                 max_num_seqs=rows, max_model_len=512, max_num_batched_tokens=2048, use_graphs=False,
+                                 enable_prefix_caching=False), model_cfg=mc, model=gm)
+    torch.manual_seed(5)
+    eng.pool.kv.normal_(0, 1)
+    _adopt(eng, rows, 90, random.Random(1))
+    sb = eng.scheduler.schedule()
+    assert len(sb.decode) == rows and not sb.prefill
+    flat, hdr, _ = eng.runner.build_host(sb)
+    ids, meta, _ = eng.runner.meta_from_device(eng.runner.to_device(flat), hdr)
+    monkeypatch.setattr(llama, "TBO", False)
+    ref = eng.model.forward(meta, input_ids=ids).float()
+    monkeypatch.setattr(llama, "TBO", True)
+    assert eng.model._tbo_ok(torch.empty(rows, 8, device="cuda", dtype=torch.bfloat16), meta, None) == \
+        llama.tbo_split(rows)
+    got = eng.model.forward(meta, input_ids=ids).float()
+    torch.cuda.synchronize()
+    scale = float(ref.abs().max())
+    assert float((got - ref).abs().max()) <= 0.02 * scale
+    # a sample of rows against the fp32 CPU model over the same KV pages
+    pick = [0, 1, rows // 2, rows - 1]
+    kv_cpu = eng.pool.kv.float().cpu()
+    for r in pick:
+        req = sb.decode[r]
+        ctx = req.num_computed + 1
+        blocks = req.blocks[: (ctx + 15) // 16]
+        lg = _cpu_decode_row(src, kv_cpu, blocks, ctx, int(ids[r]))
+        assert float((got[r].cpu() - lg).abs().max()) <= 0.03 * float(lg.abs().max()) + 0.03
+
+
+def _cpu_decode_row(model, kv, blocks, ctx, tok):
+    """fp32 CPU logits of one decode row at position ctx - 1 over paged KV ``kv`` (pages
+    ``blocks``; the row's own K/V is computed here, the rest read from the pages)."""
+    import math as _m
+    c = model.cfg
+    x = model.embed[tok].float()[None]
+    pos = torch.tensor([ctx - 1])
+    cs = ops.rope_cos_sin(c.rope_dim, c.max_position, c.rope_theta, c.rope_scaling)
+    res = None
+    for i, L in enumerate(model.layers):
+        if res is None:
+            res = x
+            h = ops.rmsnorm_ref(x, L.in_norm.float(), c.rms_eps)
+        else:
+            res = x + res
+            h = ops.rmsnorm_ref(res, L.in_norm.float(), c.rms_eps)
+        qkv = h @ L.qkv.float().t()
+        nh, nkv, hd = c.num_heads, c.num_kv_heads, c.head_dim
+        q = qkv[:, : nh * hd].view(1, nh, hd)
+        k = qkv[:, nh * hd:(nh + nkv) * hd].view(1, nkv, hd)
+        v = qkv[:, (nh + nkv) * hd:].view(1, nkv, hd)
+        q = ops._rope(q, cs[pos], 0)
+        k = ops._rope(k, cs[pos], 0)
+        K = kv[i, 0][blocks].permute(0, 2, 1, 3).reshape(-1, nkv, hd)[:ctx].clone()
+        V = kv[i, 1][blocks].permute(0, 2, 1, 3).reshape(-1, nkv, hd)[:ctx].clone()
+        K[ctx - 1], V[ctx - 1] = k[0], v[0]
+        G = nh // nkv
+        s = torch.einsum("hgd,thd->hgt", q.view(nkv, G, hd), K) / _m.sqrt(hd)
+        o = torch.einsum("hgt,thd->hgd", torch.softmax(s, -1), V).reshape(1, nh * hd)
+        x = o @ L.o.float().t()
+        res = x + res
+        h = ops.rmsnorm_ref(res, L.post_norm.float(), c.rms_eps)
+        gu = h @ L.gate_up.float().t()
+        I = gu.shape[1] // 2
+        x = (torch.nn.functional.silu(gu[:, :I]) * gu[:, I:]) @ L.down.float().t()
+    h = ops.rmsnorm_ref(x + res, model.norm.float(), c.rms_eps)
+    return (h @ model.lm_head.float().t())[0]

@@ -271,3 +271,32 @@ def test_fused_decode_honours_trim_last_on_padded_batch():
     assert calls and got.shape[0] == len(sampled) == 2
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)
     assert samp.sample(got).shape[0] == 2
+
+
+def test_gemm_table_decides_with_margin_and_round_trips_json(tmp_path):
+    """The routing table keeps the raw per-implementation times: the MFMA kernel is chosen
+    only where it beats hipBLASLt by >= 3 % (near-ties stay on hipBLASLt, so passes agree),
+    the median of several passes decides the shipped table, and a table written to JSON
+    loads back with the same choices."""
+    import json
+    from dgi.runtime.gemm_pad import MlpPadTable, RAW_KEYS
+
+    def pt(front, front_m, back, back_m, pq=(1.0, None), po=(1.0, None)):
+        r = dict.fromkeys(RAW_KEYS)
+        r.update(front=front, front_mfma=front_m, back=back, back_mfma=back_m, pq_blas=pq[0], pq_mfma=pq[1],
+                 po_blas=po[0], po_mfma=po[1])
+        return r
+    grid = [512, 544]
+    raw = [pt(10.0, 9.8, 5.0, 4.0, pq=(2.0, 1.5)), pt(10.0, 9.0, 5.0, 4.9, po=(1.0, 0.5))]
+    t = MlpPadTable.decide(grid, raw, 32)
+    assert t.impl(512) == (False, True)            # 2 % faster gate_up: not enough; down 20 %: MFMA
+    assert t.impl(544) == (True, False)            # 10 % vs 2 %
+    assert t.proj_impl(512) == (True, False) and t.proj_impl(544) == (False, True)
+    assert t.times == [10.0 + 4.0, 9.0 + 5.0]
+    runs = [raw, [pt(10.0, 9.0, 5.0, 4.0), pt(10.0, 9.0, 5.0, 4.9)], [pt(10.0, 9.9, 5.0, 4.0), pt(10.0, 9.1, 5.0, 4.9)]]
+    med = MlpPadTable.median_raw(runs)
+    assert med[0]["front_mfma"] == 9.8 and med[1]["front_mfma"] == 9.0
+    p = tmp_path / "t.json"
+    p.write_text(json.dumps(t.to_json({"k": 1})))
+    back = MlpPadTable.from_json(json.loads(p.read_text()))
+    assert back.impls == t.impls and back.proj_impls == t.proj_impls and back.source == "shipped"

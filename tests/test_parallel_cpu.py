@@ -116,7 +116,7 @@ def _pp_body(rank, world):
         while eng.has_unfinished():
             eng.step()
         eng.stop_stages()
-        return {"out": [r.output for r in reqs],
+        return {"out": [r.output for r in reqs], "relaunches": eng.relaunches,
                 "replays": eng.sgraphs.replays if eng.sgraphs is not None else 0}
     w = StageWorker(cfg, f, ranks)
     assert w.run() == "stop"
@@ -377,10 +377,10 @@ def test_plan_layer_split_gives_head_stage_fewer_layers():
 
 
 def test_node_layout_defaults():
-    # 70B at 8 GPUs: 5 prefill GPUs feed a 3-stage decode pipeline (highest disaggregated rate among
-    # layouts whose decode TPOT beats a mixed-step DP GPU; the pipeline's slack admits local prompts)
+    # 70B at 8 GPUs: 6 prefill GPUs (1024-token steps) feed a 2-stage decode pipeline — the fastest
+    # split whose TTFT and TPOT are both under 0.7 of a mixed-step DP GPU's (plan.plan_pd)
     lay = plan_node_layout(8)
-    assert lay.kind == "pdpp" and lay.decode_groups == [[5, 6, 7]] and len(lay.prefill_ranks) == 5
+    assert lay.kind == "pdpp" and lay.decode_groups == [[6, 7]] and len(lay.prefill_ranks) == 6
     assert plan_node_layout(1).kind == "single"
     assert plan_node_layout(2).kind == "pd"
     four = plan_node_layout(4)     # 70B: 3 prefill GPUs feed one decode GPU (decode-bound; prefill overflow)
@@ -388,7 +388,8 @@ def test_node_layout_defaults():
     # 8B at 8 GPUs: whole-model decode replicas (prefill is fast, decode replicas are cheap)
     eight_8b = plan_node_layout(8, model="llama3-8b")
     assert eight_8b.kind == "pd" and len(eight_8b.decode_groups) == 3 and len(eight_8b.prefill_ranks) == 5
-    assert plan_node_layout(8, "pd").decode_groups == [[5], [6], [7]]
+    pd8 = plan_node_layout(8, "pd")                # whole-model decode GPUs only
+    assert pd8.kind == "pd" and all(len(g) == 1 for g in pd8.decode_groups) and pd8.world == 8
     # explicit replica requests and legacy flat decode lists
     lay = plan_node_layout(8, "pdpp", prefill_ranks=4, decode_stages=2)
     assert lay.prefill_ranks == [0, 1, 2, 3] and lay.decode_groups == [[4, 5], [6, 7]] and lay.drivers == [4, 6]
@@ -416,9 +417,12 @@ def test_capacity_planner_balances_roles():
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_pipeline_matches_single_process(world):
+    """Pipeline outputs equal one process's; the driver relaunched microbatches from
+    metadata it built while their tokens were in flight (``PipelineEngine._retire``)."""
     ref = _reference_outputs()
     out = _spawn("_pp_body", world)
     assert out[0]["out"] == ref
+    assert out[0]["relaunches"] > 0
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -811,40 +815,36 @@ def test_layout_estimate_reports_rate_and_latency():
     assert est["filler_share"] < 0.2 and est["ttft_ms"] is not None
 
 
-def test_auto_layout_never_runs_a_pd_split_rated_below_dp():
-    """bench.py --layout auto: the P/D split only when the planner's disaggregated
-    estimate reaches N data-parallel GPUs.  The round-3 table rates
-    the 70B 8-GPU split 14.3k vs 14.9k tok/s -> DP; a capacity whose decode role is
-    fast enough flips it to the P/D pipeline."""
+def test_auto_layout_picks_pd_for_latency_at_throughput_parity():
+    """bench.py --layout auto: the planner picks the fastest P/D split whose
+    TTFT and TPOT are at most LATENCY_FRAC of a data-parallel GPU's, choosing the prefill step
+    size for TTFT, and keeps it unless its node rate falls below PD_MIN_RATIO x DP; the DP
+    estimate is reported next to the pick."""
     import dataclasses
     import bench
-    from dgi.parallel.plan import CAPACITY, set_capacity
+    from dgi.parallel.plan import CAPACITY, LATENCY_FRAC, PD_MIN_RATIO, set_capacity
     from dgi.parallel.probe import plan_from_probe
-    assert bench.auto_layout(8, "llama3-70b") == "dp"
-    assert bench.auto_layout(4, "llama3-70b") == "dp" and bench.auto_layout(2, "llama3-70b") == "dp"
     tab = CAPACITY["llama3-70b"]
     d = plan_from_probe(8, tab)
-    assert d["kind"] == "dp" and "<" in d["reason"] and d["estimate"]["disagg_tok_s"] < d["dp_tok_s"]
-    fast = dataclasses.replace(tab, decode_tok_s={k: v * 1.35 for k, v in tab.decode_tok_s.items()},
-                               decode_step_ms={k: v / 1.35 for k, v in tab.decode_step_ms.items()})
-    d = plan_from_probe(8, fast, min_ratio=1.0)
-    assert d["kind"] in ("pd", "pdpp") and d["estimate"]["disagg_tok_s"] >= d["dp_tok_s"]
-    # 2.3 % above DP is inside the box-to-box spread: the default margin (PD_MIN_RATIO 1.05) keeps DP
-    ratio = d["estimate"]["disagg_tok_s"] / d["dp_tok_s"]
-    assert 1.0 <= ratio < 1.05
-    tie = plan_from_probe(8, fast)
-    assert tie["kind"] == "dp" and "<" in tie["reason"]
-    faster = dataclasses.replace(fast, prefill_tok_s=tab.prefill_tok_s * 1.25)
-    d = plan_from_probe(8, faster)
-    assert d["kind"] in ("pd", "pdpp") and d["estimate"]["disagg_tok_s"] >= 1.05 * d["dp_tok_s"]
+    est, dp = d["estimate"], d["dp_reference"]
+    assert d["kind"] in ("pd", "pdpp") and bench.auto_layout(8, "llama3-70b") == d["kind"]
+    assert est["latency_ok"] and est["ttft_ms"] <= LATENCY_FRAC * dp["ttft_ms"]
+    assert est["tpot_ms"] <= LATENCY_FRAC * dp["tpot_ms"]
+    assert est["tok_s"] >= PD_MIN_RATIO * dp["tok_s"]
+    # the step size is a planner output: 2048-token steps miss the TTFT bound, 1024 meet it
+    assert d["prefill_mbt"] == 1024 and tab.steps()[2048] > LATENCY_FRAC * dp["ttft_ms"]
+    assert "TTFT" in d["reason"] and "-> " + d["kind"] in d["reason"]
+    # a decode role too slow for parity -> data parallel, with the reason
+    slow = dataclasses.replace(tab, decode_tok_s={k: v * 0.5 for k, v in tab.decode_tok_s.items()},
+                               decode_step_ms={k: v * 2 for k, v in tab.decode_step_ms.items()})
+    s2 = plan_from_probe(8, slow)
+    assert s2["kind"] == "dp" and ("below" in s2["reason"] or "latency bound" in s2["reason"])
     try:
-        set_capacity("llama3-70b", faster)        # what the start-up probe does with its measurement
-        assert bench.auto_layout(8, "llama3-70b@L8") == d["kind"]
-        set_capacity("llama3-70b", fast)
+        set_capacity("llama3-70b", slow)          # what the start-up probe does with its measurement
         assert bench.auto_layout(8, "llama3-70b@L8") == "dp"
     finally:
         set_capacity("llama3-70b", None)
-    assert bench.auto_layout(8, "llama3-70b") == "dp"
+    assert bench.auto_layout(8, "llama3-70b") == d["kind"]
 
 
 def test_capacity_from_probe_and_median():

@@ -86,24 +86,58 @@ def test_pure_prefill_steps_are_not_rounded():
 
 
 def test_tpot_slo_step_budget_caps_rows():
-    """dgi.sched.slo.StepBudget: learns ms per row from executed steps and caps the next
-    step at slo / cost rows, never below the decode rows + a minimum prefill chunk."""
+    """dgi.sched.slo.StepBudget: fits ms = fixed + per_row * rows over executed steps and
+    caps the next step at the rows whose predicted time meets the SLO, never below the
+    decode rows + a minimum prefill chunk."""
     from dgi.sched.slo import StepBudget
     b = StepBudget(100.0, min_prefill=128)
     assert b.budget(4096, 300) == 4096                 # nothing learned yet: no cap
-    b.observe(100, 50.0)                               # too few rows to be GEMM-bound: ignored
-    assert b.ms_per_row is None
-    b.observe(2000, 200.0)                             # 0.1 ms per row
+    b.observe(2000, 200.0)                             # one sample: a line through the origin
+    assert abs(b.ms_per_row - 0.1) < 1e-9 and b.fixed_ms == 0.0
     assert b.budget(4096, 300) == 1000 and b.capped == 1
+    b.observe(1000, 110.0)                             # two samples: 20 ms fixed + 0.09 ms per row
+    assert abs(b.ms_per_row - 0.09) < 1e-9 and abs(b.fixed_ms - 20.0) < 1e-6
+    assert b.rows_at_slo() == 888
     assert b.budget(4096, 950) == 1078                 # decode rows + the minimum prefill
     assert b.budget(512, 300) == 512
     st = b.stats()
-    assert st["budget_rows"] == 1000 and st["steps_observed"] == 1
+    assert st["budget_rows"] == b.rows_at_slo() and st["steps_observed"] == 2
+
+
+def test_tpot_slo_budget_recovers_from_a_slow_first_step():
+    """a 10x slow first step must not pin the budget low.  Capped steps are
+    observed too, and the robust (Theil-Sen) fit outvotes the outlier within a few steps."""
+    from dgi.sched.slo import StepBudget
+    cost = lambda r: 20.0 + 0.1 * r                    # noqa: E731  the true step cost
+    b = StepBudget(150.0, min_prefill=128)
+    b.observe(1536, 10 * cost(1536))                   # cold start: 10x slow
+    assert b.rows_at_slo() < 200
+    for i in range(12):
+        rows = b.budget(4096, 100)                     # the engine runs what the budget allows
+        b.observe(rows + (i % 3) * 40, cost(rows + (i % 3) * 40))
+    assert abs(b.rows_at_slo() - 1300) <= 20, b.stats()
+
+
+def test_tpot_slo_admission_cap_follows_the_load_shape():
+    """The admission cap is the decode rows of an SLO-sized step plus the prompts it
+    prefills: 512-in / 128-out at 1300 rows -> 260 decode rows + ~2 prompts."""
+    from dgi.sched.slo import StepBudget
+    b = StepBudget(150.0)
+    assert b.admission_cap(4096) is None
+    b.observe(1000, 120.0)
+    b.observe(2000, 220.0)                             # 20 ms + 0.1 ms per row: 1300 rows at 150 ms
+    assert b.admission_cap(4096) is None               # load shape not known yet
+    for _ in range(3):
+        b.observe_finished(512, 128)
+    assert b.admission_cap(4096) == 262
+    assert b.admission_cap(1024) == int(1024 * 0.2 + 1024 * 0.8 / 512 + 0.5)
+    assert b.stats()["admission_cap"] == 262
 
 
 def test_engine_with_tpot_slo_runs_smaller_mixed_steps():
     """An engine with a TPOT SLO schedules mixed steps below the SLO's row budget once it
-    has measured its step cost; outputs are unchanged (only the chunking differs)."""
+    has measured its step cost, and admits no more sequences than it sustains at the SLO;
+    outputs are unchanged (only the chunking and admission order differ)."""
     import torch
     from dgi.engine import EngineConfig, LLMEngine
     from dgi.sched.request import SamplingParams
@@ -114,7 +148,7 @@ def test_engine_with_tpot_slo_runs_smaller_mixed_steps():
                 max_num_batched_tokens=1024, use_graphs=False, enable_prefix_caching=False)
     ref = [r.output for r in LLMEngine(EngineConfig(**base)).generate(prompts, sp)]
     eng = LLMEngine(EngineConfig(**base, tpot_slo_ms=1e-3))     # unreachable: always the minimum step
-    eng.step_budget.min_rows = 1
     got = [r.output for r in eng.generate(prompts, sp)]
     assert got == ref
     assert eng.step_budget.capped > 0 and eng.step_budget.steps > 0
+    assert eng.scheduler.admit_cap is not None and eng.admission_limit() is not None
