@@ -176,6 +176,8 @@ class LLMEngine:
         req = Request(prompt_ids, params or SamplingParams(), rid=rid, user=user)
         self.scheduler.add(req)
         self.requests[req.rid] = req
+        if self.step_budget is not None:
+            self.step_budget.observe_request(len(req.prompt), req.params.max_tokens)
         return req
 
     def abort(self, rid) -> bool:

@@ -83,7 +83,8 @@ def prepare_rccl_env() -> None:
     # which transport each connection uses (P2P/IPC over xGMI vs a network fallback) goes into
     # the bench JSON: RCCL's INIT log, one file per rank, parsed by ``rccl_transports``
     # (DGI_RCCL_LOG=0, or a NCCL_DEBUG set by the user, leaves RCCL's logging alone)
-    if os.environ.get("DGI_RCCL_LOG", "1") != "0" and "NCCL_DEBUG" not in os.environ:
+    # (the image exports NCCL_DEBUG=VERSION, a one-line banner: that is not a user's logging choice)
+    if os.environ.get("DGI_RCCL_LOG", "1") != "0" and os.environ.get("NCCL_DEBUG", "VERSION") in ("", "VERSION"):
         os.environ["NCCL_DEBUG"] = "INFO"
         os.environ.setdefault("NCCL_DEBUG_SUBSYS", "INIT")
         os.environ["NCCL_DEBUG_FILE"] = rccl_log_path()

@@ -48,6 +48,7 @@ class StepBudget:
         # mean prompt / output length of finished requests (the load shape for admission)
         self.prompt_avg: Optional[float] = None
         self.output_avg: Optional[float] = None
+        self.n_finished = 0
 
     # ------------------------------------------------------------------ cost model
     def observe(self, rows: int, ms: float) -> None:
@@ -90,7 +91,19 @@ class StepBudget:
         return b
 
     # ------------------------------------------------------------------ admission
-    def observe_finished(self, prompt_len: int, output_len: int, alpha: float = 0.1) -> None:
+    def observe_request(self, prompt_len: int, max_tokens: int) -> None:
+        """A request arrived: until requests finish, its prompt length and ``max_tokens`` are
+        the load shape (so the admission cap holds from the first steps on — a closed-loop
+        client that filled the engine before it was known would queue for a whole
+        generation's worth of steps)."""
+        if self.n_finished == 0:
+            self._blend(prompt_len, max_tokens)
+
+    def observe_finished(self, prompt_len: int, output_len: int) -> None:
+        self.n_finished += 1
+        self._blend(prompt_len, output_len)
+
+    def _blend(self, prompt_len: int, output_len: int, alpha: float = 0.1) -> None:
         if self.prompt_avg is None:
             self.prompt_avg, self.output_avg = float(prompt_len), float(output_len)
         else:

@@ -67,6 +67,9 @@ def main():
     ap.add_argument("--no-adaptive", action="store_true", help="fixed tree depth")
     ap.add_argument("--sampled", action="store_true",
                     help="also run seeded temperature 0.8 / top-k 50 / top-p 0.9 requests (coupled verification)")
+    ap.add_argument("--draft-vocab", type=int, default=0,
+                    help="EAGLE-3 draft vocabulary: the N token ids the target chose most often in the draft's "
+                         "training corpus (0 = the whole vocabulary)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     cfg = EngineConfig(model=a.model, device="cuda", max_num_seqs=64, max_num_batched_tokens=8192,
@@ -79,7 +82,7 @@ def main():
         m.lm_head.copy_(m.embed.index_select(0, perm) / m.cfg.hidden_size ** 0.5)
     t0 = time.perf_counter()
     info = train_draft(spec, steps=a.train_steps, batch=16, prompt_len=64, gen_len=192, num_seqs=a.train_seqs,
-                       random_seqs=a.random_seqs, log=lambda m: print(m, flush=True))
+                       random_seqs=a.random_seqs, log=lambda m: print(m, flush=True), draft_vocab=a.draft_vocab)
     info["train_seconds"] = round(time.perf_counter() - t0, 1)
     print("draft training", info, flush=True)
     base = LLMEngine(cfg, model=spec.model)

@@ -342,3 +342,31 @@ def test_oracle_chain_acceptance_ceiling():
         se.step()
     assert [r.output for r in rs] == ref
     assert se.acceptance()["mean_accepted"] > 3.0
+
+
+def test_draft_vocabulary_keeps_spec_lossless_and_restricts_proposals():
+    """EAGLE-3 draft vocabulary: the draft scores only the target's most frequent choices
+    (a [V', H] head per depth instead of [V, H]); outputs stay identical to plain greedy
+    decoding and every drafted token is a member of the draft vocabulary."""
+    from dgi.spec.eagle3 import hot_vocab_from_targets
+    t = torch.tensor([[5, 5, 7, 9, 9, 9, 3]])
+    assert hot_vocab_from_targets(t, 16, 2).tolist() == [5, 9]
+    assert hot_vocab_from_targets(t, 16, 10).tolist()[:4] == [0, 3, 5, 7] or \
+        set(hot_vocab_from_targets(t, 16, 10).tolist()) >= {3, 5, 7, 9}
+    base, se = _engines()
+    sp = SamplingParams(max_tokens=24, temperature=0.0, ignore_eos=True)
+    ref = [r.output for r in base.generate(_prompts(), sp)]
+    info = train_draft(se, steps=40, batch=8, prompt_len=16, gen_len=48, num_seqs=16, draft_vocab=96)
+    assert info["draft_vocab"]["size"] == 96 and 0 < info["draft_vocab"]["target_tokens_covered"] <= 1
+    hot = set(se.draft.hot.tolist())
+    assert se.draft.hot_head.shape == (96, se.model_cfg.hidden_size)
+    seen = []
+    orig = se._draft_tree_eager
+
+    def spy(*a, **k):
+        tok, par = orig(*a, **k)
+        seen.append(tok[:, 1:].reshape(-1).tolist())
+        return tok, par
+    se._draft_tree_eager = spy
+    assert [r.output for r in se.generate(_prompts(), sp)] == ref
+    assert seen and all(t in hot for s in seen for t in s)
