@@ -50,16 +50,19 @@ constexpr int KT = 64;  // keys per tile
 // NW waves x 32 query rows per workgroup (one K/V tile staging shared by all of them):
 // NW = 4 -> 128-row tiles, 2 workgroups per CU; NW = 8 -> 256-row tiles, 1 per CU
 // (same 2 waves per SIMD, half the K/V staging per query row).
-template <int HD, int NW>
+// DB = 1: two LDS stages.  Tile i+1 is written into the idle stage right after the one
+// barrier of iteration i (its registers were loaded during iteration i-1), tile i+2's
+// global loads are issued, then tile i is consumed — one barrier per 64 keys instead of
+// two, and a wave's LDS write no longer waits for every other wave before its MFMAs
+// (round 5: 24 % MFMA busy with DB = 0, profiles/r5_pmc/).
+template <int HD, int NW, int DB>
 __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void prefill_attn_kernel(
     const uint16_t* __restrict__ q, int q_stride, const uint16_t* __restrict__ k_cache,
     const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_seqlens_q, const int* __restrict__ context_lens,
     const int* __restrict__ tiles, uint16_t* __restrict__ out, int out_stride, int nh, int nkv,
     int bs_log2, float scale_log2, const unsigned long long* __restrict__ tree_mask, int tree_n) {
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * KT * HD];
-  uint16_t* ks = lds;
-  uint16_t* vs = lds + KT * HD;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[(DB ? 2 : 1) * 2 * KT * HD];
 
   const int b = tiles[2 * blockIdx.x];
   const int t0 = tiles[2 * blockIdx.x + 1];  // first query row (within seq) of this tile
@@ -129,24 +132,49 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void prefill_attn_kernel(
       vr[p] = *reinterpret_cast<const u32x4*>(v_cache + base);
     }
   };
+  auto store_tile = [&](uint16_t* kst, uint16_t* vst) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int row = p * (NT / CH) + tid / CH;
+      const int ch = tid % CH;
+      *reinterpret_cast<u32x4*>(kst + k_off<HD>(row, ch)) = kr[p];
+      *reinterpret_cast<u32x4*>(vst + v_off<HD>(row, ch)) = vr[p];
+    }
+  };
   if (kv_end > 0) load_tile(0);
+  if (DB && kv_end > 0) {
+    store_tile(lds, lds + KT * HD);             // stage 0 <- tile 0
+    if (KT < kv_end) load_tile(KT);             // registers <- tile 1
+  }
   // last key this wave can see (causal); tiles beyond it are skipped
   const int wave_last_pos = pos_base + min(t0 + 32 * w + 31, qlen - 1);
   // keys <= wave_first_pos are visible to every row of the wave
   const int wave_first_pos = pos_base + t0 + 32 * w;
   const bool wave_tree = tree_mask != nullptr && (t0 + 32 * w + 31 >= tree_first);
   const bool wave_rows = t0 + 32 * w < qlen;
-  for (int kb0 = 0; kb0 < kv_end; kb0 += KT) {
-    __syncthreads();  // previous tile fully consumed
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      const int row = p * (NT / CH) + tid / CH;
-      const int ch = tid % CH;
-      *reinterpret_cast<u32x4*>(ks + k_off<HD>(row, ch)) = kr[p];
-      *reinterpret_cast<u32x4*>(vs + v_off<HD>(row, ch)) = vr[p];
+  int it = 0;
+  for (int kb0 = 0; kb0 < kv_end; kb0 += KT, ++it) {
+    uint16_t* ks;
+    uint16_t* vs;
+    if (DB) {
+      // stage it&1 holds tile it (written last iteration, or before the loop); every wave has
+      // finished reading stage (it+1)&1 (tile it-1) once it is past this barrier
+      __syncthreads();
+      ks = lds + (it & 1) * 2 * KT * HD;
+      vs = ks + KT * HD;
+      if (kb0 + KT < kv_end) {
+        uint16_t* kn = lds + ((it + 1) & 1) * 2 * KT * HD;
+        store_tile(kn, kn + KT * HD);           // tile it+1, loaded during the previous iteration
+        if (kb0 + 2 * KT < kv_end) load_tile(kb0 + 2 * KT);
+      }
+    } else {
+      ks = lds;
+      vs = lds + KT * HD;
+      __syncthreads();  // previous tile fully consumed
+      store_tile(ks, vs);
+      __syncthreads();
+      if (kb0 + KT < kv_end) load_tile(kb0 + KT);
     }
-    __syncthreads();
-    if (kb0 + KT < kv_end) load_tile(kb0 + KT);
     // whole tile above this wave's diagonal, or no valid query row in this wave
     // (it still stages K/V for the others)
     if (kb0 > wave_last_pos || !wave_rows) continue;
@@ -286,16 +314,20 @@ extern "C" int dgi_paged_prefill(const void* q, int q_stride, const void* k_cach
   while ((1 << bs_log2) < block_size) ++bs_log2;
   if ((1 << bs_log2) != block_size) return -4;
   const float scale_log2 = scale * 1.4426950408889634f;
+  const int db = (tile_rows >> 16) & 1;          // bit 16: two LDS stages (prefill_attn_kernel DB)
+  tile_rows &= 0xffff;
   if (tile_rows != 128 && tile_rows != 256) return -7;
-#define DGI_PREFILL(HDV, NWV)                                                                          \
-  prefill_attn_kernel<HDV, NWV><<<dim3(n_tiles, nh), NWV * 64, 0, s>>>(                                \
+#define DGI_PREFILL(HDV, NWV, DBV)                                                                     \
+  prefill_attn_kernel<HDV, NWV, DBV><<<dim3(n_tiles, nh), NWV * 64, 0, s>>>(                           \
       (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables,     \
       bt_stride, cu_seqlens_q, context_lens, tiles, (uint16_t*)out, out_stride, nh, nkv, bs_log2,         \
       scale_log2, tree_mask, tree_n)
   if (hd == 128) {
-    if (tile_rows == 256) DGI_PREFILL(128, 8); else DGI_PREFILL(128, 4);
+    if (tile_rows == 256) { if (db) DGI_PREFILL(128, 8, 1); else DGI_PREFILL(128, 8, 0); }
+    else { if (db) DGI_PREFILL(128, 4, 1); else DGI_PREFILL(128, 4, 0); }
   } else {
-    if (tile_rows == 256) DGI_PREFILL(64, 8); else DGI_PREFILL(64, 4);
+    if (tile_rows == 256) { if (db) DGI_PREFILL(64, 8, 1); else DGI_PREFILL(64, 8, 0); }
+    else { if (db) DGI_PREFILL(64, 4, 1); else DGI_PREFILL(64, 4, 0); }
   }
 #undef DGI_PREFILL
   DGI_CHECK_LAUNCH();

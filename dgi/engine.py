@@ -11,6 +11,7 @@ import dataclasses
 import time
 from typing import Iterable, Optional
 
+import numpy as np
 import torch
 
 from dgi.kv.block_pool import BlockPool, OutOfBlocks, num_blocks_for_budget
@@ -147,6 +148,11 @@ class LLMEngine:
         import os as _os
         self._la = None
         self.lookahead = bool(cfg.decode_lookahead) and _os.environ.get("DGI_DECODE_LOOKAHEAD", "1") == "1"
+        # mixed-step lookahead: an eager step in flight, its tokens not committed yet
+        # (``_launch_eager`` / ``_step_mixed_lookahead``); DGI_MIXED_LOOKAHEAD=0 turns it off
+        self._mx = None
+        self.mixed_lookahead = bool(cfg.decode_lookahead) and _os.environ.get("DGI_MIXED_LOOKAHEAD", "1") == "1"
+        self.mixed_chained = 0
         self.step_budget = None
         if cfg.tpot_slo_ms > 0:
             from dgi.sched.slo import StepBudget
@@ -201,7 +207,7 @@ class LLMEngine:
         return cap + queued
 
     def has_unfinished(self) -> bool:
-        return self._la is not None or self.scheduler.has_work()
+        return self._la is not None or self._mx is not None or self.scheduler.has_work()
 
     def warmup(self) -> None:
         """Capture decode graphs ahead of serving."""
@@ -213,6 +219,11 @@ class LLMEngine:
         if self._la is not None:
             n = len(self._la[0].decode)
             outs = self._step_lookahead()
+            self._account(n, time.perf_counter() - t0)
+            return outs
+        if self._mx is not None:
+            n = self._mx[0].num_tokens
+            outs = self._step_mixed_lookahead()
             self._account(n, time.perf_counter() - t0)
             return outs
         self.model.kv_cache = self.pool.kv   # engines may share one model object
@@ -234,6 +245,12 @@ class LLMEngine:
             out = self._step_lookahead()
             self._account(sb.num_tokens, time.perf_counter() - t0)
             return out
+        if self._mixed_ok(sb):
+            # eager step: launch it, then (while it runs) schedule and launch the step after it
+            self._mx = self._launch_eager(sb)
+            outs = self._step_mixed_lookahead()
+            self._account(sb.num_tokens, time.perf_counter() - t0)
+            return outs
         with phase("execute", decode=len(sb.decode), prefill=len(sb.prefill)):
             res = self.runner.execute(sb)
         with phase("apply"):
@@ -254,6 +271,10 @@ class LLMEngine:
         """Collect and apply a lookahead step still in flight (teardown, or before the
         running set is changed from outside the engine)."""
         outs = []
+        if self._mx is not None:
+            sb, sampled, _tok, host, ev = self._mx
+            self._mx = None
+            outs = self._collect_eager(sampled, host, ev)
         if self._la is not None:
             sb, h = self._la
             self._la = None
@@ -263,6 +284,94 @@ class LLMEngine:
                 outs = self._apply(type(sb)([r for r, _t in keep], [], []), [r for r, _t in keep],
                                    [t for _r, t in keep])
         return outs
+
+    # ------------------------------------------------------------------ mixed-step lookahead
+    def _mixed_ok(self, sb) -> bool:
+        """Eager (prefill / mixed / beyond-graph) steps of a plain GPU engine chain: step N+1 is
+        scheduled and launched while step N runs, its rows' input tokens read on the device."""
+        return (self.mixed_lookahead and self.device.type == "cuda" and type(self) is LLMEngine
+                and self.pre_execute is None and self.first_token_hook is None and self.step_budget is None
+                and self.host_tier is None and not sb.preempted and all(r.swapped is None for r in sb.decode))
+
+    def _launch_eager(self, sb, prev=None) -> tuple:
+        """Enqueue one eager step (forward, sampling, async copy of the tokens to the host) and
+        advance its rows' KV cursors.  ``prev`` = (sampled rows, device tokens) of the step in
+        flight: a row whose input token is one of those reads it on the device."""
+        run = self.runner
+        run.step_id += 1
+        src, dst, ahead = [], [], None
+        if prev is not None:
+            where = {id(r): j for j, r in enumerate(prev[0])}
+            for k, r in enumerate(sb.decode):
+                j = where.get(id(r))
+                if j is not None:
+                    dst.append(k)
+                    src.append(j)
+            if dst:
+                ahead = [0] * (len(sb.decode) + sum(1 for c in sb.prefill if c.sample))
+                for k in dst:
+                    ahead[k] = 1
+        with phase("execute", decode=len(sb.decode), prefill=len(sb.prefill)):
+            flat, hdr, sampled = run.build_host(sb, seed_ahead=ahead)
+            n = len(dst)
+            if n:      # the token map rides in the step's one H2D copy
+                flat = np.concatenate([flat, np.asarray(dst, np.int32), np.asarray(src, np.int32)])
+            dev = run.to_device(flat)
+            ids, meta, samp = run.meta_from_device(dev, hdr)
+            if n:
+                L = int(hdr[run.H_LEN])
+                ids.index_copy_(0, dev[L:L + n].long(), prev[1].index_select(0, dev[L + n:L + 2 * n].long())
+                                .to(ids.dtype))
+            logits = self.model.forward(meta, input_ids=ids)
+            tok = host = ev = None
+            if sampled:
+                tok = samp.sample(logits)
+                host = torch.empty(tok.shape, dtype=tok.dtype, pin_memory=True)
+                host.copy_(tok, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+        self._advance(sb)
+        return (sb, sampled, tok, host, ev)
+
+    def _collect_eager(self, sampled, host, ev) -> list[StepOutput]:
+        if ev is None:
+            return []
+        wh = self.runner.wait_hook
+        if wh is None:
+            ev.synchronize()
+        else:
+            while not ev.query():
+                wh()
+                time.sleep(0.00002)
+        toks = host.tolist()
+        with phase("apply"):
+            keep = [(r, t) for r, t in zip(sampled, toks) if r.status is Status.RUNNING]
+            return self._commit([r for r, _t in keep], [t for _r, t in keep])
+
+    def _step_mixed_lookahead(self) -> list[StepOutput]:
+        """Schedule and launch step N+1, then collect and commit step N (in flight).  Rows whose
+        step-N token ends them by length are not scheduled again; a row that step N ends by
+        EOS / stop id still runs in N+1 and that token is discarded.  The chain stops when the
+        next step is a pure-decode step the captured graphs take."""
+        sb, sampled, tok, host, ev = self._mx
+        self._mx = None
+        cap = self.cfg.max_model_len - 1
+        ending = [r for r in sampled if len(r.output) + 1 >= r.params.max_tokens
+                  or len(r.prompt) + len(r.output) + 1 >= cap]
+        for r in ending:
+            r.busy = True
+        try:
+            with phase("schedule"):
+                sb2 = self.scheduler.schedule(preempt=False)
+        finally:
+            for r in ending:
+                r.busy = False
+        g = self.runner.graphs
+        graph_next = (g is not None and not sb2.prefill and sb2.decode and len(sb2.decode) <= g.max_bucket)
+        if not sb2.empty and not graph_next and tok is not None and self._mixed_ok(sb2):
+            self._mx = self._launch_eager(sb2, prev=(sampled, tok))
+            self.mixed_chained += 1
+        return self._collect_eager(sampled, host, ev)
 
     # ------------------------------------------------------------------ decode lookahead
     def _lookahead_ok(self, sb) -> bool:
@@ -314,7 +423,11 @@ class LLMEngine:
 
     def _apply(self, sb, rows, tokens) -> list[StepOutput]:
         """Commit one executed batch: advance KV cursors, append tokens, stop checks."""
-        now = time.perf_counter()
+        self._advance(sb)
+        return self._commit(rows, tokens)
+
+    def _advance(self, sb) -> None:
+        """The KV-cursor half of applying a step (what scheduling the next step needs)."""
         st = self.stats
         st["steps"] += 1
         st["decode_tokens"] += len(sb.decode)
@@ -323,6 +436,11 @@ class LLMEngine:
             st["prefill_tokens"] += c.length
         for r in sb.decode:
             r.num_computed += 1
+
+    def _commit(self, rows, tokens) -> list[StepOutput]:
+        """The token half: append the sampled tokens, stop checks, finish requests."""
+        now = time.perf_counter()
+        st = self.stats
         outs = []
         eos = self.model_cfg.eos_token_id
         len_cap = self.cfg.max_model_len - 1

@@ -310,6 +310,8 @@ def paged_prefill_ref(q, k_cache, v_cache, block_tables, cu_seqlens_q, context_l
 # each staged K/V tile).  Every producer of ``tiles`` (model runner, EAGLE verify /
 # draft metadata, ops.paged_prefill) cuts sequences at this size.
 PREFILL_TILE = int(os.environ.get("DGI_PREFILL_TILE", "128"))
+# two LDS stages in the prefill attention kernel (one barrier per K/V tile); 0 = the round-4 loop
+PREFILL_DB = int(os.environ.get("DGI_PREFILL_DB", "1"))
 
 
 def prefill_tiles(cu_seqlens_q: list[int], tile: int = 0) -> list[tuple[int, int]]:
@@ -336,7 +338,7 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens,
             tl = prefill_tiles(cu_seqlens_q.tolist())
             tiles = torch.tensor(tl if tl else [[0, 0]], dtype=torch.int32, device=q.device)[: len(tl)]
         _call("paged_prefill", out, q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens,
-              tiles, nh, nkv, scale, tree_mask, tree_n, PREFILL_TILE)
+              tiles, nh, nkv, scale, tree_mask, tree_n, PREFILL_TILE | ((PREFILL_DB & 1) << 16))
         return out
     r = paged_prefill_ref(q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens, nh, nkv, scale,
                           tree_mask, tree_n)

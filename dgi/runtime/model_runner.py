@@ -86,12 +86,16 @@ def decode_rows(reqs: list, bs: int, bt_out: np.ndarray, ahead: int = 0):
     return ids, pos, slots.astype(np.int32), pos + 1
 
 
-def sampling_rows(sampled: list, ahead: int = 0):
-    """(temperature bits, seed, top-k, top-p bits, any filtered) of the sampled rows."""
+def sampling_rows(sampled: list, ahead=0):
+    """(temperature bits, seed, top-k, top-p bits, any filtered) of the sampled rows; ``ahead``
+    (tokens of each row still in flight) is one number or one per row."""
     n = len(sampled)
     nf = [r.params.needs_filter for r in sampled]
     temps = np.fromiter((r.params.temperature for r in sampled), np.float32, n).view(np.int32)
-    seeds = np.fromiter((r.sample_seed(ahead) for r in sampled), np.int64, n).astype(np.int32)
+    if isinstance(ahead, int):
+        seeds = np.fromiter((r.sample_seed(ahead) for r in sampled), np.int64, n).astype(np.int32)
+    else:
+        seeds = np.fromiter((r.sample_seed(a) for r, a in zip(sampled, ahead)), np.int64, n).astype(np.int32)
     topk = np.fromiter((max(0, r.params.top_k) if f else 0 for r, f in zip(sampled, nf)), np.int32, n)
     topp = np.fromiter((r.params.top_p if f else 1.0 for r, f in zip(sampled, nf)), np.float32, n).view(np.int32)
     return temps, seeds, topk, topp, any(nf)
@@ -168,10 +172,11 @@ class ModelRunner:
                 "filt": bool((samp[2] > 0).any() or (samp[3].view(np.float32) < 1.0).any())}
 
     def build_host(self, sb: ScheduledBatch, pad_decode_to: int = 0, dec_pre: Optional[dict] = None,
-                   pre_ids: Optional[np.ndarray] = None):
+                   pre_ids: Optional[np.ndarray] = None, seed_ahead=None):
         """Pack one step's metadata into a flat int32 array + int64 header.  ``dec_pre``
         (``prebuild_decode``) holds the first decode rows' metadata, built ahead; their input
-        tokens are ``pre_ids``."""
+        tokens are ``pre_ids``.  ``seed_ahead``: per sampled row, tokens still in flight (a
+        step scheduled before the previous step's tokens are applied)."""
         bs = self.bs
         nd = len(sb.decode)
         ndp = max(nd, pad_decode_to)
@@ -227,7 +232,7 @@ class ModelRunner:
             temps, seeds, topk, topp = (np.concatenate([a, b]) for a, b in zip(dec_pre["samp"], rest[:4]))
             filt = dec_pre["filt"] or rest[4]
         else:
-            temps, seeds, topk, topp, filt = sampling_rows(sampled)
+            temps, seeds, topk, topp, filt = sampling_rows(sampled, 0 if seed_ahead is None else seed_ahead)
         parts = [ids, pos, slots, dec_bt.ravel(), dec_ctx, pre_bt.ravel(), cu, pctx, tiles_np.ravel(), lidx,
                  temps, seeds, topk, topp]
         flat = np.concatenate(parts)

@@ -220,9 +220,12 @@ class Scheduler:
         self.running.append(req)
 
     def schedule(self, max_seqs: Optional[int] = None, max_tokens: Optional[int] = None,
-                 allow_prefill: bool = True) -> ScheduledBatch:
+                 allow_prefill: bool = True, preempt: bool = True) -> ScheduledBatch:
         """Form one batch.  ``max_seqs``/``max_tokens`` bound a pipeline
-        microbatch; requests already in flight (``busy``) are skipped."""
+        microbatch; requests already in flight (``busy``) are skipped.  ``preempt``
+        False: a decode row whose next page cannot be allocated waits for a later step
+        instead of preempting another sequence (a step scheduled while the previous one
+        is still in flight must not release pages that step is using)."""
         budget = self.cfg.max_num_batched_tokens if max_tokens is None else max_tokens
         seq_cap = max_seqs if max_seqs is not None else 1 << 30
         decode: list[Request] = []
@@ -248,6 +251,8 @@ class Scheduler:
                     self._grow(req, pos + 1)
                     break
                 except OutOfBlocks:
+                    if not preempt:
+                        break
                     victim = next((r for r in reversed(self.running._d) if not r.busy), None)
                     if victim is None:
                         break

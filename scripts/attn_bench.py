@@ -49,7 +49,7 @@ def prefill(B, L):
     kd = torch.randn(B, nh, L, hd, device=dev, dtype=torch.bfloat16)
     vd = torch.randn_like(kd)
     us_sdpa = timed(lambda: F.scaled_dot_product_attention(qd, kd, vd, is_causal=True))
-    return {"kernel": "prefill", "B": B, "L": L, "tile": ops.PREFILL_TILE, "us": round(us, 1),
+    return {"kernel": "prefill", "B": B, "L": L, "tile": ops.PREFILL_TILE, "db": ops.PREFILL_DB, "us": round(us, 1),
             "TFLOPs": round(flops / us / 1e6, 1),
             "sdpa_us": round(us_sdpa, 1), "sdpa_TFLOPs": round(flops / us_sdpa / 1e6, 1)}
 
@@ -74,9 +74,10 @@ def decode(B, C):
 
 if __name__ == "__main__":
     for tile in [int(t) for t in os.environ.get("ATTN_TILES", "128").split(",")]:
-        ops.PREFILL_TILE = tile
-        for B, L in [(1, 512), (3, 512), (8, 512), (4, 2048), (1, 8192)]:
-            print(json.dumps(prefill(B, L)), flush=True)
+        for db in [int(d) for d in os.environ.get("ATTN_DB", str(ops.PREFILL_DB)).split(",")]:
+            ops.PREFILL_TILE, ops.PREFILL_DB = tile, db
+            for B, L in [(1, 512), (3, 512), (8, 512), (4, 2048), (1, 8192)]:
+                print(json.dumps(prefill(B, L)), flush=True)
     if os.environ.get("ATTN_PREFILL_ONLY"):
         sys.exit(0)
     for B, C in [(1, 1024), (64, 1024), (256, 640), (384, 640), (512, 2048), (32, 8192)]:

@@ -137,7 +137,10 @@ def _paged_decode_case(nh, nkv, hd, ctx_lens, bs=16):
                                        (14, 2, 64)])
 @pytest.mark.parametrize("qlens,ctxs", [([5], [5]), ([130, 1, 64], [130, 40, 600]), ([512], [512]),
                                         ([300, 77], [1000, 77])])
-def test_paged_prefill(nh, nkv, hd, qlens, ctxs):
+@pytest.mark.parametrize("tile,db", [(128, 1), (128, 0), (256, 1)])
+def test_paged_prefill(nh, nkv, hd, qlens, ctxs, tile, db, monkeypatch):
+    monkeypatch.setattr(ops, "PREFILL_TILE", tile)
+    monkeypatch.setattr(ops, "PREFILL_DB", db)
     bs = 16
     maxw = 80
     nblocks = sum((c + bs - 1) // bs for c in ctxs) + 4
@@ -792,3 +795,48 @@ def _cpu_decode_row(model, kv, blocks, ctx, tok):
         x = (torch.nn.functional.silu(gu[:, :I]) * gu[:, I:]) @ L.down.float().t()
     h = ops.rmsnorm_ref(x + res, model.norm.float(), c.rms_eps)
     return (h @ model.lm_head.float().t())[0]
+
+
+@pytest.mark.parametrize("sampled,eos", [(False, False), (True, False), (False, True)])
+def test_mixed_step_lookahead_matches_plain_steps(sampled, eos):
+    """Mixed-step lookahead (step N+1 scheduled and launched before step N's tokens are back,
+    its input tokens read on the device): staggered arrivals, chunked prefill across steps,
+    length stops at different steps, seeded sampling and an EOS stop that lands while the
+    next step is in flight give exactly the outputs of plain steps; the chain really ran."""
+    from dgi.engine import EngineConfig, LLMEngine
+    from dgi.models.config import get_config
+    from dgi.models.llama import LlamaModel
+    from dgi.sched.request import SamplingParams
+    mc = get_config("llama-tiny-hd128")
+    src = LlamaModel(mc, "cuda", seed=13)
+    g = torch.Generator().manual_seed(2)
+    prompts = [torch.randint(5, 900, (n,), generator=g).tolist() for n in (40, 75, 9, 130, 22, 61)]
+
+    def sp(i, eos_ok):
+        return SamplingParams(max_tokens=7 + 3 * i, temperature=0.8 if sampled else 0.0, top_k=20 if sampled else 0,
+                              seed=50 + i, ignore_eos=not eos_ok)
+
+    def run(mixed, eos_tok=None):
+        cfg = EngineConfig(model="llama-tiny-hd128", device="cuda", num_blocks=256, max_num_seqs=8, max_model_len=512,
+                           max_num_batched_tokens=64, use_graphs=True, enable_prefix_caching=False)
+        e = LLMEngine(cfg, model_cfg=get_config("llama-tiny-hd128"), model=src)
+        e.mixed_lookahead = mixed
+        if eos_tok is not None:
+            e.model_cfg.eos_token_id = eos_tok
+        reqs = []
+        for i, p in enumerate(prompts):
+            reqs.append(e.add_request(p, sp(i, eos_tok is not None)))
+            e.step()
+        while e.has_unfinished():
+            e.step()
+        assert e._mx is None and e.pool.num_free == 255
+        return [r.output for r in reqs], [r.finish_reason for r in reqs], e.mixed_chained
+
+    plain, pf, n0 = run(False)
+    la, lf, n1 = run(True)
+    assert la == plain and lf == pf and n0 == 0 and n1 > 0
+    if eos:
+        tok = plain[3][4]
+        p2, f2, _ = run(False, tok)
+        l2, g2, _ = run(True, tok)
+        assert l2 == p2 and g2 == f2 and "stop" in f2
