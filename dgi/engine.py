@@ -193,7 +193,14 @@ class LLMEngine:
     def admission_limit(self) -> Optional[int]:
         """Sequences this engine keeps in flight (running + one step of queued prompts)
         without missing its TPOT SLO; None without an SLO or before it has measured
-        enough.  A closed-loop client sizes its concurrency to it."""
+        enough.  A closed-loop client sizes its concurrency to it.
+
+        The queued part is counted from the sequences running NOW, not from the
+        steady-state cap: under the SLO the prefill rate is a fixed number of prompts
+        per step, so while the running set ramps up (or after a burst of finishes)
+        anything queued beyond one step's prompts only waits — its TTFT grows by a
+        step per step's worth of prompts ahead of it (round 5: 15 queued behind a
+        1.6-prompt step = 827 ms p50 TTFT at SLO 120)."""
         sbud = self.step_budget
         if sbud is None:
             return None
@@ -204,7 +211,7 @@ class LLMEngine:
         queued = max(1, int((rows - rows * (sbud.output_avg or 0) / max(1.0, (sbud.prompt_avg or 0) +
                                                                          (sbud.output_avg or 0)))
                             / max(1.0, sbud.prompt_avg or 1.0)))
-        return cap + queued
+        return min(cap, len(self.scheduler.running)) + queued
 
     def has_unfinished(self) -> bool:
         return self._la is not None or self._mx is not None or self.scheduler.has_work()

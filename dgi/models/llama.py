@@ -54,6 +54,11 @@ ATTN_OVERLAP = os.environ.get("DGI_ATTN_OVERLAP", "1") == "1"
 # CU (32 CUs ran it 3.1x slower than 256, not 8x) and the half-size GEMMs beside it ran 1.85x
 # slower than their share; DGI_TBO=1 turns it on for experiments.
 TBO = os.environ.get("DGI_TBO", "0") == "1"
+# steps of <= 16 rows that carry prefill tokens (an EAGLE tree verify: N tree nodes per sequence
+# under a tree mask) take the fused decode layers too — the qkv / gate_up kernels are per-row
+# (norm prologue, RoPE + paged-KV epilogue at each row's own position / slot) and the attention
+# dispatch already splits decode and prefill rows; 5 kernels per layer instead of 9
+FUSED_SMALL_PREFILL = os.environ.get("DGI_FUSED_SMALL_PREFILL", "1") == "1"
 TBO_MIN_ROWS = int(os.environ.get("DGI_TBO_MIN_ROWS", "512"))
 TBO_SIDE_PER_XCD = int(os.environ.get("DGI_TBO_SIDE", "4"))
 
@@ -317,11 +322,11 @@ class LlamaModel:
 
     def _fused_decode(self, h: torch.Tensor, meta: AttnMeta) -> tuple:
         """(fuse qkv, fuse gate_up) for this step; (False, False) = unfused layers."""
-        if meta.num_prefill_tokens != 0:
+        T, H = h.shape[0], self.cfg.hidden_size
+        if meta.num_prefill_tokens != 0 and not (FUSED_SMALL_PREFILL and T <= 16):
             return False, False
         if not ((h.is_cuda and h.dtype == torch.bfloat16) or self.force_fused):
             return False, False
-        T, H = h.shape[0], self.cfg.hidden_size
         # force_fused: run the fused composition through the reference ops on CPU (tests)
         if self.force_fused:
             return True, True

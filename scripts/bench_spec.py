@@ -70,6 +70,8 @@ def main():
     ap.add_argument("--draft-vocab", type=int, default=0,
                     help="EAGLE-3 draft vocabulary: the N token ids the target chose most often in the draft's "
                          "training corpus (0 = the whole vocabulary)")
+    ap.add_argument("--save-draft", default=None, help="write the trained draft (torch.save, tensors only)")
+    ap.add_argument("--load-draft", default=None, help="skip training: load a draft --save-draft wrote for this target")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     cfg = EngineConfig(model=a.model, device="cuda", max_num_seqs=64, max_num_batched_tokens=8192,
@@ -81,9 +83,18 @@ def main():
         perm = torch.randperm(m.embed.shape[0], generator=torch.Generator().manual_seed(7)).to(m.embed.device)
         m.lm_head.copy_(m.embed.index_select(0, perm) / m.cfg.hidden_size ** 0.5)
     t0 = time.perf_counter()
-    info = train_draft(spec, steps=a.train_steps, batch=16, prompt_len=64, gen_len=192, num_seqs=a.train_seqs,
-                       random_seqs=a.random_seqs, log=lambda m: print(m, flush=True), draft_vocab=a.draft_vocab)
+    if a.load_draft:
+        blob = torch.load(a.load_draft, map_location=spec.device, weights_only=True)
+        spec.draft.load(blob["params"])
+        spec.draft.set_hot_vocab(blob.get("hot"))
+        info = dict(blob["info"], loaded_from=a.load_draft)
+    else:
+        info = train_draft(spec, steps=a.train_steps, batch=16, prompt_len=64, gen_len=192, num_seqs=a.train_seqs,
+                           random_seqs=a.random_seqs, log=lambda m: print(m, flush=True), draft_vocab=a.draft_vocab)
     info["train_seconds"] = round(time.perf_counter() - t0, 1)
+    if a.save_draft:
+        torch.save({"params": {k: v.detach() for k, v in spec.draft.parameters().items()},
+                    "hot": spec.draft.hot, "info": info}, a.save_draft)
     print("draft training", info, flush=True)
     base = LLMEngine(cfg, model=spec.model)
     base.warmup()

@@ -208,6 +208,44 @@ def test_fused_decode_layers_match_unfused_on_cpu():
             torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
 
 
+def test_fused_layers_take_small_prefill_steps(monkeypatch):
+    """Steps of <= 16 rows with prefill tokens (short prompts, an EAGLE tree verify) run
+    the fused decode layers (per-row norm / RoPE / KV-write epilogues, attention split into
+    decode and prefill rows) and produce the unfused model's logits; larger prefill steps
+    stay unfused."""
+    import dgi.models.llama as llama
+    from dgi.engine import EngineConfig, LLMEngine
+    from dgi.models.config import get_config
+    from dgi.models.llama import LlamaModel
+    from dgi.sched.request import SamplingParams
+    mc = get_config("llama-tiny-hd128")
+    res = {}
+    for flag in (False, True):
+        monkeypatch.setattr(llama, "FUSED_SMALL_PREFILL", flag)
+        m = LlamaModel(mc, "cpu", torch.float32, seed=11)
+        m.force_fused = flag
+        rows = []
+        real = m._forward_layers_fused
+        m._forward_layers_fused = lambda h, meta, *a, real=real, rows=rows: (
+            rows.append((h.shape[0], meta.num_prefill_tokens)) or real(h, meta, *a))
+        e = LLMEngine(EngineConfig(model="llama-tiny-hd128", device="cpu", dtype=torch.float32, num_blocks=64,
+                                   max_num_seqs=4, max_model_len=256, max_num_batched_tokens=16, use_graphs=False,
+                                   enable_prefix_caching=False), model_cfg=mc, model=m)
+        got = []
+        orig = m.compute_logits
+        m.compute_logits = lambda h, r, idx, orig=orig, got=got: got.append(orig(h, r, idx).detach().clone()) or got[-1]
+        reqs = e.generate([[1, 5, 9, 300, 17], [1, 2, 3], list(range(7, 47))],
+                          SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True))
+        res[flag] = ([r.output for r in reqs], got, rows)
+    outs0, logits0, rows0 = res[False]
+    outs1, logits1, rows1 = res[True]
+    assert not rows0
+    assert any(p > 0 for t, p in rows1)        # chunked prefill steps of <= 16 rows went fused
+    assert outs0 == outs1
+    for a, b in zip(logits0, logits1):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
+
+
 def test_mlp_pad_table_picks_cheapest_rows_and_reports_impl():
     from dgi.runtime.gemm_pad import MlpPadTable
     grid = [512, 544, 576, 608]
