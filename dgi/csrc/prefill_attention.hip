@@ -46,6 +46,8 @@ __device__ __forceinline__ int v_off(int row, int ch) {
 }
 
 constexpr int KT = 64;  // keys per tile
+// buffer resource word 3 of a raw (stride 0, byte-addressed) buffer on gfx9
+constexpr int kRsrcWord3 = 0x00020000;
 
 // NW waves x 32 query rows per workgroup (one K/V tile staging shared by all of them):
 // NW = 4 -> 128-row tiles, 2 workgroups per CU; NW = 8 -> 256-row tiles, 1 per CU
@@ -102,6 +104,12 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void prefill_attn_kernel(
 #pragma unroll
     for (int s = 0; s < NS; ++s)
       qf[s] = row_valid ? *reinterpret_cast<const u32x4*>(qp + 16 * s + 8 * hh) : u32x4{0, 0, 0, 0};
+    // Q lands before any K/V load is issued.  Without this wait the compiler's waitcnt pass
+    // merges "Q pending" from the preheader into the loop header and, to reach the older Q
+    // loads, emits vmcnt(0) before the first QK^T MFMA of EVERY tile — which also waits for
+    // the K/V loads of tile i+2 issued a few instructions earlier: one full HBM round trip
+    // per tile and no load/compute overlap at all (round 5 disassembly).
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), expcnt / lgkmcnt untouched (gfx9 encoding)
   }
 
   const int last_row = min(t0 + 32 * NW, qlen) - 1;
@@ -141,10 +149,50 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void prefill_attn_kernel(
       *reinterpret_cast<u32x4*>(vst + v_off<HD>(row, ch)) = vr[p];
     }
   };
-  if (kv_end > 0) load_tile(0);
+  // Full tiles of 16-token pages (the engine's page size): the rows one wave stages in one
+  // pass lie in ONE page (a wave covers 64 / CH consecutive rows, 4 or 8, and passes are
+  // whole pages apart), so that page's block id is a wave-uniform scalar load and every
+  // lane's offset inside the page is a constant — no per-lane block-table gather and no
+  // 64-bit address arithmetic per load (the decode kernel's page16 path, round 4).
+  constexpr int RP = NT / CH;                  // tile rows per staging pass (16, 32 or 64)
+  static_assert(RP % 16 == 0 && 16 % (64 / CH) == 0, "passes are whole pages");
+  const int wsub = __builtin_amdgcn_readfirstlane(w) * (64 / CH);   // first row of this wave in a pass
+  const int lane_off = ((wsub & 15) + lane / CH) * HD + (lane % CH) * 8;
+  const int wpage = wsub >> 4;
+  const bool page16 = bs_log2 == 4;
+  // Block ids of a fast tile are fetched one iteration before its loads are issued (DB), with
+  // VECTOR loads: a scalar load shares lgkmcnt with the LDS reads (and returns out of order),
+  // so the compiler waits lgkmcnt(0) for it at the next LDS use; a vector load is counted in
+  // order with the K/V loads and has landed by the time the ids are read (readfirstlane).
+  const __amdgpu_buffer_rsrc_t bt_rs = __builtin_amdgcn_make_buffer_rsrc((void*)bt, 0, bt_stride * 4, kRsrcWord3);
+  int nbt[NP];
+  auto fast = [&](int kb0) { return page16 && kb0 + KT <= kv_end; };
+  auto fetch_bt = [&](int kb0) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+      nbt[p] = (int)__builtin_amdgcn_raw_buffer_load_b32(bt_rs, ((kb0 >> 4) + p * (RP / 16) + wpage) * 4, 0, 0);
+  };
+  auto load_tile_fast = [&]() {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const size_t base = ((size_t)__builtin_amdgcn_readfirstlane(nbt[p]) * nkv + kvh) * head_stride;
+      kr[p] = *reinterpret_cast<const u32x4*>(k_cache + base + lane_off);
+      vr[p] = *reinterpret_cast<const u32x4*>(v_cache + base + lane_off);
+    }
+  };
+  auto load_any = [&](int kb0) {
+    if (fast(kb0)) {
+      fetch_bt(kb0);
+      load_tile_fast();
+    } else {
+      load_tile(kb0);
+    }
+  };
+  if (kv_end > 0) load_any(0);
   if (DB && kv_end > 0) {
     store_tile(lds, lds + KT * HD);             // stage 0 <- tile 0
-    if (KT < kv_end) load_tile(KT);             // registers <- tile 1
+    if (KT < kv_end) load_any(KT);              // registers <- tile 1
+    if (fast(2 * KT)) fetch_bt(2 * KT);         // block ids of tile 2
   }
   // last key this wave can see (causal); tiles beyond it are skipped
   const int wave_last_pos = pos_base + min(t0 + 32 * w + 31, qlen - 1);
@@ -165,7 +213,10 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void prefill_attn_kernel(
       if (kb0 + KT < kv_end) {
         uint16_t* kn = lds + ((it + 1) & 1) * 2 * KT * HD;
         store_tile(kn, kn + KT * HD);           // tile it+1, loaded during the previous iteration
-        if (kb0 + 2 * KT < kv_end) load_tile(kb0 + 2 * KT);
+        if (kb0 + 2 * KT < kv_end) {
+          if (fast(kb0 + 2 * KT)) load_tile_fast();   // block ids fetched last iteration
+          else load_tile(kb0 + 2 * KT);
+        }
       }
     } else {
       ks = lds;
@@ -173,11 +224,17 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void prefill_attn_kernel(
       __syncthreads();  // previous tile fully consumed
       store_tile(ks, vs);
       __syncthreads();
-      if (kb0 + KT < kv_end) load_tile(kb0 + KT);
+      if (kb0 + KT < kv_end) load_any(kb0 + KT);
     }
     // whole tile above this wave's diagonal, or no valid query row in this wave
     // (it still stages K/V for the others)
-    if (kb0 > wave_last_pos || !wave_rows) continue;
+    // the next tile's block ids: issued after this tile's QK^T MFMAs, where the softmax
+    // (VALU only) covers the scalar load before the next LDS wait (SMEM and LDS share lgkmcnt)
+    const bool fetch_next = DB && kb0 + 2 * KT < kv_end && fast(kb0 + 3 * KT);
+    if (kb0 > wave_last_pos || !wave_rows) {
+      if (fetch_next) fetch_bt(kb0 + 3 * KT);
+      continue;
+    }
 
     // ---- S^T = K Q^T for two 32-key blocks
     f32x16 sc[2];
@@ -191,6 +248,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void prefill_attn_kernel(
         sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a), as_bf16x8(qf[s]), sc[kb], 0, 0, 0);
       }
     }
+    if (fetch_next) fetch_bt(kb0 + 3 * KT);
     // ---- online softmax; lane owns query lr, keys kb0 + 32kb + (r&3) + 8(r>>2) + 4hh.
     // Interior tiles (every key visible to every row of this wave, no tree
     // rows) skip the per-element mask entirely.
