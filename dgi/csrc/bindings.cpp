@@ -41,6 +41,9 @@ int dgi_topkp_threshold(const void* logits, int is_bf16, int B, int V, int strid
                         const long long* top_k, const float* top_p, float* thresh, hipStream_t s);
 int dgi_topk(const void* logits, int is_bf16, int B, int V, int stride, int K, float* out_v,
              long long* out_i, hipStream_t s);
+int dgi_topk_logprobs_ws_floats(int B, int V);
+int dgi_topk_logprobs(const void* logits, int B, int V, int stride, int K, float* ws, float* out_v,
+                      long long* out_i, hipStream_t s);
 int dgi_kv_gather(const void* cache, const int* ids, int n, int LK, int num_blocks, int page_elems,
                   void* buf, hipStream_t s);
 int dgi_kv_scatter(void* cache, const int* ids, int n, int LK, int num_blocks, int page_elems,
@@ -370,6 +373,20 @@ void topk(at::Tensor out_v, at::Tensor out_i, const at::Tensor& logits, int64_t 
            "topk");
 }
 
+// top-k of log_softmax(logits) (bf16 logits, fp32 log-probs of the k winners)
+void topk_logprobs(at::Tensor out_v, at::Tensor out_i, const at::Tensor& logits, int64_t k) {
+  check_dev(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1 && logits.scalar_type() == at::kBFloat16);
+  const int B = (int)logits.size(0), V = (int)logits.size(1);
+  TORCH_CHECK(out_v.scalar_type() == at::kFloat && out_i.scalar_type() == at::kLong);
+  TORCH_CHECK(out_v.numel() >= B * k && out_i.numel() >= B * k && out_v.is_contiguous() && out_i.is_contiguous());
+  at::Tensor ws = at::empty({std::max(1, dgi_topk_logprobs_ws_floats(B, V))}, logits.options().dtype(at::kFloat));
+  check_rc(dgi_topk_logprobs(logits.data_ptr(), B, V, (int)logits.stride(0), (int)k, ws.data_ptr<float>(),
+                             out_v.data_ptr<float>(), reinterpret_cast<long long*>(out_i.data_ptr<int64_t>()),
+                             cur_stream()),
+           "topk_logprobs");
+}
+
 // cache: [L, 2, NB, nkv, bs, hd]; buf: [L, 2, n, nkv, bs, hd]
 void kv_gather(at::Tensor buf, const at::Tensor& cache, const at::Tensor& ids) {
   check_dev(cache, "cache"); check_i32(ids, "ids");
@@ -463,6 +480,7 @@ TORCH_LIBRARY(dgi, m) {
   m.def("topkp_threshold(Tensor(a!) thresh, Tensor logits, Tensor temperature, Tensor top_k, "
         "Tensor top_p) -> ()");
   m.def("topk(Tensor(a!) out_v, Tensor(b!) out_i, Tensor logits, int k) -> ()");
+  m.def("topk_logprobs(Tensor(a!) out_v, Tensor(b!) out_i, Tensor logits, int k) -> ()");
   m.def("kv_gather(Tensor(a!) buf, Tensor cache, Tensor ids) -> ()");
   m.def("kv_scatter(Tensor(a!) cache, Tensor ids, Tensor buf) -> ()");
   m.def("kv_copy(Tensor(a!) cache, Tensor src, Tensor dst) -> ()");
@@ -483,6 +501,7 @@ TORCH_LIBRARY_IMPL(dgi, CUDA, m) {
   m.impl("fused_skinny", &fused_skinny);
   m.impl("sample", &sample);
   m.impl("topk", &topk);
+  m.impl("topk_logprobs", &topk_logprobs);
   m.impl("topkp_threshold", &topkp_threshold);
   m.impl("kv_gather", &kv_gather);
   m.impl("kv_scatter", &kv_scatter);

@@ -46,8 +46,6 @@ __device__ __forceinline__ int v_off(int row, int ch) {
 }
 
 constexpr int KT = 64;  // keys per tile
-// buffer resource word 3 of a raw (stride 0, byte-addressed) buffer on gfx9
-constexpr int kRsrcWord3 = 0x00020000;
 
 // NW waves x 32 query rows per workgroup (one K/V tile staging shared by all of them):
 // NW = 4 -> 128-row tiles, 2 workgroups per CU; NW = 8 -> 256-row tiles, 1 per CU
@@ -160,22 +158,20 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void prefill_attn_kernel(
   const int lane_off = ((wsub & 15) + lane / CH) * HD + (lane % CH) * 8;
   const int wpage = wsub >> 4;
   const bool page16 = bs_log2 == 4;
-  // Block ids of a fast tile are fetched one iteration before its loads are issued (DB), with
-  // VECTOR loads: a scalar load shares lgkmcnt with the LDS reads (and returns out of order),
-  // so the compiler waits lgkmcnt(0) for it at the next LDS use; a vector load is counted in
-  // order with the K/V loads and has landed by the time the ids are read (readfirstlane).
-  const __amdgpu_buffer_rsrc_t bt_rs = __builtin_amdgcn_make_buffer_rsrc((void*)bt, 0, bt_stride * 4, kRsrcWord3);
+  // Block ids of a fast tile: wave-uniform scalar loads (s_load), issued at the top of the
+  // iteration that issues the tile's K/V loads so their latency overlaps the LDS stores.  (A
+  // vector-load prefetch one iteration ahead was tried: vmcnt is in-order, so waiting for it
+  // waited for the K/V loads issued after it — the stall the prefetch was meant to remove.)
   int nbt[NP];
   auto fast = [&](int kb0) { return page16 && kb0 + KT <= kv_end; };
   auto fetch_bt = [&](int kb0) {
 #pragma unroll
-    for (int p = 0; p < NP; ++p)
-      nbt[p] = (int)__builtin_amdgcn_raw_buffer_load_b32(bt_rs, ((kb0 >> 4) + p * (RP / 16) + wpage) * 4, 0, 0);
+    for (int p = 0; p < NP; ++p) nbt[p] = bt[(kb0 >> 4) + p * (RP / 16) + wpage];
   };
   auto load_tile_fast = [&]() {
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
-      const size_t base = ((size_t)__builtin_amdgcn_readfirstlane(nbt[p]) * nkv + kvh) * head_stride;
+      const size_t base = ((size_t)nbt[p] * nkv + kvh) * head_stride;
       kr[p] = *reinterpret_cast<const u32x4*>(k_cache + base + lane_off);
       vr[p] = *reinterpret_cast<const u32x4*>(v_cache + base + lane_off);
     }
@@ -192,7 +188,6 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void prefill_attn_kernel(
   if (DB && kv_end > 0) {
     store_tile(lds, lds + KT * HD);             // stage 0 <- tile 0
     if (KT < kv_end) load_any(KT);              // registers <- tile 1
-    if (fast(2 * KT)) fetch_bt(2 * KT);         // block ids of tile 2
   }
   // last key this wave can see (causal); tiles beyond it are skipped
   const int wave_last_pos = pos_base + min(t0 + 32 * w + 31, qlen - 1);
@@ -211,12 +206,13 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void prefill_attn_kernel(
       ks = lds + (it & 1) * 2 * KT * HD;
       vs = ks + KT * HD;
       if (kb0 + KT < kv_end) {
+        const bool nxt = kb0 + 2 * KT < kv_end;
+        const bool nfast = nxt && fast(kb0 + 2 * KT);
+        if (nfast) fetch_bt(kb0 + 2 * KT);
         uint16_t* kn = lds + ((it + 1) & 1) * 2 * KT * HD;
         store_tile(kn, kn + KT * HD);           // tile it+1, loaded during the previous iteration
-        if (kb0 + 2 * KT < kv_end) {
-          if (fast(kb0 + 2 * KT)) load_tile_fast();   // block ids fetched last iteration
-          else load_tile(kb0 + 2 * KT);
-        }
+        if (nfast) load_tile_fast();
+        else if (nxt) load_tile(kb0 + 2 * KT);
       }
     } else {
       ks = lds;
@@ -228,13 +224,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void prefill_attn_kernel(
     }
     // whole tile above this wave's diagonal, or no valid query row in this wave
     // (it still stages K/V for the others)
-    // the next tile's block ids: issued after this tile's QK^T MFMAs, where the softmax
-    // (VALU only) covers the scalar load before the next LDS wait (SMEM and LDS share lgkmcnt)
-    const bool fetch_next = DB && kb0 + 2 * KT < kv_end && fast(kb0 + 3 * KT);
-    if (kb0 > wave_last_pos || !wave_rows) {
-      if (fetch_next) fetch_bt(kb0 + 3 * KT);
-      continue;
-    }
+    if (kb0 > wave_last_pos || !wave_rows) continue;
 
     // ---- S^T = K Q^T for two 32-key blocks
     f32x16 sc[2];
@@ -248,31 +238,43 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void prefill_attn_kernel(
         sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a), as_bf16x8(qf[s]), sc[kb], 0, 0, 0);
       }
     }
-    if (fetch_next) fetch_bt(kb0 + 3 * KT);
     // ---- online softmax; lane owns query lr, keys kb0 + 32kb + (r&3) + 8(r>>2) + 4hh.
-    // Interior tiles (every key visible to every row of this wave, no tree
-    // rows) skip the per-element mask entirely.
+    // Interior tiles (every key visible to every row of this wave, no tree rows) skip the
+    // per-element mask; both kinds then share one exponent path.
     const bool interior = (kb0 + KT <= kv_end) && (kb0 + KT - 1 <= wave_first_pos) && !wave_tree;
-    float mx = -1e30f;
-    if (interior) {
+    if (!interior) {
+      // masked keys -> -inf in raw score units, in place (one select per element, no branches:
+      // the tree bit is read with a clamped shift and applied by mask).  -inf, not a large
+      // finite value: a lane whose keys are all masked must get max -inf (no rescale) and
+      // P = 2^(-inf) = 0, whatever the scale.  Causal-only tiles (the diagonal) skip the
+      // 64-bit tree-mask shifts.
+      const int lim = row_valid ? min(my_pos, kv_end - 1) : -1;    // last visible key
+      const int key0 = kb0 + 4 * hh;
+      if (wave_tree) {
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+        for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[kb][r]);
-      mx = row_valid ? mx * scale_log2 : -1e30f;
-    } else {
+          for (int r = 0; r < 16; ++r) {
+            const int key = key0 + 32 * kb + (r & 3) + 8 * (r >> 2);
+            const int dt = key - tree_key0;
+            const bool tbit = (tmask >> (dt & 63)) & 1ull;
+            const bool ok = (key <= lim) & (!is_tree | (dt < 0) | tbit);
+            sc[kb][r] = ok ? sc[kb][r] : -__builtin_inff();
+          }
+      } else {
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+        for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = kb0 + 32 * kb + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          bool ok = row_valid && key <= my_pos && key < kv_end;
-          if (is_tree && key >= tree_key0) ok = ok && ((tmask >> (key - tree_key0)) & 1ull);
-          const float x = ok ? sc[kb][r] * scale_log2 : -1e30f;
-          sc[kb][r] = x;
-          mx = fmaxf(mx, x);
-        }
+          for (int r = 0; r < 16; ++r)
+            sc[kb][r] = (key0 + 32 * kb + (r & 3) + 8 * (r >> 2) <= lim) ? sc[kb][r] : -__builtin_inff();
+      }
     }
+    float mx = -1e30f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[kb][r]);
+    mx = row_valid ? mx * scale_log2 : -1e30f;
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     // deferred max: rescale O / l only when the running max grows by > 2^8, so
     // most tiles skip the 64 O multiplies (P stays <= 256, safe in f32 / bf16)
@@ -284,28 +286,30 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void prefill_attn_kernel(
       for (int d = 0; d < ND; ++d) o[d] *= alpha;
       m_run = m_new;
     }
-    // raw v_exp_f32 (arguments <= 8; masked scores underflow to 0) and four partial row
-    // sums instead of one 32-long dependent add chain
-    float ps[4] = {0.f, 0.f, 0.f, 0.f};
-    if (interior) {
-      const float nm = -m_run;
+    // P = 2^(s * scale_log2 - m): packed fp32 (v_pk_fma_f32 / v_pk_add_f32), two scores per
+    // VALU issue for the scale and the row sums; raw v_exp_f32 (arguments <= 8; masked scores
+    // underflow to 0); four partial row sums instead of one 32-long dependent add chain
+    float ps[4];
+    {
+      const f32x2v s2 = {scale_log2, scale_log2};
+      const f32x2v n2 = {-m_run, -m_run};
+      f32x2v acc2[2] = {{0.f, 0.f}, {0.f, 0.f}};
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float pv = __builtin_amdgcn_exp2f(fmaf(sc[kb][r], scale_log2, nm));
-          sc[kb][r] = pv;
-          ps[r & 3] += pv;
+        for (int r = 0; r < 16; r += 2) {
+          f32x2v x = {sc[kb][r], sc[kb][r + 1]};
+          x = x * s2 + n2;
+          x[0] = __builtin_amdgcn_exp2f(x[0]);
+          x[1] = __builtin_amdgcn_exp2f(x[1]);
+          sc[kb][r] = x[0];
+          sc[kb][r + 1] = x[1];
+          acc2[(r >> 1) & 1] += x;
         }
-    } else {
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float pv = __builtin_amdgcn_exp2f(sc[kb][r] - m_run);
-          sc[kb][r] = pv;
-          ps[r & 3] += pv;
-        }
+      ps[0] = acc2[0][0];
+      ps[1] = acc2[0][1];
+      ps[2] = acc2[1][0];
+      ps[3] = acc2[1][1];
     }
     float psum = (ps[0] + ps[1]) + (ps[2] + ps[3]);
     psum += __shfl_xor(psum, 32, 64);

@@ -162,6 +162,156 @@ __global__ __launch_bounds__(256) void topk_kernel(const T* __restrict__ logits,
 
 
 // ---------------------------------------------------------------------------
+// Top-k of log_softmax(row) straight from bf16 logits (EAGLE draft expansion), without
+// materialising the fp32 log-probs: log_softmax is monotone, so the top-k indices are the
+// logits' and only the k winners need `v - logsumexp(row)`.
+//
+// Stage 1, grid (C chunks, B rows): each workgroup scans one chunk of a row with 16-byte
+// loads, keeping a per-thread top-k and an online (max, sum of exp) pair, merges them in
+// LDS and writes the chunk's top-k + (max, sum).  Stage 2, one workgroup per row: merges
+// the C x k candidates and the C partial sums.  A 128k-vocab row is 16 workgroups instead
+// of one (round 5 trace: the one-block-per-row kernel plus torch's log_softmax took 222 us
+// per draft depth at 3 rows).  Ties: lower index first (as topk_kernel).
+constexpr int TK_NT = 256;
+constexpr int TK_CHUNK = 8192;   // elements per stage-1 workgroup (multiple of 8 * TK_NT)
+
+__device__ __forceinline__ void tk_insert(float* tv, int* ti, int K, float v, int i) {
+  if (v > tv[K - 1]) {
+    int k = K - 1;
+    while (k > 0 && tv[k - 1] < v) { tv[k] = tv[k - 1]; ti[k] = ti[k - 1]; --k; }
+    tv[k] = v;
+    ti[k] = i;
+  }
+}
+
+// merge the NT per-thread lists in sv / si (16 slots per thread) down to slot 0
+__device__ __forceinline__ void tk_merge(float* sv, int* si, int K) {
+  for (int half = TK_NT / 2; half > 0; half >>= 1) {
+    if ((int)threadIdx.x < half) {
+      const float* a = sv + threadIdx.x * 16;
+      const int* ai = si + threadIdx.x * 16;
+      const float* bv = sv + (threadIdx.x + half) * 16;
+      const int* bi = si + (threadIdx.x + half) * 16;
+      float mv[16];
+      int mi[16];
+      int x = 0, y = 0;
+      for (int k = 0; k < K; ++k) {
+        const bool takea = (a[x] > bv[y]) || (a[x] == bv[y] && ai[x] <= bi[y]);
+        if (takea) { mv[k] = a[x]; mi[k] = ai[x]; ++x; } else { mv[k] = bv[y]; mi[k] = bi[y]; ++y; }
+      }
+      for (int k = 0; k < K; ++k) { sv[threadIdx.x * 16 + k] = mv[k]; si[threadIdx.x * 16 + k] = mi[k]; }
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(TK_NT) void topk_lse_part_kernel(const uint16_t* __restrict__ logits, int V, int stride,
+                                                              int K, float* __restrict__ ws_v, int* __restrict__ ws_i,
+                                                              float* __restrict__ ws_ms) {
+  const int c = blockIdx.x, C = gridDim.x, row = blockIdx.y;
+  const uint16_t* lp = logits + (size_t)row * stride;
+  const int lo = c * TK_CHUNK, hi = min(V, lo + TK_CHUNK);
+  float tv[16];
+  int ti[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) { tv[k] = -INFINITY; ti[k] = 0x7fffffff; }
+  float m = -INFINITY, sum = 0.f;
+  auto take = [&](float v, int i) {
+    if (v > m) {                       // online logsumexp (finite logits; -inf entries add nothing)
+      sum = sum * __expf(m - v) + 1.f;
+      m = v;
+    } else if (v > -INFINITY) {
+      sum += __expf(v - m);
+    }
+    tk_insert(tv, ti, K, v, i);
+  };
+  for (int i = lo + 8 * threadIdx.x; i < hi; i += 8 * TK_NT) {
+    if (i + 8 <= hi) {
+      const u32x4 p = *reinterpret_cast<const u32x4*>(lp + i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        take(__uint_as_float(p[j] << 16), i + 2 * j);
+        take(__uint_as_float(p[j] & 0xffff0000u), i + 2 * j + 1);
+      }
+    } else {
+      for (int j = i; j < hi; ++j) take(bf16_to_f32(lp[j]), j);
+    }
+  }
+  __shared__ float sv[TK_NT * 16];
+  __shared__ int si[TK_NT * 16];
+  __shared__ float sm[TK_NT], ss[TK_NT];
+  for (int k = 0; k < K; ++k) { sv[threadIdx.x * 16 + k] = tv[k]; si[threadIdx.x * 16 + k] = ti[k]; }
+  sm[threadIdx.x] = m;
+  ss[threadIdx.x] = sum;
+  __syncthreads();
+  tk_merge(sv, si, K);
+  const size_t o = ((size_t)row * C + c);
+  if ((int)threadIdx.x < K) {
+    ws_v[o * 16 + threadIdx.x] = sv[threadIdx.x];
+    ws_i[o * 16 + threadIdx.x] = si[threadIdx.x];
+  }
+  if (threadIdx.x == 0) {
+    float M = -INFINITY;
+    for (int t = 0; t < TK_NT; ++t) M = fmaxf(M, sm[t]);
+    float S = 0.f;
+    if (M > -INFINITY)
+      for (int t = 0; t < TK_NT; ++t) S += ss[t] > 0.f ? ss[t] * __expf(sm[t] - M) : 0.f;
+    ws_ms[2 * o] = M;
+    ws_ms[2 * o + 1] = S;
+  }
+}
+
+__global__ __launch_bounds__(TK_NT) void topk_lse_final_kernel(int C, int K, const float* __restrict__ ws_v,
+                                                               const int* __restrict__ ws_i,
+                                                               const float* __restrict__ ws_ms,
+                                                               float* __restrict__ out_v,
+                                                               long long* __restrict__ out_i) {
+  const int row = blockIdx.x;
+  float tv[16];
+  int ti[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) { tv[k] = -INFINITY; ti[k] = 0x7fffffff; }
+  // candidates in (chunk, rank) order: a thread's list stays index-ordered on ties only
+  // within a chunk, so insertion breaks value ties by index explicitly
+  for (int q = threadIdx.x; q < C * K; q += TK_NT) {
+    const int cc = q / K, k = q - cc * K;
+    const size_t o = ((size_t)row * C + cc) * 16 + k;
+    const float v = ws_v[o];
+    const int i = ws_i[o];
+    if (v > tv[K - 1] || (v == tv[K - 1] && i < ti[K - 1])) {
+      int j = K - 1;
+      while (j > 0 && (tv[j - 1] < v || (tv[j - 1] == v && ti[j - 1] > i))) {
+        tv[j] = tv[j - 1];
+        ti[j] = ti[j - 1];
+        --j;
+      }
+      tv[j] = v;
+      ti[j] = i;
+    }
+  }
+  __shared__ float sv[TK_NT * 16];
+  __shared__ int si[TK_NT * 16];
+  __shared__ float s_lse;
+  for (int k = 0; k < K; ++k) { sv[threadIdx.x * 16 + k] = tv[k]; si[threadIdx.x * 16 + k] = ti[k]; }
+  if (threadIdx.x == 0) {
+    float M = -INFINITY;
+    for (int cc = 0; cc < C; ++cc) M = fmaxf(M, ws_ms[2 * ((size_t)row * C + cc)]);
+    float S = 0.f;
+    for (int cc = 0; cc < C; ++cc) {
+      const float mc = ws_ms[2 * ((size_t)row * C + cc)], sc = ws_ms[2 * ((size_t)row * C + cc) + 1];
+      if (sc > 0.f) S += sc * __expf(mc - M);
+    }
+    s_lse = M + __logf(S);
+  }
+  __syncthreads();
+  tk_merge(sv, si, K);
+  if ((int)threadIdx.x < K) {
+    out_v[(size_t)row * K + threadIdx.x] = sv[threadIdx.x] - s_lse;
+    out_i[(size_t)row * K + threadIdx.x] = si[threadIdx.x];
+  }
+}
+
+// ---------------------------------------------------------------------------
 // top-k / top-p (nucleus) cut as one logit threshold per row.
 //
 // With u > t "strictly greater", an element v is kept iff
@@ -353,6 +503,28 @@ extern "C" int dgi_topk(const void* logits, int is_bf16, int B, int V, int strid
     topk_kernel<uint16_t><<<B, 256, 0, s>>>((const uint16_t*)logits, V, stride, K, out_v, out_i);
   else
     topk_kernel<float><<<B, 256, 0, s>>>((const float*)logits, V, stride, K, out_v, out_i);
+  DGI_CHECK_LAUNCH();
+  return 0;
+}
+
+// workspace: (B * C * 16) floats + (B * C * 16) ints + (B * C * 2) floats, C = ceil(V / TK_CHUNK)
+extern "C" int dgi_topk_logprobs_ws_floats(int B, int V) {
+  const int C = (V + TK_CHUNK - 1) / TK_CHUNK;
+  return B * C * (16 + 16 + 2);
+}
+
+extern "C" int dgi_topk_logprobs(const void* logits, int B, int V, int stride, int K, float* ws, float* out_v,
+                                 long long* out_i, hipStream_t s) {
+  if (B == 0) return 0;
+  if (K < 1 || K > 16) return -2;
+  if (stride % 8 || V < 1) return -3;
+  const int C = (V + TK_CHUNK - 1) / TK_CHUNK;
+  float* ws_v = ws;
+  int* ws_i = reinterpret_cast<int*>(ws + (size_t)B * C * 16);
+  float* ws_ms = ws + (size_t)B * C * 32;
+  topk_lse_part_kernel<<<dim3(C, B), TK_NT, 0, s>>>((const uint16_t*)logits, V, stride, K, ws_v, ws_i, ws_ms);
+  DGI_CHECK_LAUNCH();
+  topk_lse_final_kernel<<<B, TK_NT, 0, s>>>(C, K, ws_v, ws_i, ws_ms, out_v, out_i);
   DGI_CHECK_LAUNCH();
   return 0;
 }

@@ -8,6 +8,7 @@ the reference's ``LLMBaseEngine`` contract (worker/engines/llm_base.py:45-188).
 from __future__ import annotations
 
 import dataclasses
+import math
 import time
 from typing import Iterable, Optional
 
@@ -149,9 +150,13 @@ class LLMEngine:
         self._la = None
         self.lookahead = bool(cfg.decode_lookahead) and _os.environ.get("DGI_DECODE_LOOKAHEAD", "1") == "1"
         # mixed-step lookahead: an eager step in flight, its tokens not committed yet
-        # (``_launch_eager`` / ``_step_mixed_lookahead``); DGI_MIXED_LOOKAHEAD=0 turns it off
+        # (``_launch_eager`` / ``_step_mixed_lookahead``).  Off by default (DGI_MIXED_LOOKAHEAD=1
+        # turns it on): on the 70B closed-loop bench it left throughput unchanged (1,868 vs
+        # 1,869-1,887 tok/s: the 203 ms step is GEMM-bound, its host gap ~2 %) and doubled p50 TTFT
+        # (408 vs 210 ms), since a request that arrives while step N runs misses the already
+        # launched step N+1 (profiles/r5_final/README.md)
         self._mx = None
-        self.mixed_lookahead = bool(cfg.decode_lookahead) and _os.environ.get("DGI_MIXED_LOOKAHEAD", "1") == "1"
+        self.mixed_lookahead = bool(cfg.decode_lookahead) and _os.environ.get("DGI_MIXED_LOOKAHEAD", "0") == "1"
         self.mixed_chained = 0
         self.step_budget = None
         if cfg.tpot_slo_ms > 0:
@@ -208,9 +213,11 @@ class LLMEngine:
         if cap is None:
             return None
         rows = sbud.rows_at_slo() or 0
-        queued = max(1, int((rows - rows * (sbud.output_avg or 0) / max(1.0, (sbud.prompt_avg or 0) +
-                                                                         (sbud.output_avg or 0)))
-                            / max(1.0, sbud.prompt_avg or 1.0)))
+        # prompts one SLO-sized step prefills, rounded UP: the running set can only grow as fast
+        # as prompts are admitted, so rounding 1.5 down to 1 would pin it below the cap
+        # (round 5: 128 running instead of ~190, 1.51k tok/s)
+        prefill_rows = rows - rows * (sbud.output_avg or 0) / max(1.0, (sbud.prompt_avg or 0) + (sbud.output_avg or 0))
+        queued = max(1, math.ceil(prefill_rows / max(1.0, sbud.prompt_avg or 1.0)))
         return min(cap, len(self.scheduler.running)) + queued
 
     def has_unfinished(self) -> bool:

@@ -685,6 +685,20 @@ def sample(logits: torch.Tensor, temperature: Optional[torch.Tensor] = None,
     return r
 
 
+def topk_logprobs(logits: torch.Tensor, k: int):
+    """Top-k (k <= 16) of ``log_softmax(logits.float())`` per row: fp32 log-probs and int64
+    indices, descending (ties: lower index first).  Native path: two HIP kernels straight
+    from bf16 logits (sampler.hip: chunked top-k + logsumexp, then a per-row merge)."""
+    if _native(logits) and logits.dtype == torch.bfloat16 and logits.stride(-1) == 1 \
+            and logits.stride(0) % 8 == 0:
+        B = logits.shape[0]
+        v = torch.empty(B, k, dtype=torch.float32, device=logits.device)
+        i = torch.empty(B, k, dtype=torch.long, device=logits.device)
+        _call("topk_logprobs", v, i, logits, k)
+        return v, i
+    return topk(torch.log_softmax(logits.float(), dim=-1), k)
+
+
 def topk(logits: torch.Tensor, k: int):
     """Top-k (k <= 16) values (fp32) and indices (int64), descending."""
     if _native(logits):

@@ -169,6 +169,14 @@ class Eagle3Draft:
         h = ops.linear(ops.silu_mul(ops.linear(h, self.gate_up)), self.down)
         return h + residual
 
+    def topk(self, g: torch.Tensor, k: int) -> tuple:
+        """(log-prob, draft-vocabulary index) of the ``k`` most likely next tokens per row of
+        ``g`` — ``ops.topk(self.logprobs(g), k)`` without the fp32 log-prob matrix (one fused
+        top-k + logsumexp pass over the bf16 logits, ``ops.topk_logprobs``)."""
+        hn = ops.rmsnorm(g.contiguous(), self.norm, self.cfg.rms_eps)
+        head = self.hot_head if self.hot_head is not None else self.target.lm_head
+        return ops.topk_logprobs(ops.linear(hn, head), k)
+
     def logprobs(self, g: torch.Tensor) -> torch.Tensor:
         """Log-probabilities over the draft vocabulary (columns index ``hot`` when set)."""
         hn = ops.rmsnorm(g.contiguous(), self.norm, self.cfg.rms_eps)
@@ -457,8 +465,7 @@ class _DraftGraph:
         Rb, W, D, K, N = self.Rb, self.W, self.D, self.K, self.N
         dev = self.g_root.device
         H = self.g_root.shape[1]
-        lp = dr.logprobs(self.g_root)
-        v1, t1 = ops.topk(lp, K)
+        v1, t1 = dr.topk(self.g_root, K)
         t1 = dr.to_token(t1)
         tok = torch.zeros(Rb, N, dtype=torch.long, device=dev)
         par = torch.full((Rb, N), -1, dtype=torch.int32, device=dev)
@@ -481,8 +488,7 @@ class _DraftGraph:
             gc = dr.forward(tok[:, 1:m + 1].reshape(-1), hin, cm).view(Rb, m, H)
             G[:, 1:m + 1] = gc
             fr = torch.arange(m - W + 1, m + 1, device=dev)
-            lpf = dr.logprobs(gc[:, m - W:].reshape(Rb * W, H))
-            vf, tf = ops.topk(lpf, K)
+            vf, tf = dr.topk(gc[:, m - W:].reshape(Rb * W, H), K)
             tf = dr.to_token(tf)
             cand = (score[:, fr][:, :, None] + vf.view(Rb, W, K).float()).view(Rb, W * K)
             best, bi = torch.topk(cand, W, dim=1)
@@ -981,8 +987,7 @@ class SpecEngine(LLMEngine):
         R, H = g_root.shape
         dev, run, bs = self.device, self.runner, self.pool.block_size
         g = g_root
-        lp = self.draft.logprobs(g_root)                         # [R, V] (V: the draft vocabulary)
-        v1, t1 = ops.topk(lp, K)
+        v1, t1 = self.draft.topk(g_root, K)                      # log-probs over the draft vocabulary
         t1 = self.draft.to_token(t1)
         tok = torch.zeros(R, N, dtype=torch.long, device=dev)
         par = torch.full((R, N), -1, dtype=torch.int32, device=dev)
@@ -1014,8 +1019,7 @@ class SpecEngine(LLMEngine):
             gc = self.draft.forward(tok[:, 1:m + 1].reshape(-1), hin, cm).view(R, m, H)
             G[:, 1:m + 1] = gc
             fr = torch.arange(m - W + 1, m + 1, device=dev)        # frontier = depth d-1 nodes
-            lpf = self.draft.logprobs(gc[:, m - W:].reshape(R * W, H))
-            vf, tf = ops.topk(lpf, K)                              # [R*W, K]
+            vf, tf = self.draft.topk(gc[:, m - W:].reshape(R * W, H), K)   # [R*W, K]
             tf = self.draft.to_token(tf)
             cand = (score[:, fr][:, :, None] + vf.view(R, W, K).float()).view(R, W * K)
             best, bi = torch.topk(cand, W, dim=1)

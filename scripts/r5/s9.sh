@@ -19,4 +19,5 @@ step attn_ab 300 env ATTN_PREFILL_ONLY=1 ATTN_TILES=128,256 ATTN_DB=0,1 python -
 step pmc_mfma 120 timeout -s KILL 110 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d $O/pmc_mfma -o run --output-format csv -- python3 scripts/pmc_kernels.py --only prefill
 step pmc_wait 120 timeout -s KILL 110 rocprofv3 --kernel-trace --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE -d $O/pmc_wait -o run --output-format csv -- python3 scripts/pmc_kernels.py --only prefill
 step bench70b 600 python -u bench.py --steps 20 --warmup 5 --json-out $O/bench70b.json
+step slo120 600 python -u bench.py --steps 60 --warmup 10 --tpot-slo-ms 120 --json-out $O/slo120.json
 echo ALLDONE

@@ -220,6 +220,31 @@ def test_sample_greedy_and_topk(dtype):
     assert all(len(set(r)) == 8 for r in i.cpu().tolist())
 
 
+@pytest.mark.parametrize("B,V,k", [(3, 128256, 4), (48, 128256, 16), (5, 32768, 1), (2, 1000, 8), (1, 8200, 4)])
+def test_topk_logprobs_matches_log_softmax_topk(B, V, k):
+    """Fused top-k of log_softmax (chunked HIP kernels straight from bf16 logits) against
+    torch: same values to fp32 logsumexp rounding, indices pointing at the reported values,
+    lower index first among equal logits (bf16 rows tie often)."""
+    logits = (torch.randn(B, V, device=DEV) * 3).to(torch.bfloat16)
+    v, i = ops.topk_logprobs(logits, k)
+    ref = torch.log_softmax(logits.float(), dim=-1)
+    rv, _ri = ref.topk(k, dim=-1)
+    torch.testing.assert_close(v.cpu(), rv.cpu(), atol=2e-5, rtol=1e-5)
+    torch.testing.assert_close(ref.gather(1, i).cpu(), v.cpu(), atol=2e-5, rtol=1e-5)
+    il = i.cpu().tolist()
+    assert all(len(set(r)) == k for r in il)
+    lf = logits.float().cpu()
+    for b in range(B):                   # ties: the lowest index of a tied value comes first
+        for j in range(k - 1):
+            if lf[b, il[b][j]] == lf[b, il[b][j + 1]]:
+                assert il[b][j] < il[b][j + 1]
+    # a strided row view (logits of a wider buffer)
+    wide = torch.randn(B, V + 8, device=DEV).to(torch.bfloat16)
+    v2, i2 = ops.topk_logprobs(wide[:, :V], k)
+    rv2 = torch.log_softmax(wide[:, :V].float(), dim=-1).topk(k, dim=-1).values
+    torch.testing.assert_close(v2.cpu(), rv2.cpu(), atol=2e-5, rtol=1e-5)
+
+
 def test_sample_temperature_distribution():
     V = 8
     logits = torch.log(torch.tensor([[0.5, 0.25, 0.125, 0.125, 1e-9, 1e-9, 1e-9, 1e-9]], device=DEV)).repeat(4096, 1)
