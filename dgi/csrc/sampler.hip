@@ -173,141 +173,152 @@ __global__ __launch_bounds__(256) void topk_kernel(const T* __restrict__ logits,
 // of one (round 5 trace: the one-block-per-row kernel plus torch's log_softmax took 222 us
 // per draft depth at 3 rows).  Ties: lower index first (as topk_kernel).
 constexpr int TK_NT = 256;
-constexpr int TK_CHUNK = 8192;   // elements per stage-1 workgroup (multiple of 8 * TK_NT)
+constexpr int TK_CHUNK = 2048;   // elements per stage-1 workgroup: one 16-byte load per thread
 
-__device__ __forceinline__ void tk_insert(float* tv, int* ti, int K, float v, int i) {
-  if (v > tv[K - 1]) {
-    int k = K - 1;
-    while (k > 0 && tv[k - 1] < v) { tv[k] = tv[k - 1]; ti[k] = ti[k - 1]; --k; }
-    tv[k] = v;
-    ti[k] = i;
-  }
-}
-
-// merge the NT per-thread lists in sv / si (16 slots per thread) down to slot 0
-__device__ __forceinline__ void tk_merge(float* sv, int* si, int K) {
-  for (int half = TK_NT / 2; half > 0; half >>= 1) {
-    if ((int)threadIdx.x < half) {
-      const float* a = sv + threadIdx.x * 16;
-      const int* ai = si + threadIdx.x * 16;
-      const float* bv = sv + (threadIdx.x + half) * 16;
-      const int* bi = si + (threadIdx.x + half) * 16;
-      float mv[16];
-      int mi[16];
-      int x = 0, y = 0;
-      for (int k = 0; k < K; ++k) {
-        const bool takea = (a[x] > bv[y]) || (a[x] == bv[y] && ai[x] <= bi[y]);
-        if (takea) { mv[k] = a[x]; mi[k] = ai[x]; ++x; } else { mv[k] = bv[y]; mi[k] = bi[y]; ++y; }
+// Sorted (descending) per-thread list of KP entries in registers; every index below is a
+// compile-time constant after unrolling (a runtime-K insertion loop compiles to select chains
+// over all 16 slots per element).  A new element sinks below equal ones (ties: earlier first).
+template <int KP>
+__device__ __forceinline__ void tk_insert(float (&tv)[KP], int (&ti)[KP], float v, int i) {
+  if (v > tv[KP - 1] || (v == tv[KP - 1] && i < ti[KP - 1])) {
+    tv[KP - 1] = v;
+    ti[KP - 1] = i;
+#pragma unroll
+    for (int j = KP - 1; j > 0; --j) {
+      if (tv[j] > tv[j - 1] || (tv[j] == tv[j - 1] && ti[j] < ti[j - 1])) {
+        const float tvv = tv[j]; tv[j] = tv[j - 1]; tv[j - 1] = tvv;
+        const int tii = ti[j]; ti[j] = ti[j - 1]; ti[j - 1] = tii;
       }
-      for (int k = 0; k < K; ++k) { sv[threadIdx.x * 16 + k] = mv[k]; si[threadIdx.x * 16 + k] = mi[k]; }
     }
-    __syncthreads();
   }
 }
 
+// block-wide merge of the per-thread lists: each wave reduces its 64 lists with xor
+// shuffles (the partner's list inserted into this lane's, all indices compile-time), then
+// thread 0 merges the NW wave winners through LDS.  Result valid on thread 0.
+template <int KP>
+__device__ __forceinline__ void tk_merge2(float (&a)[KP], int (&ai)[KP], const float (&b)[KP], const int (&bi)[KP]) {
+#pragma unroll
+  for (int k = 0; k < KP; ++k) tk_insert<KP>(a, ai, b[k], bi[k]);
+}
+
+template <int KP>
+__device__ __forceinline__ void tk_block_reduce(float (&tv)[KP], int (&ti)[KP], float& m, float& sum,
+                                                float* s_v, int* s_i, float* s_m, float* s_s) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    float ov[KP];
+    int oi[KP];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) { ov[k] = __shfl_xor(tv[k], off); oi[k] = __shfl_xor(ti[k], off); }
+    tk_merge2<KP>(tv, ti, ov, oi);
+    const float om = __shfl_xor(m, off), os = __shfl_xor(sum, off);
+    const float nm = fmaxf(m, om);
+    sum = (sum > 0.f ? sum * __expf(m - nm) : 0.f) + (os > 0.f ? os * __expf(om - nm) : 0.f);
+    m = nm;
+  }
+  constexpr int NW = TK_NT / 64;
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < KP; ++k) { s_v[w * KP + k] = tv[k]; s_i[w * KP + k] = ti[k]; }
+    s_m[w] = m;
+    s_s[w] = sum;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int ww = 1; ww < NW; ++ww) {
+      float ov[KP];
+      int oi[KP];
+#pragma unroll
+      for (int k = 0; k < KP; ++k) { ov[k] = s_v[ww * KP + k]; oi[k] = s_i[ww * KP + k]; }
+      tk_merge2<KP>(tv, ti, ov, oi);
+      const float om = s_m[ww], os = s_s[ww];
+      const float nm = fmaxf(m, om);
+      sum = (sum > 0.f ? sum * __expf(m - nm) : 0.f) + (os > 0.f ? os * __expf(om - nm) : 0.f);
+      m = nm;
+    }
+  }
+}
+
+template <int KP>
 __global__ __launch_bounds__(TK_NT) void topk_lse_part_kernel(const uint16_t* __restrict__ logits, int V, int stride,
-                                                              int K, float* __restrict__ ws_v, int* __restrict__ ws_i,
+                                                              float* __restrict__ ws_v, int* __restrict__ ws_i,
                                                               float* __restrict__ ws_ms) {
   const int c = blockIdx.x, C = gridDim.x, row = blockIdx.y;
   const uint16_t* lp = logits + (size_t)row * stride;
   const int lo = c * TK_CHUNK, hi = min(V, lo + TK_CHUNK);
-  float tv[16];
-  int ti[16];
+  float tv[KP];
+  int ti[KP];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) { tv[k] = -INFINITY; ti[k] = 0x7fffffff; }
+  for (int k = 0; k < KP; ++k) { tv[k] = -INFINITY; ti[k] = 0x7fffffff; }
   float m = -INFINITY, sum = 0.f;
   auto take = [&](float v, int i) {
     if (v > m) {                       // online logsumexp (finite logits; -inf entries add nothing)
-      sum = sum * __expf(m - v) + 1.f;
+      sum = (sum > 0.f ? sum * __expf(m - v) : 0.f) + 1.f;
       m = v;
     } else if (v > -INFINITY) {
       sum += __expf(v - m);
     }
-    tk_insert(tv, ti, K, v, i);
+    tk_insert<KP>(tv, ti, v, i);
   };
-  for (int i = lo + 8 * threadIdx.x; i < hi; i += 8 * TK_NT) {
-    if (i + 8 <= hi) {
-      const u32x4 p = *reinterpret_cast<const u32x4*>(lp + i);
+  const int i = lo + 8 * threadIdx.x;
+  if (i + 8 <= hi) {
+    const u32x4 p = *reinterpret_cast<const u32x4*>(lp + i);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        take(__uint_as_float(p[j] << 16), i + 2 * j);
-        take(__uint_as_float(p[j] & 0xffff0000u), i + 2 * j + 1);
-      }
-    } else {
-      for (int j = i; j < hi; ++j) take(bf16_to_f32(lp[j]), j);
+    for (int j = 0; j < 4; ++j) {
+      take(__uint_as_float(p[j] << 16), i + 2 * j);
+      take(__uint_as_float(p[j] & 0xffff0000u), i + 2 * j + 1);
     }
+  } else {
+    for (int j = i; j < hi; ++j) take(bf16_to_f32(lp[j]), j);
   }
-  __shared__ float sv[TK_NT * 16];
-  __shared__ int si[TK_NT * 16];
-  __shared__ float sm[TK_NT], ss[TK_NT];
-  for (int k = 0; k < K; ++k) { sv[threadIdx.x * 16 + k] = tv[k]; si[threadIdx.x * 16 + k] = ti[k]; }
-  sm[threadIdx.x] = m;
-  ss[threadIdx.x] = sum;
-  __syncthreads();
-  tk_merge(sv, si, K);
-  const size_t o = ((size_t)row * C + c);
-  if ((int)threadIdx.x < K) {
-    ws_v[o * 16 + threadIdx.x] = sv[threadIdx.x];
-    ws_i[o * 16 + threadIdx.x] = si[threadIdx.x];
-  }
+  __shared__ float s_v[(TK_NT / 64) * KP], s_m[TK_NT / 64], s_s[TK_NT / 64];
+  __shared__ int s_i[(TK_NT / 64) * KP];
+  tk_block_reduce<KP>(tv, ti, m, sum, s_v, s_i, s_m, s_s);
   if (threadIdx.x == 0) {
-    float M = -INFINITY;
-    for (int t = 0; t < TK_NT; ++t) M = fmaxf(M, sm[t]);
-    float S = 0.f;
-    if (M > -INFINITY)
-      for (int t = 0; t < TK_NT; ++t) S += ss[t] > 0.f ? ss[t] * __expf(sm[t] - M) : 0.f;
-    ws_ms[2 * o] = M;
-    ws_ms[2 * o + 1] = S;
+    const size_t o = (size_t)row * C + c;
+#pragma unroll
+    for (int k = 0; k < KP; ++k) { ws_v[o * 16 + k] = tv[k]; ws_i[o * 16 + k] = ti[k]; }
+    ws_ms[2 * o] = m;
+    ws_ms[2 * o + 1] = sum;
   }
 }
 
+template <int KP>
 __global__ __launch_bounds__(TK_NT) void topk_lse_final_kernel(int C, int K, const float* __restrict__ ws_v,
                                                                const int* __restrict__ ws_i,
                                                                const float* __restrict__ ws_ms,
                                                                float* __restrict__ out_v,
                                                                long long* __restrict__ out_i) {
   const int row = blockIdx.x;
-  float tv[16];
-  int ti[16];
+  float tv[KP];
+  int ti[KP];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) { tv[k] = -INFINITY; ti[k] = 0x7fffffff; }
-  // candidates in (chunk, rank) order: a thread's list stays index-ordered on ties only
-  // within a chunk, so insertion breaks value ties by index explicitly
-  for (int q = threadIdx.x; q < C * K; q += TK_NT) {
-    const int cc = q / K, k = q - cc * K;
-    const size_t o = ((size_t)row * C + cc) * 16 + k;
-    const float v = ws_v[o];
-    const int i = ws_i[o];
-    if (v > tv[K - 1] || (v == tv[K - 1] && i < ti[K - 1])) {
-      int j = K - 1;
-      while (j > 0 && (tv[j - 1] < v || (tv[j - 1] == v && ti[j - 1] > i))) {
-        tv[j] = tv[j - 1];
-        ti[j] = ti[j - 1];
-        --j;
-      }
-      tv[j] = v;
-      ti[j] = i;
-    }
+  for (int k = 0; k < KP; ++k) { tv[k] = -INFINITY; ti[k] = 0x7fffffff; }
+  float m = -INFINITY, sum = 0.f;
+  for (int cc = threadIdx.x; cc < C; cc += TK_NT) {      // one chunk's list per thread
+    const size_t o = (size_t)row * C + cc;
+    float ov[KP];
+    int oi[KP];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) { ov[k] = ws_v[o * 16 + k]; oi[k] = ws_i[o * 16 + k]; }
+    tk_merge2<KP>(tv, ti, ov, oi);
+    const float om = ws_ms[2 * o], os = ws_ms[2 * o + 1];
+    const float nm = fmaxf(m, om);
+    sum = (sum > 0.f ? sum * __expf(m - nm) : 0.f) + (os > 0.f ? os * __expf(om - nm) : 0.f);
+    m = nm;
   }
-  __shared__ float sv[TK_NT * 16];
-  __shared__ int si[TK_NT * 16];
-  __shared__ float s_lse;
-  for (int k = 0; k < K; ++k) { sv[threadIdx.x * 16 + k] = tv[k]; si[threadIdx.x * 16 + k] = ti[k]; }
+  __shared__ float s_v[(TK_NT / 64) * KP], s_m[TK_NT / 64], s_s[TK_NT / 64];
+  __shared__ int s_i[(TK_NT / 64) * KP];
+  tk_block_reduce<KP>(tv, ti, m, sum, s_v, s_i, s_m, s_s);
   if (threadIdx.x == 0) {
-    float M = -INFINITY;
-    for (int cc = 0; cc < C; ++cc) M = fmaxf(M, ws_ms[2 * ((size_t)row * C + cc)]);
-    float S = 0.f;
-    for (int cc = 0; cc < C; ++cc) {
-      const float mc = ws_ms[2 * ((size_t)row * C + cc)], sc = ws_ms[2 * ((size_t)row * C + cc) + 1];
-      if (sc > 0.f) S += sc * __expf(mc - M);
+    const float lse = m + __logf(sum);
+    for (int k = 0; k < K; ++k) {
+      out_v[(size_t)row * K + k] = tv[k] - lse;
+      out_i[(size_t)row * K + k] = ti[k];
     }
-    s_lse = M + __logf(S);
-  }
-  __syncthreads();
-  tk_merge(sv, si, K);
-  if ((int)threadIdx.x < K) {
-    out_v[(size_t)row * K + threadIdx.x] = sv[threadIdx.x] - s_lse;
-    out_i[(size_t)row * K + threadIdx.x] = si[threadIdx.x];
   }
 }
 
@@ -516,16 +527,19 @@ extern "C" int dgi_topk_logprobs_ws_floats(int B, int V) {
 extern "C" int dgi_topk_logprobs(const void* logits, int B, int V, int stride, int K, float* ws, float* out_v,
                                  long long* out_i, hipStream_t s) {
   if (B == 0) return 0;
-  if (K < 1 || K > 16) return -2;
+  if (K < 1 || K > 8) return -2;     // wider draft expansions use log_softmax + topk_kernel
   if (stride % 8 || V < 1) return -3;
   const int C = (V + TK_CHUNK - 1) / TK_CHUNK;
   float* ws_v = ws;
   int* ws_i = reinterpret_cast<int*>(ws + (size_t)B * C * 16);
   float* ws_ms = ws + (size_t)B * C * 32;
-  topk_lse_part_kernel<<<dim3(C, B), TK_NT, 0, s>>>((const uint16_t*)logits, V, stride, K, ws_v, ws_i, ws_ms);
+#define DGI_TKL(KPV)                                                                                         \
+  topk_lse_part_kernel<KPV><<<dim3(C, B), TK_NT, 0, s>>>((const uint16_t*)logits, V, stride, ws_v, ws_i, ws_ms); \
+  DGI_CHECK_LAUNCH();                                                                                         \
+  topk_lse_final_kernel<KPV><<<B, TK_NT, 0, s>>>(C, K, ws_v, ws_i, ws_ms, out_v, out_i);                      \
   DGI_CHECK_LAUNCH();
-  topk_lse_final_kernel<<<B, TK_NT, 0, s>>>(C, K, ws_v, ws_i, ws_ms, out_v, out_i);
-  DGI_CHECK_LAUNCH();
+  if (K <= 1) { DGI_TKL(1) } else if (K <= 2) { DGI_TKL(2) } else if (K <= 4) { DGI_TKL(4) } else { DGI_TKL(8) }
+#undef DGI_TKL
   return 0;
 }
 

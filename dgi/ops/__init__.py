@@ -687,10 +687,10 @@ def sample(logits: torch.Tensor, temperature: Optional[torch.Tensor] = None,
 
 def topk_logprobs(logits: torch.Tensor, k: int):
     """Top-k (k <= 16) of ``log_softmax(logits.float())`` per row: fp32 log-probs and int64
-    indices, descending (ties: lower index first).  Native path: two HIP kernels straight
-    from bf16 logits (sampler.hip: chunked top-k + logsumexp, then a per-row merge)."""
+    indices, descending (ties: lower index first).  Native path (k <= 8): two HIP kernels
+    straight from bf16 logits (sampler.hip: chunked top-k + logsumexp, then a per-row merge)."""
     if _native(logits) and logits.dtype == torch.bfloat16 and logits.stride(-1) == 1 \
-            and logits.stride(0) % 8 == 0:
+            and logits.stride(0) % 8 == 0 and k <= 8:
         B = logits.shape[0]
         v = torch.empty(B, k, dtype=torch.float32, device=logits.device)
         i = torch.empty(B, k, dtype=torch.long, device=logits.device)

@@ -220,7 +220,8 @@ def test_sample_greedy_and_topk(dtype):
     assert all(len(set(r)) == 8 for r in i.cpu().tolist())
 
 
-@pytest.mark.parametrize("B,V,k", [(3, 128256, 4), (48, 128256, 16), (5, 32768, 1), (2, 1000, 8), (1, 8200, 4)])
+@pytest.mark.parametrize("B,V,k", [(3, 128256, 4), (48, 128256, 8), (5, 32768, 1), (2, 1000, 8), (1, 8200, 2),
+                                   (4, 128256, 12)])
 def test_topk_logprobs_matches_log_softmax_topk(B, V, k):
     """Fused top-k of log_softmax (chunked HIP kernels straight from bf16 logits) against
     torch: same values to fp32 logsumexp rounding, indices pointing at the reported values,
