@@ -913,9 +913,17 @@ class SpecEngine(LLMEngine):
             logits, feats = self._forward_capture(vm, tok.view(-1))
             tgt = ops.sample(logits, samp[0], samp[1], 0, top_k=samp[2], top_p=samp[3]).view(R, N)
             acc, path, toks = ops.tree_verify(par, tok, tgt, anc, depth, D + 1)
-        acc_h = acc.cpu().tolist()
-        path_h = path.cpu().numpy()
-        toks_h = toks.cpu().numpy()
+        if dev.type == "cuda":
+            # one wait for the three verify outputs (three .cpu() calls were three round trips)
+            hs = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in (acc, path, toks)]
+            for h_, t in zip(hs, (acc, path, toks)):
+                h_.copy_(t, non_blocking=True)
+            torch.cuda.current_stream(dev).synchronize()
+            acc_h, path_h, toks_h = hs[0].tolist(), hs[1].numpy(), hs[2].numpy()
+        else:
+            acc_h = acc.cpu().tolist()
+            path_h = path.cpu().numpy()
+            toks_h = toks.cpu().numpy()
         # ---- 4) compact accepted KV, keep their features, commit tokens
         src, dst = [], []
         fsel = []
