@@ -64,7 +64,8 @@ from dgi.runtime.model_runner import graph_capture
 @dataclasses.dataclass
 class SpecConfig:
     depth: int = 5            # draft tree depth D (max accepted drafts per step)
-    width: int = 4            # frontier nodes kept per depth W
+    width: int = 3            # frontier nodes kept per depth W (3 x depth 5 + root = 16 nodes: a batch-1
+                              # verify fits the fused decode layers, profiles/r5_spec/)
     topk: int = 4             # children per frontier node K (<= 16, dgi_topk)
     feature_layers: Optional[tuple] = None  # default: (2, L//2, L-3)
     graphs: bool = True       # hipGraph-capture the tree verify pass per batch bucket (GPU)

@@ -50,7 +50,7 @@ def main():
     ap.add_argument("--prompt-len", type=int, default=256)
     ap.add_argument("--output-len", type=int, default=128)
     ap.add_argument("--depth", type=int, default=5)
-    ap.add_argument("--width", type=int, default=4)
+    ap.add_argument("--width", type=int, default=3)
     ap.add_argument("--topk", type=int, default=4)
     ap.add_argument("--train-steps", type=int, default=300)
     ap.add_argument("--train-seqs", type=int, default=64)
