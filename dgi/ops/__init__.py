@@ -16,6 +16,7 @@ import math
 import os
 from typing import Optional
 
+import numpy as np
 import torch
 
 _LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_C.so")
@@ -314,14 +315,33 @@ PREFILL_TILE = int(os.environ.get("DGI_PREFILL_TILE", "128"))
 PREFILL_DB = int(os.environ.get("DGI_PREFILL_DB", "1"))
 
 
-def prefill_tiles(cu_seqlens_q: list[int], tile: int = 0) -> list[tuple[int, int]]:
+def order_prefill_tiles(cu_seqlens_q, context_lens=None, tile: int = 0) -> np.ndarray:
+    """int32 [n_tiles, 2] (sequence, first query row) of a prefill-attention launch, the
+    heaviest tiles first.  A causal tile's work is the keys it reads, kv_end = context -
+    qlen + t0 + tile, so in (sequence, row) order the longest workgroups of the last heads
+    are dispatched last and run alone at the end of the grid; longest-first ordering lets
+    the short ones fill in behind them (the grid is (tiles, heads): every head walks the
+    same order).  Ties keep (sequence, row) order."""
     tile = tile or PREFILL_TILE
-    tiles = []
-    for b in range(len(cu_seqlens_q) - 1):
-        ql = cu_seqlens_q[b + 1] - cu_seqlens_q[b]
-        for t0 in range(0, ql, tile):
-            tiles.append((b, t0))
-    return tiles
+    cu = np.asarray(cu_seqlens_q, np.int64)
+    nb = len(cu) - 1
+    ql = cu[1:] - cu[:-1]
+    ctx = ql if context_lens is None else np.asarray(context_lens, np.int64)[:nb]
+    seq, t0, work = [], [], []
+    for b in range(nb):
+        starts = np.arange(0, int(ql[b]), tile, dtype=np.int64)
+        seq.append(np.full(len(starts), b, np.int64))
+        t0.append(starts)
+        work.append(np.minimum(int(ctx[b]), int(ctx[b]) - int(ql[b]) + starts + tile))
+    if not seq:
+        return np.zeros((0, 2), np.int32)
+    seq, t0, work = np.concatenate(seq), np.concatenate(t0), np.concatenate(work)
+    order = np.argsort(-work, kind="stable")
+    return np.stack([seq[order], t0[order]], 1).astype(np.int32)
+
+
+def prefill_tiles(cu_seqlens_q: list[int], tile: int = 0, context_lens=None) -> list[tuple[int, int]]:
+    return [tuple(t) for t in order_prefill_tiles(cu_seqlens_q, context_lens, tile).tolist()]
 
 
 def paged_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens, nh, nkv, scale,
@@ -335,7 +355,7 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens,
         if out is None:
             out = torch.empty(q.shape[0], nh * hd, dtype=q.dtype, device=q.device)
         if tiles is None:
-            tl = prefill_tiles(cu_seqlens_q.tolist())
+            tl = prefill_tiles(cu_seqlens_q.tolist(), context_lens=context_lens.tolist())
             tiles = torch.tensor(tl if tl else [[0, 0]], dtype=torch.int32, device=q.device)[: len(tl)]
         _call("paged_prefill", out, q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens,
               tiles, nh, nkv, scale, tree_mask, tree_n, PREFILL_TILE | ((PREFILL_DB & 1) << 16))

@@ -219,11 +219,7 @@ class ModelRunner:
                 logit_rows.append(row + c.length - 1)
                 sampled.append(r)
             row += c.length
-        tiles = []
-        for j in range(nb):
-            for t0 in range(0, int(cu[j + 1] - cu[j]), ops.PREFILL_TILE):
-                tiles.append((j, t0))
-        tiles_np = np.asarray(tiles, np.int32).reshape(-1, 2)
+        tiles_np = ops.order_prefill_tiles(cu[: nb + 1], pctx[:nb])
         nlog = len(logit_rows)
         lidx = np.asarray(logit_rows, np.int32)
         # top-k / top-p ride in the same flat buffer (one H2D copy; pipeline stages get them too)
@@ -244,7 +240,7 @@ class ModelRunner:
         hdr = np.zeros(self.HEADER_SIZE, np.int64)
         hdr[[self.H_LEN, self.H_T, self.H_NDP, self.H_NPRE, self.H_NB, self.H_MAXW, self.H_SPLITS, self.H_PART,
              self.H_NTILES, self.H_NLOG, self.H_STEP, self.H_FILT]] = [flat.size, T, ndp, npre, nb, maxw, splits,
-                                                                      part, len(tiles), nlog, self.step_id, int(filt)]
+                                                                      part, len(tiles_np), nlog, self.step_id, int(filt)]
         return flat, hdr, sampled
 
     def meta_from_device(self, dev: torch.Tensor, hdr):

@@ -40,6 +40,8 @@ def prefill(B, L):
     ctx = torch.full((B,), L, device=dev, dtype=torch.int32)
     q = torch.randn(B * L, (nh + 2 * nkv) * hd, device=dev, dtype=torch.bfloat16)
     tl = ops.prefill_tiles(cu.tolist())
+    if os.environ.get("ATTN_TILE_ORDER", "1") == "0":      # A/B: (sequence, row) order
+        tl = sorted(tl)
     tiles = torch.tensor(tl, dtype=torch.int32, device=dev)
     out = torch.empty(B * L, nh * hd, device=dev, dtype=torch.bfloat16)
     scale = 1 / math.sqrt(hd)
@@ -49,7 +51,8 @@ def prefill(B, L):
     kd = torch.randn(B, nh, L, hd, device=dev, dtype=torch.bfloat16)
     vd = torch.randn_like(kd)
     us_sdpa = timed(lambda: F.scaled_dot_product_attention(qd, kd, vd, is_causal=True))
-    return {"kernel": "prefill", "B": B, "L": L, "tile": ops.PREFILL_TILE, "db": ops.PREFILL_DB, "us": round(us, 1),
+    return {"kernel": "prefill", "B": B, "L": L, "tile": ops.PREFILL_TILE, "db": ops.PREFILL_DB,
+            "order": os.environ.get("ATTN_TILE_ORDER", "1"), "us": round(us, 1),
             "TFLOPs": round(flops / us / 1e6, 1),
             "sdpa_us": round(us_sdpa, 1), "sdpa_TFLOPs": round(flops / us_sdpa / 1e6, 1)}
 
