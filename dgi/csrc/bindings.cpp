@@ -48,6 +48,8 @@ int dgi_kv_gather(const void* cache, const int* ids, int n, int LK, int num_bloc
                   void* buf, hipStream_t s);
 int dgi_kv_scatter(void* cache, const int* ids, int n, int LK, int num_blocks, int page_elems,
                    const void* buf, hipStream_t s);
+int dgi_kv_slot_copy(void* cache, const int* src, const int* dst, int n, int LK, int num_blocks, int nkv, int bs,
+                     int hd, void* buf, hipStream_t s);
 int dgi_kv_copy(void* cache, const int* src, const int* dst, int n, int LK, int num_blocks,
                 int page_elems, hipStream_t s);
 int dgi_tree_mask(const int* parent, int B, int N, unsigned long long* anc, int* depth,
@@ -422,6 +424,20 @@ void kv_copy(at::Tensor cache, const at::Tensor& src, const at::Tensor& dst) {
                        LK, NB, page, cur_stream()), "kv_copy");
 }
 
+// token-slot copy inside the paged cache (all layers, K and V); src / dst int32 slots
+void kv_slot_copy(at::Tensor cache, const at::Tensor& src, const at::Tensor& dst) {
+  check_dev(cache, "cache"); check_i32(src, "src"); check_i32(dst, "dst");
+  TORCH_CHECK(cache.is_contiguous() && cache.dim() == 6 && src.numel() == dst.numel());
+  TORCH_CHECK(cache.scalar_type() == at::kBFloat16 || cache.scalar_type() == at::kHalf);
+  const int n = (int)src.numel();
+  if (n == 0) return;
+  const int LK = (int)(cache.size(0) * cache.size(1));
+  const int NB = (int)cache.size(2), nkv = (int)cache.size(3), bs = (int)cache.size(4), hd = (int)cache.size(5);
+  at::Tensor buf = at::empty({(int64_t)n * LK * nkv * hd}, cache.options());
+  check_rc(dgi_kv_slot_copy(cache.data_ptr(), src.data_ptr<int>(), dst.data_ptr<int>(), n, LK, NB, nkv, bs, hd,
+                            buf.data_ptr(), cur_stream()), "kv_slot_copy");
+}
+
 void tree_mask(at::Tensor anc, at::Tensor depth, const at::Tensor& parent) {
   check_i32(parent, "parent"); check_i32(depth, "depth");
   TORCH_CHECK(anc.scalar_type() == at::kLong && anc.is_contiguous());
@@ -484,6 +500,7 @@ TORCH_LIBRARY(dgi, m) {
   m.def("kv_gather(Tensor(a!) buf, Tensor cache, Tensor ids) -> ()");
   m.def("kv_scatter(Tensor(a!) cache, Tensor ids, Tensor buf) -> ()");
   m.def("kv_copy(Tensor(a!) cache, Tensor src, Tensor dst) -> ()");
+  m.def("kv_slot_copy(Tensor(a!) cache, Tensor src, Tensor dst) -> ()");
   m.def("tree_mask(Tensor(a!) anc, Tensor(b!) depth, Tensor parent) -> ()");
   m.def("tree_verify(Tensor(a!) accept_len, Tensor(b!) path, Tensor(c!) out_tokens, Tensor parent, "
         "Tensor draft, Tensor target, Tensor anc, Tensor depth) -> ()");
@@ -506,6 +523,7 @@ TORCH_LIBRARY_IMPL(dgi, CUDA, m) {
   m.impl("kv_gather", &kv_gather);
   m.impl("kv_scatter", &kv_scatter);
   m.impl("kv_copy", &kv_copy);
+  m.impl("kv_slot_copy", &kv_slot_copy);
   m.impl("tree_mask", &tree_mask);
   m.impl("tree_verify", &tree_verify);
 }

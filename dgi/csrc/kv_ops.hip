@@ -61,6 +61,46 @@ __global__ __launch_bounds__(256) void kv_copy_kernel(u32x4* __restrict__ cache,
   }
 }
 
+// Token-slot moves (EAGLE KV compaction: accepted tree nodes -> consecutive positions):
+// slot s = block * bs + offset; a slot of one (layer, k/v) is n_kv rows of hd elements at
+// stride bs * hd.  Gather every source slot into buf [n, LK, n_kv, hd] first, then scatter:
+// the moves of one sequence chain (a node's source slot can be another move's destination),
+// so all reads must land before any write (what the torch advanced-index version did, in 36
+// launches per verify step).
+__global__ __launch_bounds__(256) void kv_slot_gather_kernel(const u32x4* __restrict__ cache,
+                                                             const int* __restrict__ src, int n, int LK,
+                                                             int num_blocks, int nkv, int bs, int hdc,
+                                                             u32x4* __restrict__ buf) {
+  const long total = (long)n * LK * nkv * hdc;
+  for (long c = (long)blockIdx.x * 256 + threadIdx.x; c < total; c += (long)gridDim.x * 256) {
+    const int d = (int)(c % hdc);
+    long r = c / hdc;
+    const int h = (int)(r % nkv);
+    r /= nkv;
+    const int lk = (int)(r % LK);
+    const int i = (int)(r / LK);
+    const int s = src[i];
+    buf[c] = cache[(((long)lk * num_blocks + s / bs) * nkv + h) * bs * hdc + (long)(s % bs) * hdc + d];
+  }
+}
+
+__global__ __launch_bounds__(256) void kv_slot_scatter_kernel(u32x4* __restrict__ cache,
+                                                              const int* __restrict__ dst, int n, int LK,
+                                                              int num_blocks, int nkv, int bs, int hdc,
+                                                              const u32x4* __restrict__ buf) {
+  const long total = (long)n * LK * nkv * hdc;
+  for (long c = (long)blockIdx.x * 256 + threadIdx.x; c < total; c += (long)gridDim.x * 256) {
+    const int d = (int)(c % hdc);
+    long r = c / hdc;
+    const int h = (int)(r % nkv);
+    r /= nkv;
+    const int lk = (int)(r % LK);
+    const int i = (int)(r / LK);
+    const int s = dst[i];
+    cache[(((long)lk * num_blocks + s / bs) * nkv + h) * bs * hdc + (long)(s % bs) * hdc + d] = buf[c];
+  }
+}
+
 int grid_for(long total) {
   long b = (total + 255) / 256;
   return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
@@ -98,6 +138,22 @@ extern "C" int dgi_kv_copy(void* cache, const int* src, const int* dst, int n, i
   const int pc = page_elems / 8;
   kv_copy_kernel<<<grid_for((long)LK * n * pc), 256, 0, s>>>((u32x4*)cache, src, dst, n,
                                                              num_blocks, pc, LK);
+  DGI_CHECK_LAUNCH();
+  return 0;
+}
+
+// cache [L, 2, NB, nkv, bs, hd] bf16; src / dst: token slots; buf: n * LK * nkv * hd elements
+extern "C" int dgi_kv_slot_copy(void* cache, const int* src, const int* dst, int n, int LK, int num_blocks,
+                                int nkv, int bs, int hd, void* buf, hipStream_t s) {
+  if (n == 0) return 0;
+  if (hd % 8) return -2;
+  const int hdc = hd / 8;
+  const long total = (long)n * LK * nkv * hdc;
+  kv_slot_gather_kernel<<<grid_for(total), 256, 0, s>>>((const u32x4*)cache, src, n, LK, num_blocks, nkv, bs, hdc,
+                                                        (u32x4*)buf);
+  DGI_CHECK_LAUNCH();
+  kv_slot_scatter_kernel<<<grid_for(total), 256, 0, s>>>((u32x4*)cache, dst, n, LK, num_blocks, nkv, bs, hdc,
+                                                         (const u32x4*)buf);
   DGI_CHECK_LAUNCH();
   return 0;
 }

@@ -273,7 +273,12 @@ def _varlen_meta(runner, positions, slots, block_rows, cu, ctx, device, tree_mas
 
 
 def kv_slot_copy(kv: torch.Tensor, src: torch.Tensor, dst: torch.Tensor, block_size: int) -> None:
-    """Copy token slots (all layers, K and V) inside a paged cache [L, 2, NB, nkv, bs, hd]."""
+    """Copy token slots (all layers, K and V) inside a paged cache [L, 2, NB, nkv, bs, hd]:
+    every source is read before any destination is written (a compaction chain's source can
+    be another move's destination).  GPU: two HIP kernels (kv_ops.hip: gather, scatter)."""
+    if ops._native(kv) and kv.dtype in (torch.bfloat16, torch.float16):
+        torch.ops.dgi.kv_slot_copy(kv, src.to(torch.int32).contiguous(), dst.to(torch.int32).contiguous())
+        return
     L, two, NB, nkv, bs, hd = kv.shape
     c = kv.view(L * two, NB, nkv, bs, hd)
     src, dst = src.long(), dst.long()

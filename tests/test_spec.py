@@ -213,6 +213,23 @@ def test_kv_slot_copy():
 
 
 @pytest.mark.gpu
+def test_kv_slot_copy_kernel_matches_reference_on_chains():
+    """HIP slot copy (gather then scatter) == the torch advanced-index copy, including move
+    chains where one move's source slot is another's destination, across pages and sequences."""
+    g = torch.Generator().manual_seed(3)
+    kv = torch.randn(4, 2, 9, 8, 16, 128, generator=g).to(torch.bfloat16)
+    src = torch.tensor([18, 20, 21, 37, 50, 17], dtype=torch.int32)
+    dst = torch.tensor([17, 18, 19, 33, 34, 16], dtype=torch.int32)   # 18 -> 17 while 20 -> 18, ...
+    ref = kv.clone()
+    c = ref.view(8, 9, 8, 16, 128)
+    vals = c[:, src.long() // 16, :, src.long() % 16]
+    c[:, dst.long() // 16, :, dst.long() % 16] = vals
+    gk = kv.cuda()
+    kv_slot_copy(gk, src.cuda(), dst.cuda(), 16)
+    assert torch.equal(gk.cpu(), ref)
+
+
+@pytest.mark.gpu
 def test_spec_gpu_greedy_trajectory():
     """Spec output is a greedy trajectory of the target.  Plain decode (decode
     kernel) and verification (prefill kernel) may order bf16 near-ties
