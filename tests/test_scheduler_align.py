@@ -152,3 +152,42 @@ def test_engine_with_tpot_slo_runs_smaller_mixed_steps():
     assert got == ref
     assert eng.step_budget.capped > 0 and eng.step_budget.steps > 0
     assert eng.scheduler.admit_cap is not None and eng.admission_limit() is not None
+
+
+def test_admission_limit_counts_the_queue_from_the_running_set():
+    """The closed-loop client's in-flight limit is min(cap, running now) + the prompts one
+    SLO-sized step prefills, rounded UP: while the running set ramps, at most one step of
+    prompts waits (no queue behind the cap), and rounding 1.5 prompts down to 1 would pin the
+    running set below the cap (round 5: 128 running instead of ~190 at SLO 120)."""
+    import types
+    from dgi.engine import LLMEngine
+    from dgi.sched.slo import StepBudget
+    b = StepBudget(150.0)
+    b.observe(1000, 120.0)
+    b.observe(2000, 220.0)                              # 1300 rows at the SLO
+    for _ in range(3):
+        b.observe_finished(512, 128)                    # 260 decode rows + 1040 prefill rows = 2.03 prompts
+    cap = b.admission_cap(4096)
+    fake = types.SimpleNamespace(step_budget=b, cfg=types.SimpleNamespace(max_num_batched_tokens=4096),
+                                 scheduler=types.SimpleNamespace(running=[None] * 40))
+    assert LLMEngine.admission_limit(fake) == 40 + 3     # ceil(2.03)
+    fake.scheduler.running = [None] * (cap + 50)
+    assert LLMEngine.admission_limit(fake) == cap + 3
+    fake.step_budget = None
+    assert LLMEngine.admission_limit(fake) is None
+
+
+def test_prefill_tiles_heaviest_first():
+    """Prefill-attention tiles are listed by the keys they read, most first (every head walks
+    the same order, so the grid's tail is the short tiles), covering every tile exactly once."""
+    from dgi import ops
+    cu = [0, 300, 301, 1325]                 # sequences of 300, 1, 1024 query rows
+    ctx = [300, 641, 1024]                   # the second has a 640-token cached prefix
+    t = ops.order_prefill_tiles(cu, ctx, tile=128)
+    assert t.dtype.name == "int32" and t.shape == (3 + 1 + 8, 2)
+    assert sorted(map(tuple, t.tolist())) == sorted([(0, 0), (0, 128), (0, 256), (1, 0)] +
+                                                    [(2, 128 * i) for i in range(8)])
+    work = [min(ctx[b], ctx[b] - (cu[b + 1] - cu[b]) + t0 + 128) for b, t0 in t.tolist()]
+    assert work == sorted(work, reverse=True)
+    assert t[0].tolist() == [2, 896] and t[3].tolist() == [1, 0]     # 1024 keys first; 641 after 896 / 768
+    assert ops.prefill_tiles([0, 5], tile=128) == [(0, 0)]
