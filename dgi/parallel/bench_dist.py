@@ -248,12 +248,14 @@ class TokenLog:
         self.firsts: list = []         # (time, ttft) of first tokens produced here
         self.finished: list = []       # requests finished here
         self.steps: list = []          # end time of every engine step that ran
+        self.seen: dict = {}           # every request this rank produced a token for
 
     def outputs(self, outs, count_first: bool = True) -> int:
         for o in outs:
             r = o.request
             t = r.token_times[-1] if r.token_times else time.perf_counter()
             self.times.append(t)
+            self.seen[id(r)] = r
             if count_first and len(r.output) == 1 and r.ttft is not None:
                 self.firsts.append((t, r.ttft))
             if o.finished:
@@ -265,7 +267,8 @@ class TokenLog:
         fin = [r for r in self.finished if r.finish_time is not None and inw(r.finish_time)]
         return {"tokens": sum(1 for t in self.times if inw(t)),
                 "ttfts": [v for t, v in self.firsts if inw(t)],
-                "tpots": _tpots(fin), "e2es": [r.finish_time - r.arrival for r in fin],
+                "tpots": _window_tpots(self.seen.values(), t0, t1),
+                "e2es": [r.finish_time - r.arrival for r in fin],
                 "steps_in_window": sum(1 for t in self.steps if inw(t))}
 
 
@@ -343,11 +346,13 @@ def _run_pp(args, f, cfg, layout, role, sp, rng, conc):
 
 # ---------------------------------------------------------------------------- P/D (+ decode pipelines)
 
-def _tpots(reqs) -> list:
-    """Mean inter-token time (s) of each finished request with >= 2 tokens."""
+def _window_tpots(reqs, t0: float, t1: float) -> list:
+    """Mean inter-token time (s) of every request with >= 2 tokens inside [t0, t1], finished or
+    not.  A window of ~20 node steps is far shorter than a 128-token generation at a 100+ ms
+    TPOT, so counting finished requests only would leave TPOT unmeasured (round-5 rehearsal)."""
     out = []
     for r in reqs:
-        tt = r.token_times
+        tt = [t for t in r.token_times if t0 <= t <= t1]
         if len(tt) >= 2:
             out.append((tt[-1] - tt[0]) / (len(tt) - 1))
     return out
@@ -483,6 +488,7 @@ def _run_pd(args, f, cfg, layout, role, sp, rng, conc):
                     seen[o.rid] = o.request
                 r = o.request
                 log.times.append(r.token_times[-1] if r.token_times else time.perf_counter())
+                log.seen[id(r)] = r
                 if o.rid in drv.local_used and len(r.output) == 1 and r.ttft is not None:
                     log.firsts.append((log.times[-1], r.ttft))
                 if o.finished:

@@ -40,7 +40,20 @@ def test_bench_pd_layouts_on_gloo(n, args):
     d = json.loads(line)
     assert d["n_gpus"] == n and d["value"] > 0
     assert d["extra"]["layout"]["kind"] in ("pd", "pdpp")
+    assert d["tpot_p50_ms"] is not None and d["tpot_p50_ms"] > 0     # in-window inter-token times
     _check_metric_fields(d)
+
+
+def test_window_tpot_counts_unfinished_requests():
+    """TPOT samples come from every request with >= 2 tokens inside the window, finished or not
+    (a 20-step window is shorter than one 128-token generation on the 8-GPU layouts)."""
+    import types
+    from dgi.parallel.bench_dist import _window_tpots
+    a = types.SimpleNamespace(token_times=[0.0, 1.0, 2.0, 3.0, 4.0])       # running, 3 in window
+    b = types.SimpleNamespace(token_times=[1.5, 5.0])                       # one token in window
+    c = types.SimpleNamespace(token_times=[2.0, 2.5, 3.5])                  # all in window
+    got = _window_tpots([a, b, c], 1.0, 3.6)
+    assert got == [1.0, 0.75]
 
 
 def _check_metric_fields(d):
