@@ -1123,6 +1123,29 @@ def hot_vocab_from_targets(tgts: torch.Tensor, vocab: int, size: int) -> torch.T
     return order[:min(size, vocab)].sort().values
 
 
+AUTO_VOCAB_SIZES = (8192, 16384, 32768, 65536)
+AUTO_VOCAB_COVERAGE = 0.99
+
+
+def auto_draft_vocab(tgts: torch.Tensor, vocab: int, coverage: float = AUTO_VOCAB_COVERAGE,
+                     sizes: tuple = AUTO_VOCAB_SIZES) -> int:
+    """Smallest draft vocabulary (of ``sizes``) whose most frequent target tokens cover
+    ``coverage`` of the training corpus's target choices; 0 (the whole vocabulary) when none
+    does.  A draft scoring 32k of Llama-3's 128k tokens streams a quarter of the LM head per
+    draft depth (6 x 180 us per batch-1 spec step with the full head, profiles/r5_spec/); on a
+    target whose choices spread over the vocabulary the hot set would cap acceptance instead
+    (48 % coverage at 32k on the random-init bench target), so the full head stays."""
+    counts = torch.bincount(tgts.reshape(-1).long().cpu(), minlength=vocab).float()
+    total = float(counts.sum())
+    if total <= 0:
+        return 0
+    csum = torch.cumsum(counts.sort(descending=True).values, 0)
+    for n in sizes:
+        if n < vocab and float(csum[n - 1]) / total >= coverage:
+            return int(n)
+    return 0
+
+
 def train_draft(engine: SpecEngine, steps: int = 200, batch: int = 8, prompt_len: int = 64, gen_len: int = 192,
                 unroll: int = 3, lr: float = 1e-3, num_seqs: int = 64, random_seqs: int = 0, seed: int = 0,
                 log=None, draft_vocab: int = 0) -> dict:
@@ -1176,6 +1199,8 @@ def train_draft(engine: SpecEngine, steps: int = 200, batch: int = 8, prompt_len
     with torch.no_grad():
         dr.load({k: v.detach() for k, v in P.items()})
     hot = None
+    if draft_vocab < 0:
+        draft_vocab = auto_draft_vocab(tgts, V)
     if 0 < draft_vocab < V:
         hot_ids = hot_vocab_from_targets(tgts, V, draft_vocab)
         dr.set_hot_vocab(hot_ids)

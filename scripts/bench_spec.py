@@ -67,9 +67,10 @@ def main():
     ap.add_argument("--no-adaptive", action="store_true", help="fixed tree depth")
     ap.add_argument("--sampled", action="store_true",
                     help="also run seeded temperature 0.8 / top-k 50 / top-p 0.9 requests (coupled verification)")
-    ap.add_argument("--draft-vocab", type=int, default=0,
+    ap.add_argument("--draft-vocab", type=int, default=-1,
                     help="EAGLE-3 draft vocabulary: the N token ids the target chose most often in the draft's "
-                         "training corpus (0 = the whole vocabulary)")
+                         "training corpus (0 = the whole vocabulary; -1 = the smallest of 8k/16k/32k/64k covering "
+                         "99 %% of the corpus, else the whole vocabulary)")
     ap.add_argument("--save-draft", default=None, help="write the trained draft (torch.save, tensors only)")
     ap.add_argument("--load-draft", default=None, help="skip training: load a draft --save-draft wrote for this target")
     ap.add_argument("--out", default=None)

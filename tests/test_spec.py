@@ -387,3 +387,16 @@ def test_draft_vocabulary_keeps_spec_lossless_and_restricts_proposals():
     se._draft_tree_eager = spy
     assert [r.output for r in se.generate(_prompts(), sp)] == ref
     assert seen and all(t in hot for s in seen for t in s)
+
+
+def test_auto_draft_vocabulary_picks_the_smallest_covering_size():
+    """draft_vocab=-1: the smallest candidate size whose most frequent target tokens cover 99 % of
+    the training corpus; the whole vocabulary when the target's choices are spread out."""
+    from dgi.spec.eagle3 import auto_draft_vocab
+    V = 1000
+    g = torch.Generator().manual_seed(0)
+    peaked = torch.randint(0, 40, (5000,), generator=g)             # 40 distinct tokens
+    assert auto_draft_vocab(peaked, V, sizes=(16, 64, 256)) == 64
+    spread = torch.randint(0, V, (5000,), generator=g)
+    assert auto_draft_vocab(spread, V, sizes=(16, 64, 256)) == 0
+    assert auto_draft_vocab(torch.zeros(0, dtype=torch.long), V) == 0
