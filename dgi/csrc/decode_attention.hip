@@ -107,16 +107,22 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_kernel(
   const int g = lane >> 4;
   uint16_t* vt = reinterpret_cast<uint16_t*>(smem + w * WREG);
 
-  // Q fragments (B operand): B[k = 8g + j][col = query qi] = Q[qi][32 s + 8 g + j]
+  // Q fragments (B operand): B[k = 8g + j][col = query qi] = Q[qi][32 s + 8 g + j].  The 8-wave
+  // one-split variant (small batch, short context: one or two tiles per wave) issues them after
+  // its first tile's K/V loads, so the two round trips overlap instead of running back to back.
   u32x4 qf[KS];
+  auto load_q = [&]() {
 #pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    if (qi < G) {
-      qf[s] = *reinterpret_cast<const u32x4*>(q + (size_t)b * q_stride + (h * G + qi) * HD + 32 * s + 8 * g);
-    } else {
-      qf[s] = u32x4{0, 0, 0, 0};
+    for (int s = 0; s < KS; ++s) {
+      if (qi < G) {
+        qf[s] = *reinterpret_cast<const u32x4*>(q + (size_t)b * q_stride + (h * G + qi) * HD + 32 * s + 8 * g);
+      } else {
+        qf[s] = u32x4{0, 0, 0, 0};
+      }
     }
-  }
+  };
+  constexpr bool LATE_Q = NW == 8;
+  if (!LATE_Q) load_q();
 
   const int* bt = block_tables + (size_t)b * bt_stride;
   const size_t head_stride = (size_t)bs * HD;
@@ -182,6 +188,7 @@ __global__ __launch_bounds__(64 * NW) void paged_decode_kernel(
         vr[k] = *reinterpret_cast<const u32x4*>(vpl + ch * 8);
       }
     }
+    if (LATE_Q && t == w) load_q();
     // ---- S^T = K Q^T
     f32x4 sacc[2];
 #pragma unroll
