@@ -419,7 +419,8 @@ def main(argv=None) -> int:
             from dgi.parallel.pipeline import StageWorker
             cfg = EngineConfig(model=args.model, device=str(fabric.device), max_num_seqs=args.max_num_seqs,
                                max_num_batched_tokens=args.max_batched_tokens, max_model_len=args.max_model_len,
-                               use_graphs=False, seed=args.seed, enable_prefix_caching=False)
+                               use_graphs=str(fabric.device).startswith("cuda") and not args.no_graphs,
+                               seed=args.seed, enable_prefix_caching=False)
             w = StageWorker(cfg, fabric, layout.group_of(fabric.rank), kv_sources=layout.prefill_ranks)
             while w.run() != "stop":
                 pass
