@@ -48,6 +48,8 @@ int dgi_kv_gather(const void* cache, const int* ids, int n, int LK, int num_bloc
                   void* buf, hipStream_t s);
 int dgi_kv_scatter(void* cache, const int* ids, int n, int LK, int num_blocks, int page_elems,
                    const void* buf, hipStream_t s);
+int dgi_mall_prefetch(const void* base, const int* rows, int nrows, int row_bytes, int blocks, void* sink,
+                      hipStream_t s);
 int dgi_kv_slot_copy(void* cache, const int* src, const int* dst, int n, int LK, int num_blocks, int nkv, int bs,
                      int hd, void* buf, hipStream_t s);
 int dgi_kv_copy(void* cache, const int* src, const int* dst, int n, int LK, int num_blocks,
@@ -438,6 +440,26 @@ void kv_slot_copy(at::Tensor cache, const at::Tensor& src, const at::Tensor& dst
                             buf.data_ptr(), cur_stream()), "kv_slot_copy");
 }
 
+// read `w`'s rows (all, the first `nrows`, or the ids in `rows`) so they sit in the MALL
+void mall_prefetch(const at::Tensor& w, const c10::optional<at::Tensor>& rows, at::Tensor sink, int64_t nrows,
+                   int64_t blocks) {
+  check_dev(w, "w"); check_dev(sink, "sink");
+  TORCH_CHECK(w.dim() == 2 && w.stride(1) == 1, "mall_prefetch: w must be a row-major matrix");
+  TORCH_CHECK(sink.numel() * sink.element_size() >= 1024, "mall_prefetch: sink needs 1 KB");
+  const int* rp = nullptr;
+  int n = (int)w.size(0);
+  if (rows.has_value()) {
+    check_i32(*rows, "rows");
+    rp = rows->data_ptr<int>();
+    n = (int)rows->numel();
+  }
+  if (nrows >= 0 && nrows < n) n = (int)nrows;
+  const int64_t rb = w.stride(0) * w.element_size();
+  TORCH_CHECK(rb < (1LL << 31), "mall_prefetch: row too long");
+  check_rc(dgi_mall_prefetch(w.data_ptr(), rp, n, (int)rb, (int)blocks, sink.data_ptr(), cur_stream()),
+           "mall_prefetch");
+}
+
 void tree_mask(at::Tensor anc, at::Tensor depth, const at::Tensor& parent) {
   check_i32(parent, "parent"); check_i32(depth, "depth");
   TORCH_CHECK(anc.scalar_type() == at::kLong && anc.is_contiguous());
@@ -501,6 +523,7 @@ TORCH_LIBRARY(dgi, m) {
   m.def("kv_scatter(Tensor(a!) cache, Tensor ids, Tensor buf) -> ()");
   m.def("kv_copy(Tensor(a!) cache, Tensor src, Tensor dst) -> ()");
   m.def("kv_slot_copy(Tensor(a!) cache, Tensor src, Tensor dst) -> ()");
+  m.def("mall_prefetch(Tensor w, Tensor? rows, Tensor(a!) sink, int nrows=-1, int blocks=256) -> ()");
   m.def("tree_mask(Tensor(a!) anc, Tensor(b!) depth, Tensor parent) -> ()");
   m.def("tree_verify(Tensor(a!) accept_len, Tensor(b!) path, Tensor(c!) out_tokens, Tensor parent, "
         "Tensor draft, Tensor target, Tensor anc, Tensor depth) -> ()");
@@ -524,6 +547,7 @@ TORCH_LIBRARY_IMPL(dgi, CUDA, m) {
   m.impl("kv_scatter", &kv_scatter);
   m.impl("kv_copy", &kv_copy);
   m.impl("kv_slot_copy", &kv_slot_copy);
+  m.impl("mall_prefetch", &mall_prefetch);
   m.impl("tree_mask", &tree_mask);
   m.impl("tree_verify", &tree_verify);
 }

@@ -525,6 +525,21 @@ def decode_proj(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return linear(x, w)
 
 
+_PREFETCH_SINKS: dict = {}
+
+
+def mall_prefetch(w: torch.Tensor, rows: Optional[torch.Tensor] = None, nrows: int = -1, blocks: int = 256) -> None:
+    """Read ``w``'s rows (all, the first ``nrows``, or the int32 ids ``rows``) so that a later
+    kernel finds them in the memory-side cache (dgi/csrc/prefetch.hip).  Nothing is written;
+    a no-op off the native path."""
+    if not _native(w):
+        return
+    sink = _PREFETCH_SINKS.get(w.device)
+    if sink is None:
+        sink = _PREFETCH_SINKS[w.device] = torch.zeros(256, dtype=torch.int32, device=w.device)
+    _call("mall_prefetch", w, rows, sink, nrows, blocks)
+
+
 def silu_mul_ref(gu: torch.Tensor) -> torch.Tensor:
     I = gu.shape[-1] // 2
     g = gu[..., :I].float()

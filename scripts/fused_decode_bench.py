@@ -189,6 +189,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--cfgs", type=int, nargs="+", default=[0, 2, 3, 4, 5])
     ap.add_argument("--skip-attn", action="store_true")
+    ap.add_argument("--skip-gemms", action="store_true", help="skip the fused qkv / gate_up table")
     ap.add_argument("--plain-fused", action="store_true", help="also o-proj / down through fused_skinny configs")
     ap.add_argument("--plain", action="store_true", help="only the plain skinny-vs-hipBLASLt table")
     a = ap.parse_args()
@@ -200,7 +201,7 @@ def main():
             with open(a.out, "w") as f:
                 json.dump(res, f, indent=1)
         return
-    res = {"gemm_8b": bench_gemms(4096, 14336, 32, 8, [1, 2, 4, 8, 16], a.cfgs)}
+    res = {} if a.skip_gemms else {"gemm_8b": bench_gemms(4096, 14336, 32, 8, [1, 2, 4, 8, 16], a.cfgs)}
     if a.plain_fused:
         res["plain_fused_8b"] = bench_plain_fused([("o", 4096, 4096), ("down", 4096, 14336)], [1, 4, 8], a.cfgs)
     if not a.skip_attn:

@@ -16,4 +16,5 @@ step() {  # name, timeout, command...
 step tests 400 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "paged_decode or decode or lookahead"
 step attn_b1 300 python -u scripts/decode_attn_b1.py
 step declat8b 600 python -u scripts/decode_latency.py --batch 1 4 16 --out $O/declat8b.json
+step profdec 600 rocprofv3 --kernel-trace --stats -d $O/profdec -o run -- python3 -u scripts/decode_latency.py --batch 1 --steps 200
 echo ALLDONE

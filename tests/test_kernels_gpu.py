@@ -627,6 +627,19 @@ def test_fused_decode_model_matches_unfused():
         assert _teacher_forced_ok("llama-tiny-hd128", src, prompts, o) == 64
 
 
+def test_mall_prefetch_reads_only():
+    """The MALL warm-up kernel reads the listed rows and writes nothing (sink stays zero)."""
+    ops.load_native(required=True)
+    w = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+    ref = w.clone()
+    rows = torch.tensor([0, 17, 4095, 2048], dtype=torch.int32, device="cuda")
+    for kw in ({}, {"nrows": 100}, {"rows": rows}, {"blocks": 7}):
+        ops.mall_prefetch(w, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(w, ref)
+    assert int(ops._PREFETCH_SINKS[w.device].abs().sum()) == 0
+
+
 @pytest.mark.parametrize("sampled", [False, True])
 def test_decode_lookahead_matches_plain_decode(sampled, monkeypatch):
     """Decode lookahead (step N+1 launched before step N's tokens are back) gives the same
