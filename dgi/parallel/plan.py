@@ -172,6 +172,24 @@ class RoleCapacity:
     prefill_steps: dict = dataclasses.field(default_factory=dict)
     prompt_len: int = 512
     output_len: int = 128
+    # every measured decode microbatch size per stage count: k -> [[rows, tok_s, step_ms], ...]
+    # (the start-up probe fills it; the planner picks the rows per layout, ``decode_choices``)
+    decode_options: dict = dataclasses.field(default_factory=dict)
+
+    def decode_choices(self, k: int) -> list:
+        """(rows, tok_s, stage step ms) options of a k-stage decode replica."""
+        opts = self.decode_options.get(k) or self.decode_options.get(str(k))
+        if opts:
+            return [tuple(o) for o in opts]
+        if k not in self.decode_tok_s:
+            return []
+        return [(self.decode_rows.get(k), self.decode_tok_s[k], self.decode_step_ms.get(k, 0.0))]
+
+    def with_decode(self, k: int, rows, tok_s: float, step_ms: float) -> "RoleCapacity":
+        """This capacity with the k-stage replica run at ``rows``-row microbatches."""
+        return dataclasses.replace(self, decode_tok_s={**self.decode_tok_s, k: tok_s},
+                                   decode_step_ms={**self.decode_step_ms, k: step_ms},
+                                   decode_rows={**self.decode_rows, k: rows})
 
     def steps(self) -> dict:
         return dict(self.prefill_steps) or {self.prefill_mbt: self.prefill_step_ms}
@@ -207,6 +225,30 @@ CAPACITY = {
                               decode_step_ms={1: 32.4, 2: 18.2, 3: 11.2}, decode_rows={1: 1024, 2: 1024, 3: 768},
                               mixed_step_ms=30.6),
 }
+
+
+HBM_BYTES = 288e9           # one MI355X
+
+
+def decode_pool_seqs(model: str, stages: int, prompt_len: int = 512, output_len: int = 128,
+                     hbm_bytes: float = HBM_BYTES, kv_fraction: float = 0.9, workspace: float = 8 * 2 ** 30,
+                     block_size: int = 16) -> Optional[int]:
+    """Full-length sequences one stage of a ``stages``-deep decode replica keeps in its KV pool
+    (as ``engine.engine_block_budget`` sizes it: ``kv_fraction`` of HBM after the stage's bf16
+    weights and the workspace).  A replica holds its k microbatches in every stage, so k x rows
+    must fit; None for a model without a config."""
+    from dgi.models.config import get_config
+    try:
+        mc = get_config(model.split("@")[0])
+    except Exception:       # noqa: BLE001 - unknown model: no constraint
+        return None
+    L = mc.num_layers
+    layers = -(-L // stages)
+    weights = 2.0 * mc.param_count() * layers / L
+    pool = max(0.0, hbm_bytes - weights - workspace) * kv_fraction
+    pages = -(-(prompt_len + output_len) // block_size)
+    per_seq = pages * block_size * mc.kv_bytes_per_token(layers=layers)
+    return int(pool // per_seq)
 
 
 _MEASURED: dict = {}     # model -> RoleCapacity measured at start-up (dgi.parallel.probe)
@@ -313,6 +355,7 @@ def choose_pd_layout(n_gpus: int, cap: RoleCapacity, max_stages: int = 3, prefer
 # unless its rate falls below PD_MIN_RATIO x data parallel.
 LATENCY_FRAC = float(os.environ.get("DGI_PD_LATENCY_FRAC", "0.7"))
 FILL_WEIGHT = 0.8
+TOK_TIE = 0.01
 # 0.85: below the ~0.9 x DP the kernels allow a P/D node on 70B (a decode row costs 1.86 us per
 # layer vs a mixed row's 1.33: profiles/r5_pd/README.md) and below the start-up probe's ~5 %
 # optimism about DP mixed steps
@@ -357,17 +400,26 @@ def plan_pd(n_gpus: int, cap: RoleCapacity, max_stages: int = 3, lat_frac: Optio
     for npre in range(1, n_gpus):
         left = n_gpus - npre
         for k in range(1, max_stages + 1):
-            if left % k or k not in cap.decode_tok_s:
+            if left % k:
                 continue
-            for mbt in sorted(cap.steps()):
-                c = pd_candidate(npre, k, left // k, mbt, cap)
-                c["latency_ok"] = bool(dp["ttft_ms"] and c["ttft_ms"] and c["tpot_ms"]
-                                       and c["ttft_ms"] <= lat * dp["ttft_ms"] and c["tpot_ms"] <= lat * dp["tpot_ms"])
-                cands.append(c)
+            # the decode microbatch size is a planner output too: every measured row count
+            for rows, ts, st in cap.decode_choices(k):
+                ck = cap.with_decode(k, rows, ts, st)
+                for mbt in sorted(cap.steps()):
+                    c = pd_candidate(npre, k, left // k, mbt, ck)
+                    c["decode_rows"] = rows
+                    c["latency_ok"] = bool(dp["ttft_ms"] and c["ttft_ms"] and c["tpot_ms"]
+                                           and c["ttft_ms"] <= lat * dp["ttft_ms"]
+                                           and c["tpot_ms"] <= lat * dp["tpot_ms"])
+                    cands.append(c)
     if not cands:
         return None, dp, []
     ok = [c for c in cands if c["latency_ok"]] or cands
-    best = max(ok, key=lambda c: (c["tok_s"], -(c["tpot_ms"] or 0), -(c["ttft_ms"] or 0)))
+    # fastest; candidates within TOK_TIE of it count as tied and the lowest TPOT, then TTFT, wins
+    # (a 512-row decode microbatch at the rate of a 768-row one is two-thirds the TPOT)
+    top = max(c["tok_s"] for c in ok)
+    near = [c for c in ok if c["tok_s"] >= (1.0 - TOK_TIE) * top]
+    best = min(near, key=lambda c: (c["tpot_ms"] or 0, c["ttft_ms"] or 0, -c["tok_s"]))
     best = dict(best, vs_dp=round(best["tok_s"] / dp["tok_s"], 3) if dp["tok_s"] else None)
     return best, dp, cands
 

@@ -195,15 +195,21 @@ def capacity_from_probe(p: ProbeResult, num_layers: Optional[int] = None, max_st
     t_pre = t(p.prefill)
     prompts_per_step = max(1, p.prefill_mbt // p.prompt_len)
     prefill_tok_s = prompts_per_step / (t_pre / 1e3) * p.output_len
-    rows = sorted(p.decode)
+    rows = sorted(int(r) for r in p.decode)
+    fit = {int(r): v for r, v in p.decode.items()}
     r1 = rows[0]
-    rk = rows[-1]
-    dec, step, drows = {}, {}, {}
+    dec, step, drows, opts = {}, {}, {}, {}
+    from dgi.parallel.plan import decode_pool_seqs
     for k in range(1, max_stages + 1):
-        R = r1 if k == 1 else rk
-        td = t(p.decode[R])
-        dec[k] = round(k * R / (td / 1e3), 1)
-        step[k] = round(td / k, 2)
+        # microbatch sizes whose k in-flight microbatches fit one stage's KV pool (the smallest
+        # probed size always stays: the engine caps a replica by its credits anyway)
+        pool = decode_pool_seqs(p.model, k, p.prompt_len, p.output_len)
+        fits = [R for R in rows if pool is None or k * R <= pool] or rows[:1]
+        opts[k] = [[R, round(k * R / (t(fit[R]) / 1e3), 1), round(t(fit[R]) / k, 2)] for R in fits]
+        # default (no planner choice): the smallest microbatch for a whole-model decode GPU (its
+        # KV pool), the largest for a pipeline
+        R = r1 if k == 1 else max(o[0] for o in opts[k])
+        _, dec[k], step[k] = next(o for o in opts[k] if o[0] == R)
         drows[k] = R
     t_mix = t(p.mixed)
     psteps = {p.prefill_mbt: round(t_pre, 2)}
@@ -213,7 +219,7 @@ def capacity_from_probe(p: ProbeResult, num_layers: Optional[int] = None, max_st
                         mixed_tok_s=round(p.mixed_rows / (t_mix / 1e3), 1), prefill_step_ms=round(t_pre, 2),
                         prefill_mbt=p.prefill_mbt, decode_step_ms=step, decode_rows=drows,
                         mixed_step_ms=round(t_mix, 2), prefill_steps=psteps, prompt_len=p.prompt_len,
-                        output_len=p.output_len)
+                        output_len=p.output_len, decode_options=opts)
 
 
 def median_capacity(caps: list):
@@ -229,7 +235,10 @@ def median_capacity(caps: list):
         prefill_mbt=c0.prefill_mbt, decode_step_ms={k: med([c.decode_step_ms[k] for c in caps]) for k in c0.decode_step_ms},
         decode_rows=dict(c0.decode_rows), mixed_step_ms=med([c.mixed_step_ms for c in caps]),
         prefill_steps={m: med([c.steps()[m] for c in caps]) for m in c0.steps()},
-        prompt_len=c0.prompt_len, output_len=c0.output_len)
+        prompt_len=c0.prompt_len, output_len=c0.output_len,
+        decode_options={k: [[o[0], med([c.decode_options[k][i][1] for c in caps]),
+                             med([c.decode_options[k][i][2] for c in caps])] for i, o in enumerate(v)]
+                        for k, v in c0.decode_options.items()})
 
 
 def plan_from_probe(world: int, cap, min_ratio: Optional[float] = None, lat_frac: Optional[float] = None) -> dict:
@@ -248,7 +257,8 @@ def plan_from_probe(world: int, cap, min_ratio: Optional[float] = None, lat_frac
     hybrid = best["filler_share"] > MAX_FILLER_SHARE
     pd_ok = best["latency_ok"] and ratio >= min_ratio and not hybrid
     kind = ("pdpp" if best["decode_stages"] > 1 else "pd") if pd_ok else "dp"
-    why = (f"P/D {best['layout']} at {best['prefill_mbt']}-token prefill steps: est {best['tok_s']:.0f} tok/s = "
+    why = (f"P/D {best['layout']} at {best['prefill_mbt']}-token prefill steps, "
+           f"{best.get('decode_rows')}-row decode microbatches: est {best['tok_s']:.0f} tok/s = "
            f"{ratio:.2f} x DP {dp['tok_s']:.0f}, TTFT {best['ttft_ms']} vs {dp['ttft_ms']} ms, TPOT "
            f"{best['tpot_ms']} vs {dp['tpot_ms']} ms -> {kind}"
            + ("" if best["latency_ok"] else " (no split meets the latency bound)")
@@ -256,5 +266,6 @@ def plan_from_probe(world: int, cap, min_ratio: Optional[float] = None, lat_frac
            + (f" (filler share {best['filler_share']:.2f} > {MAX_FILLER_SHARE:g}: a hybrid, not a split)"
               if hybrid else ""))
     return {"kind": kind, "prefill_ranks": best["prefill_ranks"], "decode_stages": best["decode_stages"],
-            "decode_replicas": best["decode_replicas"], "prefill_mbt": best["prefill_mbt"], "estimate": best,
+            "decode_replicas": best["decode_replicas"], "prefill_mbt": best["prefill_mbt"],
+            "decode_rows": best.get("decode_rows"), "estimate": best,
             "dp_reference": dp, "dp_tok_s": dp["tok_s"], "reason": why}

@@ -865,6 +865,42 @@ def test_capacity_from_probe_and_median():
     assert median_capacity([c, c3, c2]).prefill_tok_s == round(c2.prefill_tok_s, 2)
 
 
+def test_planner_picks_decode_microbatch_rows_within_the_kv_pool():
+    """Decode microbatch rows are a planner output: every probed row count whose k in-flight
+    microbatches fit a stage's KV pool is an option (70B: a whole-model decode GPU holds ~590
+    sequences, a 2-stage replica's stage ~1790), and near-ties in tok/s go to the lower TPOT."""
+    import dataclasses
+    from dgi.parallel.plan import decode_pool_seqs, plan_pd
+    from dgi.parallel.probe import ProbeResult, capacity_from_probe, median_capacity, plan_from_probe
+    assert 550 < decode_pool_seqs("llama3-70b", 1) < 640 and 1700 < decode_pool_seqs("llama3-70b", 2) < 1900
+    p = ProbeResult(model="llama3-70b", prefill=(0.0, 2.5), decode={512: (2.0, 0.98), 768: (2.4, 1.45),
+                                                                    1024: (2.8, 1.80)},
+                    mixed=(1.4, 2.4), prefill_mbt=2048, mixed_rows=384, prompt_len=512, output_len=128,
+                    layers=(4, 8), seconds=1.0, prefill_more={1024: (0.0, 1.36)})
+    c = capacity_from_probe(p)
+    assert [o[0] for o in c.decode_choices(1)] == [512]
+    assert [o[0] for o in c.decode_choices(2)] == [512, 768] and [o[0] for o in c.decode_choices(3)] == [512, 768]
+    assert c.decode_rows == {1: 512, 2: 768, 3: 768}       # defaults: smallest / largest that fits
+    assert median_capacity([c, c, c]).decode_options == c.decode_options
+    best, _dp, cands = plan_pd(8, c)
+    assert {x["decode_rows"] for x in cands if x["decode_stages"] == 2} == {512, 768}
+    assert best["decode_rows"] in (512, 768)
+    d = plan_from_probe(8, c)
+    assert d["decode_rows"] == best["decode_rows"] and "-row decode microbatches" in d["reason"]
+    # a 512-row option within 1 % of the 768-row rate wins on TPOT; 5 % slower loses
+    o2 = {k: [list(o) for o in v] for k, v in c.decode_options.items()}
+    r768 = next(o for o in o2[2] if o[0] == 768)
+    for scale, want in ((0.995, 512), (0.95, 768)):
+        for o in o2[2]:
+            if o[0] == 512:
+                o[1] = round(r768[1] * scale, 1)
+                o[2] = round(r768[2] * 512 / 768 / scale, 2)
+        cc = dataclasses.replace(c, decode_options={k: [list(o) for o in v] for k, v in o2.items()})
+        b, _dp, _c = plan_pd(8, cc, max_stages=2)
+        if b["decode_stages"] == 2:
+            assert b["decode_rows"] == want, (scale, b)
+
+
 def test_probe_runs_the_real_engine_on_cpu():
     """The probe path end to end (shortened model copies, adopted decode rows, mixed
     steps) on the CPU model: numbers are meaningless here, the plumbing is not."""
