@@ -111,14 +111,14 @@ def run_distributed(args, layout_kind: str, dist):
     ctrl_rtt = ctrl_ping(f, 0, world - 1)
     # model load (+ graph capture) of this rank's role
     phase("engine_build", float(os.environ.get("DGI_BUILD_S", "300")))
-    # decode-side concurrency: one microbatch of 768 rows per decode stage keeps the
-    # decode GEMMs out of the small-M regime (70B down-proj: 0.76 PF/s at M=512,
-    # 1.28 at 1024); a single decode GPU is capped by its KV pool (credits) instead
+    # decode-side concurrency: k microbatches of the rows the plan priced (a planner output on
+    # the 256-row GEMM tile: 512 rows on a whole-model decode GPU, whose KV pool holds ~590
+    # sequences, 768 per microbatch of a pipeline; ``plan.plan_pd``)
     k = len(layout.decode_groups[0]) if layout.decode_groups else 1
     from dgi.parallel.plan import capacity_for
     cap = capacity_for(args.model)
     rows = (cap.decode_rows.get(k) if cap is not None else None) or 768
-    conc = args.concurrency or (rows * k if k > 1 else 1024)
+    conc = args.concurrency or rows * k
     # staged rehearsal: every rank shares one GPU, so each takes a slice of its memory
     from dgi.parallel.fabric import shared_gpu
     kv_frac = float(os.environ.get("DGI_KV_FRACTION", 0.35 / world if (f.staged or shared_gpu()) else 0.9))

@@ -213,13 +213,22 @@ CAPACITY = {
     # (profiles/r3_gemm/pd_capacity_70b.jsonl, bench70b_token_align256.json): the mixed (DP) GPU
     # gained 5.5 % (1760 -> 1857 tok/s), the prefill and decode roles ~1 %.
     # r5 (profiles/r5_pd/probe70b_r5.json): start-up probe on one MI355X — prefill at 2048 and
-    # 1024 tokens per step (201.5 / 109.1 ms), decode replicas at 576 / 768-row microbatches;
-    # the mixed (DP) rate and step are the 1-GPU bench's (1,871 tok/s, 204.7 ms: the probe's
-    # short-model extrapolation reads mixed steps ~5 % fast, 1,968 tok/s / 195.1 ms).
-    "llama3-70b": RoleCapacity(prefill_tok_s=2540.5, decode_tok_s={1: 5885.8, 2: 12937.6, 3: 19406.5},
-                               mixed_tok_s=1871.0, prefill_step_ms=201.5, prefill_mbt=2048,
-                               decode_step_ms={1: 97.9, 2: 59.4, 3: 39.6}, decode_rows={1: 576, 2: 768, 3: 768},
-                               mixed_step_ms=204.7, prefill_steps={2048: 201.5, 1024: 109.1}),
+    # 1024 tokens per step, decode replicas at 576 / 768-row microbatches; the mixed (DP) rate and
+    # step are the 1-GPU bench's (1,871 tok/s, 204.7 ms: the probe's short-model extrapolation
+    # reads mixed steps ~5 % fast).  Re-probed with 256-row-aligned decode microbatches, median of
+    # two runs on one box (profiles/r5_pd/probe70b_s23_run1/2.log): 512 rows cost 1.91 us per row
+    # per layer against 2.02-2.20 at 576 (past the 512-row GEMM tile step) and 1.86 at 768; a
+    # whole-model decode GPU's KV pool holds ~590 sequences, a 2-stage replica's stage ~1,790
+    # (``decode_pool_seqs``), so 1,024-row microbatches fit no layout.
+    "llama3-70b": RoleCapacity(prefill_tok_s=2588.6, decode_tok_s={1: 6381.5, 2: 13138.4, 3: 19707.6},
+                               mixed_tok_s=1871.0, prefill_step_ms=197.8, prefill_mbt=2048,
+                               decode_step_ms={1: 80.2, 2: 58.5, 3: 39.0}, decode_rows={1: 512, 2: 768, 3: 768},
+                               mixed_step_ms=204.7, prefill_steps={2048: 197.8, 1024: 106.0},
+                               decode_options={1: [[512, 6381.5, 80.2], [576, 5837.7, 98.8]],
+                                               2: [[512, 12762.9, 40.1], [576, 11675.3, 49.4],
+                                                   [768, 13138.4, 58.5]],
+                                               3: [[512, 19144.4, 26.7], [576, 17513.0, 33.0],
+                                                   [768, 19707.6, 39.0]]}),
     "llama3-8b": RoleCapacity(prefill_tok_s=176.2 * 128, decode_tok_s={1: 31566.0, 2: 58028.0, 3: 69373.0},
                               mixed_tok_s=11842.0, prefill_step_ms=45.4, prefill_mbt=4096,
                               decode_step_ms={1: 32.4, 2: 18.2, 3: 11.2}, decode_rows={1: 1024, 2: 1024, 3: 768},
@@ -355,7 +364,10 @@ def choose_pd_layout(n_gpus: int, cap: RoleCapacity, max_stages: int = 3, prefer
 # unless its rate falls below PD_MIN_RATIO x data parallel.
 LATENCY_FRAC = float(os.environ.get("DGI_PD_LATENCY_FRAC", "0.7"))
 FILL_WEIGHT = 0.8
-TOK_TIE = 0.01
+# estimates within TOK_TIE of the fastest count as tied (the latency decides): the start-up
+# probe's own run-to-run spread on one box is ~3 % (profiles/r5_pd/probe70b_s23_run1/2.log:
+# 8-GPU estimates 13.70k / 14.10k tok/s)
+TOK_TIE = float(os.environ.get("DGI_PD_TOK_TIE", "0.02"))
 # 0.85: below the ~0.9 x DP the kernels allow a P/D node on 70B (a decode row costs 1.86 us per
 # layer vs a mixed row's 1.33: profiles/r5_pd/README.md) and below the start-up probe's ~5 %
 # optimism about DP mixed steps
@@ -415,11 +427,14 @@ def plan_pd(n_gpus: int, cap: RoleCapacity, max_stages: int = 3, lat_frac: Optio
     if not cands:
         return None, dp, []
     ok = [c for c in cands if c["latency_ok"]] or cands
-    # fastest; candidates within TOK_TIE of it count as tied and the lowest TPOT, then TTFT, wins
-    # (a 512-row decode microbatch at the rate of a 768-row one is two-thirds the TPOT)
-    top = max(c["tok_s"] for c in ok)
-    near = [c for c in ok if c["tok_s"] >= (1.0 - TOK_TIE) * top]
-    best = min(near, key=lambda c: (c["tpot_ms"] or 0, c["ttft_ms"] or 0, -c["tok_s"]))
+    # the fastest, unless a candidate within TOK_TIE of its rate cuts the TPOT by >= 10 %: then the
+    # fastest of those (a 512-row decode microbatch at the rate of a 768-row one is 2/3 the TPOT)
+    key = lambda c: (c["tok_s"], -(c["tpot_ms"] or 0), -(c["ttft_ms"] or 0))     # noqa: E731
+    best = max(ok, key=key)
+    better = [c for c in ok if c["tok_s"] >= (1.0 - TOK_TIE) * best["tok_s"]
+              and (c["tpot_ms"] or 0) <= 0.9 * (best["tpot_ms"] or 0)]
+    if better:
+        best = max(better, key=key)
     best = dict(best, vs_dp=round(best["tok_s"] / dp["tok_s"], 3) if dp["tok_s"] else None)
     return best, dp, cands
 

@@ -377,10 +377,11 @@ def test_plan_layer_split_gives_head_stage_fewer_layers():
 
 
 def test_node_layout_defaults():
-    # 70B at 8 GPUs: 6 prefill GPUs (1024-token steps) feed a 2-stage decode pipeline — the fastest
-    # split whose TTFT and TPOT are both under 0.7 of a mixed-step DP GPU's (plan.plan_pd)
+    # 70B at 8 GPUs: 6 prefill GPUs (1024-token steps) feed two whole-model decode GPUs at 512-row
+    # microbatches — within 2 % of the fastest split (6P + a 2-stage pipeline at 768 rows) at 2/3
+    # of its TPOT; every pick has TTFT and TPOT under 0.7 of a mixed-step DP GPU's (plan.plan_pd)
     lay = plan_node_layout(8)
-    assert lay.kind == "pdpp" and lay.decode_groups == [[6, 7]] and len(lay.prefill_ranks) == 6
+    assert lay.kind == "pd" and lay.decode_groups == [[6], [7]] and len(lay.prefill_ranks) == 6
     assert plan_node_layout(1).kind == "single"
     assert plan_node_layout(2).kind == "pd"
     four = plan_node_layout(4)     # 70B: 3 prefill GPUs feed one decode GPU (decode-bound; prefill overflow)
@@ -836,7 +837,9 @@ def test_auto_layout_picks_pd_for_latency_at_throughput_parity():
     assert "TTFT" in d["reason"] and "-> " + d["kind"] in d["reason"]
     # a decode role too slow for parity -> data parallel, with the reason
     slow = dataclasses.replace(tab, decode_tok_s={k: v * 0.5 for k, v in tab.decode_tok_s.items()},
-                               decode_step_ms={k: v * 2 for k, v in tab.decode_step_ms.items()})
+                               decode_step_ms={k: v * 2 for k, v in tab.decode_step_ms.items()},
+                               decode_options={k: [[r, t * 0.5, st * 2] for r, t, st in v]
+                                               for k, v in tab.decode_options.items()})
     s2 = plan_from_probe(8, slow)
     assert s2["kind"] == "dp" and ("below" in s2["reason"] or "latency bound" in s2["reason"])
     try:
