@@ -4,6 +4,7 @@
 // whole decode step can be captured into a hipGraph (torch.cuda.CUDAGraph on
 // ROCm).  Shapes are checked here, on the host, before any launch: a kernel
 // never sees operands that disagree with its grid.
+#include <cstdlib>
 #include <torch/library.h>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
@@ -36,7 +37,8 @@ int dgi_fused_skinny(const void* x, int ldx, const void* res, int ldr, void* res
                      int epi, const int* positions, const float* cos_sin, const int* slots, void* k_cache,
                      void* v_cache, int nh, int nkv, int block_size, int cfg, hipStream_t s);
 int dgi_sample(const void* logits, int is_bf16, int B, int V, int stride, const float* temperature,
-               const long long* seeds, long long step, const float* thresh, long long* out, hipStream_t s);
+               const long long* seeds, long long step, const float* thresh, long long* out, void* ws, hipStream_t s);
+int dgi_sample_ws_floats(int B, int V);
 int dgi_topkp_threshold(const void* logits, int is_bf16, int B, int V, int stride, const float* temperature,
                         const long long* top_k, const float* top_p, float* thresh, hipStream_t s);
 int dgi_topk(const void* logits, int is_bf16, int B, int V, int stride, int K, float* out_v,
@@ -340,9 +342,18 @@ void sample(at::Tensor out, const at::Tensor& logits, const c10::optional<at::Te
                 thresh->device() == logits.device());
     thp = thresh->data_ptr<float>();
   }
+  // small batches split each row over several workgroups (DGI_SAMPLE_SPLIT=0: one per row)
+  static const bool split = [] {
+    const char* e = std::getenv("DGI_SAMPLE_SPLIT");
+    return !(e && e[0] == '0');
+  }();
+  const int wsf = split ? dgi_sample_ws_floats(B, (int)logits.size(1)) : 0;
+  at::Tensor ws;
+  if (wsf > 0) ws = at::empty({wsf}, logits.options().dtype(at::kFloat));
   check_rc(dgi_sample(logits.data_ptr(), logits.scalar_type() == at::kBFloat16, B,
                       (int)logits.size(1), (int)logits.stride(0), tp, sp, step, thp,
-                      reinterpret_cast<long long*>(out.data_ptr<int64_t>()), cur_stream()),
+                      reinterpret_cast<long long*>(out.data_ptr<int64_t>()), wsf > 0 ? ws.data_ptr() : nullptr,
+                      cur_stream()),
            "sample");
 }
 

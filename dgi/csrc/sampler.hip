@@ -115,6 +115,85 @@ __global__ __launch_bounds__(1024) void sample_kernel(const T* __restrict__ logi
   }
 }
 
+// Small batches: a row split over C workgroups of SP_CHUNK logits each (one 128k-vocab row
+// on one workgroup is ~16 dependent rounds of loads, 15.5 us on the 8B decode step,
+// profiles/r5_decode/decode8b_b1_step_breakdown_r5.md).  Each part writes its (best, index);
+// the final kernel reduces the C parts of a row on one wave.  The Gumbel noise depends only on
+// (seed, step, index), so the pick is the single-workgroup kernel's, ties to the lower index.
+constexpr int SP_NT = 256;
+constexpr int SP_CHUNK = 8192;
+
+template <typename T>
+__global__ __launch_bounds__(SP_NT) void sample_part_kernel(const T* __restrict__ logits, int V, int stride,
+                                                            const float* __restrict__ temperature,
+                                                            const long long* __restrict__ seeds, long long step,
+                                                            const float* __restrict__ thresh, float* __restrict__ pv,
+                                                            int* __restrict__ pi) {
+  const int c = blockIdx.x, row = blockIdx.y, C = gridDim.x;
+  const int lo = c * SP_CHUNK;
+  const int n = min(V - lo, SP_CHUNK);
+  const T* lp = logits + (size_t)row * stride + lo;
+  const float temp = temperature ? temperature[row] : 0.f;
+  const bool greedy = temp <= 1e-5f;
+  const float inv_t = greedy ? 1.f : 1.f / temp;
+  const uint32_t seed = seeds ? (uint32_t)(seeds[row] * 2654435761ull) ^ (uint32_t)(step * 40503u) : 0u;
+  float best = -INFINITY;
+  int best_i = 0x7fffffff;
+  if (greedy) {
+    scan_row<T>(lp, n, stride, [&](float v, int i) {
+      i += lo;
+      if (v > best || (v == best && i < best_i)) { best = v; best_i = i; }
+    });
+  } else {
+    const float th = thresh ? thresh[row] : -INFINITY;
+    scan_row<T>(lp, n, stride, [&](float v, int i) {
+      i += lo;
+      if (v < th) return;
+      const uint32_t h = hash32(seed ^ hash32((uint32_t)i + 0x9e3779b9u));
+      const float u = ((h >> 8) + 0.5f) * (1.0f / 16777216.0f);
+      v = v * inv_t - __logf(-__logf(u));
+      if (v > best || (v == best && i < best_i)) { best = v; best_i = i; }
+    });
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(best_i, o, 64);
+    if (ob > best || (ob == best && oi < best_i)) { best = ob; best_i = oi; }
+  }
+  __shared__ float sb[SP_NT / 64];
+  __shared__ int si[SP_NT / 64];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sb[w] = best; si[w] = best_i; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < SP_NT / 64; ++k)
+      if (sb[k] > best || (sb[k] == best && si[k] < best_i)) { best = sb[k]; best_i = si[k]; }
+    pv[(size_t)row * C + c] = best;
+    pi[(size_t)row * C + c] = best_i;
+  }
+}
+
+// one wave per row over its C parts (C <= 64 * 4)
+__global__ __launch_bounds__(64) void sample_final_kernel(const float* __restrict__ pv, const int* __restrict__ pi,
+                                                          int C, long long* __restrict__ out) {
+  const int row = blockIdx.x, lane = threadIdx.x;
+  float best = -INFINITY;
+  int best_i = 0x7fffffff;
+  for (int c = lane; c < C; c += 64) {
+    const float v = pv[(size_t)row * C + c];
+    const int i = pi[(size_t)row * C + c];
+    if (v > best || (v == best && i < best_i)) { best = v; best_i = i; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(best_i, o, 64);
+    if (ob > best || (ob == best && oi < best_i)) { best = ob; best_i = oi; }
+  }
+  if (lane == 0) out[row] = best_i == 0x7fffffff ? 0 : best_i;
+}
+
 // top-k (k <= 16) per row: values + indices, descending.  One 256-thread
 // block per row; each thread keeps its own sorted top-k, then a tree merge in LDS.
 template <typename T>
@@ -492,10 +571,32 @@ __global__ __launch_bounds__(1024) void topkp_thresh_kernel(const T* __restrict_
 
 }  // namespace
 
+// floats of workspace dgi_sample's split path needs for B rows of V logits (0: no split)
+extern "C" int dgi_sample_ws_floats(int B, int V) {
+  if (B > 32 || V < 2 * SP_CHUNK) return 0;
+  return 2 * B * ((V + SP_CHUNK - 1) / SP_CHUNK);
+}
+
 extern "C" int dgi_sample(const void* logits, int is_bf16, int B, int V, int stride,
                           const float* temperature, const long long* seeds, long long step,
-                          const float* thresh, long long* out, hipStream_t s) {
+                          const float* thresh, long long* out, void* ws, hipStream_t s) {
   if (B == 0) return 0;
+  if (ws && dgi_sample_ws_floats(B, V) > 0) {
+    const int C = (V + SP_CHUNK - 1) / SP_CHUNK;
+    float* pv = reinterpret_cast<float*>(ws);
+    int* pi = reinterpret_cast<int*>(pv + (size_t)B * C);
+    const dim3 grid(C, B);
+    if (is_bf16)
+      sample_part_kernel<uint16_t><<<grid, SP_NT, 0, s>>>((const uint16_t*)logits, V, stride, temperature, seeds,
+                                                         step, thresh, pv, pi);
+    else
+      sample_part_kernel<float><<<grid, SP_NT, 0, s>>>((const float*)logits, V, stride, temperature, seeds, step,
+                                                      thresh, pv, pi);
+    DGI_CHECK_LAUNCH();
+    sample_final_kernel<<<B, 64, 0, s>>>(pv, pi, C, out);
+    DGI_CHECK_LAUNCH();
+    return 0;
+  }
   if (is_bf16)
     sample_kernel<uint16_t><<<B, 1024, 0, s>>>((const uint16_t*)logits, V, stride, temperature, seeds, step,
                                                thresh, out);

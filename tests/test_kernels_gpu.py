@@ -246,6 +246,30 @@ def test_topk_logprobs_matches_log_softmax_topk(B, V, k):
     torch.testing.assert_close(v2.cpu(), rv2.cpu(), atol=2e-5, rtol=1e-5)
 
 
+@pytest.mark.parametrize("V", [128256, 151936, 32000])
+def test_sample_split_rows_match_one_workgroup_per_row(V):
+    """Batches of <= 32 rows split each row over workgroups of 8192 logits (sample_part_kernel +
+    sample_final_kernel); 33+ rows take one workgroup per row.  A row's pick depends only on its
+    logits, seed and step, so the first rows of a 40-row call (unsplit) must equal an 8-row call
+    of the same rows (split): greedy, Gumbel-sampled, and with top-k / top-p thresholds."""
+    B = 40
+    logits = (torch.randn(B, V, device=DEV) * 2).to(torch.bfloat16)
+    temps = torch.rand(B, device=DEV) + 0.3
+    temps[::3] = 0.0                                          # greedy rows mixed in
+    seeds = torch.arange(B, device=DEV, dtype=torch.long) * 7 + 1
+    ks = torch.tensor([0, 5, 50, 0] * (B // 4), device=DEV, dtype=torch.long)
+    ps = torch.tensor([1.0, 1.0, 0.9, 0.7] * (B // 4), device=DEV)
+    for kw in ({}, {"top_k": ks, "top_p": ps}):
+        full = ops.sample(logits, temps, seeds, 5, **kw)
+        for n in (1, 8, 32):
+            kn = {k: v[:n] for k, v in kw.items()}
+            part = ops.sample(logits[:n], temps[:n], seeds[:n], 5, **kn)
+            assert torch.equal(part.cpu(), full[:n].cpu()), (n, kw.keys())
+    assert torch.equal(ops.sample(logits[:4]).cpu(), logits[:4].float().argmax(-1).cpu())
+    wide = torch.randn(4, V + 8, device=DEV).to(torch.bfloat16)     # strided rows
+    assert torch.equal(ops.sample(wide[:, :V]).cpu(), wide[:, :V].float().argmax(-1).cpu())
+
+
 def test_sample_temperature_distribution():
     V = 8
     logits = torch.log(torch.tensor([[0.5, 0.25, 0.125, 0.125, 1e-9, 1e-9, 1e-9, 1e-9]], device=DEV)).repeat(4096, 1)
