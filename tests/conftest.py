@@ -20,8 +20,13 @@ for p in (ROOT, os.path.join(ROOT, "worker"), os.path.join(ROOT, "server"), os.p
 # a file database: the API tests drive the app from several threads at once, and
 # an in-memory SQLite database is one shared connection (not thread-safe)
 import tempfile  # noqa: E402
-os.environ.setdefault("DATABASE_URL", "sqlite+aiosqlite:///" + os.path.join(tempfile.gettempdir(),
-                                                                       f"dgi_test_{os.getpid()}.db"))
+_DB = "sqlite+aiosqlite:///" + os.path.join(tempfile.gettempdir(), f"dgi_test_{os.getpid()}.db")
+if os.environ.get("PYTEST_XDIST_WORKER"):
+    # xdist workers inherit the controller's DATABASE_URL: one file per worker process, or one
+    # worker's table setup races another's (sqlite "no such table" under -n)
+    os.environ["DATABASE_URL"] = _DB
+else:
+    os.environ.setdefault("DATABASE_URL", _DB)
 
 
 def pytest_configure(config):
