@@ -853,7 +853,7 @@ def test_auto_layout_picks_pd_for_latency_at_throughput_parity():
 def test_capacity_from_probe_and_median():
     """Probe fits (fixed + per-layer ms) -> per-role capacity at the model's depth;
     the ranks plan with the element-wise median."""
-    from dgi.parallel.probe import ProbeResult, capacity_from_probe, median_capacity
+    from dgi.parallel.probe import MIXED_CAL, ProbeResult, capacity_from_probe, median_capacity
     p = ProbeResult(model="llama3-70b", prefill=(2.0, 2.5), decode={576: (4.0, 1.2), 768: (4.0, 1.5)},
                     mixed=(3.0, 2.3), prefill_mbt=2048, mixed_rows=384, prompt_len=512, output_len=128,
                     layers=(2, 4), seconds=1.0)
@@ -861,7 +861,7 @@ def test_capacity_from_probe_and_median():
     assert c.prefill_step_ms == 202.0 and abs(c.prefill_tok_s - 4 / 0.202 * 128) < 1
     assert c.decode_rows == {1: 576, 2: 768, 3: 768}
     assert abs(c.decode_tok_s[1] - 576 / 0.100) < 1 and abs(c.decode_tok_s[3] - 3 * 768 / 0.124) < 1
-    assert c.decode_step_ms[3] == round(124.0 / 3, 2) and abs(c.mixed_tok_s - 384 / 0.187) < 1
+    assert c.decode_step_ms[3] == round(124.0 / 3, 2) and abs(c.mixed_tok_s - 384 / (0.187 * MIXED_CAL)) < 1
     import dataclasses
     c2 = dataclasses.replace(c, prefill_tok_s=c.prefill_tok_s * 2)
     c3 = dataclasses.replace(c, prefill_tok_s=c.prefill_tok_s * 3)
