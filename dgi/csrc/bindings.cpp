@@ -225,8 +225,9 @@ void mfma_gemm(at::Tensor out, const at::Tensor& x, const at::Tensor& w, int64_t
   TORCH_CHECK(x.stride(1) == 1 && out.stride(1) == 1 && w.is_contiguous(), "mfma_gemm: row-major operands");
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
   TORCH_CHECK(w.size(1) == K && out.size(0) == M, "mfma_gemm: shape mismatch");
-  TORCH_CHECK((epi & 15) <= 1 && ((epi >> 4) & 15) <= 3 && ((epi >> 8) & 3) <= 2 && ((epi >> 10) & 3) <= 2 && (epi >> 15) == 0,
+  TORCH_CHECK((epi & 15) <= 1 && ((epi >> 4) & 15) <= 4 && ((epi >> 8) & 3) <= 2 && ((epi >> 10) & 3) <= 2 && (epi >> 15) == 0,
               "mfma_gemm: epi 0 (store) or 1 (SwiGLU), + 16 * schedule + 256 * stream-K mode");
+  TORCH_CHECK(((epi >> 4) & 15) != 4 || (epi & 15) == 0, "mfma_gemm: schedule 4 (half tile) is a plain GEMM");
   TORCH_CHECK(out.size(1) == ((epi & 15) == 1 ? N / 2 : N), "mfma_gemm: output columns");
   TORCH_CHECK(N % 256 == 0 && K % 64 == 0 && x.stride(0) % 8 == 0 && out.stride(0) % 4 == 0,
               "mfma_gemm: N%256, K%64, ldx%8, ldy%4");

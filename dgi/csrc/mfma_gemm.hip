@@ -269,6 +269,119 @@ __global__ __launch_bounds__(512) void mfma_gemm_kernel(const uint16_t* __restri
 
 
 // ---------------------------------------------------------------------------
+// Half tile (sched 4, epi 0): a 128 x 128 output tile on 4 waves (2 x 2 of 64 x 64), the same
+// lane-linear LDS image, source-side swizzle and fragment map as mfma_gemm_kernel, two 32 KB
+// stages (two workgroups per CU).  For row counts whose 256 x 256 tiles fill a fraction of the
+// chip — the decode role's qkv / o at 512 rows: 80 / 64 tiles on 256 CUs, where the full tile
+// needs a split-K round trip (0.84 PF/s) and hipBLASLt reaches 0.86-0.90 — the half tile gives
+// 320 / 256 whole tiles (profiles/r5_pd/README.md §10).
+constexpr int kHM = 128;
+constexpr int kHTile = kHM * kBK * 2;     // 16 KB: one operand, one stage
+constexpr int kHStage = 2 * kHTile;       // X tile + W tile
+
+__global__ __launch_bounds__(256) void mfma_gemm_half_kernel(const uint16_t* __restrict__ X, int ldx,
+                                                             const uint16_t* __restrict__ W,
+                                                             uint16_t* __restrict__ Y, int ldy, int M, int K,
+                                                             int tiles_m, int tiles_total) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * kHStage];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+
+  // XCD-aware, bijective block -> tile map (blocks b and b + 8 share an XCD), M-fastest
+  const int b = blockIdx.x;
+  const int xcd = b & 7, li = b >> 3;
+  const int q8 = tiles_total >> 3, r8 = tiles_total & 7;
+  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + li;
+  const int tm = t % tiles_m, tn = t / tiles_m;
+  const int m0 = tm * kHM;
+
+  // staging: pass i moves rows 32 i .. 32 i + 31 of each operand (one 1 KB wave-instruction per
+  // 8 rows); physical 16-byte chunk c of row r holds logical k-chunk c ^ ((r >> 1) & 7)
+  const int q = tid >> 3;
+  const int lc = (tid & 7) ^ ((tid >> 4) & 7);
+  const int xq = m0 + q;
+  const uint16_t* const xsrc = X + lc * 8;
+  const uint16_t* const wsrc = W + (size_t)(tn * kHM + q) * K + lc * 8;
+  const size_t wslab = (size_t)32 * K;
+  char* const lds_x = smem + w * 1024;
+  char* const lds_w = smem + kHTile + w * 1024;
+
+  auto issue = [&](int kt, int stage) {
+    const int k0 = kt * kBK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      glds16(xsrc + (size_t)min(xq + i * 32, M - 1) * ldx + k0, lds_x + stage * kHStage + i * 4096);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16(wsrc + i * wslab + k0, lds_w + stage * kHStage + i * 4096);
+  };
+
+  const int r16 = lane & 15;
+  const int sw = (lane >> 1) & 7;
+  const int ph0 = ((lane >> 4) ^ sw) * 16;
+  const int ph1 = ((4 + (lane >> 4)) ^ sw) * 16;
+  const int xbase = (wm * 64 + r16) * 128;
+  const int wbase = kHTile + (wn * 64 + r16) * 128;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 xa[4], wa[4], xb[4], wb[4];
+  auto read = [&](int stage, int ph, bf16x8* xf, bf16x8* wf) {
+    const char* sp = smem + stage * kHStage;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wf[j] = *(const bf16x8*)(sp + wbase + j * 2048 + ph);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xf[i] = *(const bf16x8*)(sp + xbase + i * 2048 + ph);
+  };
+  auto mma = [&](const bf16x8* xf, const bf16x8* wf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+  };
+
+  const int nt = K / kBK;
+  issue(0, 0);
+  if (nt > 1) issue(1, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  read(0, ph0, xa, wa);
+  for (int kt = 0; kt < nt; ++kt) {
+    const int st = kt & 1;
+    read(st, ph1, xb, wb);
+    mma(xa, wa);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's next-stage loads landed
+    __syncthreads();                                    // everyone's landed; stage st fully read
+    if (kt + 2 < nt) issue(kt + 2, st);
+    if (kt + 1 < nt) read(st ^ 1, ph0, xa, wa);
+    mma(xb, wb);
+  }
+
+  const int g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wm * 64 + i * 16 + r16;
+    if (m >= M) continue;
+    uint16_t* yrow = Y + (size_t)m * ldy;
+#pragma unroll
+    for (int j = 0; j < 4; j += 2) {
+      float x0[4], x1[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        x0[e] = acc[i][j][e];
+        x1[e] = acc[i][j + 1][e];
+      }
+      store_pair16(yrow, tn * kHM + wn * 64 + j * 16, g, x0, x1);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Ring schedule (sched 2): the K loop advances in 32-deep sub-steps through a
 // ring of four 32 KB LDS slots (X 256 x 32 and W 256 x 32, 64-byte rows).
 // Sub-step u computes on fragments of u already in registers, reads u + 1's
@@ -930,7 +1043,7 @@ void launch(const void* x, int ldx, const void* w, void* y, int ldy, int M, int 
 
 // epi & 1: 0 = Y[M, N] = X W^T with N = rows of W; 1 = Y[M, I] = SwiGLU with W = [gate; up] (2I rows).
 // epi >> 4: K-loop schedule (0 = compiler order, 1 = interleaved, 2 = 4-slot ring of 32-deep sub-steps,
-// 3 = ping-pong wave groups, 4 phases per K tile).  (epi >> 8) & 3: stream-K policy of schedule 3
+// 3 = ping-pong wave groups, 4 phases per K tile, 4 = 128 x 128 half tile, epi 0 only).  (epi >> 8) & 3: stream-K policy of schedule 3
 // (0 = auto, 1 = off, 2 = whenever the tiles leave the last wave part-empty).  (epi >> 10) & 3:
 // s_setprio variant of schedule 3, (epi >> 12) & 1: two 32-MFMA phases per K tile, (epi >> 13) & 1:
 // four 16-MFMA phases (default: two up to M = 2560, see mfma_gemm_pp_kernel), (epi >> 14) & 1: no
@@ -940,9 +1053,18 @@ extern "C" void dgi_set_gemm_cus(int cus) { g_cu_limit = cus; }
 extern "C" int dgi_mfma_gemm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K,
                              int epi, hipStream_t s) {
   if (M <= 0) return 0;
-  if (K % kBK || ldx % 8 || ldy % 4 || N % 256) return -3;
   const int swiglu = epi & 15;
   int sched = (epi >> 4) & 15;
+  if (sched == 4) {             // half tile: plain GEMM, N % 128
+    if (swiglu || K % kBK || ldx % 8 || ldy % 4 || N % kHM) return -3;
+    const int tiles_m = (M + kHM - 1) / kHM;
+    const int total = tiles_m * (N / kHM);
+    mfma_gemm_half_kernel<<<dim3(total), 256, 0, s>>>((const uint16_t*)x, ldx, (const uint16_t*)w, (uint16_t*)y,
+                                                      ldy, M, K, tiles_m, total);
+    DGI_CHECK_LAUNCH();
+    return 0;
+  }
+  if (K % kBK || ldx % 8 || ldy % 4 || N % 256) return -3;
   const int skmode = ((epi >> 8) & 3) == 0 ? 1 : ((epi >> 8) & 3) == 1 ? 0 : 2;
   int prio = ((epi >> 10) & 7) | (((epi >> 14) & 1) << 3);
   // phases per K tile: (epi >> 13) & 1 forces 4; otherwise 2 up to 10 row tiles (M <= 2560: the

@@ -41,7 +41,23 @@ def test_mfma_gemm_matches_fp32(M, N, K, epi, sched):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("sched", [0, 1, 2, 3])
+@pytest.mark.parametrize("M,N,K", [(1, 256, 64), (100, 512, 256), (128, 256, 128), (300, 768, 512),
+                                   (512, 1280, 1024), (777, 512, 8192), (512, 10240, 512)])
+def test_mfma_gemm_half_tile_matches_fp32(M, N, K):
+    """Schedule 4: the 128 x 128 half-tile kernel (plain GEMM) against fp32, M tails included."""
+    ops.load_native(required=True)
+    x = _rand(M, K, device="cuda", seed=M + K)
+    w = _rand(N, K, device="cuda", scale=0.05, seed=N)
+    ref = ops.mfma_gemm_ref(x, w, 0).float()
+    got = ops.mfma_gemm(x, w, 0, sched=4)
+    torch.cuda.synchronize()
+    err = (got.float() - ref).abs()
+    tol = 2e-2 * ref.abs().max().item() + 1e-3
+    assert err.max().item() <= tol, (err.max().item(), tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sched", [0, 1, 2, 3, 4])
 def test_mfma_gemm_strided_rows_and_asymmetric_operands(sched):
     """A = row slice of a wider buffer (ldx > K) and an asymmetric W: catches
     row/column swaps in the C write and ldx handling."""
