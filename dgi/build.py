@@ -1,4 +1,5 @@
-"""Build the gfx950 extension in-tree: ``python -m dgi.build``.
+"""Build the gfx950 extension in-tree: ``python -m dgi.build``
+(``--sanitize``: the ASan+UBSan and TSan builds of the host ring code instead).
 
 Each ``dgi/csrc/*.hip`` file is compiled by ``hipcc --offload-arch=gfx950``
 into an object, ``bindings.cpp`` (torch op registration) is compiled against
@@ -93,7 +94,7 @@ SHM_OUT = os.path.join(HERE, "_shm" + sysconfig.get_config_var("EXT_SUFFIX"))
 def build_shm(force: bool = False) -> str:
     """``dgi/_shm*.so``: the shared-memory control-plane rings (plain C++ /
     pybind11, no ROCm dependency, so the CPU test-suite uses the same code)."""
-    if not force and not _newer([SHM_SRC], SHM_OUT):
+    if not force and not _newer([SHM_SRC, os.path.join(CSRC, "host", "shm_ring.h")], SHM_OUT):
         return SHM_OUT
     import pybind11
     py_inc = sysconfig.get_paths()["include"]
@@ -102,7 +103,36 @@ def build_shm(force: bool = False) -> str:
     return SHM_OUT
 
 
+STRESS_SRC = os.path.join(CSRC, "host", "shm_ring_stress.cc")
+SANITIZERS = {
+    # ASan + UBSan: bounds of every ring copy against the mapping, misaligned cursor access
+    "asan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer"],
+    # TSan: the producer / consumer cursor protocol (release / acquire) on one mapping
+    "tsan": ["-fsanitize=thread"],
+}
+
+
+def build_sanitized(kind: str, force: bool = False, defines: tuple = (), tag: str = "") -> str:
+    """CPU sanitizer build of the native host code: the shared-memory ring
+    core (``csrc/host/shm_ring.h``, the one concurrent native component) linked into the
+    stress driver ``shm_ring_stress.cc`` with ``SANITIZERS[kind]``; returns the binary's path
+    (``build/sanitize/shm_ring_stress_<kind>``).  Host code only: no GPU code is sanitized."""
+    flags = SANITIZERS[kind]
+    out_dir = os.path.join(HERE, "..", "build", "sanitize")
+    os.makedirs(out_dir, exist_ok=True)
+    out = os.path.join(out_dir, f"shm_ring_stress_{kind}{tag}")
+    hdr = os.path.join(CSRC, "host", "shm_ring.h")
+    if force or _newer([STRESS_SRC, hdr], out):
+        _run(["g++", "-O1", "-g", "-std=c++17", "-Wall", "-Wextra", *flags, *[f"-D{d}" for d in defines],
+              STRESS_SRC, "-o", out, "-lrt", "-pthread"])
+    return out
+
+
 if __name__ == "__main__":
+    if "--sanitize" in sys.argv:
+        for k in SANITIZERS:
+            print(build_sanitized(k, force="--force" in sys.argv))
+        sys.exit(0)
     print(build_shm(force="--force" in sys.argv))
     p = build(verbose=True, force="--force" in sys.argv)
     print(p)

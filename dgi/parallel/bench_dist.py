@@ -28,12 +28,21 @@ from dgi.parallel.plan import plan_node_layout
 from dgi.sched.request import SamplingParams
 
 MSG_PHASE = 9
-# serving-phase deadline (ramp + warm-up + window) of the watchdog's phase clock
-SERVE_S = float(os.environ.get("DGI_SERVE_S", "420"))
+
+
+def dist_serve_budget(args) -> float:
+    """Serving-phase deadline (ramp + warm-up + window) of the watchdog's phase clock:
+    the ramp (2 x output_len micro-steps) plus (warmup + steps) node steps of up to 8
+    micro-steps each, at 0.25 s per micro-step, x3 (``fault.serve_budget``)."""
+    from dgi.parallel.fault import serve_budget
+    ramp = args.ramp_steps if getattr(args, "ramp_steps", -1) >= 0 else 2 * args.output_len
+    return serve_budget(ramp + 8 * (args.warmup + args.steps))
 
 
 class _FirstHop:
     """``first_hop`` phase until this rank completed its first step, then ``serve``."""
+
+    budget_s = 420.0          # set by run_distributed from the run's step counts
 
     def __init__(self):
         from dgi.parallel.fault import phase
@@ -44,7 +53,7 @@ class _FirstHop:
     def step_done(self) -> None:
         if not self.done:
             self.done = True
-            self._phase("serve", SERVE_S)
+            self._phase("serve", _FirstHop.budget_s)
 
     def teardown(self) -> None:
         self.step_done()
@@ -110,7 +119,9 @@ def run_distributed(args, layout_kind: str, dist):
     rccl = rccl_transports() if f.on_gpu else None
     ctrl_rtt = ctrl_ping(f, 0, world - 1)
     # model load (+ graph capture) of this rank's role
-    phase("engine_build", float(os.environ.get("DGI_BUILD_S", "300")))
+    from dgi.parallel.fault import BUILD_S
+    phase("engine_build", BUILD_S)
+    _FirstHop.budget_s = dist_serve_budget(args)
     # decode-side concurrency: k microbatches of the rows the plan priced (a planner output on
     # the 256-row GEMM tile: 512 rows on a whole-model decode GPU, whose KV pool holds ~590
     # sequences, 768 per microbatch of a pipeline; ``plan.plan_pd``)

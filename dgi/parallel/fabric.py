@@ -138,11 +138,20 @@ def _nccl_options():
         return None
 
 
-def init_distributed(backend: Optional[str] = None, timeout_s: float = 300.0) -> str:
+# Default budget of the process group (every collective) and of control-ring waits.  Serving
+# start-up waits span a peer's model load and graph capture (a cold 70B checkpoint load can
+# take minutes), so the default is long; the benchmark passes its short rendezvous budget
+# (DGI_INIT_S) explicitly and relies on the watchdog's phase deadlines for hangs.
+LONG_WAIT_S = float(os.environ.get("DGI_PG_TIMEOUT_S", "1800"))
+
+
+def init_distributed(backend: Optional[str] = None, timeout_s: Optional[float] = None) -> str:
     """Initialise the default process group for this process (idempotent).
 
     RCCL: eager init bound to this rank's GPU (``device_id``) with
     high-priority communicator streams.  Returns the backend in use."""
+    if timeout_s is None:
+        timeout_s = LONG_WAIT_S
     if dist.is_initialized():
         return dist.get_backend()
     be = backend or ("nccl" if torch.cuda.is_available() and os.environ.get("DGI_STAGED_GPU", "0") != "1"
@@ -167,7 +176,7 @@ class Fabric:
     """Per-rank view of the node: communicators, streams and control rings."""
 
     def __init__(self, backend: Optional[str] = None, device: Optional[torch.device] = None,
-                 timeout_s: float = 300.0):
+                 timeout_s: Optional[float] = None):
         self.owns_pg = not dist.is_initialized()
         init_distributed(backend, timeout_s)
         self.rank = dist.get_rank()
@@ -561,7 +570,9 @@ class CtrlChannel:
         self.rseq += 1
         return v
 
-    def wait_bytes(self, timeout_s: float = 300.0) -> bytes:
+    def wait_bytes(self, timeout_s: Optional[float] = None) -> bytes:
+        if timeout_s is None:
+            timeout_s = LONG_WAIT_S
         if self.shm:
             r = self._inbox(timeout_s)
             if r is None:
@@ -592,5 +603,5 @@ class CtrlChannel:
         v = self.poll_bytes()
         return None if v is None else np.frombuffer(v, dtype=np.int64).copy()
 
-    def wait(self, timeout_s: float = 300.0) -> np.ndarray:
+    def wait(self, timeout_s: Optional[float] = None) -> np.ndarray:
         return np.frombuffer(self.wait_bytes(timeout_s), dtype=np.int64).copy()

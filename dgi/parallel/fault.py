@@ -10,7 +10,9 @@
 * **Phase deadlines** (``Watchdog.phase``): a multi-rank run moves
   through named phases (rendezvous, pair warm-up, start-up probe, engine build,
   first hop, serving window, teardown), each with a time budget (``DGI_PHASE_S``,
-  default 120 s; the serving phase scales with the steps).  Every rank publishes
+  default 120 s; engine build ``DGI_BUILD_S`` 300 s; the serving phase is
+  ``serve_budget``: 3x the expected time of the steps it runs, at least
+  ``DGI_SERVE_S`` 420 s).  Every rank publishes
   its current phase in the store.  The first rank whose phase overruns prints ONE
   JSON line on stdout — ``{"status": "timeout", ...}`` with the stuck rank, its
   phase and every rank's phase — records a failure (so every other rank exits
@@ -90,6 +92,16 @@ class FaultPlan:
 # fault-injection step ids of the start-up phases (``DGI_FAULT=rank:<site>:stall``)
 PHASE_SITES = {"pair_warmup": 300001, "probe": 300002, "engine_build": 300003, "first_hop": 300004}
 DEFAULT_PHASE_S = float(os.environ.get("DGI_PHASE_S", "120"))
+BUILD_S = float(os.environ.get("DGI_BUILD_S", "300"))       # model load + graph capture of one rank
+SERVE_FLOOR_S = float(os.environ.get("DGI_SERVE_S", "420"))   # serving-window floor
+
+
+def serve_budget(n_steps: int, step_s: float = 0.25, slack: float = 3.0) -> float:
+    """Deadline of a serving phase of ``n_steps`` engine steps (ramp + warm-up + timed
+    window, counted in the steps the rank itself runs): ``slack`` x the expected time at
+    ``step_s`` per step, never below ``DGI_SERVE_S`` (420 s).  A long ``--steps`` run
+    on a slow layout is thus not mistaken for a hang."""
+    return max(SERVE_FLOOR_S, slack * max(0, int(n_steps)) * float(step_s))
 
 _plan: Optional[FaultPlan] = None
 

@@ -393,13 +393,35 @@ def pd_candidate(n_prefill: int, stages: int, replicas: int, mbt: int, cap: Role
     else:                 # prefill slack: prefill ranks decode overflow sequences themselves
         fill = (1.0 - dec / pre) * n_prefill * cap.mixed_tok_s
     tot = base + FILL_WEIGHT * fill
+    share = FILL_WEIGHT * fill / tot if tot > 0 else 0.0
+    ttft = round(cap.steps().get(mbt, cap.prefill_step_ms), 1) or None
+    tpot = round(stages * cap.decode_step_ms.get(stages, 0.0), 1) or None
+    # latency of the filler's tokens: overflow sequences decoded on a prefill
+    # rank wait one prefill step per token; local prompts of a decode replica run in mixed
+    # microbatches at DP-like latency.  Node-wide p95 over tokens: the filler's latency once its
+    # share of the output reaches 5 %.
+    if dec >= pre:
+        f_tpot = f_ttft = cap.mixed_step_ms or None
+    else:
+        f_tpot, f_ttft = ttft, ttft
+    def _p95(main, other):       # noqa: E306
+        if main is None:
+            return None
+        return round(max(main, other), 1) if (other and share >= 0.05) else main
+    def _mean(main, other):      # noqa: E306
+        if main is None:
+            return None
+        return round((1.0 - share) * main + share * (other or main), 1)
     return {"layout": f"{n_prefill}P+{replicas}D[" + "+".join([f"pp{stages}" if stages > 1 else "1"] * replicas) + "]",
             "prefill_ranks": n_prefill, "decode_stages": stages, "decode_replicas": replicas, "prefill_mbt": mbt,
             "tok_s": round(tot, 1), "disagg_tok_s": round(base, 1),
             "bound": "prefill" if pre < dec else "decode",
-            "ttft_ms": round(cap.steps().get(mbt, cap.prefill_step_ms), 1) or None,
-            "tpot_ms": round(stages * cap.decode_step_ms.get(stages, 0.0), 1) or None,
-            "filler_share": round(FILL_WEIGHT * fill / tot, 3) if tot > 0 else 0.0}
+            "ttft_ms": ttft, "tpot_ms": tpot,          # a prompt / sequence of the disaggregated path
+            "tpot_replica_ms": tpot,
+            "filler_tpot_ms": f_tpot if share > 0 else None, "filler_ttft_ms": f_ttft if share > 0 else None,
+            "tpot_mean_ms": _mean(tpot, f_tpot), "tpot_p95_ms": _p95(tpot, f_tpot),
+            "ttft_mean_ms": _mean(ttft, f_ttft), "ttft_p95_ms": _p95(ttft, f_ttft),
+            "filler_share": round(share, 3)}
 
 
 def plan_pd(n_gpus: int, cap: RoleCapacity, max_stages: int = 3, lat_frac: Optional[float] = None) -> tuple:
@@ -420,9 +442,10 @@ def plan_pd(n_gpus: int, cap: RoleCapacity, max_stages: int = 3, lat_frac: Optio
                 for mbt in sorted(cap.steps()):
                     c = pd_candidate(npre, k, left // k, mbt, ck)
                     c["decode_rows"] = rows
-                    c["latency_ok"] = bool(dp["ttft_ms"] and c["ttft_ms"] and c["tpot_ms"]
-                                           and c["ttft_ms"] <= lat * dp["ttft_ms"]
-                                           and c["tpot_ms"] <= lat * dp["tpot_ms"])
+                    # the bound holds for the filler-inclusive p95, not only the replica's TPOT
+                    c["latency_ok"] = bool(dp["ttft_ms"] and c["ttft_p95_ms"] and c["tpot_p95_ms"]
+                                           and c["ttft_p95_ms"] <= lat * dp["ttft_ms"]
+                                           and c["tpot_p95_ms"] <= lat * dp["tpot_ms"])
                     cands.append(c)
     if not cands:
         return None, dp, []

@@ -213,7 +213,21 @@ def tuned_path(key: dict) -> str:
     return os.path.join(TUNED_DIR, f"gemm_table_{key['gate_up'][1]}x{key['down'][1]}_{h}.json")
 
 
-def load_tuned(key: dict, m_max: int) -> Optional[MlpPadTable]:
+def device_tag(device=None) -> dict:
+    """What a measured routing table is only valid on: the GPU architecture (``gfx950``,
+    without feature suffixes) and the HIP major.minor of the torch build (hipBLASLt's
+    kernels change between releases).  Stored next to the key in every saved table and
+    compared on load (the key alone let any device reuse the MI355X choices)."""
+    arch, hip = None, None
+    if torch.cuda.is_available():
+        props = torch.cuda.get_device_properties(device if device is not None else torch.cuda.current_device())
+        arch = str(getattr(props, "gcnArchName", "")).split(":")[0] or None
+    if torch.version.hip:
+        hip = ".".join(torch.version.hip.split(".")[:2])
+    return {"arch": arch, "hip": hip}
+
+
+def load_tuned(key: dict, m_max: int, device=None) -> Optional[MlpPadTable]:
     import json
     p = tuned_path(key)
     if not os.path.exists(p):
@@ -221,6 +235,8 @@ def load_tuned(key: dict, m_max: int) -> Optional[MlpPadTable]:
     with open(p) as f:
         d = json.load(f)
     if d.get("key") != key or not d["grid"] or d["grid"][-1] < m_max:
+        return None
+    if d.get("device") != device_tag(device):      # another GPU / ROCm: measure its own table
         return None
     return MlpPadTable.from_json(d)
 
@@ -249,7 +265,7 @@ def build_for_model(model, m_max: int, step: int = 32) -> Optional[MlpPadTable]:
     if hit is not None and hit[0] >= m_max:
         return hit[1]
     tk = table_key(model, step, M_MIN)
-    t = load_tuned(tk, m_max) if TABLE_MODE == "auto" else None
+    t = load_tuned(tk, m_max, L.gate_up.device) if TABLE_MODE == "auto" else None
     if t is None:
         t = MlpPadTable.measure(L.gate_up, L.down, m_min=M_MIN, m_max=m_max, step=step,
                                 qkv=L.qkv if llama.QKV_PAD else None, o_w=L.o if llama.OPROJ_PAD else None,
@@ -258,6 +274,6 @@ def build_for_model(model, m_max: int, step: int = 32) -> Optional[MlpPadTable]:
         if save:
             import json
             with open(save, "w") as f:
-                json.dump(t.to_json(tk), f)
+                json.dump({**t.to_json(tk), "device": device_tag(L.gate_up.device)}, f)
     _TABLES[key] = (m_max, t)
     return t

@@ -124,9 +124,13 @@ class Eagle3Draft:
         # 128k -> 32k rows, 0.79 of 1.05 GB per depth); None = the whole vocabulary
         self.hot: Optional[torch.Tensor] = None
         self.hot_head: Optional[torch.Tensor] = None
+        self.vocab_version = 0      # bumped by set_hot_vocab: captured graphs of older versions are stale
 
     def set_hot_vocab(self, ids: Optional[torch.Tensor]) -> None:
-        """Restrict the draft's proposals to token ids ``ids`` (None: every token)."""
+        """Restrict the draft's proposals to token ids ``ids`` (None: every token).  Graphs
+        captured before the call read the old head (or the full-vocabulary path): the engine
+        drops them when it sees ``vocab_version`` move."""
+        self.vocab_version += 1
         if ids is None:
             self.hot = self.hot_head = None
             return
@@ -548,6 +552,7 @@ class SpecEngine(LLMEngine):
         self._oracle_rng = np.random.default_rng(0)
         self._vgraphs: dict = {}
         self._dgraphs: dict = {}
+        self._graphs_vocab = self.draft.vocab_version
         self._graph_pool = torch.cuda.graph_pool_handle() if self.device.type == "cuda" else None
         # plain decode steps replay the engine's hipGraphs with the EAGLE-3 feature tap on
         if self.runner.graphs is not None:
@@ -575,9 +580,18 @@ class SpecEngine(LLMEngine):
     def _bucket(self, R: int) -> int:
         return next((b for b in VERIFY_BUCKETS if b >= R), VERIFY_BUCKETS[-1])
 
+    def _check_graph_vocab(self) -> None:
+        """Drop the draft / verify graphs captured against an older draft vocabulary (they hold
+        pointers to the replaced ``hot`` / ``hot_head`` tensors)."""
+        if self._graphs_vocab != self.draft.vocab_version:
+            self._dgraphs.clear()
+            self._vgraphs.clear()
+            self._graphs_vocab = self.draft.vocab_version
+
     def _draft_graph(self, R: int) -> Optional[_DraftGraph]:
         if not (self.spec.graphs and self.device.type == "cuda" and self.cur_depth >= 2):
             return None
+        self._check_graph_vocab()
         Rb = next((b for b in VERIFY_BUCKETS if b >= R), None)
         if Rb is None:
             return None
@@ -590,6 +604,7 @@ class SpecEngine(LLMEngine):
     def _verify_graph(self, R: int) -> Optional[_VerifyGraph]:
         if not (self.spec.graphs and self.device.type == "cuda"):
             return None
+        self._check_graph_vocab()
         Rb = next((b for b in VERIFY_BUCKETS if b >= R), None)
         if Rb is None:
             return None

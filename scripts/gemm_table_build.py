@@ -49,7 +49,7 @@ def main():
     out = a.out or gemm_pad.tuned_path(key)
     os.makedirs(os.path.dirname(out), exist_ok=True)
     with open(out, "w") as f:
-        json.dump(med.to_json(key), f)
+        json.dump({**med.to_json(key), "device": gemm_pad.device_tag(L.gate_up.device)}, f)
     print(json.dumps({"out": out, "points": len(med.grid), "choice_flips_between_passes": flips,
                       "gate_up_mfma": sum(f for f, _ in med.impls), "down_mfma": sum(b for _, b in med.impls),
                       "qkv_mfma": sum(q for q, _ in med.proj_impls), "o_mfma": sum(o for _, o in med.proj_impls)}),

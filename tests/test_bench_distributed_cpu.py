@@ -198,3 +198,44 @@ def test_bench_auto_layout_plans_from_the_startup_probe():
     pl = d["extra"]["planner"]
     assert pl["source"] == "probe" and pl["kind"] in ("dp", "pd", "pdpp") and pl["reason"]
     assert d["value"] > 0 and "auto:" in d["metric_scope"]
+
+
+def test_dp_run_after_the_probe_enters_its_own_phases(monkeypatch):
+    """``--layout auto`` resolving to dp used to leave the probe's
+    120 s deadline armed over the whole DP engine build and serving window, so the
+    watchdog killed a healthy 70B DP run.  ``run_single`` now enters ``engine_build``,
+    then ``serve`` with a budget sized from the run's steps, then ``report``."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from dgi.parallel import fault
+
+    seen = []
+
+    class _WD:
+        rank = 0
+
+        def phase(self, name, budget_s=None):
+            seen.append((name, budget_s))
+
+    monkeypatch.setattr(fault, "_WATCHDOG", [_WD()])
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--model", "llama-tiny", "--steps", "3", "--warmup", "1",
+                                      "--ramp-steps", "2", "--concurrency", "4", "--output-len", "4",
+                                      "--prompt-len", "16", "--max-batched-tokens", "128", "--no-graphs"])
+    res = bench.run_single(bench.parse())
+    assert res["tokens"] > 0
+    names = [n for n, _ in seen]
+    assert names == ["engine_build", "serve", "report"], seen
+    assert seen[0][1] == fault.BUILD_S
+    assert seen[1][1] >= fault.SERVE_FLOOR_S
+    assert fault.serve_budget(10_000, step_s=0.5) == 15_000      # scales with the steps past the floor
+
+
+def test_distributed_serve_budget_scales_with_steps():
+    """the P/D serving deadline grows with --steps / --warmup."""
+    import types
+    from dgi.parallel.bench_dist import dist_serve_budget
+    from dgi.parallel.fault import SERVE_FLOOR_S
+    small = types.SimpleNamespace(ramp_steps=-1, output_len=128, warmup=10, steps=20)
+    big = types.SimpleNamespace(ramp_steps=-1, output_len=128, warmup=10, steps=2000)
+    assert dist_serve_budget(small) >= SERVE_FLOOR_S
+    assert dist_serve_budget(big) > 3 * 8 * 2000 * 0.25 - 1

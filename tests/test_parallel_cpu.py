@@ -850,6 +850,36 @@ def test_auto_layout_picks_pd_for_latency_at_throughput_parity():
     assert bench.auto_layout(8, "llama3-70b") == d["kind"]
 
 
+def test_planner_reports_filler_inclusive_latency():
+    """a P/D candidate's tokens decoded by the slack filler (overflow
+    sequences on prefill ranks wait one prefill step per token) enter its latency: the
+    planner reports the replica TPOT, the filler's TPOT / TTFT and node-wide mean / p95
+    over tokens, and the latency bound is checked on the p95."""
+    import dataclasses
+    from dgi.parallel.plan import CAPACITY, FILL_WEIGHT, LATENCY_FRAC, pd_candidate, plan_pd
+    tab = CAPACITY["llama3-70b"]
+    best, dp, cands = plan_pd(8, tab)
+    for c in cands:
+        for k in ("tpot_replica_ms", "tpot_mean_ms", "tpot_p95_ms", "ttft_mean_ms", "ttft_p95_ms"):
+            assert k in c
+        assert c["tpot_p95_ms"] >= c["tpot_replica_ms"] and c["tpot_p95_ms"] >= c["tpot_mean_ms"]
+        assert c["latency_ok"] == bool(c["ttft_p95_ms"] <= LATENCY_FRAC * dp["ttft_ms"]
+                                       and c["tpot_p95_ms"] <= LATENCY_FRAC * dp["tpot_ms"])
+    # the shipped pick (6P + 2 decode GPUs, decode-bound): ~7.7 % of its tokens are overflow
+    # decoding on prefill ranks at one 1,024-token prefill step (106 ms) per token
+    assert best["layout"] == "6P+2D[1+1]" and best["bound"] == "decode"
+    assert best["filler_share"] >= 0.05 and best["filler_tpot_ms"] == best["ttft_ms"]
+    assert best["tpot_p95_ms"] == max(best["tpot_replica_ms"], best["filler_tpot_ms"])
+    exp = (1 - best["filler_share"]) * best["tpot_replica_ms"] + best["filler_share"] * best["filler_tpot_ms"]
+    assert abs(best["tpot_mean_ms"] - exp) < 0.11
+    # no filler -> the replica's own latency
+    ck = dataclasses.replace(tab, prefill_tok_s=tab.decode_tok_s[1] * 2 / 6)
+    c = pd_candidate(6, 1, 2, tab.prefill_mbt, ck)
+    if c["filler_share"] < 0.05:
+        assert c["tpot_p95_ms"] == c["tpot_replica_ms"]
+    assert FILL_WEIGHT > 0
+
+
 def test_capacity_from_probe_and_median():
     """Probe fits (fixed + per-layer ms) -> per-role capacity at the model's depth;
     the ranks plan with the element-wise median."""
