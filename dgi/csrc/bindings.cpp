@@ -47,9 +47,9 @@ int dgi_topk_logprobs_ws_floats(int B, int V);
 int dgi_topk_logprobs(const void* logits, int B, int V, int stride, int K, float* ws, float* out_v,
                       long long* out_i, hipStream_t s);
 int dgi_kv_gather(const void* cache, const int* ids, int n, int LK, int num_blocks, int page_elems,
-                  void* buf, hipStream_t s);
+                  void* buf, int block_major, hipStream_t s);
 int dgi_kv_scatter(void* cache, const int* ids, int n, int LK, int num_blocks, int page_elems,
-                   const void* buf, hipStream_t s);
+                   const void* buf, int block_major, hipStream_t s);
 int dgi_mall_prefetch(const void* base, const int* rows, int nrows, int row_bytes, int blocks, void* sink,
                       hipStream_t s);
 int dgi_kv_slot_copy(void* cache, const int* src, const int* dst, int n, int LK, int num_blocks, int nkv, int bs,
@@ -403,8 +403,8 @@ void topk_logprobs(at::Tensor out_v, at::Tensor out_i, const at::Tensor& logits,
            "topk_logprobs");
 }
 
-// cache: [L, 2, NB, nkv, bs, hd]; buf: [L, 2, n, nkv, bs, hd]
-void kv_gather(at::Tensor buf, const at::Tensor& cache, const at::Tensor& ids) {
+// cache: [L, 2, NB, nkv, bs, hd]; buf: [L, 2, n, nkv, bs, hd], or [n, L, 2, nkv, bs, hd] when block_major
+void kv_gather(at::Tensor buf, const at::Tensor& cache, const at::Tensor& ids, bool block_major) {
   check_dev(cache, "cache"); check_i32(ids, "ids");
   TORCH_CHECK(cache.is_contiguous() && buf.is_contiguous() && cache.dim() == 6);
   const int n = (int)ids.numel();
@@ -413,10 +413,10 @@ void kv_gather(at::Tensor buf, const at::Tensor& cache, const at::Tensor& ids) {
   const int page = (int)(cache.size(3) * cache.size(4) * cache.size(5));
   TORCH_CHECK(buf.numel() >= (int64_t)LK * n * page && buf.scalar_type() == cache.scalar_type());
   check_rc(dgi_kv_gather(cache.data_ptr(), ids.data_ptr<int>(), n, LK, NB, page, buf.data_ptr(),
-                         cur_stream()), "kv_gather");
+                         block_major ? 1 : 0, cur_stream()), "kv_gather");
 }
 
-void kv_scatter(at::Tensor cache, const at::Tensor& ids, const at::Tensor& buf) {
+void kv_scatter(at::Tensor cache, const at::Tensor& ids, const at::Tensor& buf, bool block_major) {
   check_dev(cache, "cache"); check_i32(ids, "ids");
   TORCH_CHECK(cache.is_contiguous() && buf.is_contiguous() && cache.dim() == 6);
   const int n = (int)ids.numel();
@@ -425,7 +425,7 @@ void kv_scatter(at::Tensor cache, const at::Tensor& ids, const at::Tensor& buf) 
   const int page = (int)(cache.size(3) * cache.size(4) * cache.size(5));
   TORCH_CHECK(buf.numel() >= (int64_t)LK * n * page && buf.scalar_type() == cache.scalar_type());
   check_rc(dgi_kv_scatter(cache.data_ptr(), ids.data_ptr<int>(), n, LK, NB, page, buf.data_ptr(),
-                          cur_stream()), "kv_scatter");
+                          block_major ? 1 : 0, cur_stream()), "kv_scatter");
 }
 
 void kv_copy(at::Tensor cache, const at::Tensor& src, const at::Tensor& dst) {
@@ -531,8 +531,8 @@ TORCH_LIBRARY(dgi, m) {
         "Tensor top_p) -> ()");
   m.def("topk(Tensor(a!) out_v, Tensor(b!) out_i, Tensor logits, int k) -> ()");
   m.def("topk_logprobs(Tensor(a!) out_v, Tensor(b!) out_i, Tensor logits, int k) -> ()");
-  m.def("kv_gather(Tensor(a!) buf, Tensor cache, Tensor ids) -> ()");
-  m.def("kv_scatter(Tensor(a!) cache, Tensor ids, Tensor buf) -> ()");
+  m.def("kv_gather(Tensor(a!) buf, Tensor cache, Tensor ids, bool block_major) -> ()");
+  m.def("kv_scatter(Tensor(a!) cache, Tensor ids, Tensor buf, bool block_major) -> ()");
   m.def("kv_copy(Tensor(a!) cache, Tensor src, Tensor dst) -> ()");
   m.def("kv_slot_copy(Tensor(a!) cache, Tensor src, Tensor dst) -> ()");
   m.def("mall_prefetch(Tensor w, Tensor? rows, Tensor(a!) sink, int nrows=-1, int blocks=256) -> ()");

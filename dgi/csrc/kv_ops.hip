@@ -18,6 +18,10 @@ using namespace dgi;
 namespace {
 
 // page = n_kv * bs * hd elements; moved as 16-byte chunks.
+// BM (block-major): buf is [n, LK, page] — every page of one block id (all layers, K and V)
+// contiguous, the host KV tier's slot layout, so a run of consecutive host slots is ONE DMA
+// and no permute pass is needed; otherwise buf is [LK, n, page] (the migration layout).
+template <bool BM>
 __global__ __launch_bounds__(256) void kv_gather_kernel(const u32x4* __restrict__ cache,
                                                         const int* __restrict__ ids, int n,
                                                         int num_blocks, int page_chunks, int LK,
@@ -25,13 +29,14 @@ __global__ __launch_bounds__(256) void kv_gather_kernel(const u32x4* __restrict_
   const long total = (long)LK * n * page_chunks;
   for (long c = (long)blockIdx.x * 256 + threadIdx.x; c < total; c += (long)gridDim.x * 256) {
     const int within = (int)(c % page_chunks);
-    const long pg = c / page_chunks;  // (lk, i)
-    const int i = (int)(pg % n);
-    const int lk = (int)(pg / n);
+    const long pg = c / page_chunks;
+    const int i = BM ? (int)(pg / LK) : (int)(pg % n);
+    const int lk = BM ? (int)(pg % LK) : (int)(pg / n);
     buf[c] = cache[((long)lk * num_blocks + ids[i]) * page_chunks + within];
   }
 }
 
+template <bool BM>
 __global__ __launch_bounds__(256) void kv_scatter_kernel(u32x4* __restrict__ cache,
                                                          const int* __restrict__ ids, int n,
                                                          int num_blocks, int page_chunks, int LK,
@@ -40,8 +45,8 @@ __global__ __launch_bounds__(256) void kv_scatter_kernel(u32x4* __restrict__ cac
   for (long c = (long)blockIdx.x * 256 + threadIdx.x; c < total; c += (long)gridDim.x * 256) {
     const int within = (int)(c % page_chunks);
     const long pg = c / page_chunks;
-    const int i = (int)(pg % n);
-    const int lk = (int)(pg / n);
+    const int i = BM ? (int)(pg / LK) : (int)(pg % n);
+    const int lk = BM ? (int)(pg % LK) : (int)(pg / n);
     cache[((long)lk * num_blocks + ids[i]) * page_chunks + within] = buf[c];
   }
 }
@@ -108,25 +113,31 @@ int grid_for(long total) {
 
 }  // namespace
 
-// LK = L*2 (layer x {k,v}); page_elems = n_kv*bs*hd
+// LK = L*2 (layer x {k,v}); page_elems = n_kv*bs*hd; block_major: buf [n, LK, page] instead of [LK, n, page]
 extern "C" int dgi_kv_gather(const void* cache, const int* ids, int n, int LK, int num_blocks,
-                             int page_elems, void* buf, hipStream_t s) {
+                             int page_elems, void* buf, int block_major, hipStream_t s) {
   if (n == 0) return 0;
   if (page_elems % 8) return -2;
   const int pc = page_elems / 8;
-  kv_gather_kernel<<<grid_for((long)LK * n * pc), 256, 0, s>>>((const u32x4*)cache, ids, n,
-                                                               num_blocks, pc, LK, (u32x4*)buf);
+  const int g = grid_for((long)LK * n * pc);
+  if (block_major)
+    kv_gather_kernel<true><<<g, 256, 0, s>>>((const u32x4*)cache, ids, n, num_blocks, pc, LK, (u32x4*)buf);
+  else
+    kv_gather_kernel<false><<<g, 256, 0, s>>>((const u32x4*)cache, ids, n, num_blocks, pc, LK, (u32x4*)buf);
   DGI_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int dgi_kv_scatter(void* cache, const int* ids, int n, int LK, int num_blocks,
-                              int page_elems, const void* buf, hipStream_t s) {
+                              int page_elems, const void* buf, int block_major, hipStream_t s) {
   if (n == 0) return 0;
   if (page_elems % 8) return -2;
   const int pc = page_elems / 8;
-  kv_scatter_kernel<<<grid_for((long)LK * n * pc), 256, 0, s>>>((u32x4*)cache, ids, n, num_blocks,
-                                                                pc, LK, (const u32x4*)buf);
+  const int g = grid_for((long)LK * n * pc);
+  if (block_major)
+    kv_scatter_kernel<true><<<g, 256, 0, s>>>((u32x4*)cache, ids, n, num_blocks, pc, LK, (const u32x4*)buf);
+  else
+    kv_scatter_kernel<false><<<g, 256, 0, s>>>((u32x4*)cache, ids, n, num_blocks, pc, LK, (const u32x4*)buf);
   DGI_CHECK_LAUNCH();
   return 0;
 }

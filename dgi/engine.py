@@ -144,6 +144,7 @@ class LLMEngine:
         rkw = {"graph_buckets": tuple(cfg.graph_buckets)} if cfg.graph_buckets else {}
         self.runner = ModelRunner(self.model, self.pool, cfg.max_num_seqs, cfg.max_model_len,
                                   cfg.max_num_batched_tokens, cfg.use_graphs, **rkw)
+        self.runner.host_tier = self.host_tier
         self.requests: dict = {}
         # decode lookahead: (ScheduledBatch, launch handle) of a step in flight, not applied yet
         import os as _os
@@ -445,9 +446,12 @@ class LLMEngine:
         st = self.stats
         st["steps"] += 1
         st["decode_tokens"] += len(sb.decode)
+        radix = self.scheduler.radix
         for c in sb.prefill:
             c.req.num_computed += c.length
             st["prefill_tokens"] += c.length
+            if c.sample and radix is not None:      # prompt fully computed: publish its pages
+                self.scheduler.on_prefilled(c.req)
         for r in sb.decode:
             r.num_computed += 1
 

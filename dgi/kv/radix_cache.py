@@ -48,6 +48,7 @@ class RadixCache:
         self.pool = pool
         self.host = host_tier
         self.host_hits_blocks = 0
+        self.restore_event = None       # event of the last host-tier restore (``take_restore_event``)
         self.bs = pool.block_size
         self.root = _Node(None, -1, None)
         self.num_nodes = 0
@@ -96,7 +97,7 @@ class RadixCache:
             except Exception:
                 cut = path.index(need[0])
                 return path[:cut]
-            self.host.restore([n.host for n in need], fresh)
+            self.restore_event = self.host.restore([n.host for n in need], fresh)
             self.host.release([n.host for n in need])
             for n, b in zip(need, fresh):
                 n.block, n.host = b, -1
@@ -105,6 +106,11 @@ class RadixCache:
         finally:
             for n in path:
                 n.lock -= 1
+
+    def take_restore_event(self):
+        """The event of the restore the last ``match`` issued (None if it issued none)."""
+        ev, self.restore_event = self.restore_event, None
+        return ev
 
     def release(self, path: list) -> None:
         for n in path:
@@ -135,6 +141,21 @@ class RadixCache:
             child.last = now
             node = child
         return new
+
+    def insert_locked(self, tokens: list[int], blocks: list[int]) -> list:
+        """``insert`` and return the node path of the inserted full blocks, locked (the caller
+        releases it): a request publishes its prompt pages when its prefill completes and
+        keeps them pinned while it decodes."""
+        self.insert(tokens, blocks)
+        node, path = self.root, []
+        bs = self.bs
+        for j in range(min(len(tokens) // bs, len(blocks))):
+            node = node.children.get(tuple(tokens[j * bs:(j + 1) * bs]))
+            if node is None:
+                break
+            node.lock += 1
+            path.append(node)
+        return path
 
     # ------------------------------------------------------------------ evict
     def _evictable_leaves(self):

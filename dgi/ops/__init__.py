@@ -750,24 +750,32 @@ def topk(logits: torch.Tensor, k: int):
 # KV block movement
 # ----------------------------------------------------------------------------
 
-def kv_gather(cache: torch.Tensor, ids: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """cache [L,2,NB,...] -> [L,2,n,...] pages of ``ids``."""
+def kv_gather(cache: torch.Tensor, ids: torch.Tensor, out: Optional[torch.Tensor] = None,
+              block_major: bool = False) -> torch.Tensor:
+    """cache [L,2,NB,...] -> [L,2,n,...] pages of ``ids`` (``block_major``: [n,L,2,...], every
+    layer of one page contiguous — the host KV tier's slot layout)."""
     if _native(cache):
         if out is None:
-            out = torch.empty(cache.shape[0], cache.shape[1], ids.numel(), *cache.shape[3:],
-                              dtype=cache.dtype, device=cache.device)
-        _call("kv_gather", out, cache, ids)
+            shape = ((ids.numel(), cache.shape[0], cache.shape[1]) if block_major else
+                     (cache.shape[0], cache.shape[1], ids.numel())) + tuple(cache.shape[3:])
+            out = torch.empty(shape, dtype=cache.dtype, device=cache.device)
+        _call("kv_gather", out, cache, ids, bool(block_major))
         return out
     r = cache[:, :, ids.long()]
+    if block_major:
+        r = r.permute(2, 0, 1, 3, 4, 5).contiguous()
     if out is not None:
-        out.copy_(r)
+        out.copy_(r.view(out.shape))
         return out
     return r
 
 
-def kv_scatter(cache: torch.Tensor, ids: torch.Tensor, buf: torch.Tensor) -> None:
+def kv_scatter(cache: torch.Tensor, ids: torch.Tensor, buf: torch.Tensor, block_major: bool = False) -> None:
     if _native(cache):
-        _call("kv_scatter", cache, ids, buf)
+        _call("kv_scatter", cache, ids, buf, bool(block_major))
+    elif block_major:
+        cache[:, :, ids.long()] = buf.reshape(ids.numel(), cache.shape[0], cache.shape[1],
+                                              *cache.shape[3:]).permute(1, 2, 0, 3, 4, 5)
     else:
         cache[:, :, ids.long()] = buf.view(cache.shape[0], cache.shape[1], ids.numel(), *cache.shape[3:])
 

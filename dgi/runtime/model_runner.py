@@ -138,6 +138,9 @@ class ModelRunner:
         # called while the host waits for a step's sampled tokens (P/D ranks keep
         # their KV handshakes moving instead of blocking in a stream synchronize)
         self.wait_hook = None
+        # pinned host KV tier of the engine (restores run on its copy stream; every forward gates
+        # on the last one, ``gate``)
+        self.host_tier = None
         self._spans = []
         self.span_total_ms = 0.0
         self.graphs = None
@@ -279,9 +282,22 @@ class ModelRunner:
         return ids, meta, sampled
 
     # ------------------------------------------------------------------ run
+    def gate_rows(self, reqs, chunks=()) -> None:
+        """Order this step's forward after the host-tier restores of the pages its rows read
+        (``Request.kv_ready``: a GPU-side event wait, once per request; no host sync)."""
+        if self.host_tier is None:
+            return
+        for r in itertools.chain(reqs, (c.req for c in chunks)):
+            ev = r.kv_ready
+            if ev is not None:
+                r.kv_ready = None
+                torch.cuda.current_stream(self.device).wait_event(ev)
+                self.host_tier.stats["gates"] += 1
+
     @torch.inference_mode()
     def execute(self, sb: ScheduledBatch) -> StepResult:
         self.step_id += 1
+        self.gate_rows(sb.decode, sb.prefill)
         if self.graphs is not None and not sb.prefill and sb.decode and \
                 len(sb.decode) <= self.graphs.max_bucket:
             toks = self.graphs.run(sb)
@@ -469,6 +485,7 @@ class GraphRunner:
         alternate, so a launch never rewrites the host buffers of the one before it."""
         if not self.captured:
             self.capture()
+        self.r.gate_rows(dec)
         n = len(dec)
         b = next(x for x in self.buckets if x >= n)
         r = self.r

@@ -39,7 +39,7 @@ class Status(enum.Enum):
 class Request:
     __slots__ = ("rid", "prompt", "params", "output", "blocks", "num_computed", "num_cached", "status",
                  "arrival", "first_token_time", "finish_time", "finish_reason", "radix_path", "seed",
-                 "token_times", "user", "preempted", "hidden", "spec_state", "prefill_target", "busy", "swapped")
+                 "token_times", "user", "preempted", "hidden", "spec_state", "prefill_target", "busy", "swapped", "kv_ready")
 
     def __init__(self, prompt: list[int], params: SamplingParams, rid=None, user=None):
         self.rid = next(_rid) if rid is None else rid
@@ -63,7 +63,10 @@ class Request:
         self.spec_state = None
         self.prefill_target = len(self.prompt)  # tokens to (re)compute before sampling
         self.busy = False  # in flight in a pipeline microbatch
-        self.swapped = None  # (host slots, tokens) while preempted to the pinned host KV tier
+        # while preempted to the pinned host KV tier: (host slots, tokens, None), or
+        # (None, tokens, GPU pages) once the scheduler restored it one step ahead
+        self.swapped = None
+        self.kv_ready = None  # event of a host-tier restore of its pages, awaited by its first forward
 
     @property
     def total_len(self) -> int:

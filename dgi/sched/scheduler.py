@@ -140,7 +140,11 @@ class Scheduler:
                 if r.rid == rid:
                     q.remove(r)
                     if r.swapped is not None:
-                        self.host_tier.release(r.swapped[0])
+                        slots, _n, pre = r.swapped
+                        if slots:
+                            self.host_tier.release(slots)
+                        if pre:
+                            self.pool.free(pre)
                         r.swapped = None
                     self._release(r, cache=False)
                     r.status = Status.FINISHED
@@ -174,7 +178,7 @@ class Scheduler:
         tier = self.host_tier
         if tier is not None and n > 0 and nb <= len(victim.blocks) and nb <= tier.num_free:
             # swap out: the computed pages go to pinned host memory, nothing is recomputed
-            victim.swapped = (tier.spill(victim.blocks[:nb]), n)
+            victim.swapped = (tier.spill(victim.blocks[:nb]), n, None)
             self._release(victim, cache=False)
             self.num_swapped_out += 1
         else:
@@ -189,17 +193,21 @@ class Scheduler:
 
     def _swap_in(self, req: Request) -> bool:
         """Re-admit a swapped-out sequence: fresh pages, KV copied back from the
-        host tier (ordered on the compute stream before the next forward)."""
-        slots, n = req.swapped
-        nb = len(slots)
-        if nb > self.pool.num_free and not self.pool.can_allocate(nb):
-            return False
-        try:
-            blocks = self.pool.allocate(nb)
-        except OutOfBlocks:
-            return False
-        self.host_tier.restore(slots, blocks)
-        self.host_tier.release(slots)
+        host tier on its copy stream (the next forward gates on it).  A sequence
+        ``_prefetch`` already restored one step ahead just takes its pages."""
+        slots, n, pre = req.swapped
+        if pre is not None:
+            blocks = pre
+        else:
+            nb = len(slots)
+            if nb > self.pool.num_free and not self.pool.can_allocate(nb):
+                return False
+            try:
+                blocks = self.pool.allocate(nb)
+            except OutOfBlocks:
+                return False
+            req.kv_ready = self.host_tier.restore(slots, blocks)
+            self.host_tier.release(slots)
         req.swapped = None
         req.blocks = blocks
         req.radix_path = []
@@ -208,6 +216,46 @@ class Scheduler:
         self.running.append(req)
         self.num_swapped_in += 1
         return True
+
+    # restores issued one step ahead: at most this many waiting sequences, and only while the
+    # pool keeps PREFETCH_RESERVE of its pages free for the running set's growth
+    PREFETCH_SEQS = 4
+    PREFETCH_RESERVE = 0.05
+
+    def _prefetch(self) -> None:
+        """Start the host -> GPU restore of the swapped-out sequences still at the head of the
+        waiting queue (the step's budget admitted no more), so the copy overlaps the step about
+        to run and their re-admission finds the pages in place (restores one
+        step ahead, gated by an event)."""
+        tier = self.host_tier
+        if tier is None or not self.waiting:
+            return
+        reserve = int(self.PREFETCH_RESERVE * self.pool.num_blocks)
+        for req in list(self.waiting)[: self.PREFETCH_SEQS]:
+            if req.swapped is None:
+                break                       # FCFS: a prompt ahead of it is admitted first
+            slots, n, pre = req.swapped
+            if pre is not None:
+                continue
+            if self.pool.num_free - len(slots) < reserve:
+                break
+            try:
+                blocks = self.pool.allocate(len(slots))
+            except OutOfBlocks:
+                break
+            req.kv_ready = tier.restore(slots, blocks, prefetch=True)
+            tier.release(slots)
+            req.swapped = (None, n, blocks)
+
+    def on_prefilled(self, req: Request) -> None:
+        """A prompt's prefill completed: publish its full pages in the radix cache now (not
+        only when the request finishes), so prompts arriving while it decodes share them;
+        the request holds the published path locked until it is released."""
+        if self.radix is None:
+            return
+        old = req.radix_path
+        req.radix_path = self.radix.insert_locked(req.all_tokens()[: req.num_computed], req.blocks)
+        self.radix.release(old)
 
     # ------------------------------------------------------------------ schedule
     def add_prefilled(self, req: Request, blocks: list[int]) -> None:
@@ -301,20 +349,19 @@ class Scheduler:
             if self.radix is not None and not req.blocks:
                 # keep >= 1 token to compute so the chunk produces logits
                 cached_blocks, path = self.radix.match(toks[: target - 1])
+                ev = self.radix.take_restore_event()
+                if ev is not None:
+                    req.kv_ready = ev
             start = len(cached_blocks) * self.bs
             n = min(target - start, budget)
             need = (start + n + self.bs - 1) // self.bs - len(cached_blocks)
             if need > self.pool.num_free and not self.pool.can_allocate(need):
-                if self.radix is not None:
-                    self.radix.release(path)
-                    self.pool.free(cached_blocks)
+                self._unmatch(req, path, cached_blocks)
                 break
             try:
                 own = self.pool.allocate(need)
             except OutOfBlocks:
-                if self.radix is not None:
-                    self.radix.release(path)
-                    self.pool.free(cached_blocks)
+                self._unmatch(req, path, cached_blocks)
                 break
             self.waiting.popleft()
             req.blocks = cached_blocks + own
@@ -326,7 +373,21 @@ class Scheduler:
             prefill.append(PrefillChunk(req, start, n, start + n == target))
             budget -= n
             n_seqs += 1
+        self._prefetch()
         return ScheduledBatch(decode, prefill, preempted)
+
+    def _unmatch(self, req: Request, path: list, cached_blocks: list) -> None:
+        """Undo a prefix match whose admission failed.  Pages it restored from the host tier
+        stay GPU-resident in the tree for the next reader, so the compute stream is ordered
+        after that restore now (GPU-side wait) rather than by this request's forward."""
+        if self.radix is None:
+            return
+        self.radix.release(path)
+        self.pool.free(cached_blocks)
+        ev, req.kv_ready = req.kv_ready, None
+        if ev is not None:
+            import torch
+            torch.cuda.current_stream(self.pool.kv.device).wait_event(ev)
 
     def _aligned_budget(self, nd: int, budget: int, align: int, seq_cap: int) -> int:
         """Prefill budget that ends the step on a multiple of ``align`` rows (see

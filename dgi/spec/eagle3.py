@@ -862,6 +862,7 @@ class SpecEngine(LLMEngine):
         bs = self.pool.block_size
         dev = self.device
         run = self.runner
+        run.gate_rows(reqs)           # host KV tier restores (swap-ins, prefix pages) land first
         sched = self.scheduler
         # ---- blocks for the tree slots [n-1, n-1+N)
         ok = []

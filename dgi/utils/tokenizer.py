@@ -25,6 +25,11 @@ class ByteTokenizer:
         ids = [self.offset + b for b in text.encode("utf-8")]
         return ([self.bos_token_id] if add_bos else []) + ids
 
+    # ids above the byte range (a random-init model samples them almost always) decode to one
+    # U+FFFD each instead of nothing: every generated token is visible text, so a stream's
+    # first chunk arrives with the first token and SSE TTFT measures what it says
+    UNKNOWN = "\ufffd".encode("utf-8")
+
     def decode(self, ids, skip_special_tokens: bool = True) -> str:
         out = bytearray()
         for i in ids:
@@ -32,6 +37,8 @@ class ByteTokenizer:
             b = i - self.offset
             if 0 <= b < 256:
                 out.append(b)
+            elif b >= 256:
+                out.extend(self.UNKNOWN)
             elif not skip_special_tokens:
                 out.extend(f"<{i}>".encode())
         return out.decode("utf-8", errors="replace")

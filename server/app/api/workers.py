@@ -124,11 +124,8 @@ def _ip(request: Request) -> Optional[str]:
 
 
 def _load_control(w: Worker) -> LoadControlConfig:
-    raw = (w.config_override or {}).get("load_control") or {}
-    try:
-        return LoadControlConfig(**raw)
-    except Exception:
-        return LoadControlConfig()
+    from app.services.worker_config import effective_load_control
+    return effective_load_control(w)
 
 
 def _running(db: Session, worker_id: str) -> int:

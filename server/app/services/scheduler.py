@@ -107,12 +107,8 @@ class SmartScheduler:
         """Enforce the worker's remote load-control config (acceptance rate, hourly cap, working hours)."""
         if worker is None:
             return True
-        from app.services.worker_config import LoadControlConfig, WorkerConfigService
-        raw = ((worker.config_override or {}).get("load_control") or {})
-        try:
-            lc = LoadControlConfig(**raw)
-        except Exception:
-            lc = LoadControlConfig()
+        from app.services.worker_config import WorkerConfigService, effective_load_control
+        lc = effective_load_control(worker)
         hour = int(datetime.utcnow().timestamp() // 3600)
         if worker.hour_bucket != hour:
             worker.hour_bucket, worker.jobs_this_hour = hour, 0

@@ -71,6 +71,22 @@ def _in_window(hour: int, start: Optional[int], end: Optional[int]) -> bool:
     return hour >= start or hour < end    # window wraps past midnight
 
 
+def effective_load_control(worker: Worker) -> LoadControlConfig:
+    """A worker's load control: the admin override where one is set; otherwise the defaults,
+    with the concurrency the worker advertised at registration (``capabilities.
+    max_concurrent_jobs``: a continuous-batching engine serves many jobs at once).  A worker
+    that advertises nothing keeps the reference's one job at a time."""
+    raw = dict((worker.config_override or {}).get("load_control") or {})
+    if "max_concurrent_jobs" not in raw:
+        adv = (getattr(worker, "extra_caps", None) or {}).get("max_concurrent_jobs")
+        if isinstance(adv, int) and adv >= 1:
+            raw["max_concurrent_jobs"] = min(adv, 1024)
+    try:
+        return LoadControlConfig(**raw)
+    except Exception:
+        return LoadControlConfig()
+
+
 class WorkerConfigService:
     DEFAULT_MODEL_CONFIGS = {
         "llm": ModelConfig(model_id="llama3-70b", max_new_tokens=2048, temperature=0.7),
@@ -84,7 +100,7 @@ class WorkerConfigService:
 
     def get_worker_config(self, worker: Worker) -> WorkerRemoteConfig:
         override = dict(worker.config_override or {})
-        lc = LoadControlConfig(**(override.get("load_control") or {}))
+        lc = effective_load_control(worker)
         sec = SecurityConfig(**(override.get("security") or {}))
         models = {t: self.DEFAULT_MODEL_CONFIGS[t] for t in (worker.supported_types or [])
                   if t in self.DEFAULT_MODEL_CONFIGS}

@@ -154,3 +154,98 @@ def test_streams_created_are_within_the_engine_budget():
     assert set(have["normal"]) - {"capture"} <= set(budget), (have, budget)
     assert "attn_side" in have["normal"] and "kv_host_copy" in have["normal"]
     assert len(budget) <= GPU_HW_QUEUES and len(have["high"]) <= GPU_HW_QUEUES - 1
+
+
+def test_slot_runs_batch_contiguous_dmas():
+    from dgi.kv.host_tier import runs
+    assert runs([3, 4, 5, 9, 10, 2]) == [(0, 3, 3), (3, 9, 2), (5, 2, 1)]
+    assert runs([]) == []
+    pool = _pool(nb=17)
+    tier = HostKVTier(pool, 16)
+    blocks = pool.allocate(6)
+    want = pool.kv[:, :, blocks].clone()
+    slots = tier.spill(blocks)
+    assert slots == list(range(6)) and tier.stats["spill_dmas"] == 1         # lowest slots first: one run
+    fresh = pool.allocate(6)
+    tier.restore(slots, fresh)
+    tier.release(slots)
+    assert tier.stats["restore_dmas"] == 1
+    assert torch.equal(pool.kv[:, :, fresh], want)
+
+
+def test_prompt_pages_are_shared_while_the_first_request_decodes():
+    """A prompt's full pages are published in the radix cache when its prefill completes
+    (not only when it finishes): a second request with the same prefix, admitted while
+    the first still decodes, reuses them, and its output equals a cold engine's."""
+    cfg = EngineConfig(model="llama-tiny", device="cpu", max_num_seqs=4, max_num_batched_tokens=128,
+                       max_model_len=256, use_graphs=False, num_blocks=64)
+    eng = LLMEngine(cfg)
+    cold = LLMEngine(EngineConfig(**{**cfg.__dict__, "enable_prefix_caching": False}), model=eng.model)
+    g = torch.Generator().manual_seed(5)
+    shared = torch.randint(5, 500, (48,), generator=g).tolist()
+    sp = SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True)
+    r1 = eng.add_request(shared + [1, 2], sp)
+    eng.step()                        # r1's prefill
+    eng.step()                        # r1 decodes
+    r2 = eng.add_request(shared + [3, 4, 5], sp)
+    while eng.has_unfinished():
+        eng.step()
+    assert r2.num_cached == 48 and r1.num_cached == 0
+    assert [r1.output, r2.output] == [r.output for r in cold.generate([shared + [1, 2], shared + [3, 4, 5]], sp)]
+
+
+def _gpu_prompts(n, seed, base=20, step=3):
+    g = torch.Generator().manual_seed(seed)
+    return [torch.randint(5, 500, (base + step * i,), generator=g).tolist() for i in range(n)]
+
+
+@pytest.mark.gpu
+def test_gpu_prefix_hits_with_graphs_are_token_identical():
+    """prefix-hit prefill chunks under the captured decode graphs, with
+    the host tier spilling and restoring shared pages (a pool too small for every prefix).
+    Greedy outputs equal an engine without prefix caching on the same weights."""
+    base = dict(model="llama-tiny-hd128", device="cuda", max_num_seqs=8, max_num_batched_tokens=256,
+                max_model_len=512, use_graphs=True)
+    g = torch.Generator().manual_seed(11)
+    shared = [torch.randint(5, 500, (64,), generator=g).tolist() for _ in range(3)]
+    prompts = [shared[i % 3] + torch.randint(5, 500, (5 + i,), generator=g).tolist() for i in range(12)]
+    sp = SamplingParams(max_tokens=16, temperature=0.0, ignore_eos=True)
+    cold = LLMEngine(EngineConfig(**base, enable_prefix_caching=False, num_blocks=256))
+    want = [r.output for r in cold.generate(prompts, sp)]
+    eng = LLMEngine(EngineConfig(**base, enable_prefix_caching=True, num_blocks=40, host_kv_gb=0.05),
+                    model=cold.model)
+    eng.warmup()
+    got = []
+    for i in range(0, 12, 4):         # waves: later waves hit pages published / spilled by earlier ones
+        got += [r.output for r in eng.generate(prompts[i:i + 4], sp)]
+    torch.cuda.synchronize()
+    assert got == want
+    st = eng.scheduler.stats()
+    assert st["prefix_hit_rate"] > 0.3, st
+    assert eng.runner.graphs is not None and eng.runner.graphs.captured
+    assert eng.host_tier.stats["spilled"] > 0 and eng.scheduler.radix.host_hits_blocks > 0, eng.host_tier.stats
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prefix_caching", [False, True])
+def test_gpu_swap_in_feeds_captured_decode(prefix_caching):
+    """preemption swaps sequences to the pinned host tier and back
+    (restored one step ahead on the copy stream, gated by an event) and the re-admitted
+    rows decode in the captured graphs: token-identical to an unconstrained engine, no
+    prompt recomputed, restores batched into contiguous DMAs."""
+    base = dict(model="llama-tiny-hd128", device="cuda", max_num_seqs=6, max_num_batched_tokens=256,
+                max_model_len=256, use_graphs=True, enable_prefix_caching=prefix_caching)
+    prompts = _gpu_prompts(6, 3)
+    sp = SamplingParams(max_tokens=24, temperature=0.0, ignore_eos=True)
+    big = LLMEngine(EngineConfig(**base, num_blocks=256))
+    want = [r.output for r in big.generate(prompts, sp)]
+    eng = LLMEngine(EngineConfig(**base, num_blocks=17, host_kv_gb=0.05), model=big.model)
+    eng.warmup()
+    got = [r.output for r in eng.generate(prompts, sp)]
+    torch.cuda.synchronize()
+    st, ts = eng.scheduler.stats(), eng.host_tier.stats
+    assert got == want
+    assert st["swapped_out"] > 0 and st["swapped_in"] == st["swapped_out"]
+    assert eng.stats["prefill_tokens"] == sum(len(p) for p in prompts)
+    assert ts["restore_dmas"] < ts["restored"] or ts["restored"] <= st["swapped_in"], ts
+    assert ts["gates"] > 0

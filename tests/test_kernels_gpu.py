@@ -293,6 +293,14 @@ def test_kv_gather_scatter_copy():
     dst = torch.tensor([10, 11], dtype=torch.int32, device=DEV)
     ops.kv_copy(cache, src, dst)
     assert torch.equal(cache[:, :, 10], cache[:, :, 2]) and torch.equal(cache[:, :, 11], cache[:, :, 3])
+    # block-major (host KV tier slot layout): [n, L, 2, page], no permute pass
+    gb = ops.kv_gather(cache, ids, block_major=True)
+    assert gb.shape == (3, L, 2, nkv, bs, hd)
+    assert torch.equal(gb, cache[:, :, ids.long()].permute(2, 0, 1, 3, 4, 5))
+    c3 = torch.zeros_like(cache)
+    ops.kv_scatter(c3, ids, gb, block_major=True)
+    assert torch.equal(c3[:, :, ids.long()], cache[:, :, ids.long()])
+    assert int((c3 != 0).sum()) == int((cache[:, :, ids.long()] != 0).sum())     # nothing else written
 
 
 def test_tree_mask_verify():

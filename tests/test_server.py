@@ -267,6 +267,27 @@ def test_api_cancel_offline_requeue_and_concurrency(client):
                   headers={"X-Worker-Token": reg["token"]}).json()["valid"] is False
 
 
+def test_advertised_worker_concurrency_is_honoured(client):
+    """A continuous-batching worker advertises how many jobs it runs at once
+    (``capabilities.max_concurrent_jobs``): the pull API hands it that many and its remote
+    config says so (the worker applies the remote load control, so a default of 1 there
+    serialised every job of a batching engine).  An admin override still wins, and a worker
+    that advertises nothing keeps one job at a time."""
+    c = client
+    wid, hdr, _ = _register(c, capabilities={"max_concurrent_jobs": 3, "continuous_batching": True})
+    legacy, lhdr, _ = _register(c, region="europe-west")
+    assert c.get(f"/api/v1/workers/{wid}/config", headers=hdr).json()["load_control"]["max_concurrent_jobs"] == 3
+    assert c.get(f"/api/v1/workers/{legacy}/config", headers=lhdr).json()["load_control"]["max_concurrent_jobs"] == 1
+    for i in range(5):
+        c.post("/api/v1/jobs", json={"type": "llm", "params": {"prompt": str(i)}, "region": "asia-east"})
+    got = [c.get(f"/api/v1/workers/{wid}/next-job", headers=hdr).json() for _ in range(4)]
+    assert all(got[:3]) and got[3] is None
+    assert c.get(f"/api/v1/workers/{legacy}/next-job", headers=lhdr).json() is not None
+    assert c.get(f"/api/v1/workers/{legacy}/next-job", headers=lhdr).json() is None
+    c.put(f"/api/v1/workers/{wid}/config", json={"max_concurrent_jobs": 2}, headers=hdr)     # admin override
+    assert c.get(f"/api/v1/workers/{wid}/config", headers=hdr).json()["load_control"]["max_concurrent_jobs"] == 2
+
+
 def test_api_sync_job_completed_by_worker_thread(client):
     c = client
     wid, hdr, _ = _register(c)

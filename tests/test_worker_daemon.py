@@ -172,7 +172,10 @@ def _wait_http(url, timeout=60):
     raise TimeoutError(url)
 
 
-def test_end_to_end_server_worker_sdk(tmp_path):
+def _e2e(tmp_path, engine_cfg: dict, name: str, n_sync: int = 4, max_tokens: int = 6):
+    """Control plane (uvicorn thread, SQLite) + worker daemon (``llm_native``) + SDK: concurrent
+    sync jobs, a direct call and an SSE stream.  Returns (sync outputs, direct output, stream
+    pieces, worker list, the worker's NativeLLMEngine, timings)."""
     import uvicorn
     from app.db.database import Base, engine
     from app.main import app
@@ -188,50 +191,93 @@ def test_end_to_end_server_worker_sdk(tmp_path):
     base = f"http://127.0.0.1:{sport}"
     _wait_http(base + "/health")
 
-    cfg = WorkerConfig(name="cpu-worker", region="asia-east", supported_types=["llm"],
-                       engines={"llm": {"model_id": "llama-tiny", "backend": "mi355x", "max_num_seqs": 16,
-                                        "max_num_batched_tokens": 512, "max_model_len": 512}},
+    cfg = WorkerConfig(name=name, region="asia-east", supported_types=["llm"], engines={"llm": engine_cfg},
                        heartbeat_interval=1, poll_interval=0.05)
     cfg.server.url = base
     cfg.direct.enabled, cfg.direct.host, cfg.direct.port = True, "127.0.0.1", dport
     cfg.direct.public_url = f"http://127.0.0.1:{dport}"
     cfg.load_control.max_concurrent_jobs = 8
     w = Worker(cfg, config_path=str(tmp_path / "worker.yaml"))
+    timings = {}
     with patch("machine_id.Path.home", return_value=tmp_path):
         wt = threading.Thread(target=w.start, kwargs={"install_signals": False}, daemon=True)
         wt.start()
         try:
             t0 = time.time()
             while w.worker_id is None or not w.running:
-                assert time.time() - t0 < 120, "worker did not start"
+                assert time.time() - t0 < 240, "worker did not start"
                 time.sleep(0.1)
             _wait_http(f"http://127.0.0.1:{dport}/health")
-            sdk = InferenceClient(base, timeout=60)
+            sdk = InferenceClient(base, timeout=120)
             msgs = [{"role": "user", "content": "hello mi355x"}]
             # several concurrent sync jobs batch inside the engine
-            outs = [None] * 4
+            outs = [None] * n_sync
 
             def one(i):
-                outs[i] = sdk.chat(msgs, max_tokens=6, temperature=0.0, sync=True, timeout=60)
-            ts = [threading.Thread(target=one, args=(i,)) for i in range(4)]
+                outs[i] = sdk.chat(msgs, max_tokens=max_tokens, temperature=0.0, sync=True, timeout=120)
+            ts = [threading.Thread(target=one, args=(i,)) for i in range(n_sync)]
+            t1 = time.time()
             [t.start() for t in ts]
-            [t.join(90) for t in ts]
-            for o in outs:
-                assert o is not None and o["status"] == "completed", o
-                assert o["result"]["usage"]["completion_tokens"] == 6
-            assert len({o["result"]["response"] for o in outs}) == 1      # greedy: identical
-            d = sdk.chat(msgs, max_tokens=6, temperature=0.0, use_direct=True)
-            assert d["success"] and d["result"]["response"] == outs[0]["result"]["response"]
-            pieces = list(sdk.stream_chat(msgs, max_tokens=6, temperature=0.0))
-            assert len(pieces) >= 1
+            [t.join(180) for t in ts]
+            timings["sync_batch_s"] = time.time() - t1
+            t1 = time.time()
+            d = sdk.chat(msgs, max_tokens=max_tokens, temperature=0.0, use_direct=True)
+            timings["direct_s"] = time.time() - t1
+            t1 = time.time()
+            pieces = list(sdk.stream_chat(msgs, max_tokens=max_tokens, temperature=0.0))
+            timings["stream_s"] = time.time() - t1
             info = sdk.list_workers()
-            assert info[0]["total_jobs"] == 4 and saved_yaml_has_token(tmp_path / "worker.yaml")
+            return outs, d, pieces, info, w.engines["llm"], timings
         finally:
             w.request_shutdown(graceful=True)
             wt.join(60)
             server.should_exit = True
             st.join(30)
-    assert not wt.is_alive()
+            assert not wt.is_alive()
+
+
+def test_end_to_end_server_worker_sdk(tmp_path):
+    outs, d, pieces, info, _eng, _t = _e2e(
+        tmp_path, {"model_id": "llama-tiny", "backend": "mi355x", "max_num_seqs": 16,
+                   "max_num_batched_tokens": 512, "max_model_len": 512}, "cpu-worker")
+    for o in outs:
+        assert o is not None and o["status"] == "completed", o
+        assert o["result"]["usage"]["completion_tokens"] == 6
+    assert len({o["result"]["response"] for o in outs}) == 1      # greedy: identical
+    assert d["success"] and d["result"]["response"] == outs[0]["result"]["response"]
+    assert len(pieces) >= 1
+    assert info[0]["total_jobs"] == 4 and saved_yaml_has_token(tmp_path / "worker.yaml")
+
+
+@pytest.mark.gpu
+def test_end_to_end_served_path_on_gpu(tmp_path):
+    """the reference's live path — SDK -> control plane -> worker
+    daemon pull -> engine (reference worker/main.py:313-376) — with the ``llm_native`` engine
+    on cuda:0 (hipGraph decode, warm-up, prefix cache).  Sync, direct and SSE jobs return the
+    greedy continuation the in-process engine computes for the same prompt ids."""
+    import torch
+    from dgi.engine import EngineConfig, LLMEngine
+    from dgi.sched.request import SamplingParams
+    from dgi.utils.tokenizer import chat_prompt_ids
+    ecfg = {"model_id": "llama-tiny-hd128", "backend": "mi355x", "device": "cuda:0", "max_num_seqs": 16,
+            "max_num_batched_tokens": 512, "max_model_len": 512, "warmup": True, "seed": 0}
+    outs, d, pieces, info, eng, timings = _e2e(tmp_path, ecfg, "gpu-worker", n_sync=6, max_tokens=12)
+    for o in outs:
+        assert o is not None and o["status"] == "completed", o
+    texts = {o["result"]["response"] for o in outs}
+    assert len(texts) == 1 and d["success"] and d["result"]["response"] in texts
+    assert "".join(pieces) in texts
+    assert eng.device.startswith("cuda") and eng.engine.runner.graphs is not None
+    assert eng.engine.runner.graphs.captured
+    # the in-process engine on the same (seeded random-init) weights, same prompt ids
+    ref = LLMEngine(EngineConfig(model="llama-tiny-hd128", device="cuda:0", max_num_seqs=16,
+                                 max_num_batched_tokens=512, max_model_len=512, seed=0, use_graphs=False))
+    ids = chat_prompt_ids(eng.tokenizer, [{"role": "user", "content": "hello mi355x"}])
+    want = ref.generate([ids], SamplingParams(max_tokens=12, temperature=0.0))[0].output
+    assert eng.tokenizer.decode(want, skip_special_tokens=True) in texts
+    assert {o["result"]["usage"]["completion_tokens"] for o in outs} == {len(want)}
+    torch.cuda.synchronize()
+    assert info[0]["total_jobs"] == 6
 
 
 def saved_yaml_has_token(path) -> bool:

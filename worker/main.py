@@ -141,7 +141,12 @@ class Worker:
             supported_types=list(self.engines or self.config.supported_types),
             direct_url=d.public_url or (f"http://{d.host}:{d.port}" if d.enabled else None),
             supports_direct=d.enabled, machine_id=fp["machine_id"], hardware_details=fp.get("details"),
-            role=self.config.role)
+            role=self.config.role,
+            # a continuous-batching engine serves many jobs at once: advertise how many this
+            # worker runs concurrently (the control plane otherwise assigns one at a time)
+            capabilities={"max_concurrent_jobs": self.max_concurrent_jobs(),
+                          "continuous_batching": any(type(e).__name__ in ("NativeLLMEngine", "NodeLLMEngine")
+                                                     for e in self.engines.values())})
         self.worker_id = data["worker_id"]
         self.config.worker_id = self.worker_id
         self.config.signing_secret = data.get("signing_secret")
