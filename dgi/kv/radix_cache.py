@@ -191,10 +191,37 @@ class RadixCache:
         self.host.stats["dropped"] += dropped
         return dropped
 
+    def _evictable_total(self) -> int:
+        """GPU pages eviction can free by repeated leaf eviction: every unpinned node whose page
+        only the cache holds and whose GPU-resident descendants all qualify too (evicting the
+        current leaves turns their parents into leaves).  Counting the current leaves alone
+        under-reports a deep tree, and an admission that needs more pages than that waits
+        forever while the cache holds them."""
+        total = 0
+        # post-order over the tree: a node qualifies iff it and its whole GPU-resident subtree do
+        stack = [(self.root, False)]
+        ok: dict = {}
+        while stack:
+            n, done = stack.pop()
+            if not done:
+                stack.append((n, True))
+                stack.extend((c, False) for c in n.children.values())
+                continue
+            sub = all(ok[id(c)] for c in n.children.values())
+            if n is self.root:
+                break
+            if n.block < 0:
+                ok[id(n)] = sub
+            else:
+                ok[id(n)] = sub and n.lock == 0 and (self.pool.ref[n.block] == 1 or self.host is None)
+                if ok[id(n)] and self.pool.ref[n.block] == 1:
+                    total += 1
+        return total
+
     def evict(self, n: int) -> int:
         """Free >= n GPU blocks from unpinned LRU leaves.  n == 0: report capacity."""
         if n == 0:
-            return sum(1 for c in self._evictable_leaves() if self.pool.ref[c.block] == 1)
+            return self._evictable_total()
         freed = 0
         while freed < n:
             leaves = [c for c in self._evictable_leaves() if self.pool.ref[c.block] == 1] if self.host is not None \

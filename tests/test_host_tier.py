@@ -209,19 +209,22 @@ def test_gpu_prefix_hits_with_graphs_are_token_identical():
     g = torch.Generator().manual_seed(11)
     shared = [torch.randint(5, 500, (64,), generator=g).tolist() for _ in range(3)]
     prompts = [shared[i % 3] + torch.randint(5, 500, (5 + i,), generator=g).tolist() for i in range(12)]
+    # unrelated long prompts between the waves push the cached prefixes out of the 40-page pool
+    filler = [torch.randint(5, 500, (150,), generator=g).tolist() for _ in range(4)]
+    order = prompts[:8] + filler + prompts[8:]
     sp = SamplingParams(max_tokens=16, temperature=0.0, ignore_eos=True)
     cold = LLMEngine(EngineConfig(**base, enable_prefix_caching=False, num_blocks=256))
-    want = [r.output for r in cold.generate(prompts, sp)]
+    want = [r.output for r in cold.generate(order, sp)]
     eng = LLMEngine(EngineConfig(**base, enable_prefix_caching=True, num_blocks=40, host_kv_gb=0.05),
                     model=cold.model)
     eng.warmup()
     got = []
-    for i in range(0, 12, 4):         # waves: later waves hit pages published / spilled by earlier ones
-        got += [r.output for r in eng.generate(prompts[i:i + 4], sp)]
+    for i in range(0, len(order), 4):  # waves: later waves hit pages published / spilled by earlier ones
+        got += [r.output for r in eng.generate(order[i:i + 4], sp)]
     torch.cuda.synchronize()
     assert got == want
     st = eng.scheduler.stats()
-    assert st["prefix_hit_rate"] > 0.3, st
+    assert st["prefix_hit_rate"] > 0.2, st
     assert eng.runner.graphs is not None and eng.runner.graphs.captured
     assert eng.host_tier.stats["spilled"] > 0 and eng.scheduler.radix.host_hits_blocks > 0, eng.host_tier.stats
 
@@ -249,3 +252,30 @@ def test_gpu_swap_in_feeds_captured_decode(prefix_caching):
     assert eng.stats["prefill_tokens"] == sum(len(p) for p in prompts)
     assert ts["restore_dmas"] < ts["restored"] or ts["restored"] <= st["swapped_in"], ts
     assert ts["gates"] > 0
+
+
+@pytest.mark.parametrize("host_kv_gb", [0.0, 0.05])
+def test_admission_evicts_whole_cached_chains(host_kv_gb):
+    """A prompt needing more pages than the radix tree's current leaves hold is admitted by
+    evicting chain after chain (leaves first, then the parents they expose) — the capacity
+    check counts every page repeated leaf eviction frees, so the engine cannot stall with
+    nothing running while the cache holds the pages."""
+    base = dict(model="llama-tiny", device="cpu", max_num_seqs=8, max_num_batched_tokens=256,
+                max_model_len=512, use_graphs=False)
+    g = torch.Generator().manual_seed(11)
+    shared = [torch.randint(5, 500, (64,), generator=g).tolist() for _ in range(3)]
+    prompts = [shared[i % 3] + torch.randint(5, 500, (5 + i,), generator=g).tolist() for i in range(12)]
+    filler = [torch.randint(5, 500, (150,), generator=g).tolist() for _ in range(4)]
+    order = prompts[:8] + filler + prompts[8:]
+    sp = SamplingParams(max_tokens=16, temperature=0.0, ignore_eos=True)
+    cold = LLMEngine(EngineConfig(**base, enable_prefix_caching=False, num_blocks=256))
+    want = [r.output for r in cold.generate(order, sp)]
+    eng = LLMEngine(EngineConfig(**base, enable_prefix_caching=True, num_blocks=40, host_kv_gb=host_kv_gb),
+                    model=cold.model)
+    got = []
+    for i in range(0, len(order), 4):
+        got += [r.output for r in eng.generate(order[i:i + 4], sp)]
+    assert got == want
+    assert eng.scheduler.stats()["prefix_hit_rate"] > 0.1
+    if host_kv_gb:
+        assert eng.host_tier.stats["spilled"] > 0 and eng.scheduler.radix.host_hits_blocks > 0
