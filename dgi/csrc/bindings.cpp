@@ -32,6 +32,8 @@ int dgi_skinny_gemm(const void* x, int ldx, const void* w, const void* bias, voi
 int dgi_mfma_gemm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int epi,
                   hipStream_t s);
 void dgi_set_gemm_cus(int cus);
+int dgi_mfma_gemm_norm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int kind,
+                       float* ss, int ss_ld, float inv_k, float eps, int phases, hipStream_t s);
 int dgi_fused_skinny(const void* x, int ldx, const void* res, int ldr, void* res_out, const void* gamma,
                      float eps, const void* w, const void* bias, void* y, int ldy, int M, int N, int K, int pro,
                      int epi, const int* positions, const float* cos_sin, const int* slots, void* k_cache,
@@ -237,6 +239,34 @@ void mfma_gemm(at::Tensor out, const at::Tensor& x, const at::Tensor& w, int64_t
   check_rc(dgi_mfma_gemm(x.data_ptr(), (int)x.stride(0), w.data_ptr(), out.data_ptr(), (int)out.stride(0), (int)M,
                          (int)N, (int)K, (int)epi, cur_stream()),
            "mfma_gemm");
+}
+
+// Fused-RMSNorm MFMA GEMMs (ping-pong schedule, dgi/csrc/mfma_gemm.hip): kind 2 residual
+// (out += x w^T in place, per-row partial sums of squares -> ss[:, N / 256]); 3 out = rstd * x w^T;
+// 4 out = SwiGLU(rstd * x [gate; up]^T); rstd = rsqrt(sum(ss[m, :]) * inv_k + eps).
+void mfma_gemm_norm(at::Tensor out, const at::Tensor& x, const at::Tensor& w, int64_t kind, at::Tensor ss,
+                    double inv_k, double eps, int64_t phases) {
+  check_bf16(out, "out"); check_bf16(x, "x"); check_bf16(w, "w");
+  TORCH_CHECK(ss.scalar_type() == at::kFloat && ss.dim() == 2 && ss.is_contiguous(), "mfma_gemm_norm: ss fp32 [M, n]");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "mfma_gemm_norm: 2-D operands");
+  TORCH_CHECK(x.device() == w.device() && x.device() == out.device() && ss.device() == x.device(),
+              "mfma_gemm_norm: operands on one device");
+  TORCH_CHECK(x.stride(1) == 1 && out.stride(1) == 1 && w.is_contiguous(), "mfma_gemm_norm: row-major operands");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(kind >= 2 && kind <= 4, "mfma_gemm_norm: kind 2 (residual), 3 (norm), 4 (norm + SwiGLU)");
+  TORCH_CHECK(w.size(1) == K && out.size(0) == M && ss.size(0) >= M, "mfma_gemm_norm: shape mismatch");
+  TORCH_CHECK(out.size(1) == (kind == 4 ? N / 2 : N), "mfma_gemm_norm: output columns");
+  TORCH_CHECK(kind != 2 || ss.size(1) >= N / 256, "mfma_gemm_norm: ss needs N / 256 columns");
+  TORCH_CHECK(N % 256 == 0 && K % 128 == 0 && K >= 256 && x.stride(0) % 8 == 0 && out.stride(0) % 4 == 0,
+              "mfma_gemm_norm: N%256, K%128, ldx%8, ldy%4");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0 &&
+              reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0, "mfma_gemm_norm: operand alignment");
+  TORCH_CHECK((int64_t)M * x.stride(0) < (1LL << 31) && (int64_t)M * out.stride(0) < (1LL << 31),
+              "mfma_gemm_norm: activation too large for 32-bit offsets");
+  check_rc(dgi_mfma_gemm_norm(x.data_ptr(), (int)x.stride(0), w.data_ptr(), out.data_ptr(), (int)out.stride(0), (int)M,
+                              (int)N, (int)K, (int)kind, ss.data_ptr<float>(), (int)ss.size(1), (float)inv_k,
+                              (float)eps, (int)phases, cur_stream()),
+           "mfma_gemm_norm");
 }
 
 // Decode GEMM with fused RMSNorm prologue (pro 1: norm, 2: residual add + norm -> res_out) and
@@ -522,6 +552,8 @@ TORCH_LIBRARY(dgi, m) {
   m.def("silu_mul(Tensor(a!) out, Tensor gu) -> ()");
   m.def("skinny_gemm(Tensor(a!) out, Tensor x, Tensor w, Tensor? bias, int cfg=0) -> ()");
   m.def("mfma_gemm(Tensor(a!) out, Tensor x, Tensor w, int epi=0) -> ()");
+  m.def("mfma_gemm_norm(Tensor(a!) out, Tensor x, Tensor w, int kind, Tensor(b!) ss, float inv_k, float eps, "
+        "int phases=0) -> ()");
   m.def("fused_skinny(Tensor(a!) y, Tensor x, Tensor? res, Tensor(b!)? res_out, Tensor? gamma, float eps, "
         "Tensor w, Tensor? bias, int pro, int epi, Tensor? positions, Tensor? cos_sin, Tensor? slots, "
         "Tensor(c!)? k_cache, Tensor(d!)? v_cache, int nh=0, int nkv=0, int cfg=0) -> ()");
@@ -550,6 +582,7 @@ TORCH_LIBRARY_IMPL(dgi, CUDA, m) {
   m.impl("silu_mul", &silu_mul);
   m.impl("skinny_gemm", &skinny_gemm);
   m.impl("mfma_gemm", &mfma_gemm);
+  m.impl("mfma_gemm_norm", &mfma_gemm_norm);
   m.impl("fused_skinny", &fused_skinny);
   m.impl("sample", &sample);
   m.impl("topk", &topk);

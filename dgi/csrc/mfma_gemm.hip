@@ -75,9 +75,38 @@ __device__ __forceinline__ void store_pair16(uint16_t* yrow, int n0, int g, cons
   *(uint4*)(yrow + n0 + 16 * (g & 1) + 4 * (g & 2)) = v;
 }
 
+// Epilogue kinds of the ping-pong kernel (the other schedules take 0 and 1):
+//   0 plain store;  1 SwiGLU over [gate; up];
+//   2 residual:  Y <- Y + acc in place (Y is the residual stream), and the tile's per-row sum of
+//     squares of the new bf16 values to ss[m * ss_ld + tn] — the partial RMS statistics of the
+//     next RMSNorm, reduced in a fixed order (deterministic, no atomics);
+//   3 / 4 normalised plain / SwiGLU:  acc scaled per row by rstd[m] = rsqrt(sum_j ss[m, j] / K + eps)
+//     before the store / activation.  With the RMSNorm gain folded into the weights
+//     (W' = W * diag(gamma), LlamaModel.fold_norms) this is rmsnorm(x) * gamma @ W^T without
+//     the normalised copy of x: the norm kernels between the projections disappear.
+template <int EPI>
+struct EpiKind {
+  static constexpr bool swiglu = EPI == 1 || EPI == 4;
+  static constexpr bool norm = EPI == 3 || EPI == 4;
+  static constexpr bool res = EPI == 2;
+};
+
+// store_pair16's column exchange on fp32 values: f[0..7] are the lane's 8 consecutive columns
+// (A 0-7 for lane group 0, B 0-7 for 1, A 8-15 for 2, B 8-15 for 3) starting at
+// n0 + 16 (g & 1) + 4 (g & 2)
+__device__ __forceinline__ void swap_pair(const float (&a)[4], const float (&b)[4], float (&f)[8]) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[e]), __float_as_uint(b[e]), false, false);
+    f[e] = __uint_as_float(s[0]);
+    f[4 + e] = __uint_as_float(s[1]);
+  }
+}
+
+// rs: the tile's 256 per-row rstd values (LDS) for EPI 3 / 4
 template <int EPI>
 __device__ __forceinline__ void epilogue(const f32x4 (&acc)[8][4], uint16_t* __restrict__ Y, int ldy, int M, int m0,
-                                         int tn, int wm, int wn, int lane) {
+                                         int tn, int wm, int wn, int lane, const float* rs = nullptr) {
   const int r16 = lane & 15;
   const int g = lane >> 4;
 #pragma unroll
@@ -86,13 +115,20 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[8][4], uint16_t* __r
     // the swap partners (lanes l, l ^ 16) hold the same row, so a row past M drops both together
     if (m >= M) continue;
     uint16_t* yrow = Y + (size_t)m * ldy;
-    if (EPI == 1) {
+    float sc = 1.f;
+    if constexpr (EpiKind<EPI>::norm) sc = rs[wm * 128 + i * 16 + r16];
+    if constexpr (EpiKind<EPI>::swiglu) {
       float o[2][4];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const f32x4 gt = acc[i][j], u = acc[i][j + 2];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[j][e] = silu(gt[e]) * u[e];
+        for (int e = 0; e < 4; ++e) {
+          if constexpr (EpiKind<EPI>::norm)
+            o[j][e] = silu(gt[e] * sc) * (u[e] * sc);
+          else
+            o[j][e] = silu(gt[e]) * u[e];
+        }
       }
       store_pair16(yrow, tn * 128 + wn * 32, g, o[0], o[1]);
     } else {
@@ -101,13 +137,60 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[8][4], uint16_t* __r
         float x0[4], x1[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          x0[e] = acc[i][j][e];
-          x1[e] = acc[i][j + 1][e];
+          x0[e] = acc[i][j][e] * sc;
+          x1[e] = acc[i][j + 1][e] * sc;
         }
         store_pair16(yrow, tn * 256 + wn * 64 + j * 16, g, x0, x1);
       }
     }
   }
+}
+
+// EPI 2: Y <- bf16(Y + acc) and ss[m * ss_ld + tn] = sum over the tile's 256 columns of the new
+// values squared.  Per row: each lane sums its 16 columns, the 4 lane groups of a wave combine by
+// shuffles, the 4 waves of a row band through LDS (ssl: 4 x 256 floats), in a fixed order.
+// Every wave of the block must call it (one barrier).
+__device__ __forceinline__ void epilogue_res(const f32x4 (&acc)[8][4], uint16_t* __restrict__ Y, int ldy, int M,
+                                             int m0, int tn, int wm, int wn, int lane, float* ssl,
+                                             float* __restrict__ ss, int ss_ld) {
+  const int r16 = lane & 15;
+  const int g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + r16;
+    if (m >= M) continue;
+    uint16_t* yrow = Y + (size_t)m * ldy;
+    float part = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; j += 2) {
+      float x0[4], x1[4], f[8], o[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        x0[e] = acc[i][j][e];
+        x1[e] = acc[i][j + 1][e];
+      }
+      swap_pair(x0, x1, f);
+      uint4* p = (uint4*)(yrow + tn * 256 + wn * 64 + j * 16 + 16 * (g & 1) + 4 * (g & 2));
+      const uint4 old = *p;
+      const u32x4 ov = {old.x, old.y, old.z, old.w};
+      unpack8(ov, o);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] += f[e];
+      const u32x4 nv = pack8(o);
+      *p = uint4{nv[0], nv[1], nv[2], nv[3]};
+      float r[8];
+      unpack8(nv, r);                 // the rounded values the next norm reads
+#pragma unroll
+      for (int e = 0; e < 8; ++e) part += r[e] * r[e];
+    }
+    part += __shfl_xor(part, 16, 64);
+    part += __shfl_xor(part, 32, 64);
+    if (g == 0) ssl[wn * 256 + wm * 128 + i * 16 + r16] = part;
+  }
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < 256 && m0 + t < M)
+    ss[(size_t)(m0 + t) * ss_ld + tn] = ((ssl[t] + ssl[256 + t]) + ssl[512 + t]) + ssl[768 + t];
 }
 
 template <int EPI, int SCHED>
@@ -575,6 +658,9 @@ struct PPArgs {
   int ldx, ldy, M, I, K, tiles_m, tiles_total;
   int rem, splits, full, P;   // P == 0: one tile per block (grid = tiles)
   int ovl;                    // issue the next tile's prologue before the current epilogue
+  float* ss;                  // EPI 2: per-row partial sums of squares out; EPI 3 / 4: in
+  int ss_ld;                  // row stride of ss (EPI 2: its column is the N tile; EPI 3 / 4: partials per row)
+  float inv_k, eps;           // EPI 3 / 4: rstd = rsqrt(sum * inv_k + eps)
 };
 
 // buffer resource word 3 of a raw (stride 0, byte-addressed) buffer on gfx9, and the cache
@@ -697,6 +783,10 @@ __device__ __forceinline__ void drive(const PPArgs& a, char* smem, Pro&& prologu
 template <int EPI, int PRIO, int PH>
 __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kStageBytes];
+  // EPI 2: per-wave row partials of the sum of squares; EPI 3 / 4: two slots of the tile's rstd
+  // (slot per work item: a fast wave may start the next item while others still store this one)
+  __shared__ float ep_lds[EpiKind<EPI>::res ? 1024 : EpiKind<EPI>::norm ? 512 : 1];
+  int rs_slot = 0;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int w = tid >> 6;
@@ -778,7 +868,7 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) xs[i] = a.X + (size_t)min(m0 + q + i * 64, M - 1) * ldx + lc * 8 + kb * kBK;
     int wrow0, wstep;
-    if (EPI == 1) {
+    if (EpiKind<EPI>::swiglu) {
       wrow0 = tn * 128 + (q < 32 ? q : a.I + q - 32);
       wstep = 32;
     } else {
@@ -812,6 +902,19 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (EpiKind<EPI>::norm) {
+      // the tile's row statistics: partial sums in a fixed order, rstd into this item's LDS slot
+      // (visible to every wave by the K loop's barriers; the epilogue reads it)
+      rs_slot ^= 1;
+      const int t = fresh_tid();
+      if (t < 256) {
+        const int m = min(tm * kBM + t, M - 1);
+        const float* sp = a.ss + (size_t)m * a.ss_ld;
+        float s = 0.f;
+        for (int j = 0; j < a.ss_ld; ++j) s += sp[j];
+        ep_lds[rs_slot * 256 + t] = rsqrtf(s * a.inv_k + a.eps);
+      }
+    }
 
     // one K tile; ST = its LDS stage, MODE 0: t + 2 < L, 1: t + 2 == L, 2: t + 1 == L
     auto tile = [&](int t, auto ST_, auto MODE_) {
@@ -883,7 +986,7 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
     using T2 = std::integral_constant<int, 2>;
     if constexpr (PH == 2) {
       if (!ov) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-      else if constexpr (EPI == 1) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
+      else if constexpr (EpiKind<EPI>::swiglu) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(19)" ::: "memory");
       barrier();
       if (wm == 1) barrier();     // stagger: waves 4-7 run one section behind
@@ -896,7 +999,7 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
       tile2(t + 1, O{}, T2{});
     } else {
       if (!ov) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else if constexpr (EPI == 1) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+      else if constexpr (EpiKind<EPI>::swiglu) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
       barrier();
       if (wm == 1) barrier();     // stagger: waves 4-7 run one section behind
@@ -943,7 +1046,12 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
              },
              [&](int tm, int tn) {
                const int te = fresh_tid();
-               epilogue<EPI>(acc, a.Y, a.ldy, M, tm * kBM, tn, (te >> 8) & 1, (te >> 6) & 3, te & 63);
+               if constexpr (EpiKind<EPI>::res)
+                 epilogue_res(acc, a.Y, a.ldy, M, tm * kBM, tn, (te >> 8) & 1, (te >> 6) & 3, te & 63, ep_lds, a.ss,
+                              a.ss_ld);
+               else
+                 epilogue<EPI>(acc, a.Y, a.ldy, M, tm * kBM, tn, (te >> 8) & 1, (te >> 6) & 3, te & 63,
+                               ep_lds + rs_slot * 256);
              });
 }
 
@@ -988,17 +1096,28 @@ int g_cu_limit = 0;
 
 // skmode 0: whole tiles only; 1: hybrid split-K when the tiles leave the last wave at most half
 // full (and fewer than 8 full waves); 2: hybrid whenever tiles % CUs leaves room for 2 splits
+struct NormArgs {
+  float* ss = nullptr;
+  int ss_ld = 0;
+  float inv_k = 0.f, eps = 0.f;
+};
+
 template <int EPI>
 void launch_pp(const void* x, int ldx, const void* w, void* y, int ldy, int M, int I, int K, int tiles_m, int total,
-               int skmode, int prio, hipStream_t s) {
-  auto kern = (prio & 4) ? (prio & 3) == 1   ? mfma_gemm_pp_kernel<EPI, 1, 2>
-                            : (prio & 3) == 2 ? mfma_gemm_pp_kernel<EPI, 2, 2>
-                                              : mfma_gemm_pp_kernel<EPI, 0, 2>
-                          : (prio & 3) == 1   ? mfma_gemm_pp_kernel<EPI, 1, 4>
-                          : (prio & 3) == 2   ? mfma_gemm_pp_kernel<EPI, 2, 4>
-                                              : mfma_gemm_pp_kernel<EPI, 0, 4>;
+               int skmode, int prio, hipStream_t s, const NormArgs& na = NormArgs{}) {
+  decltype(&mfma_gemm_pp_kernel<EPI, 0, 2>) kern;
+  if constexpr (EPI >= 2)       // the fused-norm epilogues: default priority scheme only
+    kern = (prio & 4) ? mfma_gemm_pp_kernel<EPI, 0, 2> : mfma_gemm_pp_kernel<EPI, 0, 4>;
+  else
+    kern = (prio & 4) ? (prio & 3) == 1   ? mfma_gemm_pp_kernel<EPI, 1, 2>
+                        : (prio & 3) == 2 ? mfma_gemm_pp_kernel<EPI, 2, 2>
+                                          : mfma_gemm_pp_kernel<EPI, 0, 2>
+                      : (prio & 3) == 1   ? mfma_gemm_pp_kernel<EPI, 1, 4>
+                      : (prio & 3) == 2   ? mfma_gemm_pp_kernel<EPI, 2, 4>
+                                          : mfma_gemm_pp_kernel<EPI, 0, 4>;
+  // EPI 2 reads the tile it stores (in place): no overlap of the next tile's loads with it
   PPArgs a{(const uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, nullptr, nullptr, ldx, ldy, M, I, K, tiles_m, total,
-           0, 0, 0, 0, !(prio & 8)};
+           0, 0, 0, 0, !(prio & 8) && EPI != 2, na.ss, na.ss_ld, na.inv_k, na.eps};
   const int nt = K / kBK;
   SkWorkspace* sk = ((skmode || a.ovl) && nt >= 8) ? sk_workspace(s) : nullptr;
   if (sk) {
@@ -1049,6 +1168,35 @@ void launch(const void* x, int ldx, const void* w, void* y, int ldy, int M, int 
 // four 16-MFMA phases (default: two up to M = 2560, see mfma_gemm_pp_kernel), (epi >> 14) & 1: no
 // cross-tile overlap (next tile's prologue after the epilogue; whole waves of tiles not persistent).
 extern "C" void dgi_set_gemm_cus(int cus) { g_cu_limit = cus; }
+
+// The fused-RMSNorm GEMMs (ping-pong schedule): kind 2 = residual (y += x w^T in place, row
+// partial sums of squares to ss[:, N / 256 columns]), 3 = y = rstd * x w^T, 4 = SwiGLU of
+// rstd * x [gate; up]^T, with rstd from the ss_ld partials per row of ss.  phases: 0 auto, 2, 4.
+extern "C" int dgi_mfma_gemm_norm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K,
+                                  int kind, float* ss, int ss_ld, float inv_k, float eps, int phases, hipStream_t s) {
+  if (M <= 0) return 0;
+  if (kind < 2 || kind > 4 || K % (2 * kBK) || K < 4 * kBK || ldx % 8 || ldy % 4 || N % 256 || !ss || ss_ld <= 0)
+    return -3;
+  if (kind == 2 && ss_ld < N / 256) return -3;
+  int prio = (phases == 2 || (phases == 0 && M <= 2560)) ? 4 : 0;
+  const int I = kind == 4 ? N / 2 : 0;
+  const int tiles_n = kind == 4 ? I / 128 : N / 256;
+  const int tiles_m = (M + kBM - 1) / kBM;
+  const int total = tiles_m * tiles_n;
+  NormArgs na;
+  na.ss = ss;
+  na.ss_ld = ss_ld;
+  na.inv_k = inv_k;
+  na.eps = eps;
+  if (kind == 2)
+    launch_pp<2>(x, ldx, w, y, ldy, M, I, K, tiles_m, total, 1, prio, s, na);
+  else if (kind == 3)
+    launch_pp<3>(x, ldx, w, y, ldy, M, I, K, tiles_m, total, 1, prio, s, na);
+  else
+    launch_pp<4>(x, ldx, w, y, ldy, M, I, K, tiles_m, total, 1, prio, s, na);
+  DGI_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int dgi_mfma_gemm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K,
                              int epi, hipStream_t s) {

@@ -180,7 +180,15 @@ class LLMEngine:
                 self.model.mlp_pad = self.mlp_pad_table.pad
                 self.model.mlp_impl = self.mlp_pad_table.impl
                 self.model.proj_impl = self.mlp_pad_table.proj_impl
+                H = self.model.cfg.hidden_size
+                self.model.fold_impl = lambda rows, _t=self.mlp_pad_table: _t.fold(rows, H)
                 self.mlp_pad_seconds = time.perf_counter() - t1
+        # the fused-norm layers need the gains folded into the weights; done once, eagerly, so every
+        # engine sharing this model (and every captured graph) computes with the same weights
+        if self.device.type == "cuda" and hasattr(self.model, "fold_norms"):
+            from dgi.models import llama as _llama
+            if _llama.NORM_FOLD != "0":
+                self.model.fold_norms()
 
     # ------------------------------------------------------------------ API
     def add_request(self, prompt_ids: list[int], params: Optional[SamplingParams] = None, rid=None,

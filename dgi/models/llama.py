@@ -60,6 +60,16 @@ TBO = os.environ.get("DGI_TBO", "0") == "1"
 # dispatch already splits decode and prefill rows; 5 kernels per layer instead of 9
 FUSED_SMALL_PREFILL = os.environ.get("DGI_FUSED_SMALL_PREFILL", "1") == "1"
 TBO_MIN_ROWS = int(os.environ.get("DGI_TBO_MIN_ROWS", "512"))
+# Fused-norm layers (``LlamaModel._forward_layers_folded``): the RMSNorm gains are folded into the
+# qkv / gate_up weights once (``fold_norms``), the o-proj and down GEMMs add into the residual
+# stream in their epilogue and emit its per-row sums of squares, and the qkv / gate_up GEMMs
+# scale their rows by the resulting rstd — no norm kernel and no normalised copy of the stream
+# between the four projections (dgi/csrc/mfma_gemm.hip EPI 2-4).  "1": where the GEMM routing
+# table prices the all-MFMA layer at least as fast as the best mix plus the norm kernels it
+# removes; "force": every eligible step; "0": off.  Steps below NORM_FOLD_MIN_ROWS keep the
+# skinny / fused-decode kernels.
+NORM_FOLD = os.environ.get("DGI_NORM_FOLD", "1")
+NORM_FOLD_MIN_ROWS = int(os.environ.get("DGI_NORM_FOLD_MIN_ROWS", "256"))
 TBO_SIDE_PER_XCD = int(os.environ.get("DGI_TBO_SIDE", "4"))
 
 
@@ -139,6 +149,9 @@ class LlamaModel:
         self._pad_buf: Optional[torch.Tensor] = None
         self._attn_buf: Optional[torch.Tensor] = None
         self.load_info: Optional[dict] = None
+        self.norms_folded = False    # fold_norms ran: in_norm / post_norm are ones, qkv / gate_up carry the gains
+        self.fold_impl = None        # rows -> run the fused-norm layers? (dgi.runtime.gemm_pad)
+        self._ss_buf: Optional[torch.Tensor] = None
         if checkpoint:
             # real weights: only this rank's layers / TP slices are read (dgi.models.weights)
             from dgi.models.weights import load_checkpoint
@@ -201,8 +214,33 @@ class LlamaModel:
             else:
                 self.lm_head = _rand((c.vocab_size, H), gen, dev, dt, std)
 
+    def fold_norms(self) -> None:
+        """Fold each layer's RMSNorm gains into the projection that consumes the norm:
+        qkv <- qkv * diag(in_norm), gate_up <- gate_up * diag(post_norm) (fp32 product,
+        rounded once), and the gains become ones.  Every forward path computes the same
+        function afterwards (the unfused norms multiply by ones); the fused-norm layers need
+        it.  Idempotent; reloading weights clears the flag."""
+        if self.norms_folded:
+            return
+        with torch.no_grad():
+            for L in self.layers:
+                for w, g in ((L.qkv, L.in_norm), (L.gate_up, L.post_norm)):
+                    gf = g.float()[None]
+                    step = max(1, (64 << 20) // (4 * w.shape[1]))      # bounded fp32 temporaries
+                    for r0 in range(0, w.shape[0], step):
+                        blk = w[r0:r0 + step]
+                        blk.copy_((blk.float() * gf).to(w.dtype))
+                    g.fill_(1.0)
+            if self.layers and self.cfg.hidden_size % 256 == 0:
+                # the row statistics of the fused-norm layers, allocated here so a graph capture
+                # never allocates it (steps of more rows grow it eagerly)
+                self._ss_buf = torch.empty(16384, self.cfg.hidden_size // 256, device=self.device,
+                                           dtype=torch.float32)
+        self.norms_folded = True
+
     def load_state_dict_hf(self, sd: dict):
         """Load HF Llama tensor names (``model.layers.N.self_attn.q_proj.weight``...)."""
+        self.norms_folded = False
         c = self.cfg
         for i, li in enumerate(range(self.layer_start, self.layer_end)):
             p = f"model.layers.{li}."
@@ -246,6 +284,7 @@ class LlamaModel:
         """Copy weights of the overlapping layer range from another instance
         (any device) — used to compare CPU / GPU / sharded models exactly."""
         src = dict(other.tensors())
+        self.norms_folded = other.norms_folded
         for name, t in self.tensors():
             if name in src:
                 t.copy_(src[name])
@@ -386,6 +425,84 @@ class LlamaModel:
                 self.layer_hook(self.layer_start + i)
         return h, residual
 
+    # ------------------------------------------------------------------ fused-norm layers
+    def _fold_ok(self, h: torch.Tensor) -> bool:
+        if NORM_FOLD == "0" or self.reduce is not None:
+            return False
+        if not h.is_cuda:           # "force-cpu": the same composition through the reference ops (tests)
+            return NORM_FOLD == "force-cpu" and h.shape[0] >= NORM_FOLD_MIN_ROWS and self.layers[0].qkv_bias is None
+        if h.dtype != torch.bfloat16:
+            return False
+        T = h.shape[0]
+        if T < NORM_FOLD_MIN_ROWS:
+            return False
+        L = self.layers[0]
+        if L.qkv_bias is not None or self.cfg.hidden_size % 256:
+            return False
+        if torch.cuda.is_current_stream_capturing() and not self.norms_folded:
+            return False            # weights are folded eagerly, never inside a capture
+        ok = getattr(self, "_fold_shapes_ok", None)
+        if ok is None:
+            x = h[:1]
+            a = torch.empty(1, L.o.shape[1], device=h.device, dtype=h.dtype)
+            m = torch.empty(1, L.down.shape[1], device=h.device, dtype=h.dtype)
+            ok = self._fold_shapes_ok = (ops.mfma_norm_ok(x, L.qkv) and ops.mfma_norm_ok(a, L.o)
+                                         and ops.mfma_norm_ok(x, L.gate_up) and ops.mfma_norm_ok(m, L.down)
+                                         and (L.gate_up.shape[0] // 2) % 128 == 0)
+        if not ok:
+            return False
+        if NORM_FOLD == "force":
+            return True
+        return self.fold_impl is not None and bool(self.fold_impl(T))
+
+    def _forward_layers_folded(self, h: torch.Tensor, meta: AttnMeta, residual: Optional[torch.Tensor],
+                               trim_last: Optional[torch.Tensor]):
+        """Layers on the fused-norm MFMA GEMMs (see NORM_FOLD).  Per layer::
+
+            qkv  = rstd(ss) * (R @ qkv'^T)        (in_norm folded into qkv')
+            attn = attention(qkv)
+            R   += attn @ o^T;    ss <- row sums of squares of R
+            act  = SwiGLU(rstd(ss) * (R @ gate_up'^T))
+            R   += act @ down^T;  ss <- ...
+
+        R is the residual stream (updated in place); returns (R, None), or for ``trim_last``
+        the last layer's MLP output of the logits rows and their stream (the unfused contract)."""
+        if not self.norms_folded:
+            self.fold_norms()
+        c = self.cfg
+        eps = c.rms_eps
+        T, H = h.shape
+        R = h if residual is None else h + residual      # forward() hands over a tensor it owns
+        nt = H // 256
+        ss = self._ss_buf
+        if ss is None or ss.shape[0] < T or ss.shape[1] != nt or ss.device != h.device:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("fused-norm layers: statistics buffer must exist before capture")
+            ss = self._ss_buf = torch.empty(max(T, 4096), nt, device=h.device, dtype=torch.float32)
+        ss = ss[:T]
+        ops.row_sumsq(R, ss)
+        n = len(self.layers)
+        for i, L in enumerate(self.layers):
+            qkv = ops.mfma_gemm_norm(R, L.qkv, ops.NORM_PLAIN, ss, eps)
+            attn = self.attention(i, qkv, meta)
+            if trim_last is not None and i == n - 1:
+                attn = attn.index_select(0, trim_last)
+                Rs = R.index_select(0, trim_last)
+                ho = ops.linear(attn, L.o)
+                ops.fused_add_rmsnorm(ho, Rs, L.post_norm, eps)
+                out = ops.linear(ops.silu_mul(ops.linear(ho, L.gate_up)), L.down)
+                if self.layer_hook is not None:
+                    self.layer_hook(self.layer_start + i)
+                return out, Rs
+            ops.mfma_gemm_norm(attn, L.o, ops.NORM_RES, ss, eps, out=R)
+            act = ops.mfma_gemm_norm(R, L.gate_up, ops.NORM_SWIGLU, ss, eps)
+            ops.mfma_gemm_norm(act, L.down, ops.NORM_RES, ss, eps, out=R)
+            if self.capture_layers and (self.layer_start + i) in self.capture_layers:
+                self.captured[self.layer_start + i] = R.clone()
+            if self.layer_hook is not None:
+                self.layer_hook(self.layer_start + i)
+        return R, None
+
     # ------------------------------------------------------------------ two-batch overlap
     def _tbo_ok(self, h: torch.Tensor, meta: AttnMeta, trim_last) -> Optional[tuple]:
         if not (TBO and h.is_cuda and self.layers and meta.num_prefill_tokens == 0 and trim_last is None
@@ -496,6 +613,8 @@ class LlamaModel:
             split = self._tbo_ok(h, meta, trim_last)
             if split is not None:
                 return self._forward_layers_tbo(h, meta, residual, split)
+            if self._fold_ok(h):
+                return self._forward_layers_folded(h, meta, residual, trim_last)
             fq, fg = self._fused_decode(h, meta)
             if fq or fg:
                 h, residual = self._forward_layers_fused(h, meta, residual, fq, fg)

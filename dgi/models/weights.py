@@ -118,6 +118,7 @@ def load_checkpoint(model, path: str, tp_rank: int = 0, tp: int = 1) -> dict:
 
     ``model.cfg`` is the LOCAL config (per-rank heads / intermediate for TP);
     ``full`` is the checkpoint's.  Returns {"tensors": n, "bytes": b}."""
+    model.norms_folded = False
     rd = CheckpointReader(path)
     c = model.cfg
     full = getattr(model, "full_cfg", c)

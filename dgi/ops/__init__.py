@@ -614,6 +614,70 @@ def mfma_gemm(x: torch.Tensor, w: torch.Tensor, epi: int = 0, out: Optional[torc
     return r
 
 
+NORM_RES, NORM_PLAIN, NORM_SWIGLU = 2, 3, 4
+
+
+def mfma_gemm_norm_ref(x: torch.Tensor, w: torch.Tensor, kind: int, ss: torch.Tensor, eps: float,
+                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp32 reference of ``mfma_gemm_norm`` (same contract, any device)."""
+    y = x.float() @ w.float().t()
+    M = x.shape[0]
+    if kind == NORM_RES:
+        new = (out.float() + y).to(out.dtype)
+        out.copy_(new)
+        nf = new.float()
+        ss[:M, : w.shape[0] // 256].copy_((nf * nf).view(M, -1, 256).sum(-1))
+        return out
+    rstd = torch.rsqrt(ss[:M].sum(-1, keepdim=True) / x.shape[1] + eps)
+    y = y * rstd
+    if kind == NORM_SWIGLU:
+        I = w.shape[0] // 2
+        y = torch.nn.functional.silu(y[:, :I]) * y[:, I:]
+    r = y.to(x.dtype)
+    if out is None:
+        return r
+    out.copy_(r)
+    return out
+
+
+def mfma_gemm_norm(x: torch.Tensor, w: torch.Tensor, kind: int, ss: torch.Tensor, eps: float,
+                   out: Optional[torch.Tensor] = None, phases: int = 0) -> torch.Tensor:
+    """The ping-pong MFMA GEMM with a fused RMSNorm epilogue (dgi/csrc/mfma_gemm.hip, EPI 2-4).
+
+    ``kind`` 2 (NORM_RES): ``out`` is the residual stream, updated in place to out + x @ w.T,
+    and ``ss[m, j]`` receives the sum of squares of the new row m over columns 256 j .. 256 j + 255
+    (``ss`` has N / 256 columns): the statistics of the next RMSNorm, with no norm kernel.
+    ``kind`` 3 / 4 (NORM_PLAIN / NORM_SWIGLU): x is the un-normalised residual stream and
+    ``w`` carries the norm's gain (``LlamaModel.fold_norms``); each output row is scaled by
+    rsqrt(sum(ss[m]) / K + eps) — then SwiGLU for kind 4 — which equals
+    (rmsnorm(x) * gamma) @ w.T up to rounding."""
+    M = x.shape[0]
+    N = w.shape[0] // 2 if kind == NORM_SWIGLU else w.shape[0]
+    if kind == NORM_RES and out is None:
+        raise ValueError("mfma_gemm_norm: kind 2 updates the residual `out` in place")
+    if _native(x):
+        if out is None:
+            out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+        _call("mfma_gemm_norm", out, x, w, kind, ss, 1.0 / x.shape[1], eps, phases)
+        return out
+    return mfma_gemm_norm_ref(x, w, kind, ss, eps, out)
+
+
+def mfma_norm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    """Shapes the fused-norm GEMM takes (K % 128 and >= 256 on top of ``mfma_gemm_ok``)."""
+    return mfma_gemm_ok(x, w) and x.shape[1] % 128 == 0 and x.shape[1] >= 256
+
+
+def row_sumsq(x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """out[:, 0] = sum of squares of each row of x (fp32), the other columns zero: the
+    statistics the fused-norm GEMM reads for a stream no residual epilogue produced (the
+    first layer's input)."""
+    out.zero_()
+    xf = x.float()
+    out[: x.shape[0], 0] = (xf * xf).sum(-1)
+    return out
+
+
 # ----------------------------------------------------------------------------
 # Sampling
 # ----------------------------------------------------------------------------

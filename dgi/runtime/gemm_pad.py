@@ -176,6 +176,28 @@ class MlpPadTable:
             return False, False
         return self.proj_impls[bisect.bisect_left(self.grid, rows)]
 
+    # the two RMSNorm kernels a fused-norm layer removes, priced from their HBM traffic (read x and
+    # the residual, write both: 8 bytes per element each) plus a launch ramp; the round-2 profile
+    # measured 30.7 us per call at ~1,900 rows of the 70B stream (profiles/r2_70b_1gpu_kernel_stats.md)
+    NORM_HBM_TBS = 5.0
+    NORM_RAMP_MS = 0.004
+
+    def fold(self, rows: int, hidden: int = 8192) -> bool:
+        """Run the fused-norm layers at ``rows``?  Yes when the all-MFMA layer (qkv, o, gate_up,
+        down on the ping-pong kernel) costs no more than the best per-projection mix plus the
+        two norm kernels the fusion removes (first grid point >= rows)."""
+        if not self.raw or not self.grid or not (self.grid[0] <= rows <= self.grid[-1]):
+            return False
+        r = self.raw[bisect.bisect_left(self.grid, rows)]
+        keys = ("front", "front_mfma", "back", "back_mfma", "pq_blas", "pq_mfma", "po_blas", "po_mfma")
+        if any(r.get(k) is None for k in keys):
+            return False
+        mfma = r["front_mfma"] + r["back_mfma"] + r["pq_mfma"] + r["po_mfma"]
+        best = (min(r["front"], r["front_mfma"]) + min(r["back"], r["back_mfma"]) + min(r["pq_blas"], r["pq_mfma"])
+                + min(r["po_blas"], r["po_mfma"]))
+        norms = 2 * (self.NORM_RAMP_MS + rows * hidden * 8 / (self.NORM_HBM_TBS * 1e9))
+        return mfma <= best + norms
+
     def pad(self, T: int) -> int:
         """Rows to run the MLP on for a step of ``T`` rows (``T`` when the table has no say)."""
         r = self._cache.get(T)

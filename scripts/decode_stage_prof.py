@@ -34,7 +34,11 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--graphs", type=int, default=1)
     ap.add_argument("--out", default="")
+    ap.add_argument("--force-fold", action="store_true", help="fused-norm layers on every step (DGI_NORM_FOLD=force)")
     a = ap.parse_args()
+    if a.force_fold:
+        from dgi.models import llama
+        llama.NORM_FOLD = "force"
     mc = dataclasses.replace(get_config(a.model), num_layers=a.layers)
     bs = 16
     nb = a.rows * (a.ctx // bs + 4 + a.steps // bs + 4) + 8
@@ -48,7 +52,9 @@ def main():
         eng.step()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / a.steps * 1e3
+    from dgi.models import llama
     res = {"model": a.model, "layers": a.layers, "rows": a.rows, "ctx": a.ctx, "graphs": a.graphs,
+           "norm_fold": llama.NORM_FOLD,
            "ms_per_step": round(ms, 3), "tok_s": round(a.rows / ms * 1e3, 1)}
     print(json.dumps(res), flush=True)
     if a.out:

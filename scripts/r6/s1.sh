@@ -14,7 +14,7 @@ step() {  # name, timeout, command...
   echo "=== $name rc=$rc"; tail -3 "$O/$name.log" | cut -c1-1200
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
-step new_tests 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_host_tier.py tests/test_worker_daemon.py tests/test_kernels_gpu.py -k "host_tier or prefix or swap or served or kv_gather or kv_scatter or slot"
+step new_tests 400 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests/test_host_tier.py tests/test_worker_daemon.py tests/test_kernels_gpu.py tests/test_mfma_gemm.py -k "host_tier or prefix or swap or served or kv_gather or kv_scatter or slot or norm"
 step gpu_suite 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread
 step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
 step bench70b 600 python -u bench.py --steps 20 --warmup 5 --json-out $O/bench70b.json

@@ -911,3 +911,37 @@ def test_mixed_step_lookahead_matches_plain_steps(sampled, eos):
         p2, f2, _ = run(False, tok)
         l2, g2, _ = run(True, tok)
         assert l2 == p2 and g2 == f2 and "stop" in f2
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_fused_norm_layers_match_fp32(monkeypatch, graphs):
+    """The fused-norm layers (gains folded into qkv / gate_up, residual + row statistics in the
+    o / down epilogues, rstd in the qkv / gate_up epilogues) on every step — prefill chunks,
+    mixed steps and captured decode graphs: each generated token is an argmax of the fp32 CPU
+    model (teacher forced), and the path really ran."""
+    from dgi.engine import EngineConfig, LLMEngine
+    from dgi.models import llama
+    from dgi.models.config import get_config
+    from dgi.models.llama import LlamaModel
+    from dgi.sched.request import SamplingParams
+    monkeypatch.setattr(llama, "NORM_FOLD", "force")
+    monkeypatch.setattr(llama, "NORM_FOLD_MIN_ROWS", 1)
+    mc = get_config("llama-tiny-hd128")
+    cpu_model = LlamaModel(mc, "cpu", seed=5)
+    prompts = [[1] + list(range(3, 3 + n)) for n in (5, 40, 300, 7)]
+    gm = LlamaModel(mc, "cuda", init="empty").copy_from(cpu_model)
+    calls = [0]
+    orig = gm._forward_layers_folded
+
+    def spy(*a, **k):
+        calls[0] += 1
+        return orig(*a, **k)
+    gm._forward_layers_folded = spy
+    e = LLMEngine(EngineConfig(model="llama-tiny-hd128", device="cuda", num_blocks=256, max_num_seqs=8,
+                               max_model_len=512, max_num_batched_tokens=256, use_graphs=graphs),
+                  model_cfg=mc, model=gm)
+    assert gm.norms_folded
+    outs = [r.output for r in e.generate(prompts, SamplingParams(max_tokens=10, temperature=0.0, ignore_eos=True))]
+    torch.cuda.synchronize()
+    assert calls[0] > 0
+    assert _teacher_forced_ok("llama-tiny-hd128", cpu_model, prompts, outs) == 40

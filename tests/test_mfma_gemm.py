@@ -117,3 +117,70 @@ def test_mfma_gemm_splitk_matches_fp32_and_is_deterministic(M, N, K, epi, stream
     assert err.max().item() <= tol, (err.max().item(), tol)
     for _ in range(6):
         assert torch.equal(ops.mfma_gemm(x, w, epi, sched=3, streamk=streamk, phases=phases), got)
+
+
+# ---------------------------------------------------------------------------
+# fused RMSNorm epilogues (EPI 2 residual + row statistics, 3 / 4 rstd-scaled plain / SwiGLU)
+
+def _norm_case(M, N, K, kind, device, phases=0):
+    x = _rand(M, K, device=device, seed=M + K)
+    w = _rand(N, K, device=device, scale=0.05, seed=N)
+    if kind == ops.NORM_RES:
+        res = _rand(M, N, device=device, seed=7)
+        ss = torch.full((M, N // 256), -1.0, device=device)
+        want_res = res.clone()
+        want_ss = torch.empty_like(ss)
+        ops.mfma_gemm_norm_ref(x, w, kind, want_ss, 1e-5, want_res)
+        ops.mfma_gemm_norm(x, w, kind, ss, 1e-5, out=res, phases=phases)
+        return (res, ss), (want_res, want_ss)
+    ss = torch.rand(M, 5, device=device) * K * 0.1
+    want = ops.mfma_gemm_norm_ref(x, w, kind, ss, 1e-5)
+    got = ops.mfma_gemm_norm(x, w, kind, ss, 1e-5, phases=phases)
+    return (got,), (want,)
+
+
+def test_norm_fold_reference_equals_rmsnorm_then_gemm_cpu():
+    """Gain folded into the weights + rstd in the epilogue == rmsnorm(x) * gamma @ W^T."""
+    x = _rand(9, 512, device="cpu", seed=3)
+    w = _rand(768, 512, device="cpu", scale=0.05, seed=4)
+    gamma = (1 + 0.1 * torch.randn(512)).to(torch.bfloat16)
+    want = ops.rmsnorm_ref(x, gamma, 1e-5).float() @ w.float().t()
+    ss = torch.zeros(9, 2)
+    ops.row_sumsq(x, ss)
+    wf = (w.float() * gamma.float()[None]).to(torch.bfloat16)
+    got = ops.mfma_gemm_norm_ref(x, wf, ops.NORM_PLAIN, ss, 1e-5)
+    assert torch.allclose(got.float(), want, atol=2e-2 * want.abs().max().item())
+    # the residual kind's statistics feed the next norm exactly like row_sumsq of its output
+    res = _rand(9, 768, device="cpu", seed=5)
+    ss2 = torch.zeros(9, 3)
+    ops.mfma_gemm_norm_ref(x, w, ops.NORM_RES, ss2, 1e-5, res)
+    ref = torch.zeros(9, 3)
+    ops.row_sumsq(res, ref)
+    assert torch.allclose(ss2.sum(-1), ref.sum(-1), rtol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(1, 256, 256), (100, 512, 256), (300, 768, 512), (512, 2560, 1024),
+                                   (513, 1024, 8192), (2048, 2560, 4096)])
+@pytest.mark.parametrize("kind", [2, 3, 4])
+@pytest.mark.parametrize("phases", [2, 4])
+def test_mfma_gemm_norm_matches_fp32(M, N, K, kind, phases):
+    ops.load_native(required=True)
+    got, want = _norm_case(M, N, K, kind, "cuda", phases)
+    torch.cuda.synchronize()
+    for g, w in zip(got, want):
+        err = (g.float() - w.float()).abs()
+        tol = 2e-2 * w.float().abs().max().item() + 1e-3
+        assert err.max().item() <= tol, (err.max().item(), tol)
+
+
+@pytest.mark.gpu
+def test_mfma_gemm_norm_is_deterministic():
+    """The row statistics are reduced in a fixed order (no atomics): two runs are bit-identical."""
+    ops.load_native(required=True)
+    outs = []
+    for _ in range(2):
+        got, _w = _norm_case(1000, 8192, 1024, ops.NORM_RES, "cuda")
+        outs.append([t.clone() for t in got])
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(*outs))

@@ -338,3 +338,42 @@ def test_gemm_table_decides_with_margin_and_round_trips_json(tmp_path):
     p.write_text(json.dumps(t.to_json({"k": 1})))
     back = MlpPadTable.from_json(json.loads(p.read_text()))
     assert back.impls == t.impls and back.proj_impls == t.proj_impls and back.source == "shipped"
+
+
+def test_fused_norm_layer_composition_matches_unfused_cpu(monkeypatch):
+    """The fused-norm layer composition (gains folded into the weights, residual + row
+    statistics from the o / down epilogues, rstd applied by qkv / gate_up) through the fp32
+    reference ops equals the unfused layers: whole-sequence logits, the trimmed last layer and
+    the EAGLE-3 feature taps."""
+    from dgi.models import llama
+    from dgi.models.config import get_config
+    from dgi.models.llama import LlamaModel
+    from dgi.runtime.batch import AttnMeta
+    mc = get_config("llama-tiny-hd128")
+    ref = LlamaModel(mc, "cpu", torch.float32, seed=9)
+    fold = LlamaModel(mc, "cpu", torch.float32, init="empty").copy_from(ref)
+    fold.fold_norms()
+    assert fold.norms_folded and torch.equal(fold.layers[0].in_norm, torch.ones_like(fold.layers[0].in_norm))
+    T = 37
+    ids = torch.randint(3, 1000, (T,), generator=torch.Generator().manual_seed(2))
+    outs = {}
+    for name, m, mode in (("ref", ref, "0"), ("fold", fold, "force-cpu")):
+        monkeypatch.setattr(llama, "NORM_FOLD", mode)
+        monkeypatch.setattr(llama, "NORM_FOLD_MIN_ROWS", 1)
+        nb = 8
+        m.kv_cache = torch.zeros(mc.num_layers, 2, nb, mc.num_kv_heads, 16, mc.head_dim)
+        meta = AttnMeta(positions=torch.arange(T), slot_mapping=torch.arange(16, 16 + T), num_decode=0,
+                        num_prefill_tokens=T, pre_block_tables=torch.arange(1, nb, dtype=torch.int32)[None],
+                        pre_cu_seqlens=torch.tensor([0, T], dtype=torch.int32),
+                        pre_context_lens=torch.tensor([T], dtype=torch.int32), logits_indices=torch.tensor([T - 1]))
+        m.capture_layers, m.captured = (1, 3), {}
+        full = m.forward(AttnMeta(**{**meta.__dict__, "logits_indices": None}), input_ids=ids)
+        feats = {k: v.clone() for k, v in m.captured.items()}
+        m.capture_layers, m.captured = (), {}
+        last = m.forward(meta, input_ids=ids)          # trimmed last layer
+        outs[name] = (full, last, feats)
+    (f0, l0, c0), (f1, l1, c1) = outs["ref"], outs["fold"]
+    assert torch.allclose(f0, f1, atol=1e-3, rtol=1e-3)
+    assert torch.allclose(l0, l1, atol=1e-3, rtol=1e-3) and torch.allclose(l1[-1], f1[-1], atol=1e-3, rtol=1e-3)
+    for k in (1, 3):
+        assert torch.allclose(c0[k], c1[k], atol=1e-3, rtol=1e-3)

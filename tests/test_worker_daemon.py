@@ -227,7 +227,13 @@ def _e2e(tmp_path, engine_cfg: dict, name: str, n_sync: int = 4, max_tokens: int
             pieces = list(sdk.stream_chat(msgs, max_tokens=max_tokens, temperature=0.0))
             timings["stream_s"] = time.time() - t1
             info = sdk.list_workers()
-            return outs, d, pieces, info, w.engines["llm"], timings
+            # the engine's state before shutdown unloads it
+            ne = w.engines["llm"]
+            inner = getattr(ne, "engine", None)
+            g = getattr(getattr(inner, "runner", None), "graphs", None)
+            timings["device"] = getattr(ne, "device", "")
+            timings["graphs_captured"] = bool(g is not None and g.captured)
+            return outs, d, pieces, info, ne, timings
         finally:
             w.request_shutdown(graceful=True)
             wt.join(60)
@@ -267,8 +273,7 @@ def test_end_to_end_served_path_on_gpu(tmp_path):
     texts = {o["result"]["response"] for o in outs}
     assert len(texts) == 1 and d["success"] and d["result"]["response"] in texts
     assert "".join(pieces) in texts
-    assert eng.device.startswith("cuda") and eng.engine.runner.graphs is not None
-    assert eng.engine.runner.graphs.captured
+    assert timings["device"].startswith("cuda") and timings["graphs_captured"], timings
     # the in-process engine on the same (seeded random-init) weights, same prompt ids
     ref = LLMEngine(EngineConfig(model="llama-tiny-hd128", device="cuda:0", max_num_seqs=16,
                                  max_num_batched_tokens=512, max_model_len=512, seed=0, use_graphs=False))
