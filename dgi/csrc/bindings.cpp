@@ -257,6 +257,7 @@ void mfma_gemm_norm(at::Tensor out, const at::Tensor& x, const at::Tensor& w, in
   TORCH_CHECK(w.size(1) == K && out.size(0) == M && ss.size(0) >= M, "mfma_gemm_norm: shape mismatch");
   TORCH_CHECK(out.size(1) == (kind == 4 ? N / 2 : N), "mfma_gemm_norm: output columns");
   TORCH_CHECK(kind != 2 || ss.size(1) >= N / 256, "mfma_gemm_norm: ss needs N / 256 columns");
+  TORCH_CHECK(kind == 2 || (ss.size(1) % 8 == 0 && ss.size(1) <= 32), "mfma_gemm_norm: ss columns % 8, <= 32");
   TORCH_CHECK(N % 256 == 0 && K % 128 == 0 && K >= 256 && x.stride(0) % 8 == 0 && out.stride(0) % 4 == 0,
               "mfma_gemm_norm: N%256, K%128, ldx%8, ldy%4");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0 &&

@@ -155,37 +155,49 @@ __device__ __forceinline__ void epilogue_res(const f32x4 (&acc)[8][4], uint16_t*
                                              float* __restrict__ ss, int ss_ld) {
   const int r16 = lane & 15;
   const int g = lane >> 4;
+  const int cbase = tn * 256 + wn * 64 + 16 * (g & 1) + 4 * (g & 2);
+  // rows in batches of 4: the batch's 8 residual loads are all issued before the first is used
+  // (a load-use per 16-byte chunk would serialise 16 memory round trips per lane)
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + wm * 128 + i * 16 + r16;
-    if (m >= M) continue;
-    uint16_t* yrow = Y + (size_t)m * ldy;
-    float part = 0.f;
+  for (int i0 = 0; i0 < 8; i0 += 4) {
+    uint4 old[4][2];
 #pragma unroll
-    for (int j = 0; j < 4; j += 2) {
-      float x0[4], x1[4], f[8], o[8];
+    for (int ii = 0; ii < 4; ++ii) {
+      const int m = m0 + wm * 128 + (i0 + ii) * 16 + r16;
+      const uint16_t* yrow = Y + (size_t)min(m, M - 1) * ldy + cbase;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        x0[e] = acc[i][j][e];
-        x1[e] = acc[i][j + 1][e];
-      }
-      swap_pair(x0, x1, f);
-      uint4* p = (uint4*)(yrow + tn * 256 + wn * 64 + j * 16 + 16 * (g & 1) + 4 * (g & 2));
-      const uint4 old = *p;
-      const u32x4 ov = {old.x, old.y, old.z, old.w};
-      unpack8(ov, o);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] += f[e];
-      const u32x4 nv = pack8(o);
-      *p = uint4{nv[0], nv[1], nv[2], nv[3]};
-      float r[8];
-      unpack8(nv, r);                 // the rounded values the next norm reads
-#pragma unroll
-      for (int e = 0; e < 8; ++e) part += r[e] * r[e];
+      for (int jj = 0; jj < 2; ++jj) old[ii][jj] = *(const uint4*)(yrow + jj * 32);
     }
-    part += __shfl_xor(part, 16, 64);
-    part += __shfl_xor(part, 32, 64);
-    if (g == 0) ssl[wn * 256 + wm * 128 + i * 16 + r16] = part;
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      const int i = i0 + ii;
+      const int m = m0 + wm * 128 + i * 16 + r16;
+      float part = 0.f;
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int j = 2 * jj;
+        float x0[4], x1[4], f[8], o[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          x0[e] = acc[i][j][e];
+          x1[e] = acc[i][j + 1][e];
+        }
+        swap_pair(x0, x1, f);
+        const u32x4 ov = {old[ii][jj].x, old[ii][jj].y, old[ii][jj].z, old[ii][jj].w};
+        unpack8(ov, o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += f[e];
+        const u32x4 nv = pack8(o);
+        if (m < M) *(uint4*)(Y + (size_t)m * ldy + cbase + jj * 32) = uint4{nv[0], nv[1], nv[2], nv[3]};
+        float r[8];
+        unpack8(nv, r);               // the rounded values the next norm reads
+#pragma unroll
+        for (int e = 0; e < 8; ++e) part += r[e] * r[e];
+      }
+      part += __shfl_xor(part, 16, 64);
+      part += __shfl_xor(part, 32, 64);
+      if (g == 0) ssl[wn * 256 + wm * 128 + i * 16 + r16] = part;
+    }
   }
   __syncthreads();
   const int t = threadIdx.x;
@@ -782,10 +794,14 @@ __device__ __forceinline__ void drive(const PPArgs& a, char* smem, Pro&& prologu
 //   1      Xb (8)            Xb x (Wa, Wb)  X3, X1 of t+1, X0 of t+2      vmcnt(3): all but X3, X1 of t+1
 template <int EPI, int PRIO, int PH>
 __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * kStageBytes];
   // EPI 2: per-wave row partials of the sum of squares; EPI 3 / 4: two slots of the tile's rstd
-  // (slot per work item: a fast wave may start the next item while others still store this one)
-  __shared__ float ep_lds[EpiKind<EPI>::res ? 1024 : EpiKind<EPI>::norm ? 512 : 1];
+  // (slot per work item: a fast wave may start the next item while others still store this one).
+  // Carved from the one LDS array: with a second __shared__ object hipcc's waitcnt pass can no
+  // longer tell the staging DMA from other LDS traffic and waits vmcnt(0) before every fragment
+  // read of the K loop (measured: the gate_up kernel 349 -> 517 us at 512 rows).
+  constexpr int kEpBytes = EpiKind<EPI>::res ? 4096 : EpiKind<EPI>::norm ? 2048 : 0;
+  __shared__ __attribute__((aligned(16))) char smem[2 * kStageBytes + kEpBytes];
+  float* const ep_lds = (float*)(smem + 2 * kStageBytes);
   int rs_slot = 0;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -907,13 +923,20 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
       // (visible to every wave by the K loop's barriers; the epilogue reads it)
       rs_slot ^= 1;
       const int t = fresh_tid();
-      if (t < 256) {
-        const int m = min(tm * kBM + t, M - 1);
-        const float* sp = a.ss + (size_t)m * a.ss_ld;
-        float s = 0.f;
-        for (int j = 0; j < a.ss_ld; ++j) s += sp[j];
-        ep_lds[rs_slot * 256 + t] = rsqrtf(s * a.inv_k + a.eps);
-      }
+      // two lanes per row, each summing half of its partials (float4 loads, all in flight
+      // together: ss_ld % 8 == 0, <= 32), then one exchange — a fixed order on every run
+      const int m = min(tm * kBM + (t >> 1), M - 1);
+      const int per = a.ss_ld >> 3;
+      const f32x4* sp = (const f32x4*)(a.ss + (size_t)m * a.ss_ld) + (t & 1) * per;
+      f32x4 v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = j < per ? sp[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+      const float o2 = __shfl_xor(s, 1, 64);
+      s = (t & 1) ? o2 + s : s + o2;
+      if (!(t & 1)) ep_lds[rs_slot * 256 + (t >> 1)] = rsqrtf(s * a.inv_k + a.eps);
     }
 
     // one K tile; ST = its LDS stage, MODE 0: t + 2 < L, 1: t + 2 == L, 2: t + 1 == L
@@ -1178,6 +1201,7 @@ extern "C" int dgi_mfma_gemm_norm(const void* x, int ldx, const void* w, void* y
   if (kind < 2 || kind > 4 || K % (2 * kBK) || K < 4 * kBK || ldx % 8 || ldy % 4 || N % 256 || !ss || ss_ld <= 0)
     return -3;
   if (kind == 2 && ss_ld < N / 256) return -3;
+  if (kind != 2 && (ss_ld % 8 || ss_ld > 32)) return -3;
   int prio = (phases == 2 || (phases == 0 && M <= 2560)) ? 4 : 0;
   const int I = kind == 4 ? N / 2 : 0;
   const int tiles_n = kind == 4 ? I / 128 : N / 256;

@@ -97,6 +97,12 @@ class TboStreams:
 
 _TBO_STREAMS: dict = {}
 
+def _ss_cols(hidden: int) -> int:
+    """Columns of the fused-norm row statistics: one partial per 256-column tile of the stream,
+    padded to a multiple of 8 (the consumer's vector loads; the pad columns stay zero)."""
+    return (hidden // 256 + 7) // 8 * 8
+
+
 class LlamaLayerWeights:
     __slots__ = ("in_norm", "qkv", "o", "post_norm", "gate_up", "down", "qkv_bias")
 
@@ -234,7 +240,7 @@ class LlamaModel:
             if self.layers and self.cfg.hidden_size % 256 == 0:
                 # the row statistics of the fused-norm layers, allocated here so a graph capture
                 # never allocates it (steps of more rows grow it eagerly)
-                self._ss_buf = torch.empty(16384, self.cfg.hidden_size // 256, device=self.device,
+                self._ss_buf = torch.zeros(16384, _ss_cols(self.cfg.hidden_size), device=self.device,
                                            dtype=torch.float32)
         self.norms_folded = True
 
@@ -437,7 +443,7 @@ class LlamaModel:
         if T < NORM_FOLD_MIN_ROWS:
             return False
         L = self.layers[0]
-        if L.qkv_bias is not None or self.cfg.hidden_size % 256:
+        if L.qkv_bias is not None or self.cfg.hidden_size % 256 or self.cfg.hidden_size > 8192:
             return False
         if torch.cuda.is_current_stream_capturing() and not self.norms_folded:
             return False            # weights are folded eagerly, never inside a capture
@@ -473,12 +479,12 @@ class LlamaModel:
         eps = c.rms_eps
         T, H = h.shape
         R = h if residual is None else h + residual      # forward() hands over a tensor it owns
-        nt = H // 256
+        nt = _ss_cols(H)
         ss = self._ss_buf
         if ss is None or ss.shape[0] < T or ss.shape[1] != nt or ss.device != h.device:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("fused-norm layers: statistics buffer must exist before capture")
-            ss = self._ss_buf = torch.empty(max(T, 4096), nt, device=h.device, dtype=torch.float32)
+            ss = self._ss_buf = torch.zeros(max(T, 4096), nt, device=h.device, dtype=torch.float32)
         ss = ss[:T]
         ops.row_sumsq(R, ss)
         n = len(self.layers)

@@ -646,7 +646,8 @@ def mfma_gemm_norm(x: torch.Tensor, w: torch.Tensor, kind: int, ss: torch.Tensor
 
     ``kind`` 2 (NORM_RES): ``out`` is the residual stream, updated in place to out + x @ w.T,
     and ``ss[m, j]`` receives the sum of squares of the new row m over columns 256 j .. 256 j + 255
-    (``ss`` has N / 256 columns): the statistics of the next RMSNorm, with no norm kernel.
+    (``ss`` has at least N / 256 columns; the consumers read a multiple of 8 <= 32, extra
+    columns zero): the statistics of the next RMSNorm, with no norm kernel.
     ``kind`` 3 / 4 (NORM_PLAIN / NORM_SWIGLU): x is the un-normalised residual stream and
     ``w`` carries the norm's gain (``LlamaModel.fold_norms``); each output row is scaled by
     rsqrt(sum(ss[m]) / K + eps) — then SwiGLU for kind 4 — which equals
@@ -664,7 +665,8 @@ def mfma_gemm_norm(x: torch.Tensor, w: torch.Tensor, kind: int, ss: torch.Tensor
 
 
 def mfma_norm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
-    """Shapes the fused-norm GEMM takes (K % 128 and >= 256 on top of ``mfma_gemm_ok``)."""
+    """Shapes the fused-norm GEMM takes (K % 128 and >= 256 on top of ``mfma_gemm_ok``; a
+    normalising consumer also needs its K — the stream width — <= 8192: 32 row partials)."""
     return mfma_gemm_ok(x, w) and x.shape[1] % 128 == 0 and x.shape[1] >= 256
 
 

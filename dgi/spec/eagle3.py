@@ -406,6 +406,46 @@ class _VerifyGraph:
         return acc[:R], path[:R], toks[:R], feats[:R * N]
 
 
+def _draft_tree(dr: "Eagle3Draft", g_root, last, lv, d_bt, W: int, D: int, K: int, N: int):
+    """Tree drafting on device (root top-k, then depths 2..D), all metadata precomputed in
+    ``lv`` (per depth: offset, m, positions, slots, ctx, cu, tiles): the body of the draft
+    and whole-step graphs.  Returns (tokens, parents) [Rb, N]."""
+    Rb, H = g_root.shape
+    dev = g_root.device
+    v1, t1 = dr.topk(g_root, K)
+    t1 = dr.to_token(t1)
+    tok = torch.zeros(Rb, N, dtype=torch.long, device=dev)
+    par = torch.full((Rb, N), -1, dtype=torch.int32, device=dev)
+    score = torch.zeros(Rb, N, dtype=torch.float32, device=dev)
+    G = torch.zeros(Rb, N, H, dtype=g_root.dtype, device=dev)
+    tok[:, 0] = last
+    G[:, 0] = g_root
+    tok[:, 1:W + 1] = t1[:, :W].long()
+    par[:, 1:W + 1] = 0
+    score[:, 1:W + 1] = v1[:, :W].float()
+    for d, (_, m, pos, slots, ctx, cu, tiles) in zip(range(2, D + 1), lv):
+        cpar = par[:, 1:m + 1] - 1
+        cpar = torch.where(cpar < 0, torch.full_like(cpar, -1), cpar)
+        anc, _ = ops.tree_mask(cpar.contiguous())
+        cm = AttnMeta(positions=pos, slot_mapping=slots, num_decode=0, num_prefill_tokens=Rb * m,
+                      pre_block_tables=d_bt, pre_cu_seqlens=cu, pre_context_lens=ctx, pre_tiles=tiles,
+                      tree_mask=anc, tree_n=m)
+        pidx = par[:, 1:m + 1].long()
+        hin = torch.gather(G, 1, pidx[:, :, None].expand(Rb, m, H)).reshape(Rb * m, H)
+        gc = dr.forward(tok[:, 1:m + 1].reshape(-1), hin, cm).view(Rb, m, H)
+        G[:, 1:m + 1] = gc
+        fr = torch.arange(m - W + 1, m + 1, device=dev)
+        vf, tf = dr.topk(gc[:, m - W:].reshape(Rb * W, H), K)
+        tf = dr.to_token(tf)
+        cand = (score[:, fr][:, :, None] + vf.view(Rb, W, K).float()).view(Rb, W * K)
+        best, bi = torch.topk(cand, W, dim=1)
+        base = 1 + W * (d - 1)
+        tok[:, base: base + W] = torch.gather(tf.view(Rb, W * K).long(), 1, bi)
+        par[:, base: base + W] = fr[bi // K].int()
+        score[:, base: base + W] = best
+    return tok, par
+
+
 class _DraftGraph:
     """hipGraph of tree drafting (root top-k, then depths 2..D) for ``Rb`` sequences.
 
@@ -471,42 +511,7 @@ class _DraftGraph:
                                                      for i in range(Rb)]
 
     def _body(self):
-        eng, dr = self.eng, self.eng.draft
-        Rb, W, D, K, N = self.Rb, self.W, self.D, self.K, self.N
-        dev = self.g_root.device
-        H = self.g_root.shape[1]
-        v1, t1 = dr.topk(self.g_root, K)
-        t1 = dr.to_token(t1)
-        tok = torch.zeros(Rb, N, dtype=torch.long, device=dev)
-        par = torch.full((Rb, N), -1, dtype=torch.int32, device=dev)
-        score = torch.zeros(Rb, N, dtype=torch.float32, device=dev)
-        G = torch.zeros(Rb, N, H, dtype=self.g_root.dtype, device=dev)
-        tok[:, 0] = self.last
-        G[:, 0] = self.g_root
-        tok[:, 1:W + 1] = t1[:, :W].long()
-        par[:, 1:W + 1] = 0
-        score[:, 1:W + 1] = v1[:, :W].float()
-        for d, (_, m, pos, slots, ctx, cu, tiles) in zip(range(2, D + 1), self.lv):
-            cpar = par[:, 1:m + 1] - 1
-            cpar = torch.where(cpar < 0, torch.full_like(cpar, -1), cpar)
-            anc, _ = ops.tree_mask(cpar.contiguous())
-            cm = AttnMeta(positions=pos, slot_mapping=slots, num_decode=0, num_prefill_tokens=Rb * m,
-                          pre_block_tables=self.d_bt, pre_cu_seqlens=cu, pre_context_lens=ctx, pre_tiles=tiles,
-                          tree_mask=anc, tree_n=m)
-            pidx = par[:, 1:m + 1].long()
-            hin = torch.gather(G, 1, pidx[:, :, None].expand(Rb, m, H)).reshape(Rb * m, H)
-            gc = dr.forward(tok[:, 1:m + 1].reshape(-1), hin, cm).view(Rb, m, H)
-            G[:, 1:m + 1] = gc
-            fr = torch.arange(m - W + 1, m + 1, device=dev)
-            vf, tf = dr.topk(gc[:, m - W:].reshape(Rb * W, H), K)
-            tf = dr.to_token(tf)
-            cand = (score[:, fr][:, :, None] + vf.view(Rb, W, K).float()).view(Rb, W * K)
-            best, bi = torch.topk(cand, W, dim=1)
-            base = 1 + W * (d - 1)
-            tok[:, base: base + W] = torch.gather(tf.view(Rb, W * K).long(), 1, bi)
-            par[:, base: base + W] = fr[bi // K].int()
-            score[:, base: base + W] = best
-        return tok, par
+        return _draft_tree(self.eng.draft, self.g_root, self.last, self.lv, self.d_bt, self.W, self.D, self.K, self.N)
 
     @torch.inference_mode()
     def _capture(self) -> None:
@@ -532,6 +537,225 @@ class _DraftGraph:
         return tok[:R], par[:R]
 
 
+class _StepGraph:
+    """hipGraph of a WHOLE speculative step for ``Rb`` sequences at tree depth ``D`` (SURVEY §3.6,
+    VERDICT r5 #5; the reference loop it replaces: worker/engines/speculative.py:305-365):
+
+        draft catch-up over the last step's accepted tokens (D + 1 rows per sequence, the
+        rows past each sequence's count are padding on the scratch page)
+        -> tree drafting (root top-k, depths 2..D)
+        -> target verify over the N tree nodes (tree-masked attention, EAGLE-3 feature tap,
+           coupled sampling) -> ``tree_verify`` (accept length, path, tokens)
+        -> KV compaction of the accepted path (slot moves computed on device from the path
+           and the block table; rejected moves copy scratch-page slots onto themselves)
+        -> the accepted nodes' features, gathered for the next catch-up.
+
+    One int32 metadata buffer (block tables + the catch-up, per-depth and verify positions /
+    slots / context lengths, all derivable from each sequence's length) goes up per step and
+    only the accept lengths and tokens come back: one host round trip per step, no eager
+    launches.  Padding rows of a partial bucket live on the scratch page 0."""
+
+    def __init__(self, eng: "SpecEngine", Rb: int, depth: int):
+        sp, run = eng.spec, eng.runner
+        self.eng, self.Rb, self.D = eng, Rb, depth
+        self.W, self.K, self.N = sp.width, sp.topk, sp.nodes(depth)
+        self.C = depth + 1
+        self.maxw = run.max_blocks
+        dev = eng.device
+        H = eng.model_cfg.hidden_size
+        W, D, N, C = self.W, self.D, self.N, self.C
+        self.ms = [W * (d - 1) for d in range(2, D + 1)]
+        self.depth_np = np.concatenate([[0]] + [[d] * W for d in range(1, D + 1)]).astype(np.int64)
+        # int32 metadata: bt | catch-up pos, slots, ctx, last index | per depth pos, slots, ctx | verify pos, slots, ctx
+        n_dyn = Rb * self.maxw + (2 * Rb * C + 2 * Rb) + sum(2 * Rb * m + Rb for m in self.ms) + (2 * Rb * N + Rb)
+        self.host = torch.zeros(n_dyn, dtype=torch.int32).pin_memory()
+        self.dyn = torch.zeros(n_dyn, dtype=torch.int32, device=dev)
+        o = 0
+
+        def take(n):
+            nonlocal o
+            v = self.dyn[o:o + n]
+            o += n
+            return v
+        self.o_bt = o
+        self.d_bt = take(Rb * self.maxw).view(Rb, self.maxw)
+        self.o_c = o
+        self.c_pos, self.c_slots, self.c_ctx, self.c_last = take(Rb * C), take(Rb * C), take(Rb), take(Rb)
+        ar = torch.arange(Rb, dtype=torch.int32)
+        self.c_cu = torch.arange(0, Rb * C + 1, C, dtype=torch.int32, device=dev)
+        self.c_tiles = torch.stack([ar, torch.zeros(Rb, dtype=torch.int32)], 1).contiguous().to(dev)
+        tiles = self.c_tiles
+        self.lv = []
+        for m in self.ms:
+            off = o
+            pos, slots, ctx = take(Rb * m), take(Rb * m), take(Rb)
+            cu = torch.arange(0, Rb * m + 1, m, dtype=torch.int32, device=dev)
+            self.lv.append((off, m, pos, slots, ctx, cu, tiles))
+        self.o_v = o
+        self.v_pos, self.v_slots, self.v_ctx = take(Rb * N), take(Rb * N), take(Rb)
+        self.v_cu = torch.arange(0, Rb * N + 1, N, dtype=torch.int32, device=dev)
+        # other static inputs
+        self.c_ids = torch.zeros(Rb, C, dtype=torch.long, device=dev)
+        self.c_feat = torch.zeros(Rb, C, H, dtype=eng.cfg.dtype, device=dev)
+        self.temps = torch.zeros(Rb * N, dtype=torch.float32, device=dev)
+        self.seeds = torch.zeros(Rb * N, dtype=torch.long, device=dev)
+        self.topk = torch.zeros(Rb * N, dtype=torch.long, device=dev)
+        self.topp = torch.ones(Rb * N, dtype=torch.float32, device=dev)
+        self.greedy = True               # the sampling buffers hold temperature 0 everywhere
+        self._fill([], [], [], [])
+        self.dyn.copy_(self.host)
+        self.graph = None
+        self._capture()
+
+    # ---------------------------------------------------------------- metadata
+    def _fill(self, n_vec, p0_vec, brows, nv_vec) -> None:
+        """Host metadata of sequences with committed length n, first catch-up position p0 and
+        nv valid catch-up rows; rows past the live batch are padding on page 0."""
+        Rb, C, N, maxw = self.Rb, self.C, self.N, self.maxw
+        bs = self.eng.pool.block_size
+        R = len(n_vec)
+        h = self.host.numpy()
+        bt = h[self.o_bt:self.o_bt + Rb * maxw].reshape(Rb, maxw)
+        bt[:] = 0
+        for i, blk in enumerate(brows):
+            bt[i, :len(blk)] = blk
+
+        def slot_of(i, p):
+            if i >= R:
+                return p % bs                              # scratch page 0
+            return bt[i, p // bs].astype(np.int64) * bs + p % bs
+        # catch-up: rows p0 .. p0 + C - 1 (valid: the first nv), context p0 + C
+        o = self.o_c
+        cpos = h[o:o + Rb * C].reshape(Rb, C)
+        cslot = h[o + Rb * C:o + 2 * Rb * C].reshape(Rb, C)
+        cctx = h[o + 2 * Rb * C:o + 2 * Rb * C + Rb]
+        clast = h[o + 2 * Rb * C + Rb:o + 2 * Rb * C + 2 * Rb]
+        kk = np.arange(C)
+        for i in range(Rb):
+            p0 = int(p0_vec[i]) if i < R else 0
+            nv = int(nv_vec[i]) if i < R else 1
+            ps = p0 + kk
+            cpos[i] = ps
+            sl = slot_of(i, ps) if i < R else ps % bs
+            if i < R:
+                sl = np.where(kk < nv, sl, kk % bs)        # padding rows write scratch slots
+            cslot[i] = sl
+            cctx[i] = p0 + C
+            clast[i] = nv - 1
+        # draft depths 2..D: chunk nodes at positions n - 1 + depth, slots n .. n + m - 1
+        for off, m, *_ in self.lv:
+            dp = h[off:off + Rb * m].reshape(Rb, m)
+            dsl = h[off + Rb * m:off + 2 * Rb * m].reshape(Rb, m)
+            dctx = h[off + 2 * Rb * m:off + 2 * Rb * m + Rb]
+            for i in range(Rb):
+                n = int(n_vec[i]) if i < R else 1
+                dp[i] = n - 1 + self.depth_np[1:m + 1]
+                dsl[i] = slot_of(i, n + np.arange(m)) if i < R else np.arange(m) % bs
+                dctx[i] = n + m
+        # verify: node k at position n - 1 + depth(k), slot n - 1 + k, context n - 1 + N
+        o = self.o_v
+        vp = h[o:o + Rb * N].reshape(Rb, N)
+        vsl = h[o + Rb * N:o + 2 * Rb * N].reshape(Rb, N)
+        vctx = h[o + 2 * Rb * N:o + 2 * Rb * N + Rb]
+        for i in range(Rb):
+            if i < R:
+                n = int(n_vec[i])
+                vp[i] = n - 1 + self.depth_np
+                vsl[i] = slot_of(i, n - 1 + np.arange(N))
+                vctx[i] = n - 1 + N
+            else:
+                vp[i] = np.arange(N)
+                vsl[i] = np.arange(N) % bs
+                vctx[i] = N
+
+    # ---------------------------------------------------------------- the step
+    def _body(self):
+        eng, dr = self.eng, self.eng.draft
+        Rb, C, D, N, W = self.Rb, self.C, self.D, self.N, self.W
+        H = self.c_feat.shape[2]
+        bs = eng.pool.block_size
+        # 1) draft catch-up
+        cm = AttnMeta(positions=self.c_pos, slot_mapping=self.c_slots, num_decode=0, num_prefill_tokens=Rb * C,
+                      pre_block_tables=self.d_bt, pre_cu_seqlens=self.c_cu, pre_context_lens=self.c_ctx,
+                      pre_tiles=self.c_tiles)
+        g = dr.forward(self.c_ids.view(-1), self.c_feat.view(Rb * C, H), cm).view(Rb, C, H)
+        li = self.c_last.long()
+        g_root = torch.gather(g, 1, li[:, None, None].expand(Rb, 1, H)).squeeze(1)
+        last = torch.gather(self.c_ids, 1, li[:, None]).squeeze(1)
+        # 2) tree drafting
+        tok, par = _draft_tree(dr, g_root, last, self.lv, self.d_bt, W, D, self.K, N)
+        # 3) verify
+        anc, depth = ops.tree_mask(par)
+        ar = torch.arange(Rb, device=tok.device)
+        tiles = self.c_tiles
+        vm = AttnMeta(positions=self.v_pos, slot_mapping=self.v_slots, num_decode=0, num_prefill_tokens=Rb * N,
+                      pre_block_tables=self.d_bt, pre_cu_seqlens=self.v_cu, pre_context_lens=self.v_ctx,
+                      pre_tiles=tiles, tree_mask=anc, tree_n=N)
+        logits, feats = eng._forward_capture(vm, tok.view(-1))
+        tgt = ops.sample(logits, self.temps, self.seeds, 0, top_k=self.topk, top_p=self.topp).view(Rb, N)
+        acc, path, toks = ops.tree_verify(par, tok, tgt, anc, depth, D + 1)
+        # 4) compaction: accepted node path[k] (k = 1..acc) moves to position base + k
+        base = self.v_pos.view(Rb, N)[:, :1].long()                  # n - 1 (node 0's position)
+        kk = torch.arange(1, D + 1, device=tok.device)
+        ps = base + path[:, 1:D + 1].long()
+        pd = base + kk[None]
+        bt = self.d_bt.long()
+        slot = lambda p: torch.gather(bt, 1, (p // bs).clamp(0, bt.shape[1] - 1)) * bs + p % bs  # noqa: E731
+        src, dst = slot(ps), slot(pd)
+        move = (kk[None] <= acc[:, None].long()) & (src != dst)
+        scratch = (kk % bs)[None].expand(Rb, D)
+        src = torch.where(move, src, scratch)
+        dst = torch.where(move, dst, scratch)
+        kv_slot_copy(eng.model.kv_cache, src.reshape(-1), dst.reshape(-1), bs)
+        # 5) the accepted nodes' features (positions n - 1 .. n - 1 + acc) for the next catch-up
+        fidx = path[:, :D + 1].long().clamp(min=0)
+        fkeep = torch.gather(feats.view(Rb, N, H), 1, fidx[:, :, None].expand(Rb, D + 1, H))
+        del ar
+        return acc, toks, fkeep
+
+    @torch.inference_mode()
+    def _capture(self) -> None:
+        eng = self.eng
+        eng.model.kv_cache = eng.pool.kv
+        from dgi.utils.streams import named_stream
+        s = named_stream("capture", eng.device)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self._body()                                   # warm-up (lazy inits outside capture)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize(eng.device)
+        self.graph = torch.cuda.CUDAGraph()
+        with graph_capture(self.graph, pool=eng._graph_pool):
+            self.out = self._body()
+
+    def run(self, n_vec, p0_vec, brows, nv_vec, ids, feats, samp) -> tuple:
+        """Replay for R live sequences: ``ids`` [R][<= C] catch-up tokens, ``feats`` R feature
+        tensors [nv, H], ``samp`` (temps, seeds, top-k, top-p) host arrays [R, N] or None (all
+        greedy).  Returns device (acc [R], tokens [R, D + 1], kept features [R, D + 1, H])."""
+        R, C, N = len(n_vec), self.C, self.N
+        self._fill(n_vec, p0_vec, brows, nv_vec)
+        self.dyn.copy_(self.host, non_blocking=True)
+        ids_h = np.zeros((self.Rb, C), np.int64)
+        for i, t in enumerate(ids):
+            ids_h[i, :len(t)] = t
+        self.c_ids.copy_(torch.from_numpy(ids_h).pin_memory(), non_blocking=True)
+        for i, f in enumerate(feats):
+            self.c_feat[i, :f.shape[0]].copy_(f)
+        if samp is None:
+            if not self.greedy:
+                self.temps.zero_()
+                self.greedy = True
+        else:
+            n = R * N
+            for buf, x in zip((self.temps, self.seeds, self.topk, self.topp), samp):
+                buf[:n].copy_(torch.from_numpy(np.ascontiguousarray(x).ravel()).pin_memory(), non_blocking=True)
+            self.temps[n:].zero_()
+            self.greedy = False
+        self.graph.replay()
+        acc, toks, fkeep = self.out
+        return acc[:R], toks[:R], fkeep[:R]
+
+
 class SpecEngine(LLMEngine):
     """``LLMEngine`` with EAGLE-3 tree speculation (greedy and sampled requests)."""
 
@@ -552,6 +776,8 @@ class SpecEngine(LLMEngine):
         self._oracle_rng = np.random.default_rng(0)
         self._vgraphs: dict = {}
         self._dgraphs: dict = {}
+        self._sgraphs: dict = {}    # (bucket, depth) -> _StepGraph (whole speculative step)
+        self.whole_step = True      # speculative steps as one captured graph where eligible
         self._graphs_vocab = self.draft.vocab_version
         self._graph_pool = torch.cuda.graph_pool_handle() if self.device.type == "cuda" else None
         # plain decode steps replay the engine's hipGraphs with the EAGLE-3 feature tap on
@@ -586,6 +812,7 @@ class SpecEngine(LLMEngine):
         if self._graphs_vocab != self.draft.vocab_version:
             self._dgraphs.clear()
             self._vgraphs.clear()
+            self._sgraphs.clear()
             self._graphs_vocab = self.draft.vocab_version
 
     def _draft_graph(self, R: int) -> Optional[_DraftGraph]:
@@ -614,6 +841,20 @@ class SpecEngine(LLMEngine):
             self._captured = True
         return g
 
+    def _step_graph(self, R: int) -> Optional[_StepGraph]:
+        if not (self.whole_step and self.spec.graphs and self.device.type == "cuda" and self.cur_depth >= 2
+                and not self.oracle):
+            return None
+        self._check_graph_vocab()
+        Rb = next((b for b in VERIFY_BUCKETS if b >= R), None)
+        if Rb is None:
+            return None
+        g = self._sgraphs.get((Rb, self.cur_depth))
+        if g is None:
+            g = self._sgraphs[(Rb, self.cur_depth)] = _StepGraph(self, Rb, self.cur_depth)
+            self._captured = True
+        return g
+
     def warmup_spec(self, batches=(1,), depths=None) -> int:
         """Capture the draft / verify hipGraphs of every (batch bucket, depth) the
         adaptive controller can reach, so no capture lands in a serving step (a
@@ -626,6 +867,7 @@ class SpecEngine(LLMEngine):
                 for d in (depths or range(1, self.spec.depth + 1)):
                     self.cur_depth = d
                     n += int(self._verify_graph(R) is not None) + int(self._draft_graph(R) is not None)
+                    n += int(self._step_graph(R) is not None)
         finally:
             self.cur_depth = keep
             self._captured = False
@@ -876,6 +1118,9 @@ class SpecEngine(LLMEngine):
         if not reqs:
             return []
         R = len(reqs)
+        outs = self._whole_step(reqs)
+        if outs is not None:
+            return outs
         td = time.perf_counter()
         # ---- 1) draft catch-up over committed positions [draft_len, n-1]
         pos, slots, cu, ctx, ids, feat_rows, brows = [], [], [0], [], [], [], []
@@ -997,6 +1242,96 @@ class SpecEngine(LLMEngine):
         self._period_acc[1] += R
         self._adapt_depth(sum(acc_h) / (R * D))
         return outs
+
+    def _whole_step(self, reqs: list) -> Optional[list]:
+        """The speculative step as one captured graph (``_StepGraph``) when every sequence's
+        draft catch-up fits its D + 1 rows and its features are at hand (the steady state of a
+        speculating batch); None: the staged path runs it."""
+        D = self.cur_depth
+        C = D + 1
+        if self._step_graph_ok is False or D < 2:
+            return None
+        rows = []
+        for r in reqs:
+            st = self._state(r)
+            n = r.total_len
+            p0 = min(st.draft_len, n - 1)
+            nv = n - p0
+            f = st.feat
+            if p0 < 1 or nv > C or f is None or st.feat_start > p0 - 1 or p0 - 1 + nv > st.feat_start + f.shape[0]:
+                return None
+            rows.append((r, st, n, p0, nv, f[p0 - 1 - st.feat_start: p0 - 1 - st.feat_start + nv]))
+        sg = self._step_graph(len(reqs))
+        if sg is None:
+            return None
+        t0 = time.perf_counter()
+        N = sg.N
+        samp = None
+        if any(r.params.temperature > 0 for r in reqs):
+            samp = self._node_sampling_host(reqs, sg.depth_np)
+        acc, toks, fkeep = sg.run([x[2] for x in rows], [x[3] for x in rows], [r.blocks for r in reqs],
+                                  [x[4] for x in rows], [r.all_tokens()[x[3]:x[2]] for x, r in zip(rows, reqs)],
+                                  [x[5] for x in rows], samp)
+        hs = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in (acc, toks)]
+        for h_, t in zip(hs, (acc, toks)):
+            h_.copy_(t, non_blocking=True)
+        fk = fkeep.clone()                       # the graph's output buffer is rewritten next replay
+        torch.cuda.current_stream(self.device).synchronize()
+        acc_h, toks_h = hs[0].tolist(), hs[1].numpy()
+        self.spec_stats["verify_s"] += time.perf_counter() - t0
+        self.spec_stats["whole_steps"] = self.spec_stats.get("whole_steps", 0) + 1
+        outs = []
+        now = time.perf_counter()
+        st_all = self.stats
+        st_all["steps"] += 1
+        for i, (r, st, n, p0, nv, _f) in enumerate(rows):
+            a = acc_h[i]
+            st.draft_len = n
+            st.feat, st.feat_start = fk[i, :a + 1], n - 1
+            r.num_computed = n + a
+            st_all["decode_tokens"] += a + 1
+            self.spec_stats["accepted"] += a
+            for k in range(a + 1):
+                t = int(toks_h[i, k])
+                r.output.append(t)
+                r.token_times.append(now)
+                st_all["generated"] += 1
+                self.spec_stats["spec_tokens"] += 1
+                reason = self._check_stop(r, t)
+                if reason is not None:
+                    self.scheduler.finish(r, reason)
+                    st_all["finished"] += 1
+                    self.requests.pop(r.rid, None)
+                outs.append(StepOutput(r.rid, t, reason is not None, reason, r))
+                if reason is not None:
+                    break
+        R = len(rows)
+        self.spec_stats["spec_steps"] += 1
+        self.spec_stats["spec_rows"] += R
+        self._period_acc[0] += sum(acc_h)
+        self._period_acc[1] += R
+        self._adapt_depth(sum(acc_h) / (R * D))
+        del N
+        return outs
+
+    _step_graph_ok = None
+
+    def _node_sampling_host(self, reqs: list, depth_np: np.ndarray) -> tuple:
+        """``_node_sampling`` as host arrays [R, N] (the whole-step graph copies them into its
+        static buffers)."""
+        R, N = len(reqs), len(depth_np)
+        temps = np.empty((R, N), np.float32)
+        seeds = np.empty((R, N), np.int64)
+        topk = np.zeros((R, N), np.int64)
+        topp = np.ones((R, N), np.float32)
+        for i, r in enumerate(reqs):
+            p = r.params
+            temps[i] = p.temperature
+            seeds[i] = (r.seed * 1000003 + len(r.output) + depth_np) & 0x7FFFFFFF
+            if p.needs_filter:
+                topk[i] = max(0, p.top_k)
+                topp[i] = p.top_p
+        return temps, seeds, topk, topp
 
     def _feature_rows(self, st: _SpecState, q0: int, q1: int, H: int) -> torch.Tensor:
         """Fused target features of positions [q0, q1) (zeros where unknown)."""

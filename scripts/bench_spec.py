@@ -63,6 +63,8 @@ def main():
                          "permuted copy of the embedding / sqrt(H), so the next token is a confident function "
                          "of the current one, like a trained model's top-1 margins (same FLOPs and shapes)")
     ap.add_argument("--no-verify-graph", action="store_true", help="eager verify pass (A/B for the hipGraph)")
+    ap.add_argument("--staged", action="store_true",
+                    help="separate draft / verify graphs with host-side compaction (A/B for the whole-step graph)")
     ap.add_argument("--no-auto-off", action="store_true", help="always speculate (no plain-decode fallback)")
     ap.add_argument("--no-adaptive", action="store_true", help="fixed tree depth")
     ap.add_argument("--sampled", action="store_true",
@@ -79,6 +81,7 @@ def main():
                        max_model_len=2048, kv_fraction=0.5)
     spec = SpecEngine(cfg, SpecConfig(depth=a.depth, width=a.width, topk=a.topk, graphs=not a.no_verify_graph,
                                       auto_off=not a.no_auto_off, adaptive_depth=not a.no_adaptive))
+    spec.whole_step = not a.staged
     if a.target == "peaked":
         m = spec.model
         perm = torch.randperm(m.embed.shape[0], generator=torch.Generator().manual_seed(7)).to(m.embed.device)
@@ -115,7 +118,7 @@ def main():
         def spec_run():
             spec.reset_controller()
             spec.spec_stats.update(spec_steps=0, spec_rows=0, accepted=0, spec_tokens=0, draft_s=0.0, verify_s=0.0,
-                                   plain_steps=0, switches_off=0, depth_changes=0)
+                                   plain_steps=0, switches_off=0, depth_changes=0, whole_steps=0)
             return timed_generate(spec, prompts, sp)
         out, t_spec = median_run(spec_run, a.repeats)
         acc = spec.acceptance()
@@ -125,7 +128,9 @@ def main():
                "speedup": round(t_base / t_spec, 3), "mean_accepted": round(acc["mean_accepted"], 3),
                "tokens_per_step": round(acc["tokens_per_step"], 3), "identical": out == ref,
                "max_greedy_gap": round(gap, 4),
-               "draft_s": round(acc["draft_s"], 3), "verify_s": round(acc["verify_s"], 3)}
+               "draft_s": round(acc["draft_s"], 3), "verify_s": round(acc["verify_s"], 3),
+               "whole_step_graph": spec.whole_step, "whole_steps": acc.get("whole_steps", 0),
+               "spec_steps": acc["spec_steps"]}
         row["controller"] = {k: acc[k] for k in ("current_depth", "spec_on", "plain_steps", "switches_off",
                                                   "depth_changes")}
         if a.sampled:

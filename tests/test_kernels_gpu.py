@@ -928,7 +928,7 @@ def test_fused_norm_layers_match_fp32(monkeypatch, graphs):
     monkeypatch.setattr(llama, "NORM_FOLD_MIN_ROWS", 1)
     mc = get_config("llama-tiny-hd128")
     cpu_model = LlamaModel(mc, "cpu", seed=5)
-    prompts = [[1] + list(range(3, 3 + n)) for n in (5, 40, 300, 7)]
+    prompts = [[1] + list(range(3, 3 + n)) for n in (5, 40, 200, 7)]     # (the fp32 oracle prefills in one chunk)
     gm = LlamaModel(mc, "cuda", init="empty").copy_from(cpu_model)
     calls = [0]
     orig = gm._forward_layers_folded

@@ -133,7 +133,7 @@ def _norm_case(M, N, K, kind, device, phases=0):
         ops.mfma_gemm_norm_ref(x, w, kind, want_ss, 1e-5, want_res)
         ops.mfma_gemm_norm(x, w, kind, ss, 1e-5, out=res, phases=phases)
         return (res, ss), (want_res, want_ss)
-    ss = torch.rand(M, 5, device=device) * K * 0.1
+    ss = torch.rand(M, 8, device=device) * K * 0.1
     want = ops.mfma_gemm_norm_ref(x, w, kind, ss, 1e-5)
     got = ops.mfma_gemm_norm(x, w, kind, ss, 1e-5, phases=phases)
     return (got,), (want,)

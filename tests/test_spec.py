@@ -400,3 +400,38 @@ def test_auto_draft_vocabulary_picks_the_smallest_covering_size():
     spread = torch.randint(0, V, (5000,), generator=g)
     assert auto_draft_vocab(spread, V, sizes=(16, 64, 256)) == 0
     assert auto_draft_vocab(torch.zeros(0, dtype=torch.long), V) == 0
+
+
+@pytest.mark.gpu
+def test_spec_whole_step_graph_matches_staged_path():
+    """the whole speculative step as one captured graph (draft catch-up, tree
+    drafting, verify, accept, KV compaction, feature gather) runs in the steady state (R = 3:
+    a padded bucket of 4), stays a greedy trajectory of the target, and accepts like the staged
+    path (separate draft / verify graphs, host compaction) on the same draft."""
+    import dataclasses
+    from dgi.spec.eagle3 import greedy_gap
+    spec = SpecConfig(depth=4, width=3, topk=4, auto_off=False, adaptive_depth=False)
+    base, whole = _engines("llama-tiny-hd128", "cuda", spec)
+    train_draft(whole, steps=80, batch=8, prompt_len=32, gen_len=96, num_seqs=32, random_seqs=32)
+    staged = SpecEngine(EngineConfig(model="llama-tiny-hd128", device="cuda", max_num_seqs=8,
+                                     max_num_batched_tokens=256, max_model_len=512, use_graphs=False),
+                        dataclasses.replace(spec), model=whole.model, draft=whole.draft)
+    staged.whole_step = False
+    sp = SamplingParams(max_tokens=32, temperature=0.0, ignore_eos=True)
+    prompts = _prompts(3, 1000)
+    res = {}
+    for name, eng in (("whole", whole), ("staged", staged)):
+        eng.spec_stats.update(spec_steps=0, spec_rows=0, accepted=0, spec_tokens=0, whole_steps=0)
+        outs = [r.output for r in eng.generate(prompts, sp)]
+        for p, o in zip(prompts, outs):
+            assert len(o) == 32 and greedy_gap(eng, p, o) < 0.07
+        res[name] = (outs, eng.acceptance())
+    assert res["whole"][1]["whole_steps"] > 0 and res["staged"][1]["whole_steps"] == 0
+    assert whole._sgraphs and not staged._sgraphs
+    tw, ts = res["whole"][1]["tokens_per_step"], res["staged"][1]["tokens_per_step"]
+    assert tw > 1.3 and abs(tw - ts) < 0.35 * ts
+    # sampled requests take the graph too (coupled verification with the per-node seeds)
+    spt = SamplingParams(max_tokens=16, temperature=0.8, top_k=50, top_p=0.9, ignore_eos=True, seed=3)
+    n0 = whole.spec_stats["whole_steps"]
+    outs = [r.output for r in whole.generate(prompts, spt)]
+    assert all(len(o) == 16 for o in outs) and whole.spec_stats["whole_steps"] > n0
