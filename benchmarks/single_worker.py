@@ -34,9 +34,12 @@ def bench_engine(a) -> dict:
     reference ``BenchmarkResult``."""
     from _common import run_bench
     from results import from_bench_single, gpu_stats
+    # enough steps for ~--num-requests completions at this concurrency, so the engine row's
+    # latency percentiles come from as many requests as the HTTP rows'
+    steps = max(a.steps, -(-a.num_requests // max(1, a.concurrent)) * (a.max_tokens + 1))
     args = ["--model", a.model, "--layout", "single", "--concurrency", str(a.concurrent), "--prompt-len",
             str(a.prompt_length), "--output-len", str(a.max_tokens), "--max-batched-tokens",
-            str(a.max_batched_tokens), "--steps", str(a.steps), "--warmup", str(a.warmup)]
+            str(a.max_batched_tokens), "--steps", str(steps), "--warmup", str(a.warmup)]
     res = run_bench(1, args)
     out = from_bench_single(res, backend="mi355x", gpu=gpu_stats()).to_dict()
     out["tpot_p50_ms"] = res.get("tpot_p50_ms")
