@@ -686,7 +686,6 @@ class _StepGraph:
         tok, par = _draft_tree(dr, g_root, last, self.lv, self.d_bt, W, D, self.K, N)
         # 3) verify
         anc, depth = ops.tree_mask(par)
-        ar = torch.arange(Rb, device=tok.device)
         tiles = self.c_tiles
         vm = AttnMeta(positions=self.v_pos, slot_mapping=self.v_slots, num_decode=0, num_prefill_tokens=Rb * N,
                       pre_block_tables=self.d_bt, pre_cu_seqlens=self.v_cu, pre_context_lens=self.v_ctx,
@@ -710,7 +709,6 @@ class _StepGraph:
         # 5) the accepted nodes' features (positions n - 1 .. n - 1 + acc) for the next catch-up
         fidx = path[:, :D + 1].long().clamp(min=0)
         fkeep = torch.gather(feats.view(Rb, N, H), 1, fidx[:, :, None].expand(Rb, D + 1, H))
-        del ar
         return acc, toks, fkeep
 
     @torch.inference_mode()
@@ -1249,7 +1247,7 @@ class SpecEngine(LLMEngine):
         speculating batch); None: the staged path runs it."""
         D = self.cur_depth
         C = D + 1
-        if self._step_graph_ok is False or D < 2:
+        if D < 2:
             return None
         rows = []
         for r in reqs:
@@ -1265,7 +1263,6 @@ class SpecEngine(LLMEngine):
         if sg is None:
             return None
         t0 = time.perf_counter()
-        N = sg.N
         samp = None
         if any(r.params.temperature > 0 for r in reqs):
             samp = self._node_sampling_host(reqs, sg.depth_np)
@@ -1311,10 +1308,7 @@ class SpecEngine(LLMEngine):
         self._period_acc[0] += sum(acc_h)
         self._period_acc[1] += R
         self._adapt_depth(sum(acc_h) / (R * D))
-        del N
         return outs
-
-    _step_graph_ok = None
 
     def _node_sampling_host(self, reqs: list, depth_np: np.ndarray) -> tuple:
         """``_node_sampling`` as host arrays [R, N] (the whole-step graph copies them into its
