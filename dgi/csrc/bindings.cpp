@@ -34,6 +34,9 @@ int dgi_mfma_gemm(const void* x, int ldx, const void* w, void* y, int ldy, int M
 void dgi_set_gemm_cus(int cus);
 int dgi_mfma_gemm_norm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int kind,
                        float* ss, int ss_ld, float inv_k, float eps, int phases, hipStream_t s);
+int dgi_mfma_gemm_norm_rope(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, float* ss,
+                            int ss_ld, float inv_k, float eps, const int* pos, const float* cos_sin, const int* slots,
+                            void* k_cache, void* v_cache, int nh, int nkv, int block_size, int phases, hipStream_t s);
 int dgi_fused_skinny(const void* x, int ldx, const void* res, int ldr, void* res_out, const void* gamma,
                      float eps, const void* w, const void* bias, void* y, int ldy, int M, int N, int K, int pro,
                      int epi, const int* positions, const float* cos_sin, const int* slots, void* k_cache,
@@ -268,6 +271,43 @@ void mfma_gemm_norm(at::Tensor out, const at::Tensor& x, const at::Tensor& w, in
                               (int)N, (int)K, (int)kind, ss.data_ptr<float>(), (int)ss.size(1), (float)inv_k,
                               (float)eps, (int)phases, cur_stream()),
            "mfma_gemm_norm");
+}
+
+// The normalised qkv projection with the RoPE + paged-KV epilogue (mfma_gemm.hip EPI 5).
+void mfma_gemm_norm_rope(at::Tensor out, const at::Tensor& x, const at::Tensor& w, at::Tensor ss, double inv_k,
+                         double eps, const at::Tensor& positions, const at::Tensor& cos_sin,
+                         const at::Tensor& slot_mapping, at::Tensor k_cache, at::Tensor v_cache, int64_t nh,
+                         int64_t nkv, int64_t phases) {
+  check_bf16(out, "out"); check_bf16(x, "x"); check_bf16(w, "w"); check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  TORCH_CHECK(ss.scalar_type() == at::kFloat && ss.dim() == 2 && ss.is_contiguous() && ss.size(1) % 8 == 0 &&
+              ss.size(1) <= 32, "mfma_gemm_norm_rope: ss fp32 [M, n], n % 8, <= 32");
+  TORCH_CHECK(positions.scalar_type() == at::kInt && slot_mapping.scalar_type() == at::kInt &&
+              positions.is_contiguous() && slot_mapping.is_contiguous(), "mfma_gemm_norm_rope: int32 positions / slots");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.dim() == 2 && cos_sin.size(1) == 128 &&
+              cos_sin.is_contiguous(), "mfma_gemm_norm_rope: cos_sin fp32 [max_pos, 128]");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == nkv && k_cache.size(3) == 128 && k_cache.is_contiguous() &&
+              v_cache.sizes() == k_cache.sizes() && v_cache.is_contiguous(),
+              "mfma_gemm_norm_rope: caches [blocks, nkv, bs, 128]");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2 && x.stride(1) == 1 && out.stride(1) == 1 &&
+              w.is_contiguous(), "mfma_gemm_norm_rope: row-major 2-D operands");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && out.size(0) == M && out.size(1) == N && ss.size(0) >= M &&
+              positions.size(0) >= M && slot_mapping.size(0) >= M, "mfma_gemm_norm_rope: shape mismatch");
+  TORCH_CHECK(N == (nh + 2 * nkv) * 128 && (nh * 128) % 256 == 0 && (nkv * 128) % 256 == 0,
+              "mfma_gemm_norm_rope: fused qkv of 128-dim heads, head groups of 256 columns");
+  TORCH_CHECK(K % 128 == 0 && K >= 256 && x.stride(0) % 8 == 0 && out.stride(0) % 8 == 0,
+              "mfma_gemm_norm_rope: K%128, ldx%8, ldy%8");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0 &&
+              reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0, "mfma_gemm_norm_rope: operand alignment");
+  TORCH_CHECK((int64_t)M * x.stride(0) < (1LL << 31) && (int64_t)M * out.stride(0) < (1LL << 31),
+              "mfma_gemm_norm_rope: activation too large for 32-bit offsets");
+  check_rc(dgi_mfma_gemm_norm_rope(x.data_ptr(), (int)x.stride(0), w.data_ptr(), out.data_ptr(), (int)out.stride(0),
+                                   (int)M, (int)N, (int)K, ss.data_ptr<float>(), (int)ss.size(1), (float)inv_k,
+                                   (float)eps, positions.data_ptr<int>(), cos_sin.data_ptr<float>(),
+                                   slot_mapping.data_ptr<int>(), k_cache.data_ptr(), v_cache.data_ptr(), (int)nh,
+                                   (int)nkv, (int)k_cache.size(2), (int)phases, cur_stream()),
+           "mfma_gemm_norm_rope");
 }
 
 // Decode GEMM with fused RMSNorm prologue (pro 1: norm, 2: residual add + norm -> res_out) and
@@ -555,6 +595,9 @@ TORCH_LIBRARY(dgi, m) {
   m.def("mfma_gemm(Tensor(a!) out, Tensor x, Tensor w, int epi=0) -> ()");
   m.def("mfma_gemm_norm(Tensor(a!) out, Tensor x, Tensor w, int kind, Tensor(b!) ss, float inv_k, float eps, "
         "int phases=0) -> ()");
+  m.def("mfma_gemm_norm_rope(Tensor(a!) out, Tensor x, Tensor w, Tensor ss, float inv_k, float eps, "
+        "Tensor positions, Tensor cos_sin, Tensor slot_mapping, Tensor(b!) k_cache, Tensor(c!) v_cache, int nh, "
+        "int nkv, int phases=0) -> ()");
   m.def("fused_skinny(Tensor(a!) y, Tensor x, Tensor? res, Tensor(b!)? res_out, Tensor? gamma, float eps, "
         "Tensor w, Tensor? bias, int pro, int epi, Tensor? positions, Tensor? cos_sin, Tensor? slots, "
         "Tensor(c!)? k_cache, Tensor(d!)? v_cache, int nh=0, int nkv=0, int cfg=0) -> ()");
@@ -584,6 +627,7 @@ TORCH_LIBRARY_IMPL(dgi, CUDA, m) {
   m.impl("skinny_gemm", &skinny_gemm);
   m.impl("mfma_gemm", &mfma_gemm);
   m.impl("mfma_gemm_norm", &mfma_gemm_norm);
+  m.impl("mfma_gemm_norm_rope", &mfma_gemm_norm_rope);
   m.impl("fused_skinny", &fused_skinny);
   m.impl("sample", &sample);
   m.impl("topk", &topk);

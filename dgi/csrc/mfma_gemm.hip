@@ -36,6 +36,7 @@
 // on load and skipped on store.
 #include "common.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 using namespace dgi;
@@ -84,12 +85,21 @@ __device__ __forceinline__ void store_pair16(uint16_t* yrow, int n0, int g, cons
 //     before the store / activation.  With the RMSNorm gain folded into the weights
 //     (W' = W * diag(gamma), LlamaModel.fold_norms) this is rmsnorm(x) * gamma @ W^T without
 //     the normalised copy of x: the norm kernels between the projections disappear.
+//   5 normalised qkv with the RoPE + paged-KV epilogue: the rstd-scaled tile is rounded to bf16
+//     into LDS, then q heads are rotated (NeoX pairs d, d + 64 of each 128-dim head) in place in Y
+//     and k (rotated) / v heads go straight to the paged cache at each row's slot — the separate
+//     rope_cache kernel and its read-back of the qkv tensor disappear (k / v columns of Y are not
+//     written: attention reads them from the cache).
 template <int EPI>
 struct EpiKind {
   static constexpr bool swiglu = EPI == 1 || EPI == 4;
-  static constexpr bool norm = EPI == 3 || EPI == 4;
+  static constexpr bool norm = EPI == 3 || EPI == 4 || EPI == 5;
   static constexpr bool res = EPI == 2;
+  static constexpr bool rope = EPI == 5;
 };
+
+constexpr int kRopeLd = 264;                    // LDS row stride (elements) of the RoPE tile image
+constexpr int kRopeBytes = 256 * kRopeLd * 2;   // 135,168: the staging stages plus 4 KB
 
 // store_pair16's column exchange on fp32 values: f[0..7] are the lane's 8 consecutive columns
 // (A 0-7 for lane group 0, B 0-7 for 1, A 8-15 for 2, B 8-15 for 3) starting at
@@ -152,7 +162,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[8][4], uint16_t* __r
 // Every wave of the block must call it (one barrier).
 __device__ __forceinline__ void epilogue_res(const f32x4 (&acc)[8][4], uint16_t* __restrict__ Y, int ldy, int M,
                                              int m0, int tn, int wm, int wn, int lane, float* ssl,
-                                             float* __restrict__ ss, int ss_ld) {
+                                             float* __restrict__ ss, int ss_ld, int dbg) {
   const int r16 = lane & 15;
   const int g = lane >> 4;
   const int cbase = tn * 256 + wn * 64 + 16 * (g & 1) + 4 * (g & 2);
@@ -166,7 +176,7 @@ __device__ __forceinline__ void epilogue_res(const f32x4 (&acc)[8][4], uint16_t*
       const int m = m0 + wm * 128 + (i0 + ii) * 16 + r16;
       const uint16_t* yrow = Y + (size_t)min(m, M - 1) * ldy + cbase;
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj) old[ii][jj] = *(const uint4*)(yrow + jj * 32);
+      for (int jj = 0; jj < 2; ++jj) old[ii][jj] = (dbg & 4) ? uint4{0, 0, 0, 0} : *(const uint4*)(yrow + jj * 32);
     }
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii) {
@@ -199,6 +209,7 @@ __device__ __forceinline__ void epilogue_res(const f32x4 (&acc)[8][4], uint16_t*
       if (g == 0) ssl[wn * 256 + wm * 128 + i * 16 + r16] = part;
     }
   }
+  if (dbg & 2) return;
   __syncthreads();
   const int t = threadIdx.x;
   if (t < 256 && m0 + t < M)
@@ -673,7 +684,87 @@ struct PPArgs {
   float* ss;                  // EPI 2: per-row partial sums of squares out; EPI 3 / 4: in
   int ss_ld;                  // row stride of ss (EPI 2: its column is the N tile; EPI 3 / 4: partials per row)
   float inv_k, eps;           // EPI 3 / 4: rstd = rsqrt(sum * inv_k + eps)
+  int dbg;                    // diagnostics (DGI_NORM_GEMM_DBG): 1 = no row statistics read (rstd 1),
+                              // 2 = residual epilogue without the statistics, 4 = without the residual read
+  // EPI 5: RoPE table [positions, 128] (64 cos | 64 sin), per-row positions / cache slots, caches
+  // [blocks, nkv, bs, 128], q / kv column counts
+  const int* pos;
+  const float* cs;
+  const int* slots;
+  uint16_t* kc;
+  uint16_t* vc;
+  int qcols, kvcols, nkv, bs;
 };
+
+// EPI 5 (see EpiKind): T is the LDS tile image (256 rows x kRopeLd), rs the tile's rstd.  Every wave
+// of the block calls it (two barriers).
+__device__ __forceinline__ void epilogue_rope(const f32x4 (&acc)[8][4], const PPArgs& a, int m0, int tn, int wm,
+                                              int wn, int lane, const float* rs, uint16_t* T) {
+  const int r16 = lane & 15;
+  const int g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int rl = wm * 128 + i * 16 + r16;
+    const float sc = rs[rl];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint2 v;
+      v.x = pack_bf16x2(acc[i][j][0] * sc, acc[i][j][1] * sc);
+      v.y = pack_bf16x2(acc[i][j][2] * sc, acc[i][j][3] * sc);
+      *(uint2*)(T + rl * kRopeLd + wn * 64 + j * 16 + 4 * g) = v;
+    }
+  }
+  __syncthreads();
+  const int t = threadIdx.x;
+  const int rl = t >> 1, half = t & 1;      // two lanes per row, 32 of the 64 pairs of each head
+  const int m = m0 + rl;
+  const int col0 = tn * 256;
+  const int kind = col0 < a.qcols ? 0 : col0 < a.qcols + a.kvcols ? 1 : 2;    // q, k or v heads
+  const int slot = (m < a.M && kind) ? a.slots[m] : 0;
+  if (m < a.M && slot >= 0) {
+    const int blk = kind ? slot / a.bs : 0;
+    const int off = kind ? slot - blk * a.bs : 0;
+    const float* cs = a.cs + (size_t)a.pos[m] * 128;
+    const int head0 = kind == 1 ? (col0 - a.qcols) >> 7 : (col0 - a.qcols - a.kvcols) >> 7;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int d = half * 32 + c * 8;
+      float cv[8], sv[8];
+      if (kind != 2) {
+        *(float4*)cv = *(const float4*)(cs + d);
+        *(float4*)(cv + 4) = *(const float4*)(cs + d + 4);
+        *(float4*)sv = *(const float4*)(cs + 64 + d);
+        *(float4*)(sv + 4) = *(const float4*)(cs + 64 + d + 4);
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint16_t* tp = T + rl * kRopeLd + h * 128 + d;
+        const u32x4 p0 = *(const u32x4*)tp, p1 = *(const u32x4*)(tp + 64);
+        u32x4 o0 = p0, o1 = p1;
+        if (kind != 2) {
+          float x0[8], x1[8], y0[8], y1[8];
+          unpack8(p0, x0);
+          unpack8(p1, x1);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            y0[e] = x0[e] * cv[e] - x1[e] * sv[e];
+            y1[e] = x1[e] * cv[e] + x0[e] * sv[e];
+          }
+          o0 = pack8(y0);
+          o1 = pack8(y1);
+        }
+        uint16_t* dst;
+        if (kind == 0)
+          dst = a.Y + (size_t)m * a.ldy + col0 + h * 128 + d;
+        else
+          dst = (kind == 1 ? a.kc : a.vc) + (((size_t)blk * a.nkv + head0 + h) * a.bs + off) * 128 + d;
+        *(u32x4*)dst = o0;
+        *(u32x4*)(dst + 64) = o1;
+      }
+    }
+  }
+  __syncthreads();   // the image is read before the next work item's staging rewrites LDS
+}
 
 // buffer resource word 3 of a raw (stride 0, byte-addressed) buffer on gfx9, and the cache
 // policy bit of a write-through (sc1) access
@@ -800,8 +891,9 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
   // longer tell the staging DMA from other LDS traffic and waits vmcnt(0) before every fragment
   // read of the K loop (measured: the gate_up kernel 349 -> 517 us at 512 rows).
   constexpr int kEpBytes = EpiKind<EPI>::res ? 4096 : EpiKind<EPI>::norm ? 2048 : 0;
-  __shared__ __attribute__((aligned(16))) char smem[2 * kStageBytes + kEpBytes];
-  float* const ep_lds = (float*)(smem + 2 * kStageBytes);
+  constexpr int kMainBytes = EpiKind<EPI>::rope ? kRopeBytes : 2 * kStageBytes;
+  __shared__ __attribute__((aligned(16))) char smem[kMainBytes + kEpBytes];
+  float* const ep_lds = (float*)(smem + kMainBytes);
   int rs_slot = 0;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -926,7 +1018,7 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
       // two lanes per row, each summing half of its partials (float4 loads, all in flight
       // together: ss_ld % 8 == 0, <= 32), then one exchange — a fixed order on every run
       const int m = min(tm * kBM + (t >> 1), M - 1);
-      const int per = a.ss_ld >> 3;
+      const int per = (a.dbg & 1) ? 0 : a.ss_ld >> 3;
       const f32x4* sp = (const f32x4*)(a.ss + (size_t)m * a.ss_ld) + (t & 1) * per;
       f32x4 v[4];
 #pragma unroll
@@ -1071,7 +1163,10 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
                const int te = fresh_tid();
                if constexpr (EpiKind<EPI>::res)
                  epilogue_res(acc, a.Y, a.ldy, M, tm * kBM, tn, (te >> 8) & 1, (te >> 6) & 3, te & 63, ep_lds, a.ss,
-                              a.ss_ld);
+                              a.ss_ld, a.dbg);
+               else if constexpr (EpiKind<EPI>::rope)
+                 epilogue_rope(acc, a, tm * kBM, tn, (te >> 8) & 1, (te >> 6) & 3, te & 63, ep_lds + rs_slot * 256,
+                               (uint16_t*)smem);
                else
                  epilogue<EPI>(acc, a.Y, a.ldy, M, tm * kBM, tn, (te >> 8) & 1, (te >> 6) & 3, te & 63,
                                ep_lds + rs_slot * 256);
@@ -1123,6 +1218,13 @@ struct NormArgs {
   float* ss = nullptr;
   int ss_ld = 0;
   float inv_k = 0.f, eps = 0.f;
+  int dbg = 0;
+  const int* pos = nullptr;
+  const float* cs = nullptr;
+  const int* slots = nullptr;
+  uint16_t* kc = nullptr;
+  uint16_t* vc = nullptr;
+  int qcols = 0, kvcols = 0, nkv = 0, bs = 0;
 };
 
 template <int EPI>
@@ -1138,9 +1240,11 @@ void launch_pp(const void* x, int ldx, const void* w, void* y, int ldy, int M, i
                       : (prio & 3) == 1   ? mfma_gemm_pp_kernel<EPI, 1, 4>
                       : (prio & 3) == 2   ? mfma_gemm_pp_kernel<EPI, 2, 4>
                                           : mfma_gemm_pp_kernel<EPI, 0, 4>;
-  // EPI 2 reads the tile it stores (in place): no overlap of the next tile's loads with it
+  // EPI 2 reads the tile it stores (in place) and EPI 5 stages its tile through the staging LDS: no
+  // overlap of the next tile's loads with their epilogues
   PPArgs a{(const uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, nullptr, nullptr, ldx, ldy, M, I, K, tiles_m, total,
-           0, 0, 0, 0, !(prio & 8) && EPI != 2, na.ss, na.ss_ld, na.inv_k, na.eps};
+           0, 0, 0, 0, !(prio & 8) && EPI != 2 && EPI != 5, na.ss, na.ss_ld, na.inv_k, na.eps, na.dbg,
+           na.pos, na.cs, na.slots, na.kc, na.vc, na.qcols, na.kvcols, na.nkv, na.bs};
   const int nt = K / kBK;
   SkWorkspace* sk = ((skmode || a.ovl) && nt >= 8) ? sk_workspace(s) : nullptr;
   if (sk) {
@@ -1208,6 +1312,11 @@ extern "C" int dgi_mfma_gemm_norm(const void* x, int ldx, const void* w, void* y
   const int tiles_m = (M + kBM - 1) / kBM;
   const int total = tiles_m * tiles_n;
   NormArgs na;
+  static const int dbg = [] {
+    const char* e = getenv("DGI_NORM_GEMM_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  na.dbg = dbg;
   na.ss = ss;
   na.ss_ld = ss_ld;
   na.inv_k = inv_k;
@@ -1218,6 +1327,40 @@ extern "C" int dgi_mfma_gemm_norm(const void* x, int ldx, const void* w, void* y
     launch_pp<3>(x, ldx, w, y, ldy, M, I, K, tiles_m, total, 1, prio, s, na);
   else
     launch_pp<4>(x, ldx, w, y, ldy, M, I, K, tiles_m, total, 1, prio, s, na);
+  DGI_CHECK_LAUNCH();
+  return 0;
+}
+
+// The normalised qkv projection with the RoPE + paged-KV epilogue (EPI 5): y = rstd * x w^T with the
+// q heads rotated in place (y's k / v columns are left unwritten), k (rotated) and v written to the
+// caches [blocks, nkv, bs, 128] at slots[m] (< 0: skipped).  Head dim 128, full NeoX rotary;
+// nh * 128 and nkv * 128 multiples of 256.
+extern "C" int dgi_mfma_gemm_norm_rope(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K,
+                                       float* ss, int ss_ld, float inv_k, float eps, const int* pos,
+                                       const float* cos_sin, const int* slots, void* k_cache, void* v_cache,
+                                       int nh, int nkv, int block_size, int phases, hipStream_t s) {
+  if (M <= 0) return 0;
+  if (K % (2 * kBK) || K < 4 * kBK || ldx % 8 || ldy % 8 || N % 256 || !ss || ss_ld % 8 || ss_ld > 32 || ss_ld <= 0)
+    return -3;
+  if ((nh * 128) % 256 || (nkv * 128) % 256 || N != (nh + 2 * nkv) * 128 || block_size <= 0) return -3;
+  int prio = (phases == 2 || (phases == 0 && M <= 2560)) ? 4 : 0;
+  const int tiles_m = (M + kBM - 1) / kBM;
+  const int total = tiles_m * (N / 256);
+  NormArgs na;
+  na.ss = ss;
+  na.ss_ld = ss_ld;
+  na.inv_k = inv_k;
+  na.eps = eps;
+  na.pos = pos;
+  na.cs = cos_sin;
+  na.slots = slots;
+  na.kc = (uint16_t*)k_cache;
+  na.vc = (uint16_t*)v_cache;
+  na.qcols = nh * 128;
+  na.kvcols = nkv * 128;
+  na.nkv = nkv;
+  na.bs = block_size;
+  launch_pp<5>(x, ldx, w, y, ldy, M, 0, K, tiles_m, total, 1, prio, s, na);
   DGI_CHECK_LAUNCH();
   return 0;
 }

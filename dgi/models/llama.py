@@ -70,6 +70,9 @@ TBO_MIN_ROWS = int(os.environ.get("DGI_TBO_MIN_ROWS", "512"))
 # skinny / fused-decode kernels.
 NORM_FOLD = os.environ.get("DGI_NORM_FOLD", "1")
 NORM_FOLD_MIN_ROWS = int(os.environ.get("DGI_NORM_FOLD_MIN_ROWS", "256"))
+# fused-norm layers: RoPE + the paged-KV write in the qkv GEMM's epilogue (EPI 5) where the geometry
+# allows (NeoX rotary over 128-dim heads, q / kv column blocks of 256); "0" keeps rope_cache
+NORM_FOLD_ROPE = os.environ.get("DGI_NORM_FOLD_ROPE", "1") != "0"
 TBO_SIDE_PER_XCD = int(os.environ.get("DGI_TBO_SIDE", "4"))
 
 
@@ -488,9 +491,17 @@ class LlamaModel:
         ss = ss[:T]
         ops.row_sumsq(R, ss)
         n = len(self.layers)
+        rope_epi = (NORM_FOLD_ROPE and (R.is_cuda or NORM_FOLD == "force-cpu") and self.rope_mode == 0 and c.head_dim == 128
+                    and self.cos_sin.shape[1] == 128 and (c.num_heads * 128) % 256 == 0
+                    and (c.num_kv_heads * 128) % 256 == 0)
         for i, L in enumerate(self.layers):
-            qkv = ops.mfma_gemm_norm(R, L.qkv, ops.NORM_PLAIN, ss, eps)
-            attn = self.attention(i, qkv, meta)
+            if rope_epi:
+                qkv = ops.mfma_gemm_norm_rope(R, L.qkv, ss, eps, meta.positions, self.cos_sin, meta.slot_mapping,
+                                              self.kv_cache[i, 0], self.kv_cache[i, 1], c.num_heads, c.num_kv_heads)
+                attn = self.attention(i, qkv, meta, rope=False)
+            else:
+                qkv = ops.mfma_gemm_norm(R, L.qkv, ops.NORM_PLAIN, ss, eps)
+                attn = self.attention(i, qkv, meta)
             if trim_last is not None and i == n - 1:
                 attn = attn.index_select(0, trim_last)
                 Rs = R.index_select(0, trim_last)

@@ -664,6 +664,34 @@ def mfma_gemm_norm(x: torch.Tensor, w: torch.Tensor, kind: int, ss: torch.Tensor
     return mfma_gemm_norm_ref(x, w, kind, ss, eps, out)
 
 
+def mfma_gemm_norm_rope_ref(x, w, ss, eps, positions, cos_sin, slots, k_cache, v_cache, nh, nkv,
+                            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp32 reference of ``mfma_gemm_norm_rope``: the normalised qkv (bf16), then RoPE + paged KV
+    write (``rope_cache_ref``, NeoX, head dim 128)."""
+    y = mfma_gemm_norm_ref(x, w, NORM_PLAIN, ss, eps)
+    rope_cache_ref(y, positions[: x.shape[0]], cos_sin, nh, nkv, 128, slots[: x.shape[0]], k_cache, v_cache, 0)
+    if out is None:
+        return y
+    out.copy_(y)
+    return out
+
+
+def mfma_gemm_norm_rope(x, w, ss, eps, positions, cos_sin, slots, k_cache, v_cache, nh: int, nkv: int,
+                        out: Optional[torch.Tensor] = None, phases: int = 0) -> torch.Tensor:
+    """The normalised qkv projection with RoPE and the paged-KV write in its epilogue
+    (mfma_gemm.hip EPI 5): returns y whose q columns are rotated (its k / v columns are NOT
+    written — they go to ``k_cache`` / ``v_cache`` at ``slots``, which attention reads), i.e.
+    ``mfma_gemm_norm(x, w, NORM_PLAIN, ss)`` followed by ``rope_cache`` in one kernel.  Llama
+    geometry: head dim 128, full NeoX rotary, cos_sin [max_pos, 128]."""
+    if _native(x):
+        if out is None:
+            out = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
+        _call("mfma_gemm_norm_rope", out, x, w, ss, 1.0 / x.shape[1], eps, positions, cos_sin, slots, k_cache,
+              v_cache, nh, nkv, phases)
+        return out
+    return mfma_gemm_norm_rope_ref(x, w, ss, eps, positions, cos_sin, slots, k_cache, v_cache, nh, nkv, out)
+
+
 def mfma_norm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
     """Shapes the fused-norm GEMM takes (K % 128 and >= 256 on top of ``mfma_gemm_ok``; a
     normalising consumer also needs its K — the stream width — <= 8192: 32 row partials)."""

@@ -914,7 +914,8 @@ def test_mixed_step_lookahead_matches_plain_steps(sampled, eos):
 
 
 @pytest.mark.parametrize("graphs", [False, True])
-def test_fused_norm_layers_match_fp32(monkeypatch, graphs):
+@pytest.mark.parametrize("name", ["llama-tiny-hd128", "llama-tiny-tp"])
+def test_fused_norm_layers_match_fp32(monkeypatch, graphs, name):
     """The fused-norm layers (gains folded into qkv / gate_up, residual + row statistics in the
     o / down epilogues, rstd in the qkv / gate_up epilogues) on every step — prefill chunks,
     mixed steps and captured decode graphs: each generated token is an argmax of the fp32 CPU
@@ -926,7 +927,7 @@ def test_fused_norm_layers_match_fp32(monkeypatch, graphs):
     from dgi.sched.request import SamplingParams
     monkeypatch.setattr(llama, "NORM_FOLD", "force")
     monkeypatch.setattr(llama, "NORM_FOLD_MIN_ROWS", 1)
-    mc = get_config("llama-tiny-hd128")
+    mc = get_config(name)             # tiny-tp: 2 kv heads, so the qkv GEMM also takes the RoPE + KV epilogue
     cpu_model = LlamaModel(mc, "cpu", seed=5)
     prompts = [[1] + list(range(3, 3 + n)) for n in (5, 40, 200, 7)]     # (the fp32 oracle prefills in one chunk)
     gm = LlamaModel(mc, "cuda", init="empty").copy_from(cpu_model)
@@ -937,11 +938,11 @@ def test_fused_norm_layers_match_fp32(monkeypatch, graphs):
         calls[0] += 1
         return orig(*a, **k)
     gm._forward_layers_folded = spy
-    e = LLMEngine(EngineConfig(model="llama-tiny-hd128", device="cuda", num_blocks=256, max_num_seqs=8,
+    e = LLMEngine(EngineConfig(model=name, device="cuda", num_blocks=256, max_num_seqs=8,
                                max_model_len=512, max_num_batched_tokens=256, use_graphs=graphs),
                   model_cfg=mc, model=gm)
     assert gm.norms_folded
     outs = [r.output for r in e.generate(prompts, SamplingParams(max_tokens=10, temperature=0.0, ignore_eos=True))]
     torch.cuda.synchronize()
     assert calls[0] > 0
-    assert _teacher_forced_ok("llama-tiny-hd128", cpu_model, prompts, outs) == 40
+    assert _teacher_forced_ok(name, cpu_model, prompts, outs) == 40

@@ -184,3 +184,47 @@ def test_mfma_gemm_norm_is_deterministic():
         outs.append([t.clone() for t in got])
     torch.cuda.synchronize()
     assert all(torch.equal(a, b) for a, b in zip(*outs))
+
+
+def _rope_case(M, nh, nkv, K, device, phases=0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    N = (nh + 2 * nkv) * 128
+    x = _rand(M, K, device=device, seed=M + K)
+    w = _rand(N, K, device=device, scale=0.05, seed=N)
+    ss = (torch.rand(M, 8, generator=g) * K * 0.1).to(device)
+    cs = ops.rope_cos_sin(128, 4096, 500000.0, device=device)
+    pos = torch.randint(0, 4000, (M,), generator=g, dtype=torch.int32).to(device)
+    nb, bs = (M + 15) // 16 + 4, 16
+    slots = torch.randperm(nb * bs, generator=g)[:M].to(torch.int32)
+    slots[::7] = -1                                   # rows with no cache slot (graph padding)
+    slots = slots.to(device)
+    caches = []
+    for _ in range(2):
+        kc = torch.zeros(nb, nkv, bs, 128, dtype=torch.bfloat16, device=device)
+        vc = torch.zeros_like(kc)
+        caches.append((kc, vc))
+    want = ops.mfma_gemm_norm_rope_ref(x, w, ss, 1e-5, pos, cs, slots, *caches[0], nh, nkv)
+    got = ops.mfma_gemm_norm_rope(x, w, ss, 1e-5, pos, cs, slots, *caches[1], nh, nkv, phases=phases)
+    return (got[:, : nh * 128], caches[1][0], caches[1][1]), (want[:, : nh * 128], caches[0][0], caches[0][1])
+
+
+def test_norm_rope_reference_composes_norm_then_rope_cpu():
+    got, want = _rope_case(37, 4, 2, 256, "cpu")
+    for g, w in zip(got, want):
+        assert torch.equal(g, w)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,nh,nkv,K", [(1, 2, 2, 256), (100, 4, 2, 512), (300, 8, 2, 1024), (513, 64, 8, 1024),
+                                        (1024, 16, 2, 2048)])
+@pytest.mark.parametrize("phases", [2, 4])
+def test_mfma_gemm_norm_rope_matches_fp32(M, nh, nkv, K, phases):
+    """EPI 5: rotated q columns, rotated k and plain v in the paged caches (rows with slot -1 write
+    nothing) against the fp32 norm-then-rope reference."""
+    ops.load_native(required=True)
+    got, want = _rope_case(M, nh, nkv, K, "cuda", phases)
+    torch.cuda.synchronize()
+    for g, w in zip(got, want):
+        err = (g.float() - w.float()).abs()
+        tol = 2e-2 * w.float().abs().max().item() + 1e-3
+        assert err.max().item() <= tol, (err.max().item(), tol)

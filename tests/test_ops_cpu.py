@@ -340,7 +340,8 @@ def test_gemm_table_decides_with_margin_and_round_trips_json(tmp_path):
     assert back.impls == t.impls and back.proj_impls == t.proj_impls and back.source == "shipped"
 
 
-def test_fused_norm_layer_composition_matches_unfused_cpu(monkeypatch):
+@pytest.mark.parametrize("name", ["llama-tiny-hd128", "llama-tiny-tp"])
+def test_fused_norm_layer_composition_matches_unfused_cpu(monkeypatch, name):
     """The fused-norm layer composition (gains folded into the weights, residual + row
     statistics from the o / down epilogues, rstd applied by qkv / gate_up) through the fp32
     reference ops equals the unfused layers: whole-sequence logits, the trimmed last layer and
@@ -349,7 +350,7 @@ def test_fused_norm_layer_composition_matches_unfused_cpu(monkeypatch):
     from dgi.models.config import get_config
     from dgi.models.llama import LlamaModel
     from dgi.runtime.batch import AttnMeta
-    mc = get_config("llama-tiny-hd128")
+    mc = get_config(name)            # tiny-tp (2 kv heads): the qkv GEMM also takes the RoPE + KV epilogue
     ref = LlamaModel(mc, "cpu", torch.float32, seed=9)
     fold = LlamaModel(mc, "cpu", torch.float32, init="empty").copy_from(ref)
     fold.fold_norms()
@@ -366,7 +367,7 @@ def test_fused_norm_layer_composition_matches_unfused_cpu(monkeypatch):
                         num_prefill_tokens=T, pre_block_tables=torch.arange(1, nb, dtype=torch.int32)[None],
                         pre_cu_seqlens=torch.tensor([0, T], dtype=torch.int32),
                         pre_context_lens=torch.tensor([T], dtype=torch.int32), logits_indices=torch.tensor([T - 1]))
-        m.capture_layers, m.captured = (1, 3), {}
+        m.capture_layers, m.captured = (0, mc.num_layers - 1), {}
         full = m.forward(AttnMeta(**{**meta.__dict__, "logits_indices": None}), input_ids=ids)
         feats = {k: v.clone() for k, v in m.captured.items()}
         m.capture_layers, m.captured = (), {}
@@ -375,5 +376,5 @@ def test_fused_norm_layer_composition_matches_unfused_cpu(monkeypatch):
     (f0, l0, c0), (f1, l1, c1) = outs["ref"], outs["fold"]
     assert torch.allclose(f0, f1, atol=1e-3, rtol=1e-3)
     assert torch.allclose(l0, l1, atol=1e-3, rtol=1e-3) and torch.allclose(l1[-1], f1[-1], atol=1e-3, rtol=1e-3)
-    for k in (1, 3):
+    for k in (0, mc.num_layers - 1):
         assert torch.allclose(c0[k], c1[k], atol=1e-3, rtol=1e-3)
