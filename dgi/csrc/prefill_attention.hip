@@ -360,289 +360,6 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void prefill_attn_kernel(
 }
 
 
-// ---------------------------------------------------------------------------
-// Software-pipelined variant (PIPE): the K tiles run one tile ahead of the V tiles, so while a wave
-// finishes tile t (softmax on the VALU, then P.V) the MFMAs of S(t+1) = K(t+1) Q^T are already in
-// flight — issued first and interleaved with the softmax by sched_group_barrier (mask 0x008 MFMA,
-// 0x002 VALU).  LDS holds two K images and two V images (the DB variant's footprint): at the one
-// barrier of iteration t, K(t+1) and V(t) have landed, everybody has finished S(t) and P.V(t-1), so
-// K(t+2) goes into K(t)'s image and V(t+1) into V(t-1)'s, from registers loaded one iteration
-// earlier (K(t+3) and V(t+2) are issued right after).  The score accumulators double (S(t), S(t+1)).
-template <int HD, int NW>
-__global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void prefill_attn_pipe_kernel(
-    const uint16_t* __restrict__ q, int q_stride, const uint16_t* __restrict__ k_cache,
-    const uint16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
-    const int* __restrict__ cu_seqlens_q, const int* __restrict__ context_lens,
-    const int* __restrict__ tiles, uint16_t* __restrict__ out, int out_stride, int nh, int nkv,
-    int bs_log2, float scale_log2, const unsigned long long* __restrict__ tree_mask, int tree_n) {
-  __shared__ __attribute__((aligned(16))) uint16_t lds[4 * KT * HD];   // K0 K1 V0 V1
-
-  const int b = tiles[2 * blockIdx.x];
-  const int t0 = tiles[2 * blockIdx.x + 1];
-  const int head = blockIdx.y;
-  const int kvh = head / (nh / nkv);
-  const int q0 = cu_seqlens_q[b];
-  const int qlen = cu_seqlens_q[b + 1] - q0;
-  const int ctx = context_lens[b];
-  const int pos_base = ctx - qlen;
-  const int bs = 1 << bs_log2;
-  const int* bt = block_tables + (size_t)b * bt_stride;
-
-  const int tid = threadIdx.x;
-  const int w = tid >> 6;
-  const int lane = tid & 63;
-  const int lr = lane & 31;
-  const int hh = lane >> 5;
-
-  const int my_row = t0 + 32 * w + lr;
-  const bool row_valid = my_row < qlen;
-  const int my_pos = pos_base + my_row;
-  const int tree_first = qlen - tree_n;
-  unsigned long long tmask = 0;
-  const bool is_tree = tree_mask != nullptr && row_valid && my_row >= tree_first;
-  if (is_tree) tmask = tree_mask[(size_t)b * 64 + (my_row - tree_first)];
-  const int tree_key0 = pos_base + tree_first;
-
-  constexpr int NS = HD / 16;
-  constexpr int ND = HD / 32;
-  constexpr int CH = HD / 8;
-  constexpr int NT = NW * 64;
-  constexpr int NP = KT * CH / NT;
-  u32x4 qf[NS];
-  {
-    const uint16_t* qp = q + (size_t)(q0 + (row_valid ? my_row : 0)) * q_stride + head * HD;
-#pragma unroll
-    for (int s = 0; s < NS; ++s)
-      qf[s] = row_valid ? *reinterpret_cast<const u32x4*>(qp + 16 * s + 8 * hh) : u32x4{0, 0, 0, 0};
-    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): Q lands before any K/V load (see the DB kernel)
-  }
-
-  const int last_row = min(t0 + 32 * NW, qlen) - 1;
-  const int kv_end = min(ctx, pos_base + last_row + 1);
-  const int ntiles = (kv_end + KT - 1) / KT;
-
-  float m_run = -1e30f, l_run = 0.f;
-  f32x16 o[ND];
-#pragma unroll
-  for (int d = 0; d < ND; ++d)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
-
-  const size_t head_stride = (size_t)bs * HD;
-  u32x4 kr[NP], vr[NP];
-  // one operand (0 = K, 1 = V) of tile kb0 into registers: page16 fast path with wave-uniform
-  // block ids, or a per-lane block-table gather for partial tiles / other page sizes
-  constexpr int RP = NT / CH;
-  static_assert(RP % 16 == 0 && 16 % (64 / CH) == 0, "passes are whole pages");
-  const int wsub = __builtin_amdgcn_readfirstlane(w) * (64 / CH);
-  const int lane_off = ((wsub & 15) + lane / CH) * HD + (lane % CH) * 8;
-  const int wpage = wsub >> 4;
-  const bool page16 = bs_log2 == 4;
-  auto load = [&](int kb0, int which, u32x4 (&r)[NP]) {
-    const uint16_t* base_ptr = which ? v_cache : k_cache;
-    if (page16 && kb0 + KT <= kv_end) {
-#pragma unroll
-      for (int p = 0; p < NP; ++p) {
-        const int blk = bt[(kb0 >> 4) + p * (RP / 16) + wpage];
-        r[p] = *reinterpret_cast<const u32x4*>(base_ptr + ((size_t)blk * nkv + kvh) * head_stride + lane_off);
-      }
-    } else {
-#pragma unroll
-      for (int p = 0; p < NP; ++p) {
-        const int row = p * (NT / CH) + tid / CH;
-        const int ch = tid % CH;
-        const int key = min(kb0 + row, kv_end - 1);
-        const int blk = bt[key >> bs_log2];
-        r[p] = *reinterpret_cast<const u32x4*>(
-            base_ptr + ((size_t)blk * nkv + kvh) * head_stride + (size_t)(key & (bs - 1)) * HD + ch * 8);
-      }
-    }
-  };
-  auto store_k = [&](uint16_t* dst) {
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      const int row = p * (NT / CH) + tid / CH;
-      *reinterpret_cast<u32x4*>(dst + k_off<HD>(row, tid % CH)) = kr[p];
-    }
-  };
-  auto store_v = [&](uint16_t* dst) {
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      const int row = p * (NT / CH) + tid / CH;
-      *reinterpret_cast<u32x4*>(dst + v_off<HD>(row, tid % CH)) = vr[p];
-    }
-  };
-  auto kimg = [&](int i) { return lds + (i & 1) * KT * HD; };
-  auto vimg = [&](int i) { return lds + (2 + (i & 1)) * KT * HD; };
-
-  const int wave_last_pos = pos_base + min(t0 + 32 * w + 31, qlen - 1);
-  const int wave_first_pos = pos_base + t0 + 32 * w;
-  const bool wave_tree = tree_mask != nullptr && (t0 + 32 * w + 31 >= tree_first);
-  const bool wave_rows = t0 + 32 * w < qlen;
-  auto active = [&](int t) { return t < ntiles && wave_rows && t * KT <= wave_last_pos; };
-
-  f32x16 sc[2], sn[2];
-  auto qk = [&](const uint16_t* ks, f32x16 (&acc)[2]) {
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[kb][r] = 0.f;
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        const u32x4 a = *reinterpret_cast<const u32x4*>(ks + k_off<HD>(32 * kb + lr, 2 * s + hh));
-        acc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a), as_bf16x8(qf[s]), acc[kb], 0, 0, 0);
-      }
-    }
-  };
-
-  // ---- prologue: K(0), V(0) staged; K(1) staged after the first barrier; K(2), V(1) in registers
-  if (ntiles > 0) {
-    load(0, 0, kr);
-    load(0, 1, vr);
-    store_k(kimg(0));
-    store_v(vimg(0));
-    if (ntiles > 1) load(KT, 0, kr);
-  }
-  __syncthreads();
-  if (ntiles > 1) store_k(kimg(1));
-  if (ntiles > 2) load(2 * KT, 0, kr);
-  if (ntiles > 1) load(KT, 1, vr);
-  if (active(0)) qk(kimg(0), sc);
-
-  for (int it = 0; it < ntiles; ++it) {
-    __syncthreads();   // K(it+1), V(it) landed; S(it) and P.V(it-1) done by every wave
-    const int kb0 = it * KT;
-    if (it + 2 < ntiles) store_k(kimg(it));
-    if (it + 1 < ntiles) store_v(vimg(it + 1));
-    if (it + 3 < ntiles) load((it + 3) * KT, 0, kr);
-    if (it + 2 < ntiles) load((it + 2) * KT, 1, vr);
-    const bool act = active(it);
-    const bool nxt = active(it + 1);
-    // S(it+1) first: its MFMAs run in the matrix pipe while the softmax of tile it issues
-    if (nxt) qk(kimg(it + 1), sn);
-    if (act) {
-      const bool interior = (kb0 + KT <= kv_end) && (kb0 + KT - 1 <= wave_first_pos) && !wave_tree;
-      if (!interior) {
-        const int lim = row_valid ? min(my_pos, kv_end - 1) : -1;
-        const int key0 = kb0 + 4 * hh;
-        if (wave_tree) {
-#pragma unroll
-          for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int key = key0 + 32 * kb + (r & 3) + 8 * (r >> 2);
-              const int dt = key - tree_key0;
-              const bool tbit = (tmask >> (dt & 63)) & 1ull;
-              const bool ok = (key <= lim) & (!is_tree | (dt < 0) | tbit);
-              sc[kb][r] = ok ? sc[kb][r] : -__builtin_inff();
-            }
-        } else {
-#pragma unroll
-          for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-              sc[kb][r] = (key0 + 32 * kb + (r & 3) + 8 * (r >> 2) <= lim) ? sc[kb][r] : -__builtin_inff();
-        }
-      }
-      float mx = -1e30f;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[kb][r]);
-      mx = row_valid ? mx * scale_log2 : -1e30f;
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      if (__any(mx > m_run + 8.f)) {
-        const float m_new = fmaxf(m_run, mx);
-        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-        l_run *= alpha;
-#pragma unroll
-        for (int d = 0; d < ND; ++d) o[d] *= alpha;
-        m_run = m_new;
-      }
-      float ps[4];
-      {
-        const f32x2v s2 = {scale_log2, scale_log2};
-        const f32x2v n2 = {-m_run, -m_run};
-        f32x2v acc2[2] = {{0.f, 0.f}, {0.f, 0.f}};
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-          for (int r = 0; r < 16; r += 2) {
-            f32x2v x = {sc[kb][r], sc[kb][r + 1]};
-            x = x * s2 + n2;
-            x[0] = __builtin_amdgcn_exp2f(x[0]);
-            x[1] = __builtin_amdgcn_exp2f(x[1]);
-            sc[kb][r] = x[0];
-            sc[kb][r + 1] = x[1];
-            acc2[(r >> 1) & 1] += x;
-          }
-        ps[0] = acc2[0][0];
-        ps[1] = acc2[0][1];
-        ps[2] = acc2[1][0];
-        ps[3] = acc2[1][1];
-      }
-      float psum = (ps[0] + ps[1]) + (ps[2] + ps[3]);
-      psum += __shfl_xor(psum, 32, 64);
-      l_run += psum;
-      if (nxt) {
-        // spread the softmax VALU between S(t+1)'s 16 MFMAs (issued above in program order)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
-        }
-      }
-
-      // ---- O^T += V^T P^T
-      const uint16_t* vs = vimg(it);
-      const int g16 = lane >> 4;
-      const int idx = lane & 15;
-      const int tq = idx >> 2, tp = idx & 3;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          u32x4 pf;
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) pf[jj] = pack_bf16x2(sc[kb][8 * s2 + 2 * jj], sc[kb][8 * s2 + 2 * jj + 1]);
-#pragma unroll
-          for (int d = 0; d < ND; ++d) {
-            const int col = 32 * d + 16 * (g16 & 1) + 4 * tp;
-            const int r0 = 32 * kb + 16 * s2 + 4 * hh + tq;
-            short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (lds_short4*)(vs + v_off<HD>(r0, col >> 3) + (col & 7)));
-            short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (lds_short4*)(vs + v_off<HD>(r0 + 8, col >> 3) + (col & 7)));
-            u32x4 vf;
-            vf[0] = (uint32_t)(uint16_t)lo[0] | ((uint32_t)(uint16_t)lo[1] << 16);
-            vf[1] = (uint32_t)(uint16_t)lo[2] | ((uint32_t)(uint16_t)lo[3] << 16);
-            vf[2] = (uint32_t)(uint16_t)hi[0] | ((uint32_t)(uint16_t)hi[1] << 16);
-            vf[3] = (uint32_t)(uint16_t)hi[2] | ((uint32_t)(uint16_t)hi[3] << 16);
-            o[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(vf), as_bf16x8(pf), o[d], 0, 0, 0);
-          }
-        }
-    }
-    if (nxt) {
-      sc[0] = sn[0];
-      sc[1] = sn[1];
-    }
-  }
-
-  if (!row_valid) return;
-  const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
-  uint16_t* op = out + (size_t)(q0 + my_row) * out_stride + head * HD;
-#pragma unroll
-  for (int d = 0; d < ND; ++d)
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int dim = 32 * d + 8 * rr + 4 * hh;
-      uint2 v;
-      v.x = pack_bf16x2(o[d][4 * rr] * inv, o[d][4 * rr + 1] * inv);
-      v.y = pack_bf16x2(o[d][4 * rr + 2] * inv, o[d][4 * rr + 3] * inv);
-      *reinterpret_cast<uint2*>(op + dim) = v;
-    }
-}
-
 }  // namespace
 
 // tiles: int32 [n_tiles, 2] = (sequence index, first query row of the tile_rows-row tile)
@@ -661,7 +378,6 @@ extern "C" int dgi_paged_prefill(const void* q, int q_stride, const void* k_cach
   if ((1 << bs_log2) != block_size) return -4;
   const float scale_log2 = scale * 1.4426950408889634f;
   const int db = (tile_rows >> 16) & 1;          // bit 16: two LDS stages (prefill_attn_kernel DB)
-  const int pipe = (tile_rows >> 17) & 1;        // bit 17: software-pipelined S(t+1) (prefill_attn_pipe_kernel)
   tile_rows &= 0xffff;
   if (tile_rows != 128 && tile_rows != 256) return -7;
 #define DGI_PREFILL(HDV, NWV, DBV)                                                                     \
@@ -669,18 +385,6 @@ extern "C" int dgi_paged_prefill(const void* q, int q_stride, const void* k_cach
       (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables,     \
       bt_stride, cu_seqlens_q, context_lens, tiles, (uint16_t*)out, out_stride, nh, nkv, bs_log2,         \
       scale_log2, tree_mask, tree_n)
-  if (pipe) {
-#define DGI_PREFILL_PIPE(HDV, NWV)                                                                     \
-  prefill_attn_pipe_kernel<HDV, NWV><<<dim3(n_tiles, nh), NWV * 64, 0, s>>>(                           \
-      (const uint16_t*)q, q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables,     \
-      bt_stride, cu_seqlens_q, context_lens, tiles, (uint16_t*)out, out_stride, nh, nkv, bs_log2,         \
-      scale_log2, tree_mask, tree_n)
-    if (hd == 128) { if (tile_rows == 256) DGI_PREFILL_PIPE(128, 8); else DGI_PREFILL_PIPE(128, 4); }
-    else { if (tile_rows == 256) DGI_PREFILL_PIPE(64, 8); else DGI_PREFILL_PIPE(64, 4); }
-#undef DGI_PREFILL_PIPE
-    DGI_CHECK_LAUNCH();
-    return 0;
-  }
   if (hd == 128) {
     if (tile_rows == 256) { if (db) DGI_PREFILL(128, 8, 1); else DGI_PREFILL(128, 8, 0); }
     else { if (db) DGI_PREFILL(128, 4, 1); else DGI_PREFILL(128, 4, 0); }

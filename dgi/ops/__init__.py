@@ -313,8 +313,6 @@ def paged_prefill_ref(q, k_cache, v_cache, block_tables, cu_seqlens_q, context_l
 PREFILL_TILE = int(os.environ.get("DGI_PREFILL_TILE", "128"))
 # two LDS stages in the prefill attention kernel (one barrier per K/V tile); 0 = the round-4 loop
 PREFILL_DB = int(os.environ.get("DGI_PREFILL_DB", "1"))
-# software-pipelined prefill attention (S(t+1) MFMAs in flight during tile t's softmax); A/B switch
-PREFILL_PIPE = int(os.environ.get("DGI_PREFILL_PIPE", "0"))
 
 
 def order_prefill_tiles(cu_seqlens_q, context_lens=None, tile: int = 0) -> np.ndarray:
@@ -361,7 +359,7 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens,
             tiles = torch.tensor(tl if tl else [[0, 0]], dtype=torch.int32, device=q.device)[: len(tl)]
         _call("paged_prefill", out, q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens,
               tiles, nh, nkv, scale, tree_mask, tree_n,
-              PREFILL_TILE | ((PREFILL_DB & 1) << 16) | ((PREFILL_PIPE & 1) << 17))
+              PREFILL_TILE | ((PREFILL_DB & 1) << 16))
         return out
     r = paged_prefill_ref(q, k_cache, v_cache, block_tables, cu_seqlens_q, context_lens, nh, nkv, scale,
                           tree_mask, tree_n)

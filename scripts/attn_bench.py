@@ -52,7 +52,6 @@ def prefill(B, L):
     vd = torch.randn_like(kd)
     us_sdpa = timed(lambda: F.scaled_dot_product_attention(qd, kd, vd, is_causal=True))
     return {"kernel": "prefill", "B": B, "L": L, "tile": ops.PREFILL_TILE, "db": ops.PREFILL_DB,
-            "pipe": ops.PREFILL_PIPE,
             "order": os.environ.get("ATTN_TILE_ORDER", "1"), "us": round(us, 1),
             "TFLOPs": round(flops / us / 1e6, 1),
             "sdpa_us": round(us_sdpa, 1), "sdpa_TFLOPs": round(flops / us_sdpa / 1e6, 1)}
@@ -78,9 +77,8 @@ def decode(B, C):
 
 if __name__ == "__main__":
     for tile in [int(t) for t in os.environ.get("ATTN_TILES", "128").split(",")]:
-        for db, pipe in [(int(d), int(p)) for d in os.environ.get("ATTN_DB", str(ops.PREFILL_DB)).split(",")
-                         for p in os.environ.get("ATTN_PIPE", str(ops.PREFILL_PIPE)).split(",")]:
-            ops.PREFILL_TILE, ops.PREFILL_DB, ops.PREFILL_PIPE = tile, db, pipe
+        for db in [int(d) for d in os.environ.get("ATTN_DB", str(ops.PREFILL_DB)).split(",")]:
+            ops.PREFILL_TILE, ops.PREFILL_DB = tile, db
             for B, L in [(1, 512), (3, 512), (8, 512), (4, 2048), (1, 8192)]:
                 print(json.dumps(prefill(B, L)), flush=True)
     if os.environ.get("ATTN_PREFILL_ONLY"):

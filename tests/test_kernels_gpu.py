@@ -137,11 +137,10 @@ def _paged_decode_case(nh, nkv, hd, ctx_lens, bs=16):
                                        (14, 2, 64)])
 @pytest.mark.parametrize("qlens,ctxs", [([5], [5]), ([130, 1, 64], [130, 40, 600]), ([512], [512]),
                                         ([300, 77], [1000, 77])])
-@pytest.mark.parametrize("tile,db,pipe", [(128, 1, 0), (128, 0, 0), (256, 1, 0), (128, 1, 1), (256, 1, 1)])
-def test_paged_prefill(nh, nkv, hd, qlens, ctxs, tile, db, pipe, monkeypatch):
+@pytest.mark.parametrize("tile,db", [(128, 1), (128, 0), (256, 1)])
+def test_paged_prefill(nh, nkv, hd, qlens, ctxs, tile, db, monkeypatch):
     monkeypatch.setattr(ops, "PREFILL_TILE", tile)
     monkeypatch.setattr(ops, "PREFILL_DB", db)
-    monkeypatch.setattr(ops, "PREFILL_PIPE", pipe)
     bs = 16
     maxw = 80
     nblocks = sum((c + bs - 1) // bs for c in ctxs) + 4
@@ -157,9 +156,7 @@ def test_paged_prefill(nh, nkv, hd, qlens, ctxs, tile, db, pipe, monkeypatch):
     torch.testing.assert_close(out.float(), ref.float(), atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("pipe", [0, 1])
-def test_paged_prefill_tree_mask(pipe, monkeypatch):
-    monkeypatch.setattr(ops, "PREFILL_PIPE", pipe)
+def test_paged_prefill_tree_mask():
     nh, nkv, hd, bs = 32, 8, 128, 16
     # 2 sequences with cached prefixes 40 / 100 and a 7-node draft tree each
     par = torch.tensor([[-1, 0, 0, 1, 1, 2, 3], [-1, 0, 1, 1, 0, 4, 5]], dtype=torch.int32)
