@@ -64,11 +64,15 @@ TBO_MIN_ROWS = int(os.environ.get("DGI_TBO_MIN_ROWS", "512"))
 # qkv / gate_up weights once (``fold_norms``), the o-proj and down GEMMs add into the residual
 # stream in their epilogue and emit its per-row sums of squares, and the qkv / gate_up GEMMs
 # scale their rows by the resulting rstd — no norm kernel and no normalised copy of the stream
-# between the four projections (dgi/csrc/mfma_gemm.hip EPI 2-5).  "1" (default) / "force": every
-# eligible step of >= NORM_FOLD_MIN_ROWS rows — measured faster on the 512-row decode-role step
-# (77.6 vs 78.5 ms) and on the headline's mixed steps (profiles/r6_norm/); "table": only where the
-# GEMM routing table (timed on one warm weight) prices the all-MFMA layer at least as fast as the
-# best mix plus the norm kernels; "0": off.  Smaller steps keep the skinny / fused-decode kernels.
+# between the four projections (dgi/csrc/mfma_gemm.hip EPI 2-5).  "1" (default): every eligible
+# step of >= NORM_FOLD_MIN_ROWS rows of a model the engine routes GEMMs for (a shipped or measured
+# routing table: the production shapes) — measured faster on the 512-row decode-role step (77.6 vs
+# 78.5 ms) and on the headline's mixed steps (profiles/r6_norm/); "force": every eligible step of
+# any model; "table": only where the routing table (timed on one warm weight) prices the all-MFMA
+# layer at least as fast as the best mix plus the norm kernels; "0": off.  Smaller steps keep the
+# skinny / fused-decode kernels.  (The fused layers round differently from the unfused ones — no
+# normalised bf16 copy of the stream — so a model whose steps switch between the two computes
+# near-tied greedy tokens batch-dependently; test-size engines without a routing table stay unfused.)
 NORM_FOLD = os.environ.get("DGI_NORM_FOLD", "1")
 NORM_FOLD_MIN_ROWS = int(os.environ.get("DGI_NORM_FOLD_MIN_ROWS", "256"))
 # fused-norm layers: RoPE + the paged-KV write in the qkv GEMM's epilogue (EPI 5) where the geometry
@@ -461,9 +465,11 @@ class LlamaModel:
                                          and (L.gate_up.shape[0] // 2) % 128 == 0)
         if not ok:
             return False
-        if NORM_FOLD in ("1", "force"):
+        if NORM_FOLD == "force":
             return True
-        return NORM_FOLD == "table" and self.fold_impl is not None and bool(self.fold_impl(T))
+        if self.fold_impl is None:
+            return False
+        return NORM_FOLD == "1" or (NORM_FOLD == "table" and bool(self.fold_impl(T)))
 
     def _forward_layers_folded(self, h: torch.Tensor, meta: AttnMeta, residual: Optional[torch.Tensor],
                                trim_last: Optional[torch.Tensor]):
