@@ -184,10 +184,12 @@ class LLMEngine:
                 self.model.fold_impl = lambda rows, _t=self.mlp_pad_table: _t.fold(rows, H)
                 self.mlp_pad_seconds = time.perf_counter() - t1
         # the fused-norm layers need the gains folded into the weights; done once, eagerly, so every
-        # engine sharing this model (and every captured graph) computes with the same weights
+        # engine sharing this model (and every captured graph) computes with the same weights — for
+        # the models that will run them (dgi.models.llama.NORM_FOLD: routed production shapes by
+        # default); other models keep their weights bit for bit
         if self.device.type == "cuda" and hasattr(self.model, "fold_norms"):
             from dgi.models import llama as _llama
-            if _llama.NORM_FOLD != "0":
+            if _llama.NORM_FOLD == "force" or (_llama.NORM_FOLD in ("1", "table") and self.mlp_pad_table is not None):
                 self.model.fold_norms()
 
     # ------------------------------------------------------------------ API
