@@ -36,7 +36,6 @@
 // on load and skipped on store.
 #include "common.h"
 
-#include <cstdlib>
 #include <type_traits>
 
 using namespace dgi;
@@ -162,7 +161,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[8][4], uint16_t* __r
 // Every wave of the block must call it (one barrier).
 __device__ __forceinline__ void epilogue_res(const f32x4 (&acc)[8][4], uint16_t* __restrict__ Y, int ldy, int M,
                                              int m0, int tn, int wm, int wn, int lane, float* ssl,
-                                             float* __restrict__ ss, int ss_ld, int dbg) {
+                                             float* __restrict__ ss, int ss_ld) {
   const int r16 = lane & 15;
   const int g = lane >> 4;
   const int cbase = tn * 256 + wn * 64 + 16 * (g & 1) + 4 * (g & 2);
@@ -176,7 +175,7 @@ __device__ __forceinline__ void epilogue_res(const f32x4 (&acc)[8][4], uint16_t*
       const int m = m0 + wm * 128 + (i0 + ii) * 16 + r16;
       const uint16_t* yrow = Y + (size_t)min(m, M - 1) * ldy + cbase;
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj) old[ii][jj] = (dbg & 4) ? uint4{0, 0, 0, 0} : *(const uint4*)(yrow + jj * 32);
+      for (int jj = 0; jj < 2; ++jj) old[ii][jj] = *(const uint4*)(yrow + jj * 32);
     }
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii) {
@@ -209,7 +208,6 @@ __device__ __forceinline__ void epilogue_res(const f32x4 (&acc)[8][4], uint16_t*
       if (g == 0) ssl[wn * 256 + wm * 128 + i * 16 + r16] = part;
     }
   }
-  if (dbg & 2) return;
   __syncthreads();
   const int t = threadIdx.x;
   if (t < 256 && m0 + t < M)
@@ -684,8 +682,6 @@ struct PPArgs {
   float* ss;                  // EPI 2: per-row partial sums of squares out; EPI 3 / 4: in
   int ss_ld;                  // row stride of ss (EPI 2: its column is the N tile; EPI 3 / 4: partials per row)
   float inv_k, eps;           // EPI 3 / 4: rstd = rsqrt(sum * inv_k + eps)
-  int dbg;                    // diagnostics (DGI_NORM_GEMM_DBG): 1 = no row statistics read (rstd 1),
-                              // 2 = residual epilogue without the statistics, 4 = without the residual read
   // EPI 5: RoPE table [positions, 128] (64 cos | 64 sin), per-row positions / cache slots, caches
   // [blocks, nkv, bs, 128], q / kv column counts
   const int* pos;
@@ -1018,7 +1014,7 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
       // two lanes per row, each summing half of its partials (float4 loads, all in flight
       // together: ss_ld % 8 == 0, <= 32), then one exchange — a fixed order on every run
       const int m = min(tm * kBM + (t >> 1), M - 1);
-      const int per = (a.dbg & 1) ? 0 : a.ss_ld >> 3;
+      const int per = a.ss_ld >> 3;
       const f32x4* sp = (const f32x4*)(a.ss + (size_t)m * a.ss_ld) + (t & 1) * per;
       f32x4 v[4];
 #pragma unroll
@@ -1163,7 +1159,7 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
                const int te = fresh_tid();
                if constexpr (EpiKind<EPI>::res)
                  epilogue_res(acc, a.Y, a.ldy, M, tm * kBM, tn, (te >> 8) & 1, (te >> 6) & 3, te & 63, ep_lds, a.ss,
-                              a.ss_ld, a.dbg);
+                              a.ss_ld);
                else if constexpr (EpiKind<EPI>::rope)
                  epilogue_rope(acc, a, tm * kBM, tn, (te >> 8) & 1, (te >> 6) & 3, te & 63, ep_lds + rs_slot * 256,
                                (uint16_t*)smem);
@@ -1218,7 +1214,6 @@ struct NormArgs {
   float* ss = nullptr;
   int ss_ld = 0;
   float inv_k = 0.f, eps = 0.f;
-  int dbg = 0;
   const int* pos = nullptr;
   const float* cs = nullptr;
   const int* slots = nullptr;
@@ -1243,7 +1238,7 @@ void launch_pp(const void* x, int ldx, const void* w, void* y, int ldy, int M, i
   // EPI 2 reads the tile it stores (in place) and EPI 5 stages its tile through the staging LDS: no
   // overlap of the next tile's loads with their epilogues
   PPArgs a{(const uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, nullptr, nullptr, ldx, ldy, M, I, K, tiles_m, total,
-           0, 0, 0, 0, !(prio & 8) && EPI != 2 && EPI != 5, na.ss, na.ss_ld, na.inv_k, na.eps, na.dbg,
+           0, 0, 0, 0, !(prio & 8) && EPI != 2 && EPI != 5, na.ss, na.ss_ld, na.inv_k, na.eps,
            na.pos, na.cs, na.slots, na.kc, na.vc, na.qcols, na.kvcols, na.nkv, na.bs};
   const int nt = K / kBK;
   SkWorkspace* sk = ((skmode || a.ovl) && nt >= 8) ? sk_workspace(s) : nullptr;
@@ -1312,11 +1307,6 @@ extern "C" int dgi_mfma_gemm_norm(const void* x, int ldx, const void* w, void* y
   const int tiles_m = (M + kBM - 1) / kBM;
   const int total = tiles_m * tiles_n;
   NormArgs na;
-  static const int dbg = [] {
-    const char* e = getenv("DGI_NORM_GEMM_DBG");
-    return e ? atoi(e) : 0;
-  }();
-  na.dbg = dbg;
   na.ss = ss;
   na.ss_ld = ss_ld;
   na.inv_k = inv_k;

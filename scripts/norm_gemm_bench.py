@@ -3,8 +3,8 @@
 projection shapes: qkv / gate_up with the rstd epilogue vs plain (and hipBLASLt), o / down with the
 residual + row-statistics epilogue vs plain, plus the RMSNorm kernels the fusion removes.
 hipGraph-timed, 20 launches per replay, weights rotated through a set larger than the MALL (decode
-weights arrive cold).  One JSON line per (projection, M).  DGI_NORM_GEMM_DBG (read by the kernel
-library at load) switches parts of the fused epilogues off for diagnosis."""
+weights arrive cold).  One JSON line per (projection, M).  (The r6s7 diagnosis runs that switched
+parts of the fused epilogues off used a DGI_NORM_GEMM_DBG kernel knob since removed: commit 7b6799a has it.)"""
 import json
 import os
 import sys
@@ -77,7 +77,6 @@ def main():
                     row[k.replace("_us", "_pf")] = round(fl / row[k] / 1e9, 3)
                 if k.endswith("_us"):
                     row[k] = round(row[k], 2)
-            row["dbg"] = os.environ.get("DGI_NORM_GEMM_DBG", "0")
             print(json.dumps(row), flush=True)
         del ws
         torch.cuda.empty_cache()
