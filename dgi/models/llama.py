@@ -105,6 +105,19 @@ class TboStreams:
 
 _TBO_STREAMS: dict = {}
 
+def fold_decision(mode: str, rows: int, fold_impl) -> bool:
+    """Whether a GPU step of ``rows`` rows runs the fused-norm layers under ``DGI_NORM_FOLD`` =
+    ``mode`` (shape eligibility aside): ``fold_impl`` is the model's routing-table rule (None when
+    the engine routes no GEMMs for it, e.g. test-size models)."""
+    if mode == "0" or rows < NORM_FOLD_MIN_ROWS:
+        return False
+    if mode == "force":
+        return True
+    if fold_impl is None:
+        return False
+    return mode == "1" or (mode == "table" and bool(fold_impl(rows)))
+
+
 def _ss_cols(hidden: int) -> int:
     """Columns of the fused-norm row statistics: one partial per 256-column tile of the stream,
     padded to a multiple of 8 (the consumer's vector loads; the pad columns stay zero)."""
@@ -465,11 +478,7 @@ class LlamaModel:
                                          and (L.gate_up.shape[0] // 2) % 128 == 0)
         if not ok:
             return False
-        if NORM_FOLD == "force":
-            return True
-        if self.fold_impl is None:
-            return False
-        return NORM_FOLD == "1" or (NORM_FOLD == "table" and bool(self.fold_impl(T)))
+        return fold_decision(NORM_FOLD, T, self.fold_impl)
 
     def _forward_layers_folded(self, h: torch.Tensor, meta: AttnMeta, residual: Optional[torch.Tensor],
                                trim_last: Optional[torch.Tensor]):

@@ -34,3 +34,24 @@ def test_load_tuned_refuses_another_device(tmp_path, monkeypatch):
             json.dump(dd, f)
         t = gemm_pad.load_tuned(d["key"], m_max)
         assert (t is not None) == ok, tag
+
+
+
+def test_fused_norm_decision_modes(monkeypatch):
+    """DGI_NORM_FOLD modes: "1" folds on every step of >= the row floor of a routed model (one with
+    a GEMM routing table), "table" only where the table prices the fused layer at least as fast,
+    "force" on any model, "0" never; steps below the floor never fold."""
+    from dgi.models import llama
+    from dgi.runtime.gemm_pad import MlpPadTable
+    monkeypatch.setattr(llama, "NORM_FOLD_MIN_ROWS", 256)
+    grid = [256, 512, 1024]
+    raw = [dict(front=1.0, front_mfma=1.0, back=1.0, back_mfma=1.0, pq_blas=1.0, pq_mfma=1.0, po_blas=1.0,
+                po_mfma=1.0) for _ in grid]
+    raw[2]["front_mfma"] = 2.0                      # at 1,024 rows the all-MFMA layer loses by 1 ms
+    t = MlpPadTable.decide(grid, raw, 32)
+    rule = lambda rows: t.fold(rows, 1024)          # noqa: E731
+    d = llama.fold_decision
+    assert d("1", 300, rule) and d("1", 1000, rule) and not d("1", 300, None) and not d("1", 100, rule)
+    assert d("table", 300, rule) and not d("table", 1000, rule) and not d("table", 300, None)
+    assert d("force", 300, None) and not d("force", 100, None)
+    assert not d("0", 300, rule)
