@@ -620,53 +620,53 @@ class _StepGraph:
         for i, blk in enumerate(brows):
             bt[i, :len(blk)] = blk
 
-        def slot_of(i, p):
-            if i >= R:
-                return p % bs                              # scratch page 0
-            return bt[i, p // bs].astype(np.int64) * bs + p % bs
-        # catch-up: rows p0 .. p0 + C - 1 (valid: the first nv), context p0 + C
+        live = np.arange(R)[:, None]
+        n_l = np.asarray(n_vec[:R], dtype=np.int64)[:, None]
+
+        def slots(P):                                      # slots of live rows' positions P [R, k]
+            return bt[live, P // bs].astype(np.int64) * bs + P % bs
+        # catch-up: rows p0 .. p0 + C - 1 (valid: the first nv), context p0 + C; padding rows
+        # (past nv, or past the live batch) write scratch slots on page 0
         o = self.o_c
         cpos = h[o:o + Rb * C].reshape(Rb, C)
         cslot = h[o + Rb * C:o + 2 * Rb * C].reshape(Rb, C)
         cctx = h[o + 2 * Rb * C:o + 2 * Rb * C + Rb]
         clast = h[o + 2 * Rb * C + Rb:o + 2 * Rb * C + 2 * Rb]
         kk = np.arange(C)
-        for i in range(Rb):
-            p0 = int(p0_vec[i]) if i < R else 0
-            nv = int(nv_vec[i]) if i < R else 1
-            ps = p0 + kk
-            cpos[i] = ps
-            sl = slot_of(i, ps) if i < R else ps % bs
-            if i < R:
-                sl = np.where(kk < nv, sl, kk % bs)        # padding rows write scratch slots
-            cslot[i] = sl
-            cctx[i] = p0 + C
-            clast[i] = nv - 1
+        p0 = np.zeros(Rb, dtype=np.int64)
+        nv = np.ones(Rb, dtype=np.int64)
+        p0[:R] = np.asarray(p0_vec[:R], dtype=np.int64)
+        nv[:R] = np.asarray(nv_vec[:R], dtype=np.int64)
+        cpos[:] = p0[:, None] + kk
+        cslot[:] = kk % bs
+        if R:
+            cslot[:R] = np.where(kk < nv[:R, None], slots(cpos[:R].astype(np.int64)), kk % bs)
+        cctx[:] = p0 + C
+        clast[:] = nv - 1
         # draft depths 2..D: chunk nodes at positions n - 1 + depth, slots n .. n + m - 1
         for off, m, *_ in self.lv:
             dp = h[off:off + Rb * m].reshape(Rb, m)
             dsl = h[off + Rb * m:off + 2 * Rb * m].reshape(Rb, m)
             dctx = h[off + 2 * Rb * m:off + 2 * Rb * m + Rb]
-            for i in range(Rb):
-                n = int(n_vec[i]) if i < R else 1
-                dp[i] = n - 1 + self.depth_np[1:m + 1]
-                dsl[i] = slot_of(i, n + np.arange(m)) if i < R else np.arange(m) % bs
-                dctx[i] = n + m
+            n = np.ones(Rb, dtype=np.int64)
+            n[:R] = n_l[:, 0]
+            dp[:] = n[:, None] - 1 + self.depth_np[1:m + 1]
+            dsl[:] = np.arange(m) % bs
+            if R:
+                dsl[:R] = slots(n_l + np.arange(m))
+            dctx[:] = n + m
         # verify: node k at position n - 1 + depth(k), slot n - 1 + k, context n - 1 + N
         o = self.o_v
         vp = h[o:o + Rb * N].reshape(Rb, N)
         vsl = h[o + Rb * N:o + 2 * Rb * N].reshape(Rb, N)
         vctx = h[o + 2 * Rb * N:o + 2 * Rb * N + Rb]
-        for i in range(Rb):
-            if i < R:
-                n = int(n_vec[i])
-                vp[i] = n - 1 + self.depth_np
-                vsl[i] = slot_of(i, n - 1 + np.arange(N))
-                vctx[i] = n - 1 + N
-            else:
-                vp[i] = np.arange(N)
-                vsl[i] = np.arange(N) % bs
-                vctx[i] = N
+        vp[:] = np.arange(N)
+        vsl[:] = np.arange(N) % bs
+        vctx[:] = N
+        if R:
+            vp[:R] = n_l - 1 + self.depth_np
+            vsl[:R] = slots(n_l - 1 + np.arange(N))
+            vctx[:R] = n_l[:, 0] - 1 + N
 
     # ---------------------------------------------------------------- the step
     def _body(self):
@@ -752,6 +752,15 @@ class _StepGraph:
         self.graph.replay()
         acc, toks, fkeep = self.out
         return acc[:R], toks[:R], fkeep[:R]
+
+
+def _token_range(r, a: int, b: int) -> list:
+    """``r.all_tokens()[a:b]`` without building the whole prompt + output list (a catch-up
+    window is a few tokens at the end of a possibly long context)."""
+    P = len(r.prompt)
+    if a >= P:
+        return r.output[a - P:b - P]
+    return r.prompt[a:b] + (r.output[:b - P] if b > P else [])
 
 
 class SpecEngine(LLMEngine):
@@ -1267,7 +1276,7 @@ class SpecEngine(LLMEngine):
         if any(r.params.temperature > 0 for r in reqs):
             samp = self._node_sampling_host(reqs, sg.depth_np)
         acc, toks, fkeep = sg.run([x[2] for x in rows], [x[3] for x in rows], [r.blocks for r in reqs],
-                                  [x[4] for x in rows], [r.all_tokens()[x[3]:x[2]] for x, r in zip(rows, reqs)],
+                                  [x[4] for x in rows], [_token_range(r, x[3], x[2]) for x, r in zip(rows, reqs)],
                                   [x[5] for x in rows], samp)
         hs = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in (acc, toks)]
         for h_, t in zip(hs, (acc, toks)):
