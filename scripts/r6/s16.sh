@@ -1,0 +1,22 @@
+#!/bin/bash
+# Round 6, session 16: validation of the tree after the last kernel edits (diagnostic knob removed,
+# fold rule refactor): the whole GPU suite, smoke, the 1-GPU headline, 8B decode latency at batch
+# 1 / 4 / 16, the 512-row decode step.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r6s16
+mkdir -p $O
+export HSA_ENABLE_IPC_MODE_LEGACY=0 PYTHONUNBUFFERED=1
+step() {  # name, timeout, command...
+  local name=$1 to=$2; shift 2
+  timeout -k 10 "$to" "$@" > "$O/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"; tail -2 "$O/$name.log" | cut -c1-500
+  if [ $rc -ne 0 ]; then exit $rc; fi
+}
+step gpu_suite 900 python -u -m pytest tests -q -m gpu --timeout 300 --timeout-method thread
+step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
+step bench70b 600 python -u bench.py --steps 20 --warmup 5 --json-out $O/bench70b.json
+step declat8b 600 python -u scripts/decode_latency.py --batch 1 4 16 --out $O/declat8b.json
+step dec80_512 400 python -u scripts/decode_stage_prof.py --layers 80 --rows 512 --ctx 576 --steps 30 --out $O/dec80_512.jsonl
+echo ALLDONE
