@@ -57,11 +57,15 @@ def main():
     ap.add_argument("--random-seqs", type=int, default=192)
     ap.add_argument("--repeats", type=int, default=3, help="timed runs per measurement (median)")
     ap.add_argument("--oracle-accept", type=float, nargs="*", default=[0.6, 0.8, 1.0])
-    ap.add_argument("--target", default="random", choices=["random", "peaked"],
+    ap.add_argument("--target", default="random", choices=["random", "peaked", "concentrated"],
                     help="random: plain random init (near-flat logits: greedy choices sit on bf16 near-ties, so "
                          "kernel-order noise flips them and acceptance collapses); peaked: the LM head is a "
                          "permuted copy of the embedding / sqrt(H), so the next token is a confident function "
-                         "of the current one, like a trained model's top-1 margins (same FLOPs and shapes)")
+                         "of the current one, like a trained model's top-1 margins (same FLOPs and shapes); "
+                         "concentrated: as peaked, but every next token is one of --hot-size ids (a random "
+                         "map of the vocabulary into that set, a permutation on it), as natural text "
+                         "concentrates on its frequent tokens: what an EAGLE-3 draft vocabulary relies on")
+    ap.add_argument("--hot-size", type=int, default=32768, help="ids the concentrated target emits")
     ap.add_argument("--no-verify-graph", action="store_true", help="eager verify pass (A/B for the hipGraph)")
     ap.add_argument("--staged", action="store_true",
                     help="separate draft / verify graphs with host-side compaction (A/B for the whole-step graph)")
@@ -86,6 +90,19 @@ def main():
         m = spec.model
         perm = torch.randperm(m.embed.shape[0], generator=torch.Generator().manual_seed(7)).to(m.embed.device)
         m.lm_head.copy_(m.embed.index_select(0, perm) / m.cfg.hidden_size ** 0.5)
+    elif a.target == "concentrated":
+        # next(cur) = f(cur), f: V -> S (|S| = hot_size), a permutation on S: head row j is the sum of the
+        # embeddings of j's preimages (~V / |S| of them), rows outside S are zero
+        m = spec.model
+        V = m.embed.shape[0]
+        gen = torch.Generator().manual_seed(7)
+        hot = torch.randperm(V, generator=gen)[:a.hot_size]
+        f = hot[torch.randint(0, a.hot_size, (V,), generator=gen)]
+        f[hot] = hot[torch.randperm(a.hot_size, generator=gen)]
+        head = torch.zeros(m.lm_head.shape, dtype=torch.float32, device=m.lm_head.device)
+        head.index_add_(0, f.to(head.device), m.embed.float())
+        m.lm_head.copy_(head / m.cfg.hidden_size ** 0.5)
+        del head
     t0 = time.perf_counter()
     if a.load_draft:
         blob = torch.load(a.load_draft, map_location=spec.device, weights_only=True)
