@@ -663,19 +663,28 @@ __global__ __launch_bounds__(512) void mfma_gemm_ring_kernel(const uint16_t* __r
 // blocks of one XCD (consecutive g) work on neighbouring tiles over the SAME K
 // range and share their X / W slabs in L2 (a stream-K split, whose pieces start
 // at staggered K offsets, measured slower for that reason); every block then
-// owns `full` whole tiles.  Each piece stores its fp32 partial tile to its
-// block's workspace slab with write-through (sc1) stores, publishes it (every wave
-// drains its stores, then one relaxed counter increment; no release fence, which
-// would write back the whole L2), and the last piece to arrive for a tile acquires, sums
-// every slab in piece order (deterministic) and writes the bf16 tile (and
-// resets the counter for the next launch).  No block waits for another, so
-// the protocol holds for any block placement or dispatch order.
+// owns `full` whole tiles.  A piece that finishes its K range takes an arrival
+// ticket (one relaxed counter add).  Every piece but the last to arrive stores its
+// fp32 partial tile to its block's workspace slab with write-through (sc1) stores and
+// publishes it (every wave drains its stores, then a relaxed add on the tile's
+// "written" counter; no release fence, which would write back the whole L2).  The
+// last piece waits until the others' slabs are written, acquires, folds every
+// piece's partial in piece order (s_0 + s_1 + ..: deterministic whichever piece
+// arrived last), writes the bf16 tile and resets both counters for the next launch.
+// Pieces 0 and 1 keep their own partial in registers (s_0 + s_1 == s_1 + s_0 in
+// IEEE arithmetic, so it enters the fold at its place); a later piece stores its
+// slab too (a prefix register set spills).  The wait cannot deadlock for any block placement or dispatch
+// order: every piece it waits for has already taken its ticket, so it is resident
+// and has only its slab store left.  The wait is bounded (a broken counter ends as
+// a wrong tile, not a hung GPU).  This saves the last piece's slab store and one slab
+// read on the tile's critical path (pp_split_probe: the split-K round trip cost
+// ~30 us per GEMM at the decode role's 512 rows).
 struct PPArgs {
   const uint16_t* X;
   const uint16_t* W;
   uint16_t* Y;
   float* ws;     // one 256 x 256 fp32 slab per block (hybrid launches)
-  int* cnt;      // one arrival counter per split tile, zero between launches
+  int* cnt;      // per split tile: arrivals at [t], slabs written at [P + t]; zero between launches
   int ldx, ldy, M, I, K, tiles_m, tiles_total;
   int rem, splits, full, P;   // P == 0: one tile per block (grid = tiles)
   int ovl;                    // issue the next tile's prologue before the current epilogue
@@ -770,15 +779,16 @@ constexpr int kSc1 = 16;
 // The work items of one block (see "Work decomposition" above): its one tile
 // (P == 0), its split-K piece, then its whole tiles.  prologue(tm, tn, kb) issues the
 // staging loads of output tile (tm, tn) from K tile kb on, body(tm, tn, kb, L, ov) accumulates
-// L K tiles into the caller's registers; slab_store(store16) / slab_add(load16, first) move them to /
-// from a 256 x 256 fp32 slab through store16(e, v) / load16(e) (16-byte element e of
-// this thread; NT threads interleaved by 16 bytes); epi stores the bf16 tile.  With a.ovl,
+// L K tiles into the caller's registers; slab_store(store16) moves them to a 256 x 256 fp32 slab
+// through store16(e, v) (16-byte element e of this thread; NT threads interleaved by 16 bytes),
+// slab_sum(load16, own, n) folds the n pieces' slabs (load16(piece, e)) in piece order into them,
+// they being piece own; epi stores the bf16 tile.  With a.ovl,
 // the next whole tile's prologue is issued before the current whole tile's epilogue
 // (which does not touch LDS: the body ends with every LDS read retired), so its first
 // K tiles load while the stores drain.
-template <int NT, class Pro, class Body, class Store, class Add, class Epi>
+template <int NT, class Pro, class Body, class Store, class Sum, class Epi>
 __device__ __forceinline__ void drive(const PPArgs& a, char* smem, Pro&& prologue, Body&& body, Store&& slab_store,
-                                      Add&& slab_add, Epi&& epi) {
+                                      Sum&& slab_sum, Epi&& epi) {
   const int tid = threadIdx.x;
   const int nt = a.K / kBK;
   const int nt2 = nt >> 1;                    // 128-deep units per tile
@@ -822,42 +832,51 @@ __device__ __forceinline__ void drive(const PPArgs& a, char* smem, Pro&& prologu
     bool store = true;
     if (cur.piece) {
       const int t = cur.t;
+      const int own = g / a.rem;                // this block's piece of tile t
       // slab offsets from a laundered thread id: otherwise hipcc hoists every per-lane
       // address out of the work-item loop and spills them
       int lt = tid;
       asm volatile("" : "+v"(lt));
       const int lo = lt * 16;
-      // publish: write-through (sc1) 16-byte stores drained by every wave, then one relaxed
-      // counter add — no release fence (an agent release writes back the whole L2)
-      const __amdgpu_buffer_rsrc_t rs =
-          __builtin_amdgcn_make_buffer_rsrc((void*)(a.ws + (size_t)g * 65536), 0, 65536 * 4, kRsrcWord3);
-      slab_store([&](int e, const f32x4& v) {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, e * NT * 16 + lo, 0, kSc1);
-      });
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
       if (tid == 0) {
         const int old = __hip_atomic_fetch_add(a.cnt + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = old == a.splits - 1;
-        if (last) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __hip_atomic_store(a.cnt + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        *(volatile int*)smem = last;
+        *(volatile int*)smem = old == a.splits - 1;
       }
       __syncthreads();
       store = *(volatile int*)smem;
       __syncthreads();          // flag read by every wave before the next item's staging overwrites it
+      // every piece but the last stores its slab; so does a last piece past the second (its
+      // registers cannot enter the fold without a prefix register set)
+      if (!store || own >= 2) {
+        // publish: write-through (sc1) 16-byte stores drained by every wave, then one relaxed
+        // counter add — no release fence (an agent release writes back the whole L2)
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(a.ws + (size_t)g * 65536), 0, 65536 * 4, kRsrcWord3);
+        slab_store([&](int e, const f32x4& v) {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, e * NT * 16 + lo, 0, kSc1);
+        });
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0 && !store)
+          __hip_atomic_fetch_add(a.cnt + a.P + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       if (store) {
-        // every slab, own included, in piece order: the sum does not depend on which piece arrived last
-        for (int jj = 0; jj < a.splits; ++jj) {
+        if (tid == 0) {
+          for (int spin = 0; spin < (1 << 22); ++spin) {
+            if (__hip_atomic_load(a.cnt + a.P + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.splits - 1) break;
+            __builtin_amdgcn_s_sleep(2);
+          }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_store(a.cnt + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(a.cnt + a.P + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        slab_sum([&](int jj, int e) {
           const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
               (void*)(a.ws + (size_t)(jj * a.rem + t) * 65536), 0, 65536 * 4, kRsrcWord3);
-          slab_add([&](int e) {
-            return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rl, e * NT * 16 + lo, 0, 0));
-          }, jj == 0);
-        }
+          return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rl, e * NT * 16 + lo, 0, 0));
+        }, own >= 2 ? -1 : own, a.splits);
         // a real s_waitcnt (not inline asm) so that the waitcnt pass knows the accumulators are
         // written: otherwise it merges this path's pending loads into the epilogue as vmcnt(0)
         __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
@@ -1132,27 +1151,31 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
 #pragma unroll
                  for (int j = 0; j < 4; ++j) store16(i * 4 + j, acc[i][j]);
              },
-             [&](auto&& load16, bool first) {
-               if (first) {
+             [&](auto&& load16, int own, int n) {
+               // the left fold s_0 + s_1 + .. of every piece in order; with own 0 / 1 the registers are
+               // s_own (x + y == y + x exactly: s_0 + s_1 == s_1 + s_0), with own < 0 every slab is read.
+               // 16 loads in flight per batch (a load-add pair per element serialises on vmcnt(0); the
+               // fragment registers are free here).  A prefix register set for own >= 2 spills (hipcc).
+               if (own < 0) {
 #pragma unroll
                  for (int i = 0; i < 8; ++i)
 #pragma unroll
-                   for (int j = 0; j < 4; ++j) acc[i][j] = load16(i * 4 + j);
-                 return;
+                   for (int j = 0; j < 4; ++j) acc[i][j] = load16(0, i * 4 + j);
                }
-               // 16 loads in flight per batch (a load-add pair per element serialises on vmcnt(0);
-               // the fragment registers are free here)
+               for (int jj = own == 1 ? 0 : 1; jj < n; ++jj) {
+                 if (jj == own) continue;
 #pragma unroll
-               for (int i0 = 0; i0 < 8; i0 += 4) {
-                 f32x4 v[4][4];
+                 for (int i0 = 0; i0 < 8; i0 += 4) {
+                   f32x4 v[4][4];
 #pragma unroll
-                 for (int i = 0; i < 4; ++i)
+                   for (int i = 0; i < 4; ++i)
 #pragma unroll
-                   for (int j = 0; j < 4; ++j) v[i][j] = load16((i0 + i) * 4 + j);
+                     for (int j = 0; j < 4; ++j) v[i][j] = load16(jj, (i0 + i) * 4 + j);
 #pragma unroll
-                 for (int i = 0; i < 4; ++i)
+                   for (int i = 0; i < 4; ++i)
 #pragma unroll
-                   for (int j = 0; j < 4; ++j) acc[i0 + i][j] += v[i][j];
+                     for (int j = 0; j < 4; ++j) acc[i0 + i][j] += v[i][j];
+                 }
                }
              },
              [&](int tm, int tn) {
@@ -1169,7 +1192,7 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
              });
 }
 
-// Per-device split-K workspace (one fp32 slab per block + one counter per tile),
+// Per-device split-K workspace (one fp32 slab per block + two counters per tile),
 // allocated on first use outside stream capture.  Shared by every stream of
 // the process: the engine issues its projection GEMMs on one stream at a time.
 struct SkWorkspace {
@@ -1192,7 +1215,8 @@ SkWorkspace* sk_workspace(hipStream_t s) {
   float* ws = nullptr;
   int* cnt = nullptr;
   if (hipMalloc(&ws, (size_t)P * 65536 * sizeof(float)) != hipSuccess) return nullptr;
-  if (hipMalloc(&cnt, (size_t)P * sizeof(int)) != hipSuccess || hipMemset(cnt, 0, (size_t)P * sizeof(int)) != hipSuccess) {
+  if (hipMalloc(&cnt, (size_t)2 * P * sizeof(int)) != hipSuccess ||
+      hipMemset(cnt, 0, (size_t)2 * P * sizeof(int)) != hipSuccess) {
     hipFree(ws);
     return nullptr;
   }

@@ -96,7 +96,7 @@ def test_mfma_gemm_pingpong_bitwise_stable(M, N, K, epi, phases):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K", [(2048, 2560, 512), (1920, 10240, 8192), (1000, 768, 2048), (2432, 8192, 1024),
-                                   (300, 57344 // 8, 4096), (2048, 19200, 1024)])
+                                   (300, 57344 // 8, 4096), (2048, 19200, 1024), (512, 10240, 8192)])
 @pytest.mark.parametrize("epi", [0, 1])
 @pytest.mark.parametrize("streamk", [0, 2])
 @pytest.mark.parametrize("phases", [4, 2])
