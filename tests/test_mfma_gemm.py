@@ -96,7 +96,8 @@ def test_mfma_gemm_pingpong_bitwise_stable(M, N, K, epi, phases):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K", [(2048, 2560, 512), (1920, 10240, 8192), (1000, 768, 2048), (2432, 8192, 1024),
-                                   (300, 57344 // 8, 4096), (2048, 19200, 1024), (512, 10240, 8192)])
+                                   (300, 57344 // 8, 4096), (2048, 19200, 1024), (512, 10240, 8192),
+                                   (512, 57344, 1024), (200, 57344, 1024), (1000, 48896, 1024)])
 @pytest.mark.parametrize("epi", [0, 1])
 @pytest.mark.parametrize("streamk", [0, 2])
 @pytest.mark.parametrize("phases", [4, 2])
@@ -104,8 +105,10 @@ def test_mfma_gemm_splitk_matches_fp32_and_is_deterministic(M, N, K, epi, stream
     """Hybrid split-K of the last partial wave (persistent launch, 2-4 K pieces per
     remainder tile reduced by the last arriving block through fp32 slabs; uneven
     piece lengths at K = 512; N = 19200 at M = 2048: a split piece, then two whole
-    tiles whose second loads under the first's epilogue): matches the fp32 reference,
-    and repeated launches agree bit for bit (slabs are summed in piece order)."""
+    tiles whose second loads under the first's epilogue; N = 57344 at M = 512 / 200 and
+    N = 48896 at M = 1000: a last wave more than half full, no split): matches the fp32
+    reference, and repeated launches agree bit for bit (slabs are summed in piece order
+    whichever piece arrives last)."""
     ops.load_native(required=True)
     x = _rand(M, K, device="cuda", seed=M + 1)
     w = _rand(N, K, device="cuda", scale=0.05, seed=N + 1)
@@ -133,7 +136,7 @@ def _norm_case(M, N, K, kind, device, phases=0):
         ops.mfma_gemm_norm_ref(x, w, kind, want_ss, 1e-5, want_res)
         ops.mfma_gemm_norm(x, w, kind, ss, 1e-5, out=res, phases=phases)
         return (res, ss), (want_res, want_ss)
-    ss = torch.rand(M, 8, device=device) * K * 0.1
+    ss = (torch.rand(M, 8, generator=torch.Generator().manual_seed(M + N)) * K * 0.1).to(device)
     want = ops.mfma_gemm_norm_ref(x, w, kind, ss, 1e-5)
     got = ops.mfma_gemm_norm(x, w, kind, ss, 1e-5, phases=phases)
     return (got,), (want,)
@@ -161,7 +164,7 @@ def test_norm_fold_reference_equals_rmsnorm_then_gemm_cpu():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K", [(1, 256, 256), (100, 512, 256), (300, 768, 512), (512, 2560, 1024),
-                                   (513, 1024, 8192), (2048, 2560, 4096)])
+                                   (513, 1024, 8192), (2048, 2560, 4096), (512, 57344, 1024)])
 @pytest.mark.parametrize("kind", [2, 3, 4])
 @pytest.mark.parametrize("phases", [2, 4])
 def test_mfma_gemm_norm_matches_fp32(M, N, K, kind, phases):
@@ -175,15 +178,18 @@ def test_mfma_gemm_norm_matches_fp32(M, N, K, kind, phases):
 
 
 @pytest.mark.gpu
-def test_mfma_gemm_norm_is_deterministic():
-    """The row statistics are reduced in a fixed order (no atomics): two runs are bit-identical."""
+@pytest.mark.parametrize("M,N,K,kind", [(1000, 8192, 1024, 2), (512, 57344, 1024, 4)])
+def test_mfma_gemm_norm_is_deterministic(M, N, K, kind):
+    """The row statistics are reduced in a fixed order (no atomics), split-K slabs in piece order:
+    repeated runs are bit-identical."""
     ops.load_native(required=True)
     outs = []
-    for _ in range(2):
-        got, _w = _norm_case(1000, 8192, 1024, ops.NORM_RES, "cuda")
+    for _ in range(4):
+        got, _w = _norm_case(M, N, K, kind, "cuda")
         outs.append([t.clone() for t in got])
     torch.cuda.synchronize()
-    assert all(torch.equal(a, b) for a, b in zip(*outs))
+    for o in outs[1:]:
+        assert all(torch.equal(a, b) for a, b in zip(outs[0], o))
 
 
 def _rope_case(M, nh, nkv, K, device, phases=0, seed=0):
