@@ -25,6 +25,14 @@ if os.environ.get("PYTEST_XDIST_WORKER"):
     # xdist workers inherit the controller's DATABASE_URL: one file per worker process, or one
     # worker's table setup races another's (sqlite "no such table" under -n)
     os.environ["DATABASE_URL"] = _DB
+    # each worker's torch would start one OpenMP thread per CPU: under -n 6 on 8 CPUs the
+    # spin-waiting pools made single tests 100x slower (a 6 s spec test took 659 s); give each
+    # worker its share (subprocesses the tests start inherit it)
+    _n = int(os.environ.get("PYTEST_XDIST_WORKER_COUNT", "1") or 1)
+    _share = str(max(1, (os.cpu_count() or 1) // max(1, _n)))
+    os.environ["OMP_NUM_THREADS"] = _share
+    import torch  # noqa: E402
+    torch.set_num_threads(int(_share))
 else:
     os.environ.setdefault("DATABASE_URL", _DB)
 
