@@ -122,6 +122,31 @@ def test_mfma_gemm_splitk_matches_fp32_and_is_deterministic(M, N, K, epi, stream
         assert torch.equal(ops.mfma_gemm(x, w, epi, sched=3, streamk=streamk, phases=phases), got)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("cus,N", [(160, 10240), (192, 8192), (128, 4096)])
+def test_mfma_gemm_splitk_on_a_cu_limited_grid(cus, N):
+    """Split-K on a grid sized for fewer CUs (``set_gemm_cus``, what a CU-masked two-batch-overlap
+    stream uses): 2 / 3 / 4 pieces per tile, the "written" counters at [P + t] of a smaller P, the
+    last piece's registers folded in piece order.  Matches fp32, bit-identical on repeats, and the
+    counters are back to zero for the next full-grid launch."""
+    ops.load_native(required=True)
+    x = _rand(512, 2048, device="cuda", seed=11)
+    w = _rand(N, 2048, device="cuda", scale=0.05, seed=12)
+    ref = ops.mfma_gemm_ref(x, w, 0).float()
+    ops.set_gemm_cus(cus)
+    try:
+        got = ops.mfma_gemm(x, w, 0, sched=3)
+        again = [ops.mfma_gemm(x, w, 0, sched=3) for _ in range(4)]
+    finally:
+        ops.set_gemm_cus(0)
+    full = ops.mfma_gemm(x, w, 0, sched=3)
+    torch.cuda.synchronize()
+    tol = 2e-2 * ref.abs().max().item() + 1e-3
+    assert (got.float() - ref).abs().max().item() <= tol
+    assert all(torch.equal(a, got) for a in again)
+    assert (full.float() - ref).abs().max().item() <= tol
+
+
 # ---------------------------------------------------------------------------
 # fused RMSNorm epilogues (EPI 2 residual + row statistics, 3 / 4 rstd-scaled plain / SwiGLU)
 
