@@ -32,6 +32,7 @@ int dgi_skinny_gemm(const void* x, int ldx, const void* w, const void* bias, voi
 int dgi_mfma_gemm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int epi,
                   hipStream_t s);
 void dgi_set_gemm_cus(int cus);
+int dgi_gemm_split_timeouts(int reset);
 int dgi_mfma_gemm_norm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int kind,
                        float* ss, int ss_ld, float inv_k, float eps, int phases, hipStream_t s);
 int dgi_mfma_gemm_norm_rope(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, float* ss,
@@ -575,11 +576,13 @@ void tree_verify(at::Tensor accept_len, at::Tensor path, at::Tensor out_tokens,
 // CUs the MFMA GEMM's persistent launches size their grid for (0 = the device's; a CU-masked
 // two-batch-overlap step sets the GEMM stream's share)
 void set_gemm_cus(int64_t cus) { dgi_set_gemm_cus(static_cast<int>(cus)); }
+int64_t gemm_split_timeouts(bool reset) { return dgi_gemm_split_timeouts(reset ? 1 : 0); }
 
 }  // namespace
 
 TORCH_LIBRARY(dgi, m) {
   m.def("set_gemm_cus(int cus) -> ()", &set_gemm_cus);
+  m.def("gemm_split_timeouts(bool reset) -> int", &gemm_split_timeouts);
   m.def("rmsnorm(Tensor(a!) out, Tensor x, Tensor w, float eps) -> ()");
   m.def("fused_add_rmsnorm(Tensor(a!) x, Tensor(b!) residual, Tensor w, float eps) -> ()");
   m.def("rope_cache(Tensor(a!) qkv, Tensor positions, Tensor cos_sin, int nh, int nkv, int hd, "

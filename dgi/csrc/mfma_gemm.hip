@@ -862,10 +862,14 @@ __device__ __forceinline__ void drive(const PPArgs& a, char* smem, Pro&& prologu
       }
       if (store) {
         if (tid == 0) {
-          for (int spin = 0; spin < (1 << 22); ++spin) {
-            if (__hip_atomic_load(a.cnt + a.P + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.splits - 1) break;
-            __builtin_amdgcn_s_sleep(2);
+          bool landed = false;
+          for (int spin = 0; spin < (1 << 22) && !landed; ++spin) {
+            landed = __hip_atomic_load(a.cnt + a.P + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.splits - 1;
+            if (!landed) __builtin_amdgcn_s_sleep(2);
           }
+          // a wait that ran out (a broken counter): counted in the workspace's error word, which
+          // dgi_gemm_split_timeouts reads (DGI_DEBUG_SYNC checks it after every GEMM)
+          if (!landed) __hip_atomic_fetch_add(a.cnt - 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __hip_atomic_store(a.cnt + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1197,15 +1201,18 @@ __global__ __launch_bounds__(512) void mfma_gemm_pp_kernel(PPArgs a) {
 // the process: the engine issues its projection GEMMs on one stream at a time.
 struct SkWorkspace {
   float* ws = nullptr;
-  int* cnt = nullptr;
+  int* cnt = nullptr;   // 2 P counters, preceded by the error word cnt[-1] (timed-out waits)
   int P = 0;
 };
 
+SkWorkspace g_sk_per_dev[64];
+
+SkWorkspace* sk_peek(int dev) { return g_sk_per_dev[dev].ws ? &g_sk_per_dev[dev] : nullptr; }
+
 SkWorkspace* sk_workspace(hipStream_t s) {
-  static SkWorkspace per_dev[64];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  SkWorkspace& w = per_dev[dev];
+  SkWorkspace& w = g_sk_per_dev[dev];
   if (w.ws) return &w;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
@@ -1215,15 +1222,28 @@ SkWorkspace* sk_workspace(hipStream_t s) {
   float* ws = nullptr;
   int* cnt = nullptr;
   if (hipMalloc(&ws, (size_t)P * 65536 * sizeof(float)) != hipSuccess) return nullptr;
-  if (hipMalloc(&cnt, (size_t)2 * P * sizeof(int)) != hipSuccess ||
-      hipMemset(cnt, 0, (size_t)2 * P * sizeof(int)) != hipSuccess) {
+  if (hipMalloc(&cnt, (size_t)(2 * P + 1) * sizeof(int)) != hipSuccess ||
+      hipMemset(cnt, 0, (size_t)(2 * P + 1) * sizeof(int)) != hipSuccess) {
     hipFree(ws);
     return nullptr;
   }
   w.ws = ws;
-  w.cnt = cnt;
+  w.cnt = cnt + 1;
   w.P = P;
   return &w;
+}
+
+// Split-K waits of this device that ran out since the last reset (0 unless a counter broke).
+int sk_timeouts(bool reset) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -1;
+  SkWorkspace* w = sk_peek(dev);
+  if (!w) return 0;
+  int v = 0;
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(&v, w->cnt - 1, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  if (reset && v && hipMemset(w->cnt - 1, 0, sizeof(int)) != hipSuccess) return -1;
+  return v;
 }
 
 // CUs the persistent / split-K launches size their grid for (0 = all of the device's): a GEMM
@@ -1314,6 +1334,8 @@ void launch(const void* x, int ldx, const void* w, void* y, int ldy, int M, int 
 // four 16-MFMA phases (default: two up to M = 2560, see mfma_gemm_pp_kernel), (epi >> 14) & 1: no
 // cross-tile overlap (next tile's prologue after the epilogue; whole waves of tiles not persistent).
 extern "C" void dgi_set_gemm_cus(int cus) { g_cu_limit = cus; }
+
+extern "C" int dgi_gemm_split_timeouts(int reset) { return sk_timeouts(reset != 0); }
 
 // The fused-RMSNorm GEMMs (ping-pong schedule): kind 2 = residual (y += x w^T in place, row
 // partial sums of squares to ss[:, N / 256 columns]), 3 = y = rstd * x w^T, 4 = SwiGLU of

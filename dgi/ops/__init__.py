@@ -586,6 +586,16 @@ def set_gemm_cus(cus: int) -> None:
         torch.ops.dgi.set_gemm_cus(int(cus))
 
 
+def gemm_split_timeouts(reset: bool = False) -> int:
+    """Split-K waits of the MFMA GEMM on the current device that ran out since the last reset
+    (the last piece of a tile waits, bounded, for the other pieces' slabs; a timeout means a wrong
+    tile).  0 in a healthy process; synchronizes the device.  DGI_DEBUG_SYNC=1 checks it after
+    every GEMM."""
+    if not native_available() or not torch.cuda.is_available():
+        return 0
+    return int(torch.ops.dgi.gemm_split_timeouts(bool(reset)))
+
+
 def mfma_gemm(x: torch.Tensor, w: torch.Tensor, epi: int = 0, out: Optional[torch.Tensor] = None,
               sched: Optional[int] = None, streamk: int = 0, prio: int = 0, phases: int = 0,
               overlap: bool = True) -> torch.Tensor:

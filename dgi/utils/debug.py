@@ -6,7 +6,10 @@ opt-in modes, all off by default and free when off:
 * ``DGI_DEBUG_SYNC=1`` — *serialized* execution: every dgi HIP op is followed
   by a device synchronize and an error check, so an asynchronous fault is
   reported at the op that caused it (with its name and input shapes) instead
-  of at some later, unrelated sync.  ``enable_serialized()`` also exports
+  of at some later, unrelated sync.  After every MFMA GEMM it also reads the
+  split-K error word (``ops.gemm_split_timeouts``: a last piece whose bounded
+  wait for the other pieces' slabs ran out) and raises on a nonzero count.
+  ``enable_serialized()`` also exports
   ``HIP_LAUNCH_BLOCKING=1`` / ``AMD_SERIALIZE_KERNEL=3`` for processes spawned
   afterwards (the HIP runtime reads them at start-up).
 * ``DGI_DEBUG_STREAMS=1`` — *stream-ordering checker* on the RCCL fabric:
@@ -56,6 +59,12 @@ def after_op(name: str, *tensors) -> None:
     except Exception as e:  # pragma: no cover - needs a faulting kernel
         shapes = [tuple(t.shape) for t in tensors if isinstance(t, torch.Tensor)]
         raise RuntimeError(f"dgi op {name} failed (inputs {shapes}): {e}") from e
+    if name.startswith("mfma_gemm"):
+        from dgi import ops
+        n = ops.gemm_split_timeouts(reset=True)
+        if n:  # pragma: no cover - needs a broken split-K counter
+            shapes = [tuple(t.shape) for t in tensors if isinstance(t, torch.Tensor)]
+            raise RuntimeError(f"dgi op {name}: {n} split-K wait(s) timed out (inputs {shapes}): wrong tiles")
 
 
 class StreamOrderChecker:

@@ -13,6 +13,10 @@ def _rand(*shape, device, scale=1.0, seed=0):
     return ((torch.rand(*shape, generator=g, device=device) * 2 - 1) * scale).to(torch.bfloat16)
 
 
+def test_split_timeout_counter_is_zero_without_a_gpu_cpu():
+    assert ops.gemm_split_timeouts() == 0
+
+
 def test_reference_swiglu_matches_silu_mul_cpu():
     x = _rand(7, 64, device="cpu")
     w = _rand(512, 64, device="cpu", seed=1)
@@ -120,6 +124,7 @@ def test_mfma_gemm_splitk_matches_fp32_and_is_deterministic(M, N, K, epi, stream
     assert err.max().item() <= tol, (err.max().item(), tol)
     for _ in range(6):
         assert torch.equal(ops.mfma_gemm(x, w, epi, sched=3, streamk=streamk, phases=phases), got)
+    assert ops.gemm_split_timeouts(reset=True) == 0
 
 
 @pytest.mark.gpu
@@ -145,6 +150,7 @@ def test_mfma_gemm_splitk_on_a_cu_limited_grid(cus, N):
     assert (got.float() - ref).abs().max().item() <= tol
     assert all(torch.equal(a, got) for a in again)
     assert (full.float() - ref).abs().max().item() <= tol
+    assert ops.gemm_split_timeouts(reset=True) == 0        # no last piece's wait ran out
 
 
 # ---------------------------------------------------------------------------
