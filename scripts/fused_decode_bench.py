@@ -192,6 +192,8 @@ def main():
     ap.add_argument("--skip-gemms", action="store_true", help="skip the fused qkv / gate_up table")
     ap.add_argument("--plain-fused", action="store_true", help="also o-proj / down through fused_skinny configs")
     ap.add_argument("--plain", action="store_true", help="only the plain skinny-vs-hipBLASLt table")
+    ap.add_argument("--plain-fused-ms", type=int, nargs="+", default=[1, 4, 8], help="row counts of --plain-fused")
+    ap.add_argument("--plain-fused-qkv", action="store_true", help="--plain-fused also times the qkv shape")
     a = ap.parse_args()
     if a.plain:
         ops.load_native(required=True)
@@ -203,7 +205,8 @@ def main():
         return
     res = {} if a.skip_gemms else {"gemm_8b": bench_gemms(4096, 14336, 32, 8, [1, 2, 4, 8, 16], a.cfgs)}
     if a.plain_fused:
-        res["plain_fused_8b"] = bench_plain_fused([("o", 4096, 4096), ("down", 4096, 14336)], [1, 4, 8], a.cfgs)
+        shapes = [("o", 4096, 4096), ("down", 4096, 14336)] + ([("qkv", 6144, 4096)] if a.plain_fused_qkv else [])
+        res["plain_fused_8b"] = bench_plain_fused(shapes, a.plain_fused_ms, a.cfgs)
     if not a.skip_attn:
         res["attn_8b"] = bench_attn(32, 8, [1, 4, 16], [256, 384, 1024, 4096])
     if a.out:
