@@ -19,6 +19,7 @@ from app.api.deps import lookup_api_key
 from app.db.database import get_db
 from app.models.models import Job, JobStatus, Worker, WorkerStatus
 from app.services.geo import detect_client_region
+from app.services.job_signal import job_queued
 from app.services.pd_runtime import coordinator
 from app.services.scheduler import SmartScheduler, get_region_distance
 from app.services.task_guarantee import TaskGuaranteeService
@@ -85,6 +86,7 @@ def _new_job(db: Session, payload: JobCreateRequest, client_ip, client_region, a
     db.refresh(job)
     if pd:
         coordinator.on_created(job)
+    job_queued.notify()          # long-polling workers (GET next-job?wait=) try to claim it now
     return job
 
 

@@ -12,6 +12,7 @@ once (the reference allowed exactly one); it is BUSY only at that limit.
 """
 from __future__ import annotations
 
+import time
 from datetime import datetime
 from typing import Any, Dict, List, Optional
 
@@ -25,6 +26,7 @@ from app.db.database import get_db
 from app.models.models import Job, JobStatus, Worker, WorkerStatus
 from app.models.usage import Enterprise
 from app.services.pd_runtime import coordinator
+from app.services.job_signal import RECHECK_S, job_queued
 from app.services.reliability import ReliabilityService
 from app.services.scheduler import SmartScheduler
 from app.services.security import SecurityService
@@ -187,7 +189,10 @@ async def heartbeat(worker_id: str, payload: HeartbeatRequest, request: Request,
 
 @router.get("/{worker_id}/next-job", response_model=Optional[JobAssignment])
 async def get_next_job(worker_id: str, request: Request, x_worker_token: Optional[str] = Header(None),
-                       db: Session = Depends(get_db)):
+                       wait: float = Query(0.0, ge=0.0, le=30.0), db: Session = Depends(get_db)):
+    """The next job for this worker, or null.  ``wait`` > 0 (seconds) long-polls: an empty queue
+    keeps the request open until a job is queued (``services/job_signal.py``) or ``wait`` runs
+    out, so a job reaches an idle worker at once instead of at its next poll."""
     w = authenticate_worker(db, worker_id, x_worker_token, _ip(request))
     w.last_heartbeat = datetime.utcnow()
     if w.status in (WorkerStatus.GOING_OFFLINE.value, WorkerStatus.OFFLINE.value):
@@ -197,10 +202,20 @@ async def get_next_job(worker_id: str, request: Request, x_worker_token: Optiona
     if _running(db, w.id) >= lc.max_concurrent_jobs:
         db.commit()
         return None
-    job = SmartScheduler(db).atomic_assign_job(str(w.id), list(w.supported_types or []), worker=w)
-    if job is None:
+    deadline = time.monotonic() + wait
+    while True:
+        job = SmartScheduler(db).atomic_assign_job(str(w.id), list(w.supported_types or []), worker=w)
+        if job is not None:
+            break
         db.commit()
-        return None
+        left = deadline - time.monotonic()
+        if left <= 0:
+            return None
+        await job_queued.wait(min(left, RECHECK_S))
+        db.expire_all()
+        w = db.get(Worker, w.id)
+        if w is None or w.status in (WorkerStatus.GOING_OFFLINE.value, WorkerStatus.OFFLINE.value):
+            return None
     w.current_job_id = job.id
     w.status = WorkerStatus.BUSY.value if _running(db, w.id) >= lc.max_concurrent_jobs else WorkerStatus.ONLINE.value
     db.commit()
@@ -233,6 +248,7 @@ async def complete_job(worker_id: str, job_id: str, payload: JobCompleteRequest,
             w.current_job_id = None
         ReliabilityService(db).update_score(w, "job_completed", commit=False, latency_ms=payload.processing_time_ms)
         db.commit()
+        job_queued.notify()
         return {"status": "ok", "job_id": job_id, "next_phase": "decode", "decode_worker": nxt["target_worker_id"]}
     if job.phase:
         if payload.success:

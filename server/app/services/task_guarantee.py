@@ -16,6 +16,7 @@ from sqlalchemy.orm import Session
 
 from app.config import settings
 from app.models.models import Job, JobStatus, Worker, WorkerStatus
+from app.services.job_signal import job_queued
 from app.services.reliability import ReliabilityService
 
 logger = logging.getLogger(__name__)
@@ -73,22 +74,27 @@ class TaskGuaranteeService:
             w.current_job_id = None
             self.reliability.update_score(w, "graceful_offline" if graceful else "unexpected_offline", commit=False)
         self.db.commit()
+        if requeued:
+            job_queued.notify()
         return {"requeued": requeued, "failed": failed}
 
     def check_stale_jobs(self) -> int:
         now = datetime.utcnow()
-        n = 0
+        n = requeued = 0
         for j in self.db.execute(select(Job).where(Job.status == JobStatus.RUNNING.value)).scalars():
             limit = max(self.STALE_JOB_MINUTES * 60, j.timeout_seconds or settings.job_timeout_seconds)
             if j.started_at and (now - j.started_at).total_seconds() > limit:
                 if (j.retry_count or 0) < (j.max_retries or 3):
                     j.status, j.worker_id, j.started_at = JobStatus.QUEUED.value, None, None
                     j.retry_count = (j.retry_count or 0) + 1
+                    requeued += 1
                 else:
                     j.status, j.error, j.completed_at = JobStatus.TIMEOUT.value, "job timed out", now
                     notify_job_done(j.id)
                 n += 1
         self.db.commit()
+        if requeued:
+            job_queued.notify()
         return n
 
     def check_dead_workers(self, timeout_seconds: Optional[int] = None) -> int:

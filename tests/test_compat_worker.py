@@ -86,6 +86,17 @@ def test_client_no_job_codes(code):
         assert c.fetch_next_job("w") is None
 
 
+def test_client_long_poll_sends_wait_and_a_longer_timeout():
+    c = APIClient(base_url="http://example", timeout=3)
+    with patch.object(c.client, "get", return_value=_resp(204)) as m:
+        assert c.fetch_next_job("w", wait=5.0) is None
+    kw = m.call_args.kwargs
+    assert kw["params"] == {"wait": 5.0} and kw["timeout"] >= 15.0
+    with patch.object(c.client, "get", return_value=_resp(204)) as m:
+        c.fetch_next_job("w")
+    assert "params" not in m.call_args.kwargs                 # plain poll: the reference's request
+
+
 def test_client_verify_and_config_failures_are_soft():
     c = APIClient(base_url="http://example")
     with patch.object(c.client, "post", side_effect=RuntimeError("boom")):

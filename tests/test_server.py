@@ -315,6 +315,55 @@ def test_api_sync_job_completed_by_worker_thread(client):
     assert r.status_code == 408
 
 
+def test_next_job_long_poll_wakes_on_a_new_job(client):
+    """GET next-job?wait=S keeps the request open and hands over a job queued while it waits (the
+    reference's workers only see it at their next poll, 2 s by default); with nothing queued it
+    returns null after ``wait``; without ``wait`` it answers at once as before."""
+    c = client
+    wid, hdr, _ = _register(c)
+    t0 = time.perf_counter()
+    assert c.get(f"/api/v1/workers/{wid}/next-job", headers=hdr).json() is None
+    assert time.perf_counter() - t0 < 0.2
+    t0 = time.perf_counter()
+    assert c.get(f"/api/v1/workers/{wid}/next-job?wait=0.3", headers=hdr).json() is None
+    assert time.perf_counter() - t0 >= 0.3
+    got = {}
+
+    def poll():
+        from fastapi.testclient import TestClient
+        from app.main import app
+        wc = TestClient(app)
+        t = time.perf_counter()
+        got["a"] = wc.get(f"/api/v1/workers/{wid}/next-job?wait=10", headers=hdr).json()
+        got["t"] = time.perf_counter() - t
+    th = threading.Thread(target=poll, daemon=True)
+    th.start()
+    time.sleep(0.4)
+    t_sub = time.perf_counter()
+    job_id = c.post("/api/v1/jobs", json={"type": "llm", "params": {"prompt": "p"}}).json()["job_id"]
+    th.join(10)
+    assert got["a"] and got["a"]["job_id"] == job_id
+    assert got["t"] < 2.0                                  # not the 10 s wait
+    assert time.perf_counter() - t_sub < 1.0
+
+
+def test_job_signal_wakes_waiters_across_threads():
+    from app.services.job_signal import JobSignal
+    sig = JobSignal()
+
+    async def main():
+        assert await sig.wait(0.05) is False                  # timeout
+        loop = asyncio.get_running_loop()
+        loop.call_later(0.05, sig.notify)                     # same loop
+        assert await sig.wait(5.0) is True
+        threading.Timer(0.05, sig.notify).start()             # another thread
+        t = time.perf_counter()
+        assert await sig.wait(5.0) is True
+        assert time.perf_counter() - t < 2.0
+    asyncio.run(main())
+    sig.notify()                                              # no waiter: a no-op
+
+
 def test_api_no_worker_503_and_direct(client):
     c = client
     r = c.post("/api/v1/jobs/sync?wait_for_worker=false", json={"type": "llm", "params": {}})

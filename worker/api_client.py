@@ -103,9 +103,15 @@ class APIClient:
             payload["engine_stats"] = engine_stats
         return self._post(f"/api/v1/workers/{worker_id}/heartbeat", payload).json()
 
-    def fetch_next_job(self, worker_id: str) -> Optional[Dict[str, Any]]:
+    def fetch_next_job(self, worker_id: str, wait: float = 0.0) -> Optional[Dict[str, Any]]:
+        """The next job or None.  ``wait`` > 0 long-polls: the server holds the request until a
+        job is queued or ``wait`` seconds pass (a server without long-poll answers at once)."""
         try:
-            r = self.client.get(f"{self.base_url}/api/v1/workers/{worker_id}/next-job", headers=self._headers())
+            kw: Dict[str, Any] = {"headers": self._headers()}
+            if wait > 0:
+                kw["params"] = {"wait": wait}
+                kw["timeout"] = max(float(self.timeout), wait + 10.0)
+            r = self.client.get(f"{self.base_url}/api/v1/workers/{worker_id}/next-job", **kw)
         except httpx.RequestError as e:
             logger.warning("next-job failed: %s", e)
             return None

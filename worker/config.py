@@ -175,6 +175,9 @@ class WorkerConfig(BaseModel):
     engines: Dict[str, Dict[str, Any]] = Field(default_factory=dict)
     heartbeat_interval: int = Field(default_factory=_env("GPU_HEARTBEAT_INTERVAL", 30, int))
     poll_interval: float = Field(default_factory=_env("GPU_POLL_INTERVAL", 2.0, float))
+    # long-poll the next-job endpoint for up to this many seconds (0: plain polling every
+    # poll_interval); a job then reaches an idle worker as soon as it is queued
+    long_poll_s: float = Field(default_factory=_env("GPU_LONG_POLL_S", 5.0, float))
     inference: InferenceConfig = Field(default_factory=InferenceConfig)
     distributed: DistributedConfig = Field(default_factory=DistributedConfig)
     speculative: SpeculativeSection = Field(default_factory=SpeculativeSection)

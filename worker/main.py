@@ -409,7 +409,8 @@ class Worker:
             got = False
             if self.inflight_count() < self.max_concurrent_jobs() and self._should_accept_job():
                 try:
-                    job = self.api_client.fetch_next_job(self.worker_id)
+                    job = self.api_client.fetch_next_job(self.worker_id,
+                                                         wait=float(getattr(self.config, "long_poll_s", 0.0) or 0.0))
                 except Exception as e:
                     logger.error("fetch failed: %s", e)
                     job = None
