@@ -187,42 +187,61 @@ async def heartbeat(worker_id: str, payload: HeartbeatRequest, request: Request,
     return HeartbeatResponse(status="ok", action=action, config_changed=changed)
 
 
-@router.get("/{worker_id}/next-job", response_model=Optional[JobAssignment])
-async def get_next_job(worker_id: str, request: Request, x_worker_token: Optional[str] = Header(None),
-                       wait: float = Query(0.0, ge=0.0, le=30.0), db: Session = Depends(get_db)):
-    """The next job for this worker, or null.  ``wait`` > 0 (seconds) long-polls: an empty queue
-    keeps the request open until a job is queued (``services/job_signal.py``) or ``wait`` runs
-    out, so a job reaches an idle worker at once instead of at its next poll."""
-    w = authenticate_worker(db, worker_id, x_worker_token, _ip(request))
+async def _claim(db: Session, request: Request, worker_id: str, token: Optional[str], n: int,
+                 wait: float) -> List[JobAssignment]:
+    """Up to ``n`` jobs (bounded by the worker's free job slots) claimed in one transaction.
+    ``wait`` > 0 long-polls: an empty queue keeps the request open until a job is queued
+    (``services/job_signal.py``) or ``wait`` runs out."""
+    w = authenticate_worker(db, worker_id, token, _ip(request))
     w.last_heartbeat = datetime.utcnow()
     if w.status in (WorkerStatus.GOING_OFFLINE.value, WorkerStatus.OFFLINE.value):
         db.commit()
-        return None
+        return []
     lc = _load_control(w)
-    if _running(db, w.id) >= lc.max_concurrent_jobs:
+    free = lc.max_concurrent_jobs - _running(db, w.id)
+    if free <= 0:
         db.commit()
-        return None
+        return []
     deadline = time.monotonic() + wait
     while True:
-        job = SmartScheduler(db).atomic_assign_job(str(w.id), list(w.supported_types or []), worker=w)
-        if job is not None:
+        jobs = SmartScheduler(db).atomic_assign_jobs(str(w.id), list(w.supported_types or []), worker=w,
+                                                     n=min(n, free))
+        if jobs:
             break
         db.commit()
         left = deadline - time.monotonic()
         if left <= 0:
-            return None
+            return []
         await job_queued.wait(min(left, RECHECK_S))
         db.expire_all()
         w = db.get(Worker, w.id)
         if w is None or w.status in (WorkerStatus.GOING_OFFLINE.value, WorkerStatus.OFFLINE.value):
-            return None
-    w.current_job_id = job.id
+            return []
+    w.current_job_id = jobs[-1].id
     w.status = WorkerStatus.BUSY.value if _running(db, w.id) >= lc.max_concurrent_jobs else WorkerStatus.ONLINE.value
     db.commit()
-    if job.phase:
-        coordinator.on_assigned(job, w)
-    return JobAssignment(job_id=str(job.id), type=job.type, params=job.params or {},
-                         timeout_seconds=job.timeout_seconds, priority=job.priority)
+    for job in jobs:
+        if job.phase:
+            coordinator.on_assigned(job, w)
+    return [JobAssignment(job_id=str(job.id), type=job.type, params=job.params or {},
+                          timeout_seconds=job.timeout_seconds, priority=job.priority) for job in jobs]
+
+
+@router.get("/{worker_id}/next-job", response_model=Optional[JobAssignment])
+async def get_next_job(worker_id: str, request: Request, x_worker_token: Optional[str] = Header(None),
+                       wait: float = Query(0.0, ge=0.0, le=30.0), db: Session = Depends(get_db)):
+    """The next job for this worker, or null (``wait``: long-poll seconds, see ``_claim``)."""
+    jobs = await _claim(db, request, worker_id, x_worker_token, 1, wait)
+    return jobs[0] if jobs else None
+
+
+@router.get("/{worker_id}/next-jobs", response_model=List[JobAssignment])
+async def get_next_jobs(worker_id: str, request: Request, x_worker_token: Optional[str] = Header(None),
+                        max_jobs: int = Query(8, ge=1, le=64, alias="max"),
+                        wait: float = Query(0.0, ge=0.0, le=30.0), db: Session = Depends(get_db)):
+    """Up to ``max`` jobs at once (a burst of queued jobs in one round trip and one commit);
+    [] when none.  Not in the reference: its workers use ``next-job``."""
+    return await _claim(db, request, worker_id, x_worker_token, max_jobs, wait)
 
 
 @router.post("/{worker_id}/jobs/{job_id}/complete")

@@ -117,11 +117,19 @@ class SmartScheduler:
 
     def atomic_assign_job(self, worker_id: str, supported_types: List[str], worker: Optional[Worker] = None,
                           candidates: int = 8) -> Optional[Job]:
-        if not supported_types:
-            return None
+        jobs = self.atomic_assign_jobs(worker_id, supported_types, worker, 1, candidates)
+        return jobs[0] if jobs else None
+
+    def atomic_assign_jobs(self, worker_id: str, supported_types: List[str], worker: Optional[Worker] = None,
+                           n: int = 1, candidates: int = 8) -> List[Job]:
+        """Claim up to ``n`` queued jobs for the worker in one transaction (one commit: a burst of
+        jobs reaches a worker in one round trip instead of one claim + commit each).  Each claim is
+        a conditional UPDATE on QUEUED, so concurrent claimers never share a job."""
+        if not supported_types or n <= 0:
+            return []
         q = (select(Job).where(Job.status == JobStatus.QUEUED.value, Job.type.in_(list(supported_types)),
                                or_(Job.target_worker_id.is_(None), Job.target_worker_id == str(worker_id)))
-             .order_by(Job.priority.desc(), Job.created_at.asc()).limit(candidates))
+             .order_by(Job.priority.desc(), Job.created_at.asc()).limit(max(candidates, 2 * n)))
         jobs = list(self.db.execute(q).scalars())
         if worker is not None and (worker.role or "hybrid") in ("prefill", "decode"):
             # a P/D-phase job only goes to a worker of that role (or a hybrid one)
@@ -135,10 +143,12 @@ class SmartScheduler:
                 phase_ok = role == "hybrid" or (j.phase or "prefill") == role or j.phase is None
                 return (j.priority < top, not phase_ok, not region_ok, j.created_at)
             jobs.sort(key=pref)
-        if jobs and not self._accepts(worker, jobs[0].type):
-            self.db.commit()   # persist the hour-bucket roll-over
-            return None
+        got: List[Job] = []
         for job in jobs:
+            if len(got) >= n:
+                break
+            if not self._accepts(worker, job.type):
+                break
             if worker is not None and job.preferred_region and not job.allow_cross_region \
                     and job.preferred_region != worker.region:
                 continue
@@ -147,14 +157,14 @@ class SmartScheduler:
                                   .values(status=JobStatus.RUNNING.value, worker_id=worker_id, started_at=now,
                                           actual_region=worker.region if worker is not None else None))
             if res.rowcount == 1:
+                got.append(job)
                 if worker is not None:
                     worker.current_job_id = job.id
                     worker.jobs_this_hour = (worker.jobs_this_hour or 0) + 1
-                self.db.commit()
-                self.db.refresh(job)
-                return job
-            self.db.rollback()
-        return None
+        self.db.commit()       # the claims (and the hour-bucket roll-over) in one transaction
+        for job in got:
+            self.db.refresh(job)
+        return got
 
     def get_queue_stats(self, region: Optional[str] = None) -> dict:
         q = select(Job).where(Job.status == JobStatus.QUEUED.value)

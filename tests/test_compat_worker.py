@@ -97,6 +97,21 @@ def test_client_long_poll_sends_wait_and_a_longer_timeout():
     assert "params" not in m.call_args.kwargs                 # plain poll: the reference's request
 
 
+def test_client_batch_fetch_falls_back_on_a_reference_server():
+    c = APIClient(base_url="http://example")
+    jobs = [{"job_id": "a"}, {"job_id": "b"}]
+    with patch.object(c.client, "get", return_value=_resp(200, json=jobs)) as m:
+        assert c.fetch_next_jobs("w", 4, wait=2.0) == jobs
+    assert m.call_args.args[0].endswith("/next-jobs") and m.call_args.kwargs["params"] == {"max": 4, "wait": 2.0}
+    # a server without next-jobs: 404, then one job per request from then on
+    with patch.object(c.client, "get", side_effect=[_resp(404), _resp(200, json={"job_id": "x"})]) as m:
+        assert c.fetch_next_jobs("w", 4) == [{"job_id": "x"}]
+    assert m.call_args.args[0].endswith("/next-job")
+    with patch.object(c.client, "get", return_value=_resp(200, json={"job_id": "y"})) as m:
+        assert c.fetch_next_jobs("w", 4) == [{"job_id": "y"}]
+    assert m.call_count == 1 and m.call_args.args[0].endswith("/next-job")
+
+
 def test_client_verify_and_config_failures_are_soft():
     c = APIClient(base_url="http://example")
     with patch.object(c.client, "post", side_effect=RuntimeError("boom")):

@@ -347,6 +347,31 @@ def test_next_job_long_poll_wakes_on_a_new_job(client):
     assert time.perf_counter() - t_sub < 1.0
 
 
+def test_next_jobs_claims_a_burst_in_one_request(client):
+    """GET next-jobs?max=N claims up to N queued jobs (bounded by the worker's free job slots) in
+    one transaction; each job goes to exactly one claimer; [] when the queue is empty."""
+    c = client
+    wid, hdr, _ = _register(c)
+    c.put(f"/api/v1/workers/{wid}/config", json={"max_concurrent_jobs": 6}, headers=hdr)
+    ids = [c.post("/api/v1/jobs", json={"type": "llm", "params": {"prompt": str(i)}}).json()["job_id"]
+           for i in range(7)]
+    a = c.get(f"/api/v1/workers/{wid}/next-jobs?max=3", headers=hdr).json()
+    assert len(a) == 3 and len({x["job_id"] for x in a}) == 3
+    b = c.get(f"/api/v1/workers/{wid}/next-jobs?max=8", headers=hdr).json()
+    assert len(b) == 3                                        # 6 job slots: 3 + 3, two stay queued
+    assert len({x["job_id"] for x in a} | {x["job_id"] for x in b}) == 6
+    assert c.get(f"/api/v1/workers/{wid}/next-jobs?max=8", headers=hdr).json() == []
+    wid2, hdr2, _ = _register(c)
+    c.put(f"/api/v1/workers/{wid2}/config", json={"max_concurrent_jobs": 8}, headers=hdr2)
+    rest = c.get(f"/api/v1/workers/{wid2}/next-jobs?max=8", headers=hdr2).json()
+    assert {x["job_id"] for x in a + b + rest} == set(ids) and len(rest) == 1
+    for x in a + b:
+        assert c.get(f"/api/v1/jobs/{x['job_id']}").json()["status"] == "running"
+    t0 = time.perf_counter()
+    assert c.get(f"/api/v1/workers/{wid2}/next-jobs?max=2&wait=0.2", headers=hdr2).json() == []
+    assert time.perf_counter() - t0 >= 0.2
+
+
 def test_job_signal_wakes_waiters_across_threads():
     from app.services.job_signal import JobSignal
     sig = JobSignal()

@@ -33,6 +33,7 @@ class APIClient:
         self.timeout = timeout
         self.max_retries = max_retries
         self.client = httpx.Client(timeout=timeout, verify=verify_ssl)
+        self._batch_claim = True        # GET next-jobs until a server answers that it has none
 
     def set_credentials(self, token: str, signing_secret: Optional[str] = None) -> None:
         self.token = token
@@ -120,6 +121,32 @@ class APIClient:
         r.raise_for_status()
         data = r.json() if r.content else None
         return data or None
+
+    def fetch_next_jobs(self, worker_id: str, max_jobs: int, wait: float = 0.0) -> List[Dict[str, Any]]:
+        """Up to ``max_jobs`` jobs in one request (``GET next-jobs``, one claim transaction on the
+        server).  A server without that endpoint (the reference's) answers 404/405: from then on
+        this client falls back to ``fetch_next_job``."""
+        if max_jobs <= 1 or not self._batch_claim:
+            job = self.fetch_next_job(worker_id, wait)
+            return [job] if job else []
+        try:
+            kw: Dict[str, Any] = {"headers": self._headers(), "params": {"max": int(max_jobs)}}
+            if wait > 0:
+                kw["params"]["wait"] = wait
+                kw["timeout"] = max(float(self.timeout), wait + 10.0)
+            r = self.client.get(f"{self.base_url}/api/v1/workers/{worker_id}/next-jobs", **kw)
+        except httpx.RequestError as e:
+            logger.warning("next-jobs failed: %s", e)
+            return []
+        if r.status_code in (404, 405):
+            self._batch_claim = False
+            job = self.fetch_next_job(worker_id, wait)
+            return [job] if job else []
+        if r.status_code == 204:
+            return []
+        r.raise_for_status()
+        data = r.json() if r.content else None
+        return list(data or [])
 
     def complete_job(self, worker_id: str, job_id: str, success: bool, result: Optional[Dict[str, Any]] = None,
                      error: Optional[str] = None, processing_time_ms: Optional[int] = None,

@@ -407,14 +407,16 @@ class Worker:
                 self.shutdown_event.wait(0.2)
                 continue
             got = False
-            if self.inflight_count() < self.max_concurrent_jobs() and self._should_accept_job():
+            free = self.max_concurrent_jobs() - self.inflight_count()
+            if free > 0 and self._should_accept_job():
+                wait = float(getattr(self.config, "long_poll_s", 0.0) or 0.0)
                 try:
-                    job = self.api_client.fetch_next_job(self.worker_id,
-                                                         wait=float(getattr(self.config, "long_poll_s", 0.0) or 0.0))
+                    # a burst of queued jobs in one round trip (GET next-jobs), else one (next-job)
+                    jobs = self.api_client.fetch_next_jobs(self.worker_id, free, wait=wait)
                 except Exception as e:
                     logger.error("fetch failed: %s", e)
-                    job = None
-                if job:
+                    jobs = []
+                for job in jobs:
                     self._dispatch(job)
                     got = True
             if not got:
