@@ -319,12 +319,15 @@ def build_app(sup: NodeSupervisor, tok, on_shutdown=None):
         asyncio.create_task(sup.run_job(job))
         if r.stream:
             async def events():
+                from dgi.utils.tokenizer import StreamDecoder
+                dec = StreamDecoder(tok)        # text pieces concatenate to the full decode
                 while True:
                     kind, v = await job.events.get()
                     if kind == "token":
-                        yield f"data: {json.dumps({'token_id': v, 'text': tok.decode([v])})}\n\n"
+                        yield f"data: {json.dumps({'token_id': v, 'text': dec.add(v)})}\n\n"
                     else:
-                        yield f"data: {json.dumps({'done': True, 'finish_reason': v})}\n\n"
+                        tail = dec.flush()
+                        yield f"data: {json.dumps({'done': True, 'finish_reason': v, 'text': tail})}\n\n"
                         return
             return StreamingResponse(events(), media_type="text/event-stream")
         await job.done.wait()

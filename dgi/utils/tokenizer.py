@@ -26,9 +26,10 @@ class ByteTokenizer:
         return ([self.bos_token_id] if add_bos else []) + ids
 
     # ids above the byte range (a random-init model samples them almost always) decode to one
-    # U+FFFD each instead of nothing: every generated token is visible text, so a stream's
-    # first chunk arrives with the first token and SSE TTFT measures what it says
-    UNKNOWN = "\ufffd".encode("utf-8")
+    # U+25A1 each instead of nothing: every generated token is visible text, so a stream's
+    # first chunk arrives with the first token and SSE TTFT measures what it says.  (Not U+FFFD:
+    # that marks an incomplete UTF-8 sequence, which a StreamDecoder holds back.)
+    UNKNOWN = "\u25a1".encode("utf-8")
 
     def decode(self, ids, skip_special_tokens: bool = True) -> str:
         out = bytearray()
@@ -64,6 +65,45 @@ class ByteTokenizer:
             t = torch.tensor([ids])
             return _Enc(input_ids=t, attention_mask=torch.ones_like(t))
         return {"input_ids": ids}
+
+
+class StreamDecoder:
+    """Incremental detokenization of one generated sequence: ``add(token_id)`` returns the text
+    the token completes ("" while it only starts a multi-byte character).
+
+    Decoding every token alone loses what depends on its neighbours (SentencePiece word-boundary
+    spaces, UTF-8 characters split over byte tokens), and re-decoding the whole output each token
+    costs O(n) per token.  This decodes a short window instead: the tokens since the last
+    emitted prefix, against the text that prefix already produced (the prefix / read offset
+    scheme of streaming LLM servers).  A trailing U+FFFD is an incomplete UTF-8 sequence and is
+    held back until the next token completes it.  The emitted pieces concatenate to the full
+    decode."""
+
+    def __init__(self, tokenizer, skip_special_tokens: bool = True):
+        self.tok = tokenizer
+        self.skip = skip_special_tokens
+        self.ids: List[int] = []
+        self.prefix = 0          # start of the decode window
+        self.read = 0            # tokens whose text is already emitted
+
+    def _decode(self, ids) -> str:
+        return self.tok.decode(ids, skip_special_tokens=self.skip)
+
+    def add(self, token_id: int) -> str:
+        self.ids.append(int(token_id))
+        prefix_text = self._decode(self.ids[self.prefix:self.read])
+        text = self._decode(self.ids[self.prefix:])
+        if len(text) > len(prefix_text) and not text.endswith("\ufffd"):
+            self.prefix, self.read = self.read, len(self.ids)
+            return text[len(prefix_text):]
+        return ""
+
+    def flush(self) -> str:
+        """Text still held back at the end of the sequence (an incomplete character)."""
+        prefix_text = self._decode(self.ids[self.prefix:self.read])
+        text = self._decode(self.ids[self.prefix:])
+        self.prefix = self.read = len(self.ids)
+        return text[len(prefix_text):] if len(text) > len(prefix_text) else ""
 
 
 def load_tokenizer(model_id: Optional[str], vocab_size: int = 32000, bos: int = 1, eos: int = 2):

@@ -28,7 +28,7 @@ from typing import Any, AsyncIterator, Dict, List, Optional
 
 import torch
 
-from dgi.utils.tokenizer import chat_prompt_ids, load_tokenizer
+from dgi.utils.tokenizer import StreamDecoder, chat_prompt_ids, load_tokenizer
 
 from .llm_base import GenerationConfig, GenerationResult, LLMBackend, LLMBaseEngine
 
@@ -334,17 +334,17 @@ class NativeLLMEngine(LLMBaseEngine):
     async def stream_generate(self, messages: List[Dict[str, str]],
                               config: Optional[GenerationConfig] = None) -> AsyncIterator[str]:
         p = self._submit(messages, config or GenerationConfig(), stream=True)
-        toks: List[int] = []
-        prev = ""
+        dec = StreamDecoder(self.tokenizer)          # O(window) per token, multi-byte safe
         while True:
             t = await p.stream_q.get()
             if t is None:
                 break
-            toks.append(t)
-            text = self.tokenizer.decode(toks, skip_special_tokens=True)
-            if len(text) > len(prev):
-                yield text[len(prev):]
-                prev = text
+            piece = dec.add(t)
+            if piece:
+                yield piece
+        tail = dec.flush()
+        if tail:
+            yield tail
         await p.future
 
     def batch_inference(self, params_list: List[Dict[str, Any]]) -> List[Dict[str, Any]]:
