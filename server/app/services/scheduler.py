@@ -10,7 +10,6 @@ acceptance rate / hourly cap from its remote config (reference E-33, E-35).
 from __future__ import annotations
 
 import logging
-import random
 from datetime import datetime
 from typing import List, Optional
 
