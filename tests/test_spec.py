@@ -435,3 +435,14 @@ def test_spec_whole_step_graph_matches_staged_path():
     n0 = whole.spec_stats["whole_steps"]
     outs = [r.output for r in whole.generate(prompts, spt)]
     assert all(len(o) == 16 for o in outs) and whole.spec_stats["whole_steps"] > n0
+
+
+def test_token_range_equals_slicing_the_full_token_list_cpu():
+    """_whole_step slices each sequence's catch-up window without building prompt + output."""
+    import types
+    from dgi.spec.eagle3 import _token_range
+    r = types.SimpleNamespace(prompt=list(range(10)), output=list(range(100, 105)))
+    full = r.prompt + r.output
+    for a in range(len(full) + 2):
+        for b in range(a, len(full) + 2):
+            assert _token_range(r, a, b) == full[a:b]
