@@ -446,3 +446,59 @@ def test_token_range_equals_slicing_the_full_token_list_cpu():
     for a in range(len(full) + 2):
         for b in range(a, len(full) + 2):
             assert _token_range(r, a, b) == full[a:b]
+
+
+def test_step_graph_metadata_fill_matches_the_per_row_rule_cpu():
+    """_StepGraph._fill (vectorized) against the per-row rule it encodes: catch-up rows p0 .. p0+C-1
+    (past nv, or past the live batch: scratch slots on page 0), draft depths at n - 1 + depth with
+    slots n .., verify nodes at n - 1 + depth(k) with slots n - 1 + k; padding rows on page 0."""
+    import types
+    import numpy as np
+    import torch
+    from dgi.spec.eagle3 import _StepGraph
+    rng = np.random.default_rng(3)
+    bs, maxw = 16, 12
+    for _ in range(50):
+        Rb, C = int(rng.integers(1, 6)), int(rng.integers(2, 6))
+        depth = np.array([0] + sorted(rng.integers(1, 4, size=int(rng.integers(2, 7))).tolist()), dtype=np.int64)
+        N = len(depth)
+        lv, tot = [], Rb * maxw + 2 * Rb * C + 2 * Rb
+        for m in range(2, min(N, 4)):
+            lv.append((tot, m))
+            tot += 2 * Rb * m + Rb
+        o_v = tot
+        tot += 2 * Rb * N + Rb
+        g = object.__new__(_StepGraph)
+        g.Rb, g.C, g.N, g.maxw = Rb, C, N, maxw
+        g.eng = types.SimpleNamespace(pool=types.SimpleNamespace(block_size=bs))
+        g.host = torch.full((tot,), -7, dtype=torch.int32)
+        g.o_bt, g.o_c, g.o_v, g.lv, g.depth_np = 0, Rb * maxw, o_v, lv, depth
+        R = int(rng.integers(0, Rb + 1))
+        n_vec = rng.integers(C + 1, 150, size=R)
+        nv_vec = rng.integers(1, C + 1, size=R)
+        p0_vec = n_vec - nv_vec
+        brows = [rng.integers(1, 500, size=maxw).tolist() for _ in range(R)]
+        g._fill(n_vec, p0_vec, brows, nv_vec)
+        h = g.host.numpy()
+
+        def slot(i, p):
+            return brows[i][p // bs] * bs + p % bs
+        o = Rb * maxw
+        for i in range(Rb):
+            for k in range(C):
+                pos, sl = h[o + i * C + k], h[o + Rb * C + i * C + k]
+                if i < R:
+                    assert pos == p0_vec[i] + k
+                    assert sl == (slot(i, p0_vec[i] + k) if k < nv_vec[i] else k % bs)
+                else:
+                    assert pos == k and sl == k % bs
+            assert h[o + 2 * Rb * C + i] == (p0_vec[i] if i < R else 0) + C
+            assert h[o + 2 * Rb * C + Rb + i] == (nv_vec[i] - 1 if i < R else 0)
+        for i in range(Rb):
+            for k in range(N):
+                pos, sl = h[o_v + i * N + k], h[o_v + Rb * N + i * N + k]
+                if i < R:
+                    assert pos == n_vec[i] - 1 + depth[k] and sl == slot(i, n_vec[i] - 1 + k)
+                else:
+                    assert pos == k and sl == k % bs
+            assert h[o_v + 2 * Rb * N + i] == (n_vec[i] - 1 + N if i < R else N)
