@@ -193,6 +193,7 @@ def main():
     ap.add_argument("--plain-fused", action="store_true", help="also o-proj / down through fused_skinny configs")
     ap.add_argument("--plain", action="store_true", help="only the plain skinny-vs-hipBLASLt table")
     ap.add_argument("--plain-fused-ms", type=int, nargs="+", default=[1, 4, 8], help="row counts of --plain-fused")
+    ap.add_argument("--gemm-ms", type=int, nargs="+", default=[1, 2, 4, 8, 16], help="row counts of the fused table")
     ap.add_argument("--plain-fused-qkv", action="store_true", help="--plain-fused also times the qkv shape")
     a = ap.parse_args()
     if a.plain:
@@ -203,7 +204,7 @@ def main():
             with open(a.out, "w") as f:
                 json.dump(res, f, indent=1)
         return
-    res = {} if a.skip_gemms else {"gemm_8b": bench_gemms(4096, 14336, 32, 8, [1, 2, 4, 8, 16], a.cfgs)}
+    res = {} if a.skip_gemms else {"gemm_8b": bench_gemms(4096, 14336, 32, 8, a.gemm_ms, a.cfgs)}
     if a.plain_fused:
         shapes = [("o", 4096, 4096), ("down", 4096, 14336)] + ([("qkv", 6144, 4096)] if a.plain_fused_qkv else [])
         res["plain_fused_8b"] = bench_plain_fused(shapes, a.plain_fused_ms, a.cfgs)
